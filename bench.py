@@ -1,0 +1,314 @@
+#!/usr/bin/env python3
+"""Benchmark: mel-frames/s of the Conformer-S 1.58-bit training step (BASELINE.json metric).
+
+One "step" = the reference's full training step body (onebit_asr/train.py:82-120): the
+2-bit teacher, 1-bit student and stochastic-precision passes with decoder and
+CTC/CE/KL losses, backward, clip 5.0, AdamW, warmup-cosine -- on one synthetic padded
+batch of B=32 utterances x 1000 frames x 80 mels per GPU (configs[1]; configs[2] for N>1
+with one process per GPU, DDP gradient all-reduce over RCCL).
+
+value = mel frames processed by ALL ranks / max-over-ranks wall time of the K timed steps.
+
+Also reported:
+  roofline     -- the dominant BitLinear kernel: algorithmic bytes/FLOPs per launch (step mix)
+                  / its average launch duration, timed with HIP events on its stream;
+  cpu_baseline -- the CPU oracle (oracle/conformer_oracle.py, a restatement of the
+                  reference) on the host cores, bounded sample, rank 0 at N=1 only.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "cmu-11785-idl-1.58bit-asr_amd"
+for _p in (str(ROOT), str(PKG)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# gfx950 peaks (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+PEAK_FP32_MFMA_TFLOPS = 157.3
+
+N_MELS, VOCAB = 80, 5004
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--tokens", type=int, default=40)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------- roofline
+def ql_shapes(batch: int, frames: int, d: int = 144, d_ff: int = 576, layers: int = 16):
+    """(name, M, K, N, count_per_step) of every BitLinear call in one step (3 passes)."""
+    from onebit_asr.conformer import subsampled_length
+
+    t = subsampled_length(frames)
+    m = batch * t
+    per_pass = [("lin1", m, d, d_ff, 2), ("lin2", m, d_ff, d, 2), ("qkvo", m, d, d, 4),
+                ("pos", t, d, d, 1)]
+    return [(n, M, K, N, c * layers * 3) for (n, M, K, N, c) in per_pass]
+
+
+def roofline(batch, frames, dev, reps=20):
+    """Time each BitLinear kernel family at the step's shapes with HIP events on the current
+    stream; the dominant family (largest time per step) is reported against its roof."""
+    from onebit_asr import _lib
+    from onebit_asr.quant import pack_codes
+
+    lib = _lib.load()
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0], "dw_partial+ste_reduce": [0.0, 0.0, 0.0, 0]}
+    # fam value: [total_time_us_per_step, total_bytes_per_step, total_flops_per_step, launches]
+    detail = []
+    for name, M, K, N, count in ql_shapes(batch, frames):
+        g = torch.Generator(device=dev).manual_seed(M + K + N)
+        X = torch.randn(M, K, device=dev, generator=g)
+        dY = torch.randn(M, N, device=dev, generator=g)
+        W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
+        alpha = W.abs().mean()
+        b = torch.zeros(N, device=dev)
+        codes, codes_t = pack_codes(W, alpha, 2)
+        Y = torch.empty(M, N, device=dev)
+        dX = torch.empty(M, K, device=dev)
+        dW = torch.empty(N, K, device=dev)
+        da = torch.empty((), device=dev)
+        db = torch.empty(N, device=dev)
+        wsb = lib.ob_bitlinear_bwd_dw_workspace(M, N, K)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+
+        def fwd():
+            lib.ob_bitlinear_fwd(X.data_ptr(), M, K, codes.data_ptr(), alpha.data_ptr(), 1,
+                                 b.data_ptr(), N, Y.data_ptr(), s)
+
+        def bdx():
+            lib.ob_bitlinear_bwd_dx(dY.data_ptr(), M, N, codes_t.data_ptr(), alpha.data_ptr(), 1,
+                                    K, dX.data_ptr(), s)
+
+        def bdw():
+            lib.ob_bitlinear_bwd_dw(dY.data_ptr(), X.data_ptr(), M, N, K, W.data_ptr(),
+                                    alpha.data_ptr(), 1, 2, dW.data_ptr(), da.data_ptr(),
+                                    db.data_ptr(), ws.data_ptr(), wsb, s)
+
+        def timed(fn):
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            e1.synchronize()
+            return e0.elapsed_time(e1) * 1e3 / reps  # us per launch
+
+        t_f, t_dx, t_dw = timed(fwd), timed(bdx), timed(bdw)
+        cw = 4 * N * ((K + 15) // 16)
+        by_f = 4 * (M * K + M * N + N) + cw           # X, Y, bias, codes
+        by_dx = 4 * (M * N + M * K) + cw               # dY, dX, codes_t
+        by_dw = 4 * (M * N + M * K + 2 * N * K + N)    # dY, X, W, dW, db
+        fl = 2.0 * M * K * N
+        n_dx = 0 if name == "pos" else count  # pos_emb needs no input gradient
+        f = fam["ternary_gemm"]
+        f[0] += count * t_f + n_dx * t_dx
+        f[1] += count * by_f + n_dx * by_dx
+        f[2] += (count + n_dx) * fl
+        f[3] += count + n_dx
+        f = fam["dw_partial+ste_reduce"]
+        f[0] += count * t_dw
+        f[1] += count * by_dw
+        f[2] += count * fl
+        f[3] += count
+        detail.append({"layer": name, "M": M, "K": K, "N": N, "per_step": count,
+                       "fwd_us": round(t_f, 2), "dx_us": round(t_dx, 2), "dw_us": round(t_dw, 2)})
+    dom = max(fam, key=lambda k: fam[k][0])
+    t_us, by, fl, n = fam[dom]
+    avg_t = t_us / n
+    gbs = (by / n) / (avg_t * 1e-6) / 1e9
+    tfs = (fl / n) / (avg_t * 1e-6) / 1e12
+    # fp32-MFMA kernels: the binding roof is whichever takes longer at peak
+    bound_mfma = (fl / PEAK_FP32_MFMA_TFLOPS / 1e12) > (by / PEAK_HBM_GBS / 1e9)
+    if bound_mfma:
+        roof = {"bound": "mfma", "achieved": round(tfs, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(tfs / PEAK_FP32_MFMA_TFLOPS, 4)}
+    else:
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    roof.update({"kernel": dom, "avg_launch_us": round(avg_t, 3),
+                 "bytes_per_launch": int(by / n), "flops_per_launch": int(fl / n),
+                 "achieved_GBs": round(gbs, 1), "achieved_TFLOPs": round(tfs, 2),
+                 "ql_kernel_ms_per_step": {k: round(v[0] / 1e3, 3) for k, v in fam.items()},
+                 "shapes": detail})
+    return roof
+
+
+def traffic_from(path, kernel):
+    try:
+        data = json.loads(Path(path).read_text())
+        return data.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+# ------------------------------------------------------------------------- cpu baseline
+def cpu_baseline(seconds: float):
+    """The oracle step (CPU restatement) on a bounded sample of the same workload."""
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CONFORMER_S, synthetic_batch
+    from oracle.conformer_oracle import OracleConformer, oracle_step_loss
+
+    threads = min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1234)
+    prod = ConformerASR(N_MELS, VOCAB, **CONFORMER_S)
+    orc = OracleConformer(prod.state_dict(), input_dim=N_MELS, vocab_size=VOCAB, d_model=144,
+                          n_layers=16, n_heads=4, d_ff=576, conv_kernel=31, dec_layers=2,
+                          dec_heads=4, dec_d_ff=1024, dropout=0.1)
+    orc.train()
+    opt = torch.optim.AdamW(orc.parameters(), lr=5e-4, betas=(0.9, 0.98), weight_decay=1e-2)
+    bsz = 2
+    b = synthetic_batch([1000] * bsz, [40] * bsz, seed=99)
+    g = torch.Generator().manual_seed(4321)
+    from onebit_asr.train_step import sample_sp_mask
+
+    def one():
+        loss, _ = oracle_step_loss(orc, b, sample_sp_mask(16, generator=g))
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(orc.parameters(), 5.0)
+        opt.step()
+
+    one()  # warm-up
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end and len(times) < 20:
+        t0 = time.perf_counter()
+        one()
+        times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"value": round(bsz * 1000 / t, 1), "unit": "mel-frames/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle (CPU fp32 restatement) full 3-pass step + AdamW on Conformer-S, "
+                      f"B={bsz} x 1000 frames, median of {len(times)} steps after 1 warm-up; "
+                      f"{threads} threads on {cpu}"}
+
+
+# ------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CONFORMER_S, synthetic_batch
+    from onebit_asr.train_step import OneBitStep, WarmupCosine, make_optimizer, sample_sp_mask, train_step
+
+    torch.manual_seed(1234)  # identical init on every rank (DDP also broadcasts)
+    model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S).to(dev)
+    step_mod = OneBitStep(model, n_layers=CONFORMER_S["enc_layers"])
+    if distributed:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        step_mod = DDP(step_mod, device_ids=[local], broadcast_buffers=False,
+                       gradient_as_bucket_view=True)
+    opt = make_optimizer(model.parameters())
+    sched = WarmupCosine(opt, warmup_steps=4000, total_steps=100000)
+    batch = synthetic_batch([args.frames] * args.batch, [args.tokens] * args.batch,
+                            seed=1234 + rank, device=dev)
+    sp_gen = torch.Generator().manual_seed(4321)  # same SP masks on every rank
+
+    def step():
+        return train_step(step_mod, opt, sched, batch, sample_sp_mask(CONFORMER_S["enc_layers"], generator=sp_gen))
+
+    for _ in range(args.warmup):
+        loss, _ = step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, _ = step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_val = float(loss.item())
+
+    frames_total = world * args.batch * args.frames * args.steps
+    value = frames_total / elapsed
+    out = {
+        "metric": "mel-frames/sec (Conformer-S 1.58-bit train step)",
+        "value": round(value, 1),
+        "unit": "mel-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (N(0,1) 80-mel x 1000-frame padded batches, random-init weights)",
+        "config": {"workload": "conformer-s-1.58bit-train-step", "global_batch": args.batch * world,
+                   "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
+                   "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
+                   "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP"},
+        "final_loss": round(loss_val, 4),
+    }
+    if rank == 0 and world == 1 and not args.no_roofline:
+        roof = roofline(args.batch, args.frames, dev)
+        roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
+        out["roofline"] = roof
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

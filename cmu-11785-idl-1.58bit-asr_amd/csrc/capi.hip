@@ -1,0 +1,155 @@
+// capi.hip — the C ABI declared in include/onebit_hip.h: argument validation, workspace
+// carving and launch-error reporting around the launchers in quant.hip / gemm.hip.
+#include "../../include/onebit_hip.h"
+#include "ob_launch.h"
+
+using namespace ob;
+
+namespace {
+
+constexpr int kAbiVersion = 1;
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+
+inline int check_bits(int bits) { return (bits == 1 || bits == 2) ? OB_OK : OB_ERR_BITWIDTH; }
+
+inline int launched() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? OB_OK : OB_ERR_HIP;
+}
+
+inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct DwWorkspace {
+  size_t part, part_db, apart, total;
+};
+
+DwWorkspace dw_layout(int64_t M, int64_t N, int64_t K) {
+  const DwPlan p = plan_dw(M, N, K);
+  DwWorkspace w;
+  w.part = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N * (size_t)K);
+  w.part_db = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N);
+  w.apart = align_up(sizeof(float) * (size_t)ste_reduce_blocks(N * K + N) + sizeof(float));
+  w.total = w.part + w.part_db + w.apart;
+  return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ob_abi_version(void) { return kAbiVersion; }
+
+const char* ob_status_string(int status) {
+  switch (status) {
+    case OB_OK: return "ok";
+    case OB_ERR_NULL: return "null pointer argument";
+    case OB_ERR_SHAPE: return "invalid shape";
+    case OB_ERR_BITWIDTH: return "bitwidth must be one of {1,2,32}";
+    case OB_ERR_WORKSPACE: return "workspace too small";
+    case OB_ERR_ALIGN: return "pointer not 4-byte aligned";
+    case OB_ERR_HIP: return "HIP launch error";
+    default: return "unknown status";
+  }
+}
+
+int ob_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits, int64_t N,
+                  int64_t K, uint32_t* codes, uint32_t* codes_t, void* stream) {
+  if (int st = check_bits(bits)) return st;
+  if (N < 0 || K < 0) return OB_ERR_SHAPE;
+  if (!alpha || (N * K > 0 && !W)) return OB_ERR_NULL;
+  if (!aligned4(W) || !aligned4(codes) || !aligned4(codes_t)) return OB_ERR_ALIGN;
+  launch_quant_pack(W, alpha, alpha_raw, bits, N, K, codes, codes_t, as_stream(stream));
+  return launched();
+}
+
+int ob_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
+                     float* W_hat, void* stream) {
+  if (int st = check_bits(bits)) return st;
+  if (n < 0) return OB_ERR_SHAPE;
+  if (!alpha || (n > 0 && (!W || !W_hat))) return OB_ERR_NULL;
+  if (!aligned4(W) || !aligned4(W_hat)) return OB_ERR_ALIGN;
+  launch_quant_dequant(W, alpha, alpha_raw, bits, n, W_hat, as_stream(stream));
+  return launched();
+}
+
+size_t ob_quant_ste_bwd_workspace(int64_t n) {
+  if (n < 0) return 0;
+  return align_up(sizeof(float) * (size_t)ste_reduce_blocks(n) + sizeof(float));
+}
+
+int ob_quant_ste_bwd(const float* grad_W_hat, const float* W, const float* alpha, int alpha_raw,
+                     int bits, int64_t n, float* grad_W, float* grad_alpha, void* ws,
+                     size_t ws_bytes, void* stream) {
+  if (int st = check_bits(bits)) return st;
+  if (n < 0) return OB_ERR_SHAPE;
+  if (!alpha || !grad_alpha || !ws || (n > 0 && (!grad_W_hat || !W || !grad_W)))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_quant_ste_bwd_workspace(n)) return OB_ERR_WORKSPACE;
+  launch_ste_reduce(grad_W_hat, 1, n, nullptr, 0, W, alpha, alpha_raw, bits, grad_W, nullptr,
+                    static_cast<float*>(ws), grad_alpha, as_stream(stream));
+  return launched();
+}
+
+int ob_bitlinear_fwd(const float* X, int64_t M, int64_t K, const uint32_t* codes,
+                     const float* alpha, int alpha_raw, const float* bias, int64_t N, float* Y,
+                     void* stream) {
+  if (M < 0 || K < 0 || N < 0) return OB_ERR_SHAPE;
+  if (!alpha || (M * N > 0 && !Y) || (M * K > 0 && !X) || (N * K > 0 && !codes))
+    return OB_ERR_NULL;
+  if (!aligned4(X) || !aligned4(Y) || !aligned4(bias)) return OB_ERR_ALIGN;
+  launch_ternary_gemm(X, M, K, codes, N, alpha, alpha_raw, bias, Y, as_stream(stream));
+  return launched();
+}
+
+int ob_bitlinear_bwd_dx(const float* dY, int64_t M, int64_t N, const uint32_t* codes_t,
+                        const float* alpha, int alpha_raw, int64_t K, float* dX, void* stream) {
+  if (M < 0 || K < 0 || N < 0) return OB_ERR_SHAPE;
+  if (!alpha || (M * K > 0 && !dX) || (M * N > 0 && !dY) || (N * K > 0 && !codes_t))
+    return OB_ERR_NULL;
+  if (!aligned4(dY) || !aligned4(dX)) return OB_ERR_ALIGN;
+  // dX = a * dY . Q: the same ternary GEMM with the roles of N and K exchanged.
+  launch_ternary_gemm(dY, M, N, codes_t, K, alpha, alpha_raw, nullptr, dX, as_stream(stream));
+  return launched();
+}
+
+size_t ob_bitlinear_bwd_dw_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return 0;
+  return dw_layout(M, N, K).total;
+}
+
+int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                        const float* W, const float* alpha, int alpha_raw, int bits, float* dW,
+                        float* dalpha, float* db, void* ws, size_t ws_bytes, void* stream) {
+  if (int st = check_bits(bits)) return st;
+  if (M < 0 || N < 0 || K < 0) return OB_ERR_SHAPE;
+  if (!alpha || !dalpha || !ws || (N * K > 0 && (!W || !dW)) || (M > 0 && (!dY || (K > 0 && !X))))
+    return OB_ERR_NULL;
+  if (!aligned4(dY) || !aligned4(X) || !aligned4(dW) || !aligned4(db)) return OB_ERR_ALIGN;
+  const DwWorkspace L = dw_layout(M, N, K);
+  if (ws_bytes < L.total) return OB_ERR_WORKSPACE;
+  const DwPlan p = plan_dw(M, N, K);
+  char* base = static_cast<char*>(ws);
+  float* part = reinterpret_cast<float*>(base);
+  float* part_db = db ? reinterpret_cast<float*>(base + L.part) : nullptr;
+  float* apart = reinterpret_cast<float*>(base + L.part + L.part_db);
+  hipStream_t s = as_stream(stream);
+  int chunks = (int)p.chunks;
+  if (M == 0) {
+    // No rows: every gradient is zero. Zero the first slab and reduce one chunk.
+    if (N * K > 0 && hipMemsetAsync(part, 0, sizeof(float) * N * K, s) != hipSuccess)
+      return OB_ERR_HIP;
+    if (db && N > 0 && hipMemsetAsync(part_db, 0, sizeof(float) * N, s) != hipSuccess)
+      return OB_ERR_HIP;
+    chunks = 1;
+  } else {
+    launch_dw_partial(dY, X, M, N, K, p, part, part_db, s);
+  }
+  launch_ste_reduce(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, bits, dW, db,
+                    apart, dalpha, s);
+  return launched();
+}
+
+}  // extern "C"

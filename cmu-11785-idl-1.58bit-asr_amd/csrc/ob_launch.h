@@ -1,0 +1,42 @@
+// ob_launch.h — internal (C++) launchers behind the C ABI in capi.hip.
+// Arguments are validated by capi.hip before any of these is called.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ob {
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// quant.hip
+void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits, int64_t N,
+                       int64_t K, uint32_t* codes, uint32_t* codes_t, hipStream_t s);
+void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
+                          float* W_hat, hipStream_t s);
+
+// Split-reduction finish shared by both backward entries: sums `chunks` fp32 slabs of
+// length nk (+ an optional [chunks][n_db] bias slab), applies the STE mask, writes dW and
+// the per-block alpha partials, then a one-block finalize writes dalpha.
+// `apart` must hold ste_reduce_blocks(nk + n_db) floats.
+int64_t ste_reduce_blocks(int64_t total);
+void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* part_db,
+                       int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,
+                       float* dW, float* db, float* apart, float* dalpha, hipStream_t s);
+
+// gemm.hip
+// C[M][N] = a * (A[M][K] . Q^T) + bias, Q given as 2-bit codes [N][ceil(K/16)].
+void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
+                         const float* alpha, int alpha_raw, const float* bias, float* C,
+                         hipStream_t s);
+
+// Split-M partial of G = dY^T . X: part[c][N*K] for chunk c, part_db[c][N] (optional).
+struct DwPlan {
+  int64_t tiles_n, tiles_k, chunks, rows_per_chunk;
+};
+DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
+void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                       const DwPlan& p, float* part, float* part_db, hipStream_t s);
+
+}  // namespace ob

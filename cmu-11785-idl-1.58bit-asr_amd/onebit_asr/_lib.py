@@ -1,0 +1,92 @@
+"""ctypes binding of libonebit_hip.so, the C ABI declared in include/onebit_hip.h.
+
+The library is built in-tree (``make -C cmu-11785-idl-1.58bit-asr_amd/csrc`` or
+``__graft_entry__.build()``). There is deliberately no fallback: if the library is
+missing or a call fails, every caller raises. The reference's eager-torch quantizer
+(onebit_asr/quant.py:38-127) is re-stated only under ``oracle/`` as a test checker.
+
+``torch`` is imported before the library is opened so that the ``libamdhip64.so.7``
+torch already loaded (same SONAME) is the HIP runtime the kernels run on, and a
+``torch.cuda`` stream handle is a valid ``hipStream_t`` for every entry point.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
+
+LIB_NAME = "libonebit_hip.so"
+LIB_PATH = Path(os.environ.get("ONEBIT_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
+
+OB_OK = 0
+OB_ERR_BITWIDTH = -3
+
+_c_f = ctypes.c_void_p  # device pointers are passed as raw addresses
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/onebit_hip.h one-to-one.
+SIGNATURES = {
+    "ob_abi_version": (_int, []),
+    "ob_status_string": (ctypes.c_char_p, [_int]),
+    "ob_quant_pack": (_int, [_c_f, _c_f, _int, _int, _i64, _i64, _c_f, _c_f, _c_f]),
+    "ob_quant_dequant": (_int, [_c_f, _c_f, _int, _int, _i64, _c_f, _c_f]),
+    "ob_quant_ste_bwd_workspace": (_sz, [_i64]),
+    "ob_quant_ste_bwd": (_int, [_c_f, _c_f, _c_f, _int, _int, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_bitlinear_fwd": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dx": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _int, _i64, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dw_workspace": (_sz, [_i64, _i64, _i64]),
+    "ob_bitlinear_bwd_dw": (
+        _int,
+        [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _int, _int, _c_f, _c_f, _c_f, _c_f, _sz, _c_f],
+    ),
+}
+
+ABI_VERSION = 1
+
+_lib = None
+
+
+class OneBitHipError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Open the library once; raise if it is absent or its ABI does not match."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.is_file():
+        raise OneBitHipError(
+            f"{LIB_PATH} is missing: build it with `make -C cmu-11785-idl-1.58bit-asr_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback for the BitLinear path"
+        )
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ob_abi_version() != ABI_VERSION:
+        raise OneBitHipError(f"ABI mismatch: library {lib.ob_abi_version()} != {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status == OB_OK:
+        return
+    msg = load().ob_status_string(status).decode()
+    if status == OB_ERR_BITWIDTH:
+        raise ValueError("bitwidth must be one of {1,2,32}")
+    raise OneBitHipError(f"{what}: {msg} (status {status})")
+
+
+def ptr(t: "torch.Tensor | None") -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream

@@ -1,0 +1,318 @@
+"""Conformer encoder/decoder around the BitLinear hot path (call sites of QuantizedLinear).
+
+Module tree, constructor signatures, forward signatures and parameter names follow the
+reference's onebit_asr/conformer.py so that checkpoints (state-dict keys, eval.py:282)
+and ``train.py`` call sites carry over unchanged:
+
+* ``ConformerASR(input_dim, vocab_size, enc_d_model=256, enc_layers=12, enc_heads=4,
+  enc_d_ff=1024, enc_conv_kernel=31, enc_dropout=0.1, dec_layers=2, dec_heads=4,
+  dec_d_ff=1024, dec_dropout=0.1, pad_id=0)``                      (conformer.py:302-313)
+* ``ConformerASR.forward(batch, precision, sp_mask=None) -> (enc_out, enc_mask, logits)``
+  and ``decode_logits(enc_out, enc_mask, tgt_inp, tgt_pad_mask)``  (conformer.py:315-322)
+* ``ConformerEncoder.forward(feats, feat_lens, precision, sp_mask=None)`` (:243-272)
+* ``ConformerBlock.forward(x, src_mask, bitwidth_linear, pos_emb)``     (:222-228)
+* ``MHSA.forward(x, mask, bitwidth, pos_emb)`` / ``FeedForwardModule.forward(x, bitwidth,
+  mask=None)``                                                           (:105, :34)
+
+Per block 9 QuantizedLinear call sites take the block's bitwidth: ff1.lin1/lin2,
+mhsa.q/k/v/pos/out_proj, ff2.lin1/lin2. Everything else is full precision in the
+reference (conv module "kept full-precision per paper recommendation", :225; subsampling
+``out``, ``ctc_head``, decoder) and stays stock PyTorch-ROCm here.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .quant import QuantizedLinear
+
+__all__ = [
+    "LayerNorm", "FeedForwardModule", "RelPositionalEncoding", "MHSA", "ConvModule",
+    "Conv2dSubsampling", "ConformerBlock", "ConformerEncoder", "TransformerDecoder",
+    "ConformerASR", "block_bitwidths", "subsampled_length",
+]
+
+
+def swish(x: torch.Tensor) -> torch.Tensor:
+    # conformer.py:15-16 (x * sigmoid(x)); silu is the same function in one kernel.
+    return F.silu(x)
+
+
+class LayerNorm(nn.Module):
+    """Wrapper kept for the ``<...>.ln.ln.weight`` checkpoint keys (conformer.py:19-24)."""
+
+    def __init__(self, d_model: int):
+        super().__init__()
+        self.ln = nn.LayerNorm(d_model)
+
+    def forward(self, x):
+        return self.ln(x)
+
+
+def _pad_rows(y: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
+    # Zero padded frames: mask is the [B,T,T] attention mask, mask[:, :, 0] the frame mask.
+    if mask is None:
+        return y
+    return y * mask[:, :, 0].unsqueeze(-1)
+
+
+class FeedForwardModule(nn.Module):
+    """Macaron half-step FFN (conformer.py:27-45): x + 0.5*lin2(drop(swish(lin1(LN x))))."""
+
+    def __init__(self, d_model: int, d_ff: int, dropout: float):
+        super().__init__()
+        self.ln = LayerNorm(d_model)
+        self.lin1 = QuantizedLinear(d_model, d_ff)
+        self.lin2 = QuantizedLinear(d_ff, d_model)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, bitwidth: int, mask=None):
+        h = self.lin1(self.ln(x), bitwidth)
+        h = self.dropout(swish(h))
+        h = self.dropout(self.lin2(h, bitwidth))
+        return x + 0.5 * _pad_rows(h, mask)
+
+
+class RelPositionalEncoding(nn.Module):
+    """Absolute sinusoid table for positions 0..T-1 (conformer.py:48-76); x is not
+    scaled by sqrt(d). The table is a persistent buffer ``pe`` [1, L, d] (L >= 5000),
+    grown on demand."""
+
+    def __init__(self, d_model: int, dropout_rate: float = 0.1, max_len: int = 5000):
+        super().__init__()
+        self.d_model = d_model
+        self.dropout = nn.Dropout(p=dropout_rate)
+        self.register_buffer("pe", self._table(max_len, torch.device("cpu")))
+
+    def _table(self, length: int, device) -> torch.Tensor:
+        pos = torch.arange(length, dtype=torch.float32).unsqueeze(1)
+        freq = torch.exp(torch.arange(0, self.d_model, 2, dtype=torch.float32)
+                         * -(math.log(10000.0) / self.d_model))
+        table = torch.zeros(length, self.d_model)
+        table[:, 0::2] = torch.sin(pos * freq)
+        table[:, 1::2] = torch.cos(pos * freq)
+        return table.unsqueeze(0).to(device)
+
+    def extend_pe(self, length: int) -> None:
+        if self.pe.size(1) < length:
+            self.pe = self._table(length, self.pe.device)
+
+    def forward(self, x):
+        t = x.size(1)
+        self.extend_pe(t)
+        return self.dropout(x), self.pe[:, :t]
+
+
+def rel_shift(scores: torch.Tensor) -> torch.Tensor:
+    """Transformer-XL shift of a [B,H,T,T] score tensor exactly as conformer.py:97-103:
+    prepend a zero column, reinterpret the (T, T+1) rows as a flat sequence and drop its
+    first T entries."""
+    b, h, t1, t2 = scores.shape
+    padded = F.pad(scores, (1, 0))  # [B,H,T1,T2+1], zero column first
+    return padded.reshape(b, h, -1)[:, :, t1:].reshape(b, h, t1, t2)
+
+
+class MHSA(nn.Module):
+    """Relative-position multi-head self-attention (conformer.py:79-138). Five BitLinear
+    projections: q/k/v on LN(x), pos_proj on the batch-1 sinusoid table, out_proj."""
+
+    def __init__(self, d_model: int, n_heads: int, dropout: float):
+        super().__init__()
+        assert d_model % n_heads == 0
+        self.d_model = d_model
+        self.n_heads = n_heads
+        self.d_head = d_model // n_heads
+        self.ln = LayerNorm(d_model)
+        self.q_proj = QuantizedLinear(d_model, d_model)
+        self.k_proj = QuantizedLinear(d_model, d_model)
+        self.v_proj = QuantizedLinear(d_model, d_model)
+        self.pos_proj = QuantizedLinear(d_model, d_model)
+        self.out_proj = QuantizedLinear(d_model, d_model)
+        self.dropout = nn.Dropout(dropout)
+        self.pos_bias_u = nn.Parameter(torch.randn(self.n_heads, self.d_head) * 0.01)
+        self.pos_bias_v = nn.Parameter(torch.randn(self.n_heads, self.d_head) * 0.01)
+
+    def rel_shift(self, x):
+        return rel_shift(x)
+
+    def _heads(self, t: torch.Tensor, batch: int) -> torch.Tensor:
+        return t.view(batch, -1, self.n_heads, self.d_head).transpose(1, 2)
+
+    def forward(self, x, mask, bitwidth: int, pos_emb: torch.Tensor):
+        bsz, tlen, width = x.shape
+        assert width == self.d_model, f"Expected {self.d_model}, got {width}"
+        h = self.ln(x)
+        q = self._heads(self.q_proj(h, bitwidth), bsz)
+        k = self._heads(self.k_proj(h, bitwidth), bsz)
+        v = self._heads(self.v_proj(h, bitwidth), bsz)
+        p = self._heads(self.pos_proj(pos_emb, bitwidth), 1)
+        u_bias = self.pos_bias_u.view(1, self.n_heads, 1, self.d_head)
+        v_bias = self.pos_bias_v.view(1, self.n_heads, 1, self.d_head)
+        content = torch.matmul(q + u_bias, k.transpose(-2, -1))
+        position = rel_shift(torch.matmul(q + v_bias, p.transpose(-2, -1)))
+        scores = (content + position) / math.sqrt(self.d_head)
+        if mask is not None:
+            scores = scores.masked_fill(mask[:, None, :, :] == 0, float("-inf"))
+        # Fully masked rows are all -inf -> NaN; the reference zeroes them (:124-127).
+        attn = self.dropout(torch.nan_to_num(torch.softmax(scores, dim=-1), nan=0.0))
+        ctx = torch.matmul(attn, v).transpose(1, 2).contiguous().view(bsz, tlen, width)
+        out = self.dropout(self.out_proj(ctx, bitwidth))
+        return x + _pad_rows(out, mask)
+
+
+class ConvModule(nn.Module):
+    """LN -> pw1 -> GLU -> depthwise k -> BatchNorm(batch stats, track_running_stats=False)
+    -> swish -> pw2 (conformer.py:141-167). Full precision."""
+
+    def __init__(self, d_model: int, kernel_size: int = 31, dropout: float = 0.1):
+        super().__init__()
+        self.ln = LayerNorm(d_model)
+        self.pw1 = nn.Conv1d(d_model, 2 * d_model, kernel_size=1)
+        self.glu = nn.GLU(dim=1)
+        self.dw = nn.Conv1d(d_model, d_model, kernel_size=kernel_size,
+                            padding=kernel_size // 2, groups=d_model)
+        self.bn = nn.BatchNorm1d(d_model, track_running_stats=False)
+        self.pw2 = nn.Conv1d(d_model, d_model, kernel_size=1)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, mask=None):
+        h = self.glu(self.pw1(self.ln(x).transpose(1, 2)))
+        h = self.pw2(swish(self.bn(self.dw(h))))
+        h = self.dropout(h).transpose(1, 2)
+        return x + _pad_rows(h, mask)
+
+
+def subsampled_length(t: int) -> int:
+    """Frames after two k=3, s=2 valid convolutions (conformer.py:183-185)."""
+    return ((t - 3) // 2 + 1 - 3) // 2 + 1
+
+
+class Conv2dSubsampling(nn.Module):
+    """[B,T,F] -> [B,T',d] with two 3x3 stride-2 Conv2d + ReLU and a Linear over
+    (d x F') (conformer.py:170-208)."""
+
+    def __init__(self, idim: int, d_model: int):
+        super().__init__()
+        self.d_model = d_model
+        self.conv = nn.Sequential(
+            nn.Conv2d(1, d_model, kernel_size=3, stride=2),
+            nn.ReLU(),
+            nn.Conv2d(d_model, d_model, kernel_size=3, stride=2),
+            nn.ReLU(),
+        )
+        f_out = ((idim - 1) // 2 - 1) // 2
+        if f_out <= 0:
+            raise ValueError(f"Input dim too small for Conv2dSubsampling: idim={idim}")
+        self.out = nn.Linear(d_model * f_out, d_model)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        y = self.conv(x.unsqueeze(1))                      # [B, C, T', F']
+        bsz, ch, tsub, fsub = y.shape
+        y = y.transpose(1, 2).reshape(bsz, tsub, ch * fsub)  # channel-major per frame
+        return self.out(y)
+
+
+class ConformerBlock(nn.Module):
+    """ff1 -> mhsa -> conv (FP) -> ff2 -> LN (conformer.py:212-228)."""
+
+    def __init__(self, d_model: int, d_ff: int, n_heads: int, conv_kernel: int, dropout: float,
+                 block_index: int):
+        super().__init__()
+        self.block_index = block_index
+        self.ff1 = FeedForwardModule(d_model, d_ff, dropout)
+        self.mhsa = MHSA(d_model, n_heads, dropout)
+        self.conv = ConvModule(d_model, kernel_size=conv_kernel, dropout=dropout)
+        self.ff2 = FeedForwardModule(d_model, d_ff, dropout)
+        self.ln = LayerNorm(d_model)
+
+    def forward(self, x, src_mask, bitwidth_linear: int, pos_emb: torch.Tensor):
+        x = self.ff1(x, bitwidth_linear)
+        x = self.mhsa(x, src_mask, bitwidth_linear, pos_emb)
+        x = self.conv(x)  # the reference does not pass the mask here (:225)
+        x = self.ff2(x, bitwidth_linear)
+        return self.ln(x)
+
+
+def block_bitwidths(n_layers: int, precision: int, sp_mask: Optional[Sequence[int]]) -> List[int]:
+    """Per-block BitLinear bitwidth (conformer.py:265-269): ``precision`` everywhere, or with
+    an SP mask 1 where sp_mask[i] == 1 else 2; anything outside {1, 2} runs at 32."""
+    out = []
+    for i in range(n_layers):
+        bw = precision if sp_mask is None else (1 if sp_mask[i] == 1 else 2)
+        out.append(bw if bw in (1, 2) else 32)
+    return out
+
+
+class ConformerEncoder(nn.Module):
+    def __init__(self, input_dim: int, d_model: int, n_layers: int, n_heads: int,
+                 d_ff: int, conv_kernel: int, dropout: float):
+        super().__init__()
+        self.subsample = Conv2dSubsampling(input_dim, d_model)
+        self.pos_enc = RelPositionalEncoding(d_model, dropout)
+        self.blocks = nn.ModuleList([
+            ConformerBlock(d_model, d_ff, n_heads, conv_kernel, dropout, i)
+            for i in range(n_layers)
+        ])
+        self.ln_out = LayerNorm(d_model)
+
+    def forward(self, feats: torch.Tensor, feat_lens: torch.Tensor,
+                precision: int, sp_mask: Optional[List[int]] = None):
+        """conformer.py:243-272. Frame validity uses feat_lens // 4 against the T' actually
+        produced by the convolutions (so it can disagree by one frame, as in the reference)."""
+        x = self.subsample(feats)
+        tsub = x.size(1)
+        x, pos_emb = self.pos_enc(x)
+        frames = torch.arange(tsub, device=feats.device).unsqueeze(0)
+        key_mask = frames < (feat_lens // 4).unsqueeze(1)            # [B, T'] bool
+        attn_mask = key_mask.unsqueeze(2) & key_mask.unsqueeze(1)     # [B, T', T']
+        for blk, bw in zip(self.blocks, block_bitwidths(len(self.blocks), precision, sp_mask)):
+            x = blk(x, attn_mask, bw, pos_emb)
+        return self.ln_out(x), key_mask
+
+
+class TransformerDecoder(nn.Module):
+    """Stock 2-layer nn.TransformerDecoder head (conformer.py:275-299), full precision."""
+
+    def __init__(self, vocab_size: int, d_model: int, n_layers: int, n_heads: int,
+                 d_ff: int, dropout: float, pad_id: int):
+        super().__init__()
+        self.emb = nn.Embedding(vocab_size, d_model, padding_idx=pad_id)
+        layer = nn.TransformerDecoderLayer(d_model=d_model, nhead=n_heads, dim_feedforward=d_ff,
+                                           dropout=dropout, batch_first=True)
+        self.dec = nn.TransformerDecoder(layer, num_layers=n_layers)
+        self.ln = LayerNorm(d_model)
+        self.out = nn.Linear(d_model, vocab_size)
+
+    def forward(self, tgt_inp, memory, memory_mask, tgt_key_padding_mask):
+        tt = tgt_inp.size(1)
+        future = torch.ones(tt, tt, device=tgt_inp.device).triu(diagonal=1).bool()
+        causal = torch.zeros(tt, tt, device=tgt_inp.device).masked_fill(future, float("-inf"))
+        y = self.dec(self.emb(tgt_inp), memory, tgt_mask=causal,
+                     memory_key_padding_mask=(memory_mask == 0),
+                     tgt_key_padding_mask=tgt_key_padding_mask)
+        return self.out(self.ln(y))
+
+
+class ConformerASR(nn.Module):
+    def __init__(self, input_dim: int, vocab_size: int,
+                 enc_d_model=256, enc_layers=12, enc_heads=4, enc_d_ff=1024,
+                 enc_conv_kernel=31, enc_dropout=0.1,
+                 dec_layers=2, dec_heads=4, dec_d_ff=1024, dec_dropout=0.1,
+                 pad_id=0):
+        super().__init__()
+        self.encoder = ConformerEncoder(input_dim, enc_d_model, enc_layers, enc_heads,
+                                        enc_d_ff, enc_conv_kernel, enc_dropout)
+        self.decoder = TransformerDecoder(vocab_size, enc_d_model, dec_layers, dec_heads,
+                                          dec_d_ff, dec_dropout, pad_id)
+        self.ctc_head = nn.Linear(enc_d_model, vocab_size)
+
+    def forward(self, batch, precision: int, sp_mask=None):
+        enc_out, enc_mask = self.encoder(batch["feats"], batch["feat_lens"], precision, sp_mask)
+        return enc_out, enc_mask, self.ctc_head(enc_out)
+
+    def decode_logits(self, enc_out, enc_mask, tgt_inp, tgt_pad_mask):
+        return self.decoder(tgt_inp, enc_out, enc_mask, tgt_pad_mask)

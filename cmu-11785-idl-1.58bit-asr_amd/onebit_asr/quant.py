@@ -1,0 +1,232 @@
+"""BitLinear / QuantizedLinear on MI355X: the reference's layer surface over HIP kernels.
+
+Reference surface kept verbatim (onebit_asr/quant.py of y00njaekim/CMU-11785-IDL-1.58bit-ASR):
+
+* ``QuantizedLinear(in_features, out_features, bias=True)`` with parameters ``weight``
+  ``[out, in]``, ``alpha`` (0-dim) and ``bias`` ``[out]`` -- the checkpoint keys
+  (quant.py:99-118, eval.py:282);
+* ``QuantizedLinear.forward(x, bitwidth)`` with ``bitwidth`` in {1, 2, 32}
+  (quant.py:120-127);
+* ``quantize_weight(W, alpha, bitwidth)`` and ``_QuantizeSTE`` (quant.py:38-96);
+* ``ValueError("bitwidth must be one of {1,2,32}")`` for any other bitwidth (quant.py:65-66).
+
+What changes is the execution: for bitwidth 1/2 the layer never materialises
+``W_hat = alpha * Q``. One launch packs W into 2-bit codes (cached per weight version,
+so the three passes of a training step share it), one launch runs the ternary GEMM
+with the scale and bias in its epilogue, and the backward is one dX GEMM plus one
+split-M dW GEMM whose reduction applies the STE mask and the alpha gradient
+(quant.py:72-92) in the same pass. The bitwidth is a Python int: there is no
+``torch.tensor(bitwidth)`` H2D copy per call and no ``.item()`` sync in backward
+(quant.py:69,75).
+
+bitwidth 32 stays ``F.linear`` on the weight, as in the reference (quant.py:121-122).
+There is no CPU path for bitwidth 1/2: the oracle under ``oracle/`` is the checker.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+__all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes"]
+
+_VALID = (1, 2, 32)
+
+
+def _check_bitwidth(bitwidth: int) -> int:
+    if bitwidth not in _VALID:
+        raise ValueError("bitwidth must be one of {1,2,32}")
+    return int(bitwidth)
+
+
+def _require_device(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "BitLinear bitwidth 1/2 runs only on a ROCm device (HIP kernels, no CPU "
+                "fallback); move the module and inputs to 'cuda'"
+            )
+        if t is not None and t.dtype != torch.float32:
+            raise TypeError(f"BitLinear parity path computes in fp32, got {t.dtype}")
+
+
+def pack_codes(weight: torch.Tensor, alpha: torch.Tensor, bits: int, alpha_raw: bool = True):
+    """2-bit codes of Q(W / a): ``codes [N, ceil(K/16)]`` and ``codes_t [K, ceil(N/16)]``
+    (int32 views of the uint32 words described in include/onebit_hip.h)."""
+    _require_device(weight, alpha)
+    n, k = weight.shape
+    w = weight.detach().contiguous()
+    codes = torch.empty((n, (k + 15) // 16), dtype=torch.int32, device=w.device)
+    codes_t = torch.empty((k, (n + 15) // 16), dtype=torch.int32, device=w.device)
+    lib = _lib.load()
+    _lib.check(
+        lib.ob_quant_pack(w.data_ptr(), alpha.data_ptr(), int(alpha_raw), bits, n, k,
+                          codes.data_ptr(), codes_t.data_ptr(), _lib.stream_of(w)),
+        "ob_quant_pack",
+    )
+    return codes, codes_t
+
+
+class _BitLinearFn(torch.autograd.Function):
+    """y = |alpha|_eps * (x . Q^T) + b with STE backward (quant.py:44-92 + F.linear)."""
+
+    @staticmethod
+    def forward(ctx, x2d, weight, alpha, bias, bits, codes, codes_t):
+        m, k = x2d.shape
+        n = weight.shape[0]
+        y = torch.empty((m, n), dtype=torch.float32, device=x2d.device)
+        lib = _lib.load()
+        _lib.check(
+            lib.ob_bitlinear_fwd(x2d.data_ptr(), m, k, codes.data_ptr(), alpha.data_ptr(), 1,
+                                 _lib.ptr(bias), n, y.data_ptr(), _lib.stream_of(x2d)),
+            "ob_bitlinear_fwd",
+        )
+        ctx.bits = bits
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x2d, weight, alpha, codes_t)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2d, weight, alpha, codes_t = ctx.saved_tensors
+        gy = gy.contiguous()
+        m, k = x2d.shape
+        n = weight.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(gy)
+        gx = gw = galpha = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty((m, k), dtype=torch.float32, device=gy.device)
+            _lib.check(
+                lib.ob_bitlinear_bwd_dx(gy.data_ptr(), m, n, codes_t.data_ptr(),
+                                        alpha.data_ptr(), 1, k, gx.data_ptr(), stream),
+                "ob_bitlinear_bwd_dx",
+            )
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            gw = torch.empty_like(weight)
+            galpha = torch.empty((), dtype=torch.float32, device=gy.device)
+            gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            ws_bytes = lib.ob_bitlinear_bwd_dw_workspace(m, n, k)
+            ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
+            _lib.check(
+                lib.ob_bitlinear_bwd_dw(gy.data_ptr(), x2d.data_ptr(), m, n, k,
+                                        weight.data_ptr(), alpha.data_ptr(), 1, ctx.bits,
+                                        gw.data_ptr(), galpha.data_ptr(), _lib.ptr(gb),
+                                        ws.data_ptr(), ws_bytes, stream),
+                "ob_bitlinear_bwd_dw",
+            )
+            if not ctx.needs_input_grad[1]:
+                gw = None
+            if not ctx.needs_input_grad[2]:
+                galpha = None
+        return gx, gw, galpha, gb, None, None, None
+
+
+class _QuantizeSTE(torch.autograd.Function):
+    """quantize_weight's autograd function (quant.py:38-92): W_hat = a * Q(W/a) with the
+    STE / LSQ-style alpha gradient. ``alpha`` is used as given (no abs/eps), as in the
+    reference, where QuantizedLinear applies ``|alpha| + 1e-8`` before calling it."""
+
+    @staticmethod
+    def forward(ctx, W, alpha, bitwidth: int):
+        bitwidth = _check_bitwidth(bitwidth)
+        ctx.bits = bitwidth
+        if bitwidth == 32:  # quant.py:61-64 passthrough
+            return W
+        _require_device(W, alpha)
+        w = W.contiguous()
+        out = torch.empty_like(w)
+        lib = _lib.load()
+        _lib.check(
+            lib.ob_quant_dequant(w.data_ptr(), alpha.data_ptr(), 0, bitwidth, w.numel(),
+                                 out.data_ptr(), _lib.stream_of(w)),
+            "ob_quant_dequant",
+        )
+        ctx.save_for_backward(w, alpha)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        if ctx.bits == 32:  # quant.py:76-78
+            return grad_out, grad_out.new_zeros(()), None
+        w, alpha = ctx.saved_tensors
+        g = grad_out.contiguous()
+        gw = torch.empty_like(w)
+        galpha = torch.empty((), dtype=torch.float32, device=w.device)
+        lib = _lib.load()
+        ws_bytes = lib.ob_quant_ste_bwd_workspace(w.numel())
+        ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=w.device)
+        _lib.check(
+            lib.ob_quant_ste_bwd(g.data_ptr(), w.data_ptr(), alpha.data_ptr(), 0, ctx.bits,
+                                 w.numel(), gw.data_ptr(), galpha.data_ptr(), ws.data_ptr(),
+                                 ws_bytes, _lib.stream_of(w)),
+            "ob_quant_ste_bwd",
+        )
+        return gw, galpha.reshape(alpha.shape), None
+
+
+def quantize_weight(W: torch.Tensor, alpha: torch.Tensor, bitwidth: int) -> torch.Tensor:
+    """quant.py:95-96."""
+    return _QuantizeSTE.apply(W, alpha, bitwidth)
+
+
+class QuantizedLinear(nn.Module):
+    """quant.py:99-127, same constructor, parameters, init and forward signature."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        # quant.py:104-108: kaiming_uniform(a=sqrt(5)) then x2, i.e. U(-2/sqrt(in), 2/sqrt(in)).
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        with torch.no_grad():
+            self.weight.mul_(2.0)
+            init_alpha = self.weight.abs().mean()  # quant.py:111-113
+        self.alpha = nn.Parameter(init_alpha)
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(out_features))  # quant.py:115-116
+        else:
+            self.register_parameter("bias", None)
+        self._codes_cache: dict = {}
+
+    def extra_repr(self) -> str:
+        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
+
+    def _codes(self, bits: int):
+        """Codes for the current (weight, alpha) values: repacked only when either
+        parameter was modified in place (optimizer step, load_state_dict, DDP broadcast)."""
+        key = (self.weight.data_ptr(), self.weight._version, self.alpha.data_ptr(),
+               self.alpha._version)
+        hit = self._codes_cache.get(bits)
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        codes, codes_t = pack_codes(self.weight, self.alpha, bits, alpha_raw=True)
+        self._codes_cache[bits] = (key, codes, codes_t)
+        return codes, codes_t
+
+    def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
+        bitwidth = _check_bitwidth(bitwidth)
+        if bitwidth == 32:  # quant.py:121-122
+            return F.linear(x, self.weight, self.bias)
+        _require_device(x, self.weight)
+        lead = x.shape[:-1]
+        x2d = x.reshape(-1, self.in_features)
+        if not x2d.is_contiguous():
+            x2d = x2d.contiguous()
+        codes, codes_t = self._codes(bitwidth)
+        y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bitwidth, codes, codes_t)
+        return y.view(*lead, self.out_features)
+
+    def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate cached codes
+        self._codes_cache = {}
+        return super()._apply(fn, *args, **kwargs)
+
+
+# north_star's name for the same layer.
+BitLinear = QuantizedLinear

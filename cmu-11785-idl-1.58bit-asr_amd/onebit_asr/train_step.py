@@ -1,0 +1,126 @@
+"""The measured unit of work: one training step of the reference (onebit_asr/train.py:76-120).
+
+Per batch the reference runs three encoder+decoder passes -- a 2-bit teacher, a 1-bit
+student and a stochastic-precision (SP) mix -- and combines their attention-CE, CTC and
+KL terms into one loss (train.py:82-111), then backward, grad-norm clip 5.0, AdamW and the
+warmup-cosine schedule (train.py:114-120, 259-264).
+
+``OneBitStep`` wraps the three passes in ONE module forward, so that a
+``DistributedDataParallel`` wrapper sees one forward per backward (the reference calls
+``model`` three times plus ``decode_logits`` outside ``forward``, which DDP's reducer would
+not pair with a single backward). With DDP every rank draws the same SP mask from a
+generator seeded identically on all ranks (train.py:56-59 draws from the global RNG).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from .losses import att_ce_loss, ctc_loss_from_logits, kl_logits, make_att_targets
+
+__all__ = ["OneBitStep", "WarmupCosine", "sample_sp_mask", "train_step", "SPECIAL_IDS",
+           "make_optimizer"]
+
+# dataloader_stub.py:199-207: pad 0, bos 1, eos 2, blank 3; SPM ids offset by +4.
+SPECIAL_IDS = {"pad_id": 0, "bos_id": 1, "eos_id": 2, "blank_id": 3}
+
+
+def sample_sp_mask(n_layers: int, low_p: float = 0.2, high_p: float = 0.9,
+                   generator: Optional[torch.Generator] = None) -> List[int]:
+    """train.py:56-59: block i runs 1-bit with probability logspace(0.2..0.9)[i]."""
+    probs = torch.logspace(math.log10(low_p), math.log10(high_p), steps=n_layers)
+    draws = torch.rand((n_layers,), generator=generator)
+    return [int(d < p) for d, p in zip(draws.tolist(), probs.tolist())]
+
+
+class WarmupCosine:
+    """train.py:32-53. lr is rewritten after each optimizer step (so the first step runs at
+    the optimizer's initial lr -- a reference quirk kept as is)."""
+
+    def __init__(self, optimizer, warmup_steps: int, total_steps: int, min_lr_ratio: float = 0.1):
+        self.optimizer = optimizer
+        self.warmup_steps = warmup_steps
+        self.total_steps = total_steps
+        self.min_lr_ratio = min_lr_ratio
+        self.step_num = 0
+        for group in optimizer.param_groups:
+            group.setdefault("initial_lr", group.get("lr", 1e-3))
+
+    def scale(self, step: int) -> float:
+        if step < self.warmup_steps:
+            return step / max(1, self.warmup_steps)
+        span = max(1, self.total_steps - self.warmup_steps)
+        progress = min(max((step - self.warmup_steps) / span, 0.0), 1.0)
+        return self.min_lr_ratio + 0.5 * (1 - self.min_lr_ratio) * (1 + math.cos(math.pi * progress))
+
+    def step(self):
+        self.step_num += 1
+        s = self.scale(self.step_num)
+        for group in self.optimizer.param_groups:
+            group["lr"] = group["initial_lr"] * s
+
+
+def make_optimizer(params, lr: float = 5e-4) -> torch.optim.Optimizer:
+    """train.py:259: AdamW(lr, betas=(0.9, 0.98), weight_decay=1e-2) over all parameters
+    (weight decay therefore also applies to every alpha)."""
+    return torch.optim.AdamW(params, lr=lr, betas=(0.9, 0.98), weight_decay=1e-2)
+
+
+class OneBitStep(nn.Module):
+    """train.py:82-111 as one forward returning the combined loss."""
+
+    def __init__(self, model: nn.Module, n_layers: int, special: Optional[Dict[str, int]] = None,
+                 gamma_ctc: float = 0.2, lambda1: float = 0.5, lambda2: float = 1.0,
+                 label_smoothing: float = 0.1):
+        super().__init__()
+        self.model = model
+        self.n_layers = n_layers
+        self.special = dict(SPECIAL_IDS if special is None else special)
+        self.gamma_ctc = gamma_ctc
+        self.lambda1 = lambda1
+        self.lambda2 = lambda2
+        self.label_smoothing = label_smoothing
+
+    def _pass(self, batch, t_inp, t_out, t_pad, precision, sp_mask=None):
+        enc, mask, ctc = self.model(batch, precision=precision, sp_mask=sp_mask)
+        logits = self.model.decode_logits(enc, mask, t_inp, t_pad)
+        l_att = att_ce_loss(logits, t_out, self.special["pad_id"], label_smoothing=self.label_smoothing)
+        l_ctc = ctc_loss_from_logits(ctc, mask.sum(dim=1).long(), batch["tokens"],
+                                     batch["token_lens"], self.special["blank_id"])
+        l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
+        return logits, l_int, l_ctc
+
+    def forward(self, batch: Dict[str, torch.Tensor], sp_mask: List[int]):
+        sp = self.special
+        t_inp, t_out, t_pad = make_att_targets(batch["tokens"], sp["bos_id"], sp["eos_id"], sp["pad_id"])
+        logits2, lint2, lctc2 = self._pass(batch, t_inp, t_out, t_pad, 2)          # teacher
+        logits1, lint1, lctc1 = self._pass(batch, t_inp, t_out, t_pad, 1)          # student
+        teacher = logits2.detach()
+        lkl1 = kl_logits(logits1, teacher, t_pad)
+        logits_s, lint_s, lctc_s = self._pass(batch, t_inp, t_out, t_pad, 2, sp_mask)  # SP
+        lkl_s = kl_logits(logits_s, teacher, t_pad)
+        loss = lint2 + self.lambda1 * (lint1 + lint_s) + self.lambda2 * (lkl1 + lkl_s)
+        parts = torch.stack([lint2, lint1, lint_s, lkl1, lkl_s, lctc2, lctc1, lctc_s]).detach()
+        return loss, parts
+
+
+PART_NAMES = ["Lint2", "Lint1", "Lint_s", "Lkl1", "Lkl_s", "Lctc2", "Lctc1", "Lctc_s"]
+
+
+def train_step(step_module: nn.Module, optimizer: torch.optim.Optimizer,
+               sched: Optional[WarmupCosine], batch: Dict[str, torch.Tensor],
+               sp_mask: List[int], max_norm: float = 5.0):
+    """train.py:114-120: zero_grad, backward, clip_grad_norm_(5.0), step, sched.step().
+    Returns the (device) loss and loss parts; nothing here synchronises with the host."""
+    loss, parts = step_module(batch, sp_mask)
+    optimizer.zero_grad(set_to_none=True)
+    loss.backward()
+    params = [p for p in step_module.parameters() if p.grad is not None]
+    torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm)
+    optimizer.step()
+    if sched is not None:
+        sched.step()
+    return loss.detach(), parts

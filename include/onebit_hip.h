@@ -1,0 +1,122 @@
+/*
+ * onebit_hip.h — C ABI of the MI355X (gfx950) BitLinear / QuantizedLinear hot path.
+ *
+ * This is the drop-in boundary for the reference's quantized linear layer
+ * (y00njaekim/CMU-11785-IDL-1.58bit-ASR, onebit_asr/quant.py). The reference is
+ * pure Python over torch eager ops; each entry point below replaces the torch
+ * op sequence cited next to it. The Python host side
+ * (cmu-11785-idl-1.58bit-asr_amd/onebit_asr/quant.py) binds these with ctypes.
+ *
+ * Conventions (all entry points):
+ *   - plain C types only: device pointers, int64 sizes, a hipStream_t passed as void*;
+ *   - every tensor is dense row-major fp32 (last dim contiguous) unless stated;
+ *   - caller owns every buffer, including workspaces; nothing here allocates,
+ *     synchronises the device or copies to/from the host, so every call is legal
+ *     inside hipStreamBeginCapture/hipGraph capture;
+ *   - return value: OB_OK (0) or a negative OB_ERR_* status; no exceptions cross
+ *     the ABI; launch failures are reported as OB_ERR_HIP;
+ *   - alpha is a DEVICE pointer to one fp32. With alpha_raw = 1 it is the raw
+ *     learnable parameter and the kernels use a = |alpha| + 1e-8f exactly as
+ *     QuantizedLinear.forward does (quant.py:124); with alpha_raw = 0 it is used
+ *     as given (the quantize_weight(W, alpha, bits) entry, quant.py:95-96).
+ *   - bits is 1 (binary {-1,+1}, zero -> +1) or 2 (ternary {-1,0,+1}, threshold 0.5)
+ *     (quant.py:52-60). bits = 32 is the full-precision passthrough and never
+ *     reaches this library (quant.py:121-122); any other value -> OB_ERR_BITWIDTH,
+ *     which the host maps to ValueError("bitwidth must be one of {1,2,32}")
+ *     (quant.py:65-66).
+ *
+ * Packed weight codes (2 bits / weight, 16 per uint32, little-end first):
+ *   00 -> 0, 01 -> +1, 11 -> -1 (10 unused).
+ *   codes   [N][ceil(K/16)] : code of W[n][16*w + j] in bits 2j..2j+1 of codes[n][w]
+ *   codes_t [K][ceil(N/16)] : code of W[16*w + j][k] in bits 2j..2j+1 of codes_t[k][w]
+ *   Padding positions hold 00.
+ */
+#ifndef ONEBIT_HIP_H_
+#define ONEBIT_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OB_API __attribute__((visibility("default")))
+
+enum {
+  OB_OK = 0,
+  OB_ERR_NULL = -1,      /* a required pointer is NULL */
+  OB_ERR_SHAPE = -2,     /* negative / inconsistent size */
+  OB_ERR_BITWIDTH = -3,  /* bits not in {1,2} */
+  OB_ERR_WORKSPACE = -4, /* workspace smaller than the *_workspace() query */
+  OB_ERR_ALIGN = -5,     /* pointer not 4-byte aligned */
+  OB_ERR_HIP = -6        /* hipGetLastError() after launch was not hipSuccess */
+};
+
+/* ABI version (bumped on any signature change). */
+OB_API int ob_abi_version(void);
+/* Static string for a status code. */
+OB_API const char* ob_status_string(int status);
+
+/*
+ * Quantize + pack (replaces _QuantizeSTE.forward's quantization, quant.py:49-60,
+ * without materialising W_hat): codes and codes_t from W[N][K] and alpha.
+ * Either output may be NULL to skip it.
+ */
+OB_API int ob_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits,
+                         int64_t N, int64_t K, uint32_t* codes, uint32_t* codes_t,
+                         void* stream);
+
+/*
+ * quantize_weight forward, elementwise (quant.py:49-70): W_hat[i] = a * Q(W[i]/a).
+ */
+OB_API int ob_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits,
+                            int64_t n, float* W_hat, void* stream);
+
+/*
+ * quantize_weight backward (quant.py:72-92): grad_W = g * 1[|W/a| <= 1];
+ * grad_alpha[0] = sum(g * term(W/a)) (times sign(alpha) when alpha_raw = 1,
+ * i.e. the chain through alpha.abs() at quant.py:124). Deterministic.
+ */
+OB_API size_t ob_quant_ste_bwd_workspace(int64_t n);
+OB_API int ob_quant_ste_bwd(const float* grad_W_hat, const float* W, const float* alpha,
+                            int alpha_raw, int bits, int64_t n, float* grad_W,
+                            float* grad_alpha, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * BitLinear forward (replaces F.linear(x, alpha*Q, bias), quant.py:124-126):
+ *   Y[M][N] = a * (X[M][K] . Q^T) + bias        (bias may be NULL)
+ */
+OB_API int ob_bitlinear_fwd(const float* X, int64_t M, int64_t K, const uint32_t* codes,
+                            const float* alpha, int alpha_raw, const float* bias, int64_t N,
+                            float* Y, void* stream);
+
+/*
+ * BitLinear backward, input gradient (autograd of F.linear at quant.py:126):
+ *   dX[M][K] = a * (dY[M][N] . Q)       using codes_t (layout above)
+ */
+OB_API int ob_bitlinear_bwd_dx(const float* dY, int64_t M, int64_t N, const uint32_t* codes_t,
+                               const float* alpha, int alpha_raw, int64_t K, float* dX,
+                               void* stream);
+
+/*
+ * BitLinear backward, weight / scale / bias gradients (F.linear autograd at
+ * quant.py:126 fused with _QuantizeSTE.backward, quant.py:72-92):
+ *   G        = dY^T . X                       ([N][K], summed over all M rows)
+ *   dW       = G * 1[|W/a| <= 1]
+ *   dalpha[0]= sum(G * term(W/a)) (* sign(alpha) when alpha_raw = 1)
+ *   db[n]    = sum_m dY[m][n]                 (db may be NULL)
+ * Deterministic (fixed-order split-M reduction); ws must hold
+ * ob_bitlinear_bwd_dw_workspace(M, N, K) bytes.
+ */
+OB_API size_t ob_bitlinear_bwd_dw_workspace(int64_t M, int64_t N, int64_t K);
+OB_API int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                               const float* W, const float* alpha, int alpha_raw, int bits,
+                               float* dW, float* dalpha, float* db, void* ws, size_t ws_bytes,
+                               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ONEBIT_HIP_H_ */
