@@ -13,7 +13,6 @@ namespace ob {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kReduceEPT = 4;  // elements per thread in ste_reduce
 
 // One thread per output word. Words [0, N*KW) are codes (row n, word w: K-contiguous);
 // words [N*KW, N*KW + K*NW) are codes_t, indexed w-major / k-minor so that consecutive
@@ -83,33 +82,54 @@ __device__ __forceinline__ float block_sum(float v, float* lds4) {
 }
 
 // quant.py:80-91 applied to the fixed-order sum of `chunks` partial slabs.
+// Block = 64 elements x 4 chunk groups: group q sums chunks q, q+4, q+8, ... (independent,
+// coalesced loads), the 4 group sums are added in group order through LDS, then wave 0
+// applies the STE mask / alpha term and reduces its alpha partial. Deterministic.
+constexpr int kReduceElems = 64;
+
 __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
     const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
     int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
     int bits, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ apart) {
-  __shared__ float lds4[kThreads / 64];
-  const float a = effective_alpha(alpha, alpha_raw);
-  const int64_t base = blockIdx.x * (int64_t)(kThreads * kReduceEPT);
-  float asum = 0.0f;
-#pragma unroll
-  for (int i = 0; i < kReduceEPT; ++i) {
-    const int64_t e = base + i * kThreads + threadIdx.x;
-    if (e < nk) {
-      float g = 0.0f;
-      for (int c = 0; c < chunks; ++c) g += part[(int64_t)c * nk + e];
-      const float wa = W[e] / a;
-      dW[e] = g * ste_indicator(wa);  // quant.py:81-82 (multiply, so inf*0 -> NaN as in torch)
-      const float prod = g * alpha_term(wa, bits);  // quant.py:91 grad_out * term
-      asum += prod;
-    } else if (e < nk + n_db) {
-      const int64_t n = e - nk;
-      float s = 0.0f;
-      for (int c = 0; c < chunks; ++c) s += part_db[(int64_t)c * n_db + n];
-      db[n] = s;
+  __shared__ float grp_sum[4][kReduceElems];
+  const int lane = threadIdx.x & 63;
+  const int grp = threadIdx.x >> 6;
+  const int64_t e = blockIdx.x * (int64_t)kReduceElems + lane;
+  const bool is_w = e < nk;
+  const bool is_b = !is_w && e < nk + n_db;
+  const float* src = is_w ? part + e : (is_b ? part_db + (e - nk) : nullptr);
+  const int64_t stride = is_w ? nk : n_db;
+  float s = 0.0f;
+  if (src) {
+    int c = grp;
+    for (; c + 12 < chunks; c += 16) {
+      const float v0 = src[(int64_t)c * stride];
+      const float v1 = src[(int64_t)(c + 4) * stride];
+      const float v2 = src[(int64_t)(c + 8) * stride];
+      const float v3 = src[(int64_t)(c + 12) * stride];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
     }
+    for (; c < chunks; c += 4) s += src[(int64_t)c * stride];
   }
-  const float t = block_sum(asum, lds4);
-  if (threadIdx.x == 0) apart[blockIdx.x] = t;
+  grp_sum[grp][lane] = s;
+  __syncthreads();
+  if (grp != 0) return;
+  const float g = ((grp_sum[0][lane] + grp_sum[1][lane]) + grp_sum[2][lane]) + grp_sum[3][lane];
+  float prod = 0.0f;
+  if (is_w) {
+    const float a = effective_alpha(alpha, alpha_raw);
+    const float wa = W[e] / a;
+    dW[e] = g * ste_indicator(wa);  // quant.py:81-82 (multiply: inf*0 -> NaN as in torch)
+    prod = g * alpha_term(wa, bits);  // quant.py:91 grad_out * term
+  } else if (is_b) {
+    db[e - nk] = g;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
+  if (lane == 0) apart[blockIdx.x] = prod;
 }
 
 // quant.py:91 .sum() finished over the block partials, then the abs() chain of
@@ -147,7 +167,7 @@ void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int
                      alpha, alpha_raw, bits, n, W_hat);
 }
 
-int64_t ste_reduce_blocks(int64_t total) { return ceil_div(total, kThreads * kReduceEPT); }
+int64_t ste_reduce_blocks(int64_t total) { return ceil_div(total, kReduceElems); }
 
 void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* part_db,
                        int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,

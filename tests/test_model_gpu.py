@@ -73,7 +73,8 @@ def test_step_loss_and_grads(pair, batch, gpu):
     ref = dict(orc.named_reference_parameters())
     checked = 0
     for name, p in prod.named_parameters():
-        if not any(s in name for s in ("lin1", "lin2", "_proj")):
+        if not name.startswith("encoder.blocks.") or not any(
+                s in name for s in (".lin1.", ".lin2.", "_proj.")):
             continue
         g_p = p.grad.detach().cpu().double()
         g_o = ref[name].grad.detach().double()
