@@ -31,7 +31,7 @@ DwWorkspace dw_layout(int64_t M, int64_t N, int64_t K) {
   DwWorkspace w;
   w.part = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N * (size_t)K);
   w.part_db = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N);
-  w.apart = align_up(sizeof(float) * (size_t)ste_reduce_blocks(N * K + N) + sizeof(float));
+  w.apart = align_up(16 + sizeof(float) * (size_t)ste_reduce_blocks(N * K + N));
   w.total = w.part + w.part_db + w.apart;
   return w;
 }
@@ -77,7 +77,7 @@ int ob_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits
 
 size_t ob_quant_ste_bwd_workspace(int64_t n) {
   if (n < 0) return 0;
-  return align_up(sizeof(float) * (size_t)ste_reduce_blocks(n) + sizeof(float));
+  return align_up(16 + sizeof(float) * (size_t)(ste_reduce_blocks(n) + 1));
 }
 
 int ob_quant_ste_bwd(const float* grad_W_hat, const float* W, const float* alpha, int alpha_raw,
@@ -88,8 +88,13 @@ int ob_quant_ste_bwd(const float* grad_W_hat, const float* W, const float* alpha
   if (!alpha || !grad_alpha || !ws || (n > 0 && (!grad_W_hat || !W || !grad_W)))
     return OB_ERR_NULL;
   if (ws_bytes < ob_quant_ste_bwd_workspace(n)) return OB_ERR_WORKSPACE;
+  // ws: [ticket (16 B)][block partials]
+  uint32_t* ticket = static_cast<uint32_t*>(ws);
+  float* apart = reinterpret_cast<float*>(static_cast<char*>(ws) + 16);
+  if (hipMemsetAsync(ticket, 0, sizeof(uint32_t), as_stream(stream)) != hipSuccess)
+    return OB_ERR_HIP;
   launch_ste_reduce(grad_W_hat, 1, n, nullptr, 0, W, alpha, alpha_raw, bits, grad_W, nullptr,
-                    static_cast<float*>(ws), grad_alpha, as_stream(stream));
+                    apart, ticket, grad_alpha, as_stream(stream));
   return launched();
 }
 
@@ -134,21 +139,24 @@ int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, i
   char* base = static_cast<char*>(ws);
   float* part = reinterpret_cast<float*>(base);
   float* part_db = db ? reinterpret_cast<float*>(base + L.part) : nullptr;
-  float* apart = reinterpret_cast<float*>(base + L.part + L.part_db);
+  // apart region: [ticket (16 B)][block partials]
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(base + L.part + L.part_db);
+  float* apart = reinterpret_cast<float*>(base + L.part + L.part_db + 16);
   hipStream_t s = as_stream(stream);
   int chunks = (int)p.chunks;
-  if (M == 0) {
+  if (M == 0 || N == 0) {
     // No rows: every gradient is zero. Zero the first slab and reduce one chunk.
     if (N * K > 0 && hipMemsetAsync(part, 0, sizeof(float) * N * K, s) != hipSuccess)
       return OB_ERR_HIP;
     if (db && N > 0 && hipMemsetAsync(part_db, 0, sizeof(float) * N, s) != hipSuccess)
       return OB_ERR_HIP;
+    if (hipMemsetAsync(ticket, 0, sizeof(uint32_t), s) != hipSuccess) return OB_ERR_HIP;
     chunks = 1;
   } else {
-    launch_dw_partial(dY, X, M, N, K, p, part, part_db, s);
+    launch_dw_partial(dY, X, M, N, K, p, part, part_db, ticket, s);
   }
   launch_ste_reduce(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, bits, dW, db,
-                    apart, dalpha, s);
+                    apart, ticket, dalpha, s);
   return launched();
 }
 

@@ -136,23 +136,38 @@ __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Loads are issued unconditionally from a clamped (always valid) address and zeroed
+// afterwards with a select: a guarded `cond ? *p : 0` load makes hipcc branch around the
+// load and wait vmcnt(0) at it, which serialises the prefetch pipeline.
+__device__ __forceinline__ f32x4 zero_unless(bool ok, f32x4 v) {
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  return ok ? v : z;
+}
+
 template <bool VEC>
 __device__ __forceinline__ void load8(const float* __restrict__ arow, bool rvalid, int k, int K,
                                       f32x4& a, f32x4& b) {
-  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  if (VEC) {
-    a = (rvalid && k < K) ? *reinterpret_cast<const f32x4*>(arow + k) : z;
-    b = (rvalid && k + 4 < K) ? *reinterpret_cast<const f32x4*>(arow + k + 4) : z;
+  if (VEC) {  // K % 4 == 0, K >= 4
+    const int ka = k < K - 4 ? k : K - 4;
+    const int kb = k + 4 < K - 4 ? k + 4 : K - 4;
+    const f32x4 va = *reinterpret_cast<const f32x4*>(arow + ka);
+    const f32x4 vb = *reinterpret_cast<const f32x4*>(arow + kb);
+    a = zero_unless(rvalid && k < K, va);
+    b = zero_unless(rvalid && k + 4 < K, vb);
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      a[e] = (rvalid && k + e < K) ? arow[k + e] : 0.0f;
-      b[e] = (rvalid && k + 4 + e < K) ? arow[k + 4 + e] : 0.0f;
+      const int k0 = k + e < K - 1 ? k + e : K - 1;
+      const int k1 = k + 4 + e < K - 1 ? k + 4 + e : K - 1;
+      const float v0 = arow[k0 < 0 ? 0 : k0];
+      const float v1 = arow[k1 < 0 ? 0 : k1];
+      a[e] = (rvalid && k + e < K) ? v0 : 0.0f;
+      b[e] = (rvalid && k + 4 + e < K) ? v1 : 0.0f;
     }
   }
 }
 
-template <int NT, bool VEC>
+template <int NT, bool VEC, int NCH>
 __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, const float* __restrict__ alpha, int alpha_raw, const float* __restrict__ bias,
@@ -189,21 +204,16 @@ __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
   const int64_t m0 = (int64_t)blockIdx.x * kGemmRows + wave * 16;
   const int64_t row = m0 + r;
   const bool rvalid = row < M;
-  const float* arow = A + (rvalid ? row : 0) * (int64_t)K;
+  const float* arow = A + (rvalid ? row : M - 1) * (int64_t)K;
   const __bf16* brow = bimg + r * stride + 8 * g;
 
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f32x4 c0, c1, n0v, n1v;
-  load8<VEC>(arow, rvalid, 8 * g, K, c0, c1);
-  load8<VEC>(arow, rvalid, 32 + 8 * g, K, n0v, n1v);
-  for (int kc = 0; kc < kpad; kc += 32) {
-    f32x4 p0, p1;
-    load8<VEC>(arow, rvalid, kc + 64 + 8 * g, K, p0, p1);
+  auto compute = [&](const f32x4& x0, const f32x4& x1, int kc) {
     bf16x8 hi, mid, lo;
-    split3(c0, c1, hi, mid, lo);
+    split3(x0, x1, hi, mid, lo);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const bf16x8 bq = *reinterpret_cast<const bf16x8*>(brow + t * 16 * stride + kc);
@@ -211,10 +221,39 @@ __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
       acc[t] = mfma_bf16(mid, bq, acc[t]);
       acc[t] = mfma_bf16(hi, bq, acc[t]);
     }
-    c0 = n0v;
-    c1 = n1v;
-    n0v = p0;
-    n1v = p1;
+  };
+  const int kg = 8 * g;
+  if constexpr (NCH > 0) {
+    // K is a compile-time chunk count: fully unrolled, a window of kWin chunks in flight,
+    // every wait a counted vmcnt.
+    constexpr int kWin = NCH < 6 ? NCH : 6;
+    f32x4 buf[NCH > 0 ? NCH : 1][2];
+#pragma unroll
+    for (int c = 0; c < kWin; ++c) load8<VEC>(arow, rvalid, 32 * c + kg, K, buf[c][0], buf[c][1]);
+    // sched_barrier keeps hipcc's scheduler from sinking each load next to its use
+    // (which would leave one load in flight and a vmcnt(0) per chunk).
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + kWin < NCH)
+        load8<VEC>(arow, rvalid, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(buf[c][0], buf[c][1], 32 * c);
+    }
+  } else if (K > 0) {  // K == 0: A may have no storage at all
+    // Generic K: three rotating register sets, unrolled so no register copy of an
+    // in-flight load exists (a copy would make hipcc wait for it).
+    f32x4 r0a, r0b, r1a, r1b, r2a, r2b;
+    load8<VEC>(arow, rvalid, kg, K, r0a, r0b);
+    load8<VEC>(arow, rvalid, 32 + kg, K, r1a, r1b);
+    for (int kc = 0; kc < kpad; kc += 96) {
+      load8<VEC>(arow, rvalid, kc + 64 + kg, K, r2a, r2b);
+      compute(r0a, r0b, kc);
+      load8<VEC>(arow, rvalid, kc + 96 + kg, K, r0a, r0b);
+      if (kc + 32 < kpad) compute(r1a, r1b, kc + 32);
+      load8<VEC>(arow, rvalid, kc + 128 + kg, K, r1a, r1b);
+      if (kc + 64 < kpad) compute(r2a, r2b, kc + 64);
+    }
   }
 
   const float a = effective_alpha(alpha, alpha_raw);
@@ -252,15 +291,25 @@ void launch_gemm_nt(const float* A, int64_t M, int64_t K, const uint32_t* codes,
                     hipStream_t s) {
   const int64_t KW = ceil_div(K, 16);
   dim3 grid((unsigned)ceil_div(M, kGemmRows), (unsigned)ceil_div(N, 16 * NT));
-  const bool vec = (K % 4 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const size_t lds = bimg_bytes(NT, K);
   if (!use_f32_gemm() && lds <= kMaxDynLds) {
-    if (vec)
-      hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, true>), grid, dim3(kThreads), lds, s, A, M,
-                         (int)K, codes, (int)KW, (int)N, alpha, alpha_raw, bias, C);
-    else
-      hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, false>), grid, dim3(kThreads), lds, s, A, M,
-                         (int)K, codes, (int)KW, (int)N, alpha, alpha_raw, bias, C);
+#define OB_TGEMM(NCH)                                                                        \
+  hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, true, NCH>), grid, dim3(kThreads), lds, s, A, M, \
+                     (int)K, codes, (int)KW, (int)N, alpha, alpha_raw, bias, C)
+    if (vec) {
+      switch ((K + 31) / 32) {  // Conformer widths: 64, 144, 256, 576
+        case 2: OB_TGEMM(2); break;
+        case 5: OB_TGEMM(5); break;
+        case 8: OB_TGEMM(8); break;
+        case 18: OB_TGEMM(18); break;
+        default: OB_TGEMM(0); break;
+      }
+    } else {
+      hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, false, 0>), grid, dim3(kThreads), lds, s, A,
+                         M, (int)K, codes, (int)KW, (int)N, alpha, alpha_raw, bias, C);
+    }
+#undef OB_TGEMM
     return;
   }
   // fp32-MFMA path: exact fma chain; also the fallback for K too large for the LDS image.
@@ -284,11 +333,11 @@ void launch_gemm_nt(const float* A, int64_t M, int64_t K, const uint32_t* codes,
 // ---------------------------------------------------------------------------------
 constexpr int kDwTile = 64;
 
-template <bool VEC>
+template <bool VEC, int S>
 __global__ __launch_bounds__(kThreads) void dw_partial_kernel(
     const float* __restrict__ dY, const float* __restrict__ X, int64_t M, int64_t N, int64_t K,
     int64_t tiles_k, int64_t rows_per_chunk, float* __restrict__ part,
-    float* __restrict__ part_db) {
+    float* __restrict__ part_db, uint32_t* __restrict__ ticket) {
   __shared__ float red[2][kDwTile * kDwTile];  // 32 KB: waves pair up (0+2, 1+3)
   __shared__ float dbred[4][kDwTile];
 
@@ -305,6 +354,7 @@ __global__ __launch_bounds__(kThreads) void dw_partial_kernel(
   const int64_t ncol = n0 + 4 * r;
   const int64_t kcol = k0 + 4 * r;
   const bool do_db = (part_db != nullptr) && (tk == 0);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ticket = 0u;
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -316,42 +366,52 @@ __global__ __launch_bounds__(kThreads) void dw_partial_kernel(
 
   // Rows are streamed with a two-step register prefetch so the dwordx4 latency hides
   // under the 16 MFMAs of the step before.
+  // Unconditional loads from clamped addresses + selects (see zero_unless).
+  const int64_t ncl = ncol < N - 4 ? ncol : (N >= 4 ? N - 4 : 0);
+  const int64_t kcl = kcol < K - 4 ? kcol : (K >= 4 ? K - 4 : 0);
   auto load_step = [&](int64_t step, f32x4& dy, f32x4& x) {
     const int64_t m = step + g;
     const bool mv = m < m_end;
+    const int64_t mc = mv ? m : M - 1;
     if (VEC) {
-      dy = (mv && ncol < N) ? *reinterpret_cast<const f32x4*>(dY + m * N + ncol)
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
-      x = (mv && kcol < K) ? *reinterpret_cast<const f32x4*>(X + m * K + kcol)
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
+      dy = zero_unless(mv && ncol < N, *reinterpret_cast<const f32x4*>(dY + mc * N + ncl));
+      x = zero_unless(mv && kcol < K, *reinterpret_cast<const f32x4*>(X + mc * K + kcl));
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        dy[e] = (mv && ncol + e < N) ? dY[m * N + ncol + e] : 0.0f;
-        x[e] = (mv && kcol + e < K) ? X[m * K + kcol + e] : 0.0f;
+        const int64_t nn = ncol + e < N ? ncol + e : N - 1;
+        const int64_t kk = kcol + e < K ? kcol + e : (K > 0 ? K - 1 : 0);
+        const float vy = dY[mc * N + nn];
+        const float vx = K > 0 ? X[mc * K + kk] : 0.0f;
+        dy[e] = (mv && ncol + e < N) ? vy : 0.0f;
+        x[e] = (mv && kcol + e < K) ? vx : 0.0f;
       }
     }
   };
-  int64_t step = m_begin + 4 * wave;
-  f32x4 dy0, x0, dy1, x1;
-  load_step(step, dy0, x0);
-  load_step(step + 16, dy1, x1);
-  for (; step < m_end; step += 16) {
-    f32x4 dy2, x2;
-    load_step(step + 32, dy2, x2);
+  auto compute = [&](const f32x4& dy, const f32x4& x) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) acc[e][f] = mfma4(dy0[e], x0[f], acc[e][f]);
+      for (int f = 0; f < 4; ++f) acc[e][f] = mfma4(dy[e], x[f], acc[e][f]);
     }
     if (do_db) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dbacc[e] += dy0[e];
+      for (int e = 0; e < 4; ++e) dbacc[e] += dy[e];
     }
-    dy0 = dy1;
-    x0 = x1;
-    dy1 = dy2;
-    x1 = x2;
+  };
+  // The chunk is S steps of 16 rows (4 per wave): fully unrolled with a window of kWin
+  // steps in flight; rows past the chunk / M load clamped and contribute zero.
+  constexpr int kWin = S < 4 ? S : 4;
+  const int64_t s0 = m_begin + 4 * wave;
+  f32x4 bdy[S], bx[S];
+#pragma unroll
+  for (int i = 0; i < kWin; ++i) load_step(s0 + 16 * i, bdy[i], bx[i]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if (i + kWin < S) load_step(s0 + 16 * (i + kWin), bdy[i + kWin], bx[i + kWin]);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(bdy[i], bx[i]);
   }
 
   // Combine the 4 wave tiles in a fixed order: (w0 + w2) + (w1 + w3).
@@ -439,32 +499,37 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   p.tiles_n = N > 0 ? ceil_div(N, kDwTile) : 1;
   p.tiles_k = K > 0 ? ceil_div(K, kDwTile) : 1;
   const int64_t tiles = p.tiles_n * p.tiles_k;
-  // Aim for ~512 blocks (2 per CU, 8 waves) but keep >= 128 rows per chunk: fewer
-  // partial slabs for the reduction to read back.
-  int64_t chunks = ceil_div(512, tiles > 0 ? tiles : 1);
-  const int64_t max_chunks = ceil_div(M, 128);
-  if (chunks > max_chunks) chunks = max_chunks;
-  if (chunks < 1) chunks = 1;
-  int64_t rows = ceil_div(M, chunks);
-  rows = ceil_div(rows, 16) * 16;
-  p.rows_per_chunk = rows > 0 ? rows : 16;
+  // Chunk = S steps x 16 rows, S in {8, 16, 32}: the longest chunk that still gives
+  // >= 256 blocks (one per CU), so the partial slabs stay few.
+  int64_t steps = 32;
+  while (steps > 8 && tiles * ceil_div(M, 16 * steps) < 256) steps /= 2;
+  p.rows_per_chunk = 16 * steps;
   p.chunks = M > 0 ? ceil_div(M, p.rows_per_chunk) : 1;
   return p;
 }
 
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
-                       const DwPlan& p, float* part, float* part_db, hipStream_t s) {
+                       const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
+                       hipStream_t s) {
   if (M == 0 || N == 0) return;
   dim3 grid((unsigned)(p.tiles_n * p.tiles_k), (unsigned)p.chunks);
-  const bool vec = (N % 4 == 0) && (K % 4 == 0) &&
+  const bool vec = (N % 4 == 0) && (K % 4 == 0) && N >= 4 && K >= 4 &&
                    ((reinterpret_cast<uintptr_t>(dY) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  if (vec)
-    hipLaunchKernelGGL(dw_partial_kernel<true>, grid, dim3(kThreads), 0, s, dY, X, M, N, K,
-                       p.tiles_k, p.rows_per_chunk, part, part_db);
-  else
-    hipLaunchKernelGGL(dw_partial_kernel<false>, grid, dim3(kThreads), 0, s, dY, X, M, N, K,
-                       p.tiles_k, p.rows_per_chunk, part, part_db);
+#define OB_DW(V, S)                                                                        \
+  hipLaunchKernelGGL((dw_partial_kernel<V, S>), grid, dim3(kThreads), 0, s, dY, X, M, N, K,   \
+                     p.tiles_k, p.rows_per_chunk, part, part_db, ticket)
+  const int64_t steps = p.rows_per_chunk / 16;
+  if (vec) {
+    if (steps == 32) OB_DW(true, 32);
+    else if (steps == 16) OB_DW(true, 16);
+    else OB_DW(true, 8);
+  } else {
+    if (steps == 32) OB_DW(false, 32);
+    else if (steps == 16) OB_DW(false, 16);
+    else OB_DW(false, 8);
+  }
+#undef OB_DW
 }
 
 }  // namespace ob

@@ -16,14 +16,16 @@ void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bi
 void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
                           float* W_hat, hipStream_t s);
 
-// Split-reduction finish shared by both backward entries: sums `chunks` fp32 slabs of
-// length nk (+ an optional [chunks][n_db] bias slab), applies the STE mask, writes dW and
-// the per-block alpha partials, then a one-block finalize writes dalpha.
-// `apart` must hold ste_reduce_blocks(nk + n_db) floats.
+// Split-reduction finish shared by both backward entries (one launch): sums `chunks` fp32
+// slabs of length nk (+ an optional [chunks][n_db] bias slab), applies the STE mask, writes
+// dW, and the last-arriving block sums the per-block alpha partials into dalpha.
+// `apart` must hold ste_reduce_blocks(nk + n_db) floats; *ticket must be 0 on entry (it is
+// 0 again on exit).
 int64_t ste_reduce_blocks(int64_t total);
 void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* part_db,
                        int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,
-                       float* dW, float* db, float* apart, float* dalpha, hipStream_t s);
+                       float* dW, float* db, float* apart, uint32_t* ticket, float* dalpha,
+                       hipStream_t s);
 
 // gemm.hip
 // C[M][N] = a * (A[M][K] . Q^T) + bias, Q given as 2-bit codes [N][ceil(K/16)].
@@ -36,7 +38,9 @@ struct DwPlan {
   int64_t tiles_n, tiles_k, chunks, rows_per_chunk;
 };
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
+// Also zeroes *ticket (for the ste_reduce launch that follows on the same stream).
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
-                       const DwPlan& p, float* part, float* part_db, hipStream_t s);
+                       const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
+                       hipStream_t s);
 
 }  // namespace ob

@@ -14,41 +14,45 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// One thread per output word. Words [0, N*KW) are codes (row n, word w: K-contiguous);
-// words [N*KW, N*KW + K*NW) are codes_t, indexed w-major / k-minor so that consecutive
-// threads read consecutive W columns (coalesced) while building a transposed word.
+// One thread per code: 16 consecutive lanes build one 32-bit word with a 4-step
+// shuffle OR-reduction (lane j contributes code << 2j).
+// Threads [0, 16*N*KW) build codes (row n, word w: K-contiguous, coalesced reads);
+// threads [16*N*KW, 16*(N*KW + K*NW)) build codes_t with lanes (j = lane&15, kk = lane>>4)
+// reading W[16w+j][k0+kk] (16 rows x 4 consecutive columns per wave).
+__device__ __forceinline__ uint32_t or16(uint32_t v) {
+  v |= __shfl_xor(v, 1, 64);
+  v |= __shfl_xor(v, 2, 64);
+  v |= __shfl_xor(v, 4, 64);
+  v |= __shfl_xor(v, 8, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(kThreads) void quant_pack_kernel(
     const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw, int bits,
     int64_t N, int64_t K, int64_t KW, int64_t NW, uint32_t* __restrict__ codes,
     uint32_t* __restrict__ codes_t) {
   const float a = effective_alpha(alpha, alpha_raw);
-  int64_t t = blockIdx.x * (int64_t)kThreads + threadIdx.x;
-  const int64_t n_codes = codes ? N * KW : 0;
-  const int64_t n_codes_t = codes_t ? K * NW : 0;
-  if (t < n_codes) {
-    const int64_t n = t / KW;
-    const int64_t w = t - n * KW;
-    const float* row = W + n * K;
-    uint32_t word = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t k = 16 * w + j;
-      if (k < K) word |= quant_code(row[k], a, bits) << (2 * j);
-    }
-    codes[n * KW + w] = word;
+  const int64_t t = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  const int j = threadIdx.x & 15;
+  const int64_t n_words = codes ? N * KW : 0;
+  const int64_t n_words_t = codes_t ? K * NW : 0;
+  const int64_t wi = t >> 4;  // wave-uniform per 16-lane group
+  if (wi < n_words) {
+    const int64_t n = wi / KW, w = wi - n * KW;
+    const int64_t k = 16 * w + j;
+    const uint32_t c = (k < K) ? quant_code(W[n * K + k], a, bits) : 0u;
+    const uint32_t word = or16(c << (2 * j));
+    if (j == 0) codes[wi] = word;
     return;
   }
-  t -= n_codes;
-  if (t < n_codes_t) {
-    const int64_t w = t / K;
-    const int64_t k = t - w * K;
-    uint32_t word = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t n = 16 * w + j;
-      if (n < N) word |= quant_code(W[n * K + k], a, bits) << (2 * j);
-    }
-    codes_t[k * NW + w] = word;
+  // codes_t: 4 words per wave; word index = (w, k) with k fastest across the 4 groups.
+  const int64_t wt = wi - n_words;
+  if (wt < n_words_t) {
+    const int64_t w = wt / K, k = wt - w * K;
+    const int64_t n = 16 * w + j;
+    const uint32_t c = (n < N) ? quant_code(W[n * K + k], a, bits) : 0u;
+    const uint32_t word = or16(c << (2 * j));
+    if (j == 0) codes_t[k * NW + w] = word;
   }
 }
 
@@ -65,22 +69,6 @@ __global__ __launch_bounds__(kThreads) void quant_dequant_kernel(const float* __
   }
 }
 
-// Deterministic block sum: fixed xor-butterfly inside each wave, then wave 0 adds the
-// four wave sums in wave order.
-__device__ __forceinline__ float block_sum(float v, float* lds4) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) lds4[wave] = v;
-  __syncthreads();
-  float t = 0.0f;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < kThreads / 64; ++i) t += lds4[i];
-  }
-  return t;  // valid in thread 0 only
-}
-
 // quant.py:80-91 applied to the fixed-order sum of `chunks` partial slabs.
 // Block = 64 elements x 4 chunk groups: group q sums chunks q, q+4, q+8, ... (independent,
 // coalesced loads), the 4 group sums are added in group order through LDS, then wave 0
@@ -90,7 +78,8 @@ constexpr int kReduceElems = 64;
 __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
     const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
     int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
-    int bits, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ apart) {
+    int bits, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ apart,
+    uint32_t* __restrict__ ticket, float* __restrict__ dalpha) {
   __shared__ float grp_sum[4][kReduceElems];
   const int lane = threadIdx.x & 63;
   const int grp = threadIdx.x >> 6;
@@ -129,21 +118,33 @@ __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
-  if (lane == 0) apart[blockIdx.x] = prod;
-}
 
-// quant.py:91 .sum() finished over the block partials, then the abs() chain of
-// quant.py:124 (torch abs backward multiplies by sgn(alpha)).
-__global__ __launch_bounds__(kThreads) void ste_finalize_kernel(const float* __restrict__ apart,
-                                                                int64_t nb,
-                                                                const float* __restrict__ alpha,
-                                                                int alpha_raw,
-                                                                float* __restrict__ dalpha) {
-  __shared__ float lds4[kThreads / 64];
-  float s = 0.0f;
-  for (int64_t i = threadIdx.x; i < nb; i += kThreads) s += apart[i];
-  const float t = block_sum(s, lds4);
-  if (threadIdx.x == 0) dalpha[0] = t * alpha_chain(alpha, alpha_raw);
+  // Last-arriver finish of quant.py:91 .sum() (MI355X_MICROARCH / Guideline 16 counter
+  // form): publish this block's partial, release at agent scope, take a ticket; the block
+  // that draws the last ticket acquires and sums every partial in index order, so the
+  // result does not depend on which block finishes last. `ticket` was zeroed by the
+  // previous kernel on this stream (dw_partial) or by a memset, and is re-zeroed here.
+  int last = 0;
+  if (lane == 0) {
+    apart[blockIdx.x] = prod;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1) ? 1 : 0;
+  }
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float s2 = 0.0f;
+  for (uint32_t i = lane; i < gridDim.x; i += 64) s2 += apart[i];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 64);
+  if (lane == 0) {
+    dalpha[0] = s2 * alpha_chain(alpha, alpha_raw);
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void ste_finalize_kernel(const float* __r
 void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits, int64_t N,
                        int64_t K, uint32_t* codes, uint32_t* codes_t, hipStream_t s) {
   const int64_t KW = ceil_div(K, 16), NW = ceil_div(N, 16);
-  const int64_t total = (codes ? N * KW : 0) + (codes_t ? K * NW : 0);
+  const int64_t total = 16 * ((codes ? N * KW : 0) + (codes_t ? K * NW : 0));
   if (total == 0) return;
   const int64_t blocks = ceil_div(total, kThreads);
   hipLaunchKernelGGL(quant_pack_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, W, alpha,
@@ -171,14 +172,12 @@ int64_t ste_reduce_blocks(int64_t total) { return ceil_div(total, kReduceElems);
 
 void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* part_db,
                        int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,
-                       float* dW, float* db, float* apart, float* dalpha, hipStream_t s) {
-  const int64_t nb = ste_reduce_blocks(nk + n_db);
-  if (nb > 0) {
-    hipLaunchKernelGGL(ste_reduce_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, chunks,
-                       nk, part_db, n_db, W, alpha, alpha_raw, bits, dW, db, apart);
-  }
-  hipLaunchKernelGGL(ste_finalize_kernel, dim3(1), dim3(kThreads), 0, s, apart, nb, alpha,
-                     alpha_raw, dalpha);
+                       float* dW, float* db, float* apart, uint32_t* ticket, float* dalpha,
+                       hipStream_t s) {
+  int64_t nb = ste_reduce_blocks(nk + n_db);
+  if (nb == 0) nb = 1;  // an empty tensor still writes dalpha = 0
+  hipLaunchKernelGGL(ste_reduce_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, chunks,
+                     nk, part_db, n_db, W, alpha, alpha_raw, bits, dW, db, apart, ticket, dalpha);
 }
 
 }  // namespace ob

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Per-kernel timing of the BitLinear C ABI at the Conformer-S shapes (HIP events on the
+launch stream, back-to-back launches). Usage: python tools/kbench.py [--reps 50]"""
+import argparse
+import math
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "cmu-11785-idl-1.58bit-asr_amd")]
+
+import torch  # noqa: E402
+
+from onebit_asr import _lib  # noqa: E402
+from onebit_asr.quant import pack_codes  # noqa: E402
+
+SHAPES = [("lin1", 7968, 144, 576), ("lin2", 7968, 576, 144), ("qkvo", 7968, 144, 144),
+          ("pos", 249, 144, 144)]
+
+
+def timed(fn, reps, graph):
+    """us per launch. graph=True replays `reps` captured launches (no host launch cost in
+    the measured span, as in a captured training step)."""
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                cs = torch.cuda.current_stream().cuda_stream
+                for _ in range(reps):
+                    fn(cs)
+        g.replay()
+        torch.cuda.synchronize()
+        run = g.replay
+        n = reps
+    else:
+        run = lambda: [fn() for _ in range(reps)]  # noqa: E731
+        n = reps
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    run()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--shape", default=None, help="only this layer (lin1|lin2|qkvo|pos)")
+    ap.add_argument("--op", default=None, help="only this op (pack|fwd|dx|dw)")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    lib = _lib.load()
+    st = torch.cuda.current_stream(dev)
+    s = st.cuda_stream
+    print(f"{'layer':6s} {'M':>5s} {'K':>4s} {'N':>4s} | {'pack':>7s} {'fwd':>7s} {'dx':>7s} {'dw':>7s} us | fwd GB/s  dw GB/s")
+    for name, M, K, N in SHAPES:
+        if args.shape and name != args.shape:
+            continue
+        X = torch.randn(M, K, device=dev)
+        dY = torch.randn(M, N, device=dev)
+        W = (torch.rand(N, K, device=dev) * 2 - 1) * (2 / math.sqrt(K))
+        alpha = W.abs().mean()
+        b = torch.zeros(N, device=dev)
+        codes, codes_t = pack_codes(W, alpha, 2)
+        Y = torch.empty(M, N, device=dev)
+        dX = torch.empty(M, K, device=dev)
+        dW = torch.empty(N, K, device=dev)
+        da = torch.empty((), device=dev)
+        db = torch.empty(N, device=dev)
+        wsb = lib.ob_bitlinear_bwd_dw_workspace(M, N, K)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fns = {
+            "pack": lambda cs=s: lib.ob_quant_pack(W.data_ptr(), alpha.data_ptr(), 1, 2, N, K,
+                                              codes.data_ptr(), codes_t.data_ptr(), cs),
+            "fwd": lambda cs=s: lib.ob_bitlinear_fwd(X.data_ptr(), M, K, codes.data_ptr(), alpha.data_ptr(), 1,
+                                                b.data_ptr(), N, Y.data_ptr(), cs),
+            "dx": lambda cs=s: lib.ob_bitlinear_bwd_dx(dY.data_ptr(), M, N, codes_t.data_ptr(),
+                                                  alpha.data_ptr(), 1, K, dX.data_ptr(), cs),
+            "dw": lambda cs=s: lib.ob_bitlinear_bwd_dw(dY.data_ptr(), X.data_ptr(), M, N, K, W.data_ptr(),
+                                                  alpha.data_ptr(), 1, 2, dW.data_ptr(), da.data_ptr(),
+                                                  db.data_ptr(), ws.data_ptr(), wsb, cs),
+        }
+        res = {}
+        for k, fn in fns.items():
+            res[k] = timed(fn, args.reps, args.graph) if (not args.op or k == args.op) else float("nan")
+        gb_f = 4 * (M * K + M * N) / res["fwd"] / 1e3
+        gb_w = 4 * (M * K + M * N) / res["dw"] / 1e3
+        print(f"{name:6s} {M:5d} {K:4d} {N:4d} | {res['pack']:7.2f} {res['fwd']:7.2f} {res['dx']:7.2f} {res['dw']:7.2f} us | {gb_f:8.0f} {gb_w:8.0f}")
+
+
+if __name__ == "__main__":
+    main()
