@@ -119,26 +119,27 @@ __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
 
-  // Last-arriver finish of quant.py:91 .sum() (MI355X_MICROARCH / Guideline 16 counter
-  // form): publish this block's partial, release at agent scope, take a ticket; the block
-  // that draws the last ticket acquires and sums every partial in index order, so the
-  // result does not depend on which block finishes last. `ticket` was zeroed by the
-  // previous kernel on this stream (dw_partial) or by a memset, and is re-zeroed here.
+  // Last-arriver finish of quant.py:91 .sum() (Guideline 16, write-through form, no
+  // fences): the partial is stored sc1 (agent-scope relaxed atomic store = write-through),
+  // drained, then a relaxed agent ticket is taken; the block that draws the last ticket
+  // reads every partial with sc1 loads (L1 bypass) and sums them in index order, so the
+  // result does not depend on which block finishes last. A release fence here instead
+  // writes back the XCD L2 per block (measured 20 us for this kernel at Conformer-S).
+  // `ticket` was zeroed by dw_partial (previous kernel on this stream) or a memset, and
+  // is re-zeroed by the last block.
   int last = 0;
   if (lane == 0) {
-    apart[blockIdx.x] = prod;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&apart[blockIdx.x], prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = (t == gridDim.x - 1) ? 1 : 0;
   }
   last = __shfl(last, 0, 64);
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
   float s2 = 0.0f;
-  for (uint32_t i = lane; i < gridDim.x; i += 64) s2 += apart[i];
+  for (uint32_t i = lane; i < gridDim.x; i += 64)
+    s2 += __hip_atomic_load(&apart[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 64);
   if (lane == 0) {

@@ -1,0 +1,330 @@
+// tgemm.hip — the ternary BitLinear GEMM on gfx950 matrix cores.
+//
+//   forward  Y  = a * X . Q^T + b     (quant.py:126, F.linear with W_hat = a*Q)
+//   backward dX = a * dY . Q          (autograd of quant.py:126; same kernel, codes_t)
+//
+// fp32 parity with the reference's fp32 F.linear: each fp32 activation is split exactly
+// into three bf16 parts x = hi + mid + lo (8+8+8 significand bits); Q in {-1,0,+1} is
+// exact in bf16, so three v_mfma_f32_16x16x32_bf16 per k-step accumulate exact products
+// in fp32 -- an fp32 GEMM up to summation order, at 3/16 of the fp32-MFMA cost. The scale
+// `a` is applied once in the epilogue (Y = a*(X.Q^T)).
+//
+// Block = 4 waves, 64 rows x BN = 16*NT columns. At entry the block decodes its BN code
+// rows into a bf16 image of Q in LDS ([BN][Kpad+8], the row pad keeps the B-fragment
+// ds_read_b128 conflict-free at K = 144 / 576), then loops over its row tiles: each wave
+// streams 16 rows of A (two dwordx4 per lane per 32-wide k-chunk, all chunks of a row in
+// flight at once when K is a compile-time size), splits them in registers and issues 3
+// MFMAs per 16-column tile. Blocks sharing a row tile are dealt to the same XCD so their
+// A reads hit one L2.
+//
+// Fragment map of v_mfma_f32_16x16x32_bf16 (lane l, r = l&15, g = l>>4):
+//   A[i=r][kk=8g+j] (j<8), B[kk=8g+j][col=r], D[row=4g+reg][col=r].
+//
+// OB_GEMM=f32 in the environment selects an fp32-MFMA kernel (v_mfma_f32_16x16x4_f32,
+// exact fp32 fma chain) for A/B checks; it is also the path for shapes the bf16x3 kernel
+// does not take (K % 4 != 0, misaligned A, B image over 64 KB).
+#include <cstdlib>
+
+#include "ob_launch.h"
+#include "ob_quant.h"
+
+namespace ob {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kRows = 64;      // rows per row tile (16 per wave)
+constexpr size_t kMaxLds = 64 * 1024;
+constexpr int kTargetBlocks = 512;  // 2 per CU
+
+__device__ __forceinline__ uint32_t code_bf16(uint32_t c) {
+  return ((c & 1u) * 0x3F80u) | ((c & 2u) << 14);  // 0 -> 0, 1 -> +1.0, 3 -> -1.0
+}
+
+// x = hi + mid + lo exactly (RNE at each step; the residuals are exact in fp32).
+__device__ __forceinline__ void split3(const f32x4& a, const f32x4& b, bf16x8& hi, bf16x8& mid,
+                                       bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = j < 4 ? a[j] : b[j - 4];
+    const __bf16 h = (__bf16)x;
+    const float r1 = x - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    hi[j] = h;
+    mid[j] = m;
+    lo[j] = (__bf16)r2;
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): consecutive logical ids land on one XCD under round-robin dispatch.
+__device__ __forceinline__ int xcd_logical(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// Two dwordx4 of one row at k and k+4. The address is clamped into the row instead of
+// guarding the load: a guarded `cond ? *p : 0` makes hipcc branch around the load and wait
+// vmcnt(0) at it. Clamped k positions (k >= K) meet zero codes, so they add nothing; rows
+// past M are clamped to a valid row and never stored.
+__device__ __forceinline__ void load8(const float* __restrict__ arow, int k, int K, f32x4& a,
+                                      f32x4& b) {
+  const int ka = k < K - 4 ? k : K - 4;
+  const int kb = k + 4 < K - 4 ? k + 4 : K - 4;
+  a = *reinterpret_cast<const f32x4*>(arow + ka);
+  b = *reinterpret_cast<const f32x4*>(arow + kb);
+}
+
+template <int NT, int NCH>
+__global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
+    const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
+    int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
+    const float* __restrict__ bias, float* __restrict__ C) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* bimg = reinterpret_cast<__bf16*>(smem);
+  const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
+  const int stride = kpad + 8;
+  const int kwp = kpad >> 4;
+
+  const int L = xcd_logical(blockIdx.x, gridDim.x);
+  const int ct = L % n_ct;
+  const int rg = L / n_ct;
+  const int n0 = ct * (16 * NT);
+
+  // Decode this block's Q rows: one code word -> 16 bf16 (two 16-byte LDS stores).
+  for (int idx = threadIdx.x; idx < 16 * NT * kwp; idx += kThreads) {
+    const int nl = idx / kwp, w = idx - nl * kwp;
+    const int n = n0 + nl;
+    const uint32_t word = (n < N && w < KW) ? codes[(int64_t)n * KW + w] : 0u;
+    u32x4 lo4, hi4;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      lo4[p] = code_bf16((word >> (4 * p)) & 3u) | (code_bf16((word >> (4 * p + 2)) & 3u) << 16);
+      hi4[p] = code_bf16((word >> (4 * p + 16)) & 3u) |
+               (code_bf16((word >> (4 * p + 18)) & 3u) << 16);
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(bimg + nl * stride + 16 * w);
+    dst[0] = lo4;
+    dst[1] = hi4;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int kg = 8 * g;
+  const __bf16* brow = bimg + r * stride + kg;
+  const float a_eff = effective_alpha(alpha, alpha_raw);
+  float bcol[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 16 * t + r;
+    bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
+  }
+
+  for (int rt = rg; rt < n_rt; rt += rgroups) {
+    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
+    const int64_t row = m0 + r < M ? m0 + r : M - 1;
+    const float* arow = A + row * (int64_t)K;
+
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // All B fragments of the chunk are read first and the split runs while they are in
+    // flight; each tile's MFMAs then wait only for their own read (counted lgkmcnt).
+    auto compute = [&](const f32x4& x0, const f32x4& x1, int kc) {
+      bf16x8 bq[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        bq[t] = *reinterpret_cast<const bf16x8*>(brow + t * 16 * stride + kc);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (hipcc would pair them up)
+      bf16x8 hi, mid, lo;
+      split3(x0, x1, hi, mid, lo);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t] = mfma_bf16(lo, bq[t], acc[t]);
+        acc[t] = mfma_bf16(mid, bq[t], acc[t]);
+        acc[t] = mfma_bf16(hi, bq[t], acc[t]);
+      }
+    };
+
+    if constexpr (NCH > 0) {
+      // Fully unrolled; a window of kWin chunks in flight. sched_barrier keeps hipcc from
+      // sinking each load next to its use (one load in flight, vmcnt(0) per chunk).
+      constexpr int kWin = NCH < (NT > 6 ? 3 : 5) ? NCH : (NT > 6 ? 3 : 5);
+      f32x4 buf[NCH][2];
+#pragma unroll
+      for (int c = 0; c < kWin; ++c) load8(arow, 32 * c + kg, K, buf[c][0], buf[c][1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + kWin < NCH) load8(arow, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(buf[c][0], buf[c][1], 32 * c);
+      }
+    } else {
+      // Generic K: three rotating register sets, unrolled so no register copy of an
+      // in-flight load exists (a copy would make hipcc wait for it).
+      f32x4 r0a, r0b, r1a, r1b, r2a, r2b;
+      load8(arow, kg, K, r0a, r0b);
+      load8(arow, 32 + kg, K, r1a, r1b);
+      for (int kc = 0; kc < kpad; kc += 96) {
+        load8(arow, kc + 64 + kg, K, r2a, r2b);
+        compute(r0a, r0b, kc);
+        load8(arow, kc + 96 + kg, K, r0a, r0b);
+        if (kc + 32 < kpad) compute(r1a, r1b, kc + 32);
+        load8(arow, kc + 128 + kg, K, r1a, r1b);
+        if (kc + 64 < kpad) compute(r2a, r2b, kc + 64);
+      }
+    }
+
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 16 * t + r;
+      if (col >= N) continue;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t orow = m0 + 4 * g + reg;
+        if (orow < M) C[orow * N + col] = fmaf(a_eff, acc[t][reg], bcol[t]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// fp32-MFMA ternary GEMM (exact fp32 fma chain), 64 rows x 48 columns per block.
+// Per 16-wide k chunk a lane loads X[row][kc+4g .. kc+4g+3] and one code word per n tile;
+// byte g of that word holds the 4 codes of k = kc+4g+e, e = 0..3.
+// ---------------------------------------------------------------------------------
+constexpr int kF32NT = 3;
+
+__global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
+    const float* __restrict__ A, int64_t M, int64_t K, const uint32_t* __restrict__ codes,
+    int64_t KW, int64_t N, const float* __restrict__ alpha, int alpha_raw,
+    const float* __restrict__ bias, float* __restrict__ C) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * kRows + wave * 16;
+  const int64_t n0 = (int64_t)blockIdx.y * (16 * kF32NT);
+  const int64_t row = m0 + r < M ? m0 + r : M - 1;
+  const float* arow = A + row * K;
+  f32x4 acc[kF32NT];
+#pragma unroll
+  for (int t = 0; t < kF32NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t kc = 0; kc < K; kc += 16) {
+    float xa[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t k = kc + 4 * g + e;
+      xa[e] = arow[k < K ? k : K - 1];  // k >= K meets a zero code
+    }
+#pragma unroll
+    for (int t = 0; t < kF32NT; ++t) {
+      const int64_t n = n0 + 16 * t + r;
+      const uint32_t word = codes[(n < N ? n : N - 1) * KW + (kc >> 4)];
+      const uint32_t byte = (n < N) ? (word >> (8 * g)) : 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], code_value((byte >> (2 * e)) & 3u),
+                                                       acc[t], 0, 0, 0);
+    }
+  }
+  const float a = effective_alpha(alpha, alpha_raw);
+#pragma unroll
+  for (int t = 0; t < kF32NT; ++t) {
+    const int64_t col = n0 + 16 * t + r;
+    if (col >= N) continue;
+    const float b = bias ? bias[col] : 0.0f;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int64_t orow = m0 + 4 * g + reg;
+      if (orow < M) C[orow * N + col] = fmaf(a, acc[t][reg], b);
+    }
+  }
+}
+
+bool use_f32_gemm() {
+  static const int v = [] {
+    const char* e = getenv("OB_GEMM");
+    return (e && e[0] == 'f') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
+size_t bimg_bytes(int nt, int64_t K) {
+  const int64_t kpad = (K + 31) & ~int64_t(31);
+  return sizeof(uint16_t) * (size_t)(16 * nt) * (size_t)(kpad + 8);
+}
+
+// Widest column tile whose bf16 image fits the LDS budget, preferring tiles that divide N.
+int pick_nt(int64_t N, int64_t K) {
+  static const int cands[] = {12, 9, 6, 4, 3, 2, 1};
+  for (int nt : cands)
+    if (N % (16 * nt) == 0 && bimg_bytes(nt, K) <= kMaxLds) return nt;
+  for (int nt : cands)
+    if (16 * nt <= ((N + 15) & ~int64_t(15)) && bimg_bytes(nt, K) <= kMaxLds) return nt;
+  return 0;
+}
+
+template <int NT>
+void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
+                   const float* alpha, int alpha_raw, const float* bias, float* C, hipStream_t s) {
+  const int n_ct = (int)ceil_div(N, 16 * NT);
+  const int n_rt = (int)ceil_div(M, kRows);
+  int rgroups = kTargetBlocks / n_ct;
+  if (rgroups < 1) rgroups = 1;
+  if (rgroups > n_rt) rgroups = n_rt;
+  const dim3 grid((unsigned)(rgroups * n_ct));
+  const size_t lds = bimg_bytes(NT, K);
+  const int KW = (int)ceil_div(K, 16);
+#define OB_TGEMM(NCH)                                                                        \
+  hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH>), grid, dim3(kThreads), lds, s, A, M, (int)K, \
+                     codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C)
+  switch ((K + 31) / 32) {  // Conformer widths: 64, 144, 256, 576
+    case 2: OB_TGEMM(2); break;
+    case 5: OB_TGEMM(5); break;
+    case 8: OB_TGEMM(8); break;
+    case 18: OB_TGEMM(18); break;
+    default: OB_TGEMM(0); break;
+  }
+#undef OB_TGEMM
+}
+
+}  // namespace
+
+void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
+                         const float* alpha, int alpha_raw, const float* bias, float* C,
+                         hipStream_t s) {
+  if (M == 0 || N == 0) return;
+  const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const int nt = vec && !use_f32_gemm() ? pick_nt(N, K) : 0;
+  switch (nt) {
+    case 12: launch_bf16x3<12>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    case 9: launch_bf16x3<9>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    case 6: launch_bf16x3<6>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    case 4: launch_bf16x3<4>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    case 3: launch_bf16x3<3>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    case 2: launch_bf16x3<2>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    case 1: launch_bf16x3<1>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
+    default: break;
+  }
+  // fp32 path (K == 0 included: its k-loop is empty and never reads A).
+  const dim3 grid((unsigned)ceil_div(M, kRows), (unsigned)ceil_div(N, 16 * kF32NT));
+  hipLaunchKernelGGL(tgemm_f32_kernel, grid, dim3(kThreads), 0, s, A, M, K, codes,
+                     ceil_div(K, 16), N, alpha, alpha_raw, bias, C);
+}
+
+}  // namespace ob

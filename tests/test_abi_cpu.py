@@ -1,0 +1,85 @@
+"""CPU: the C-ABI library loads, exports every entry point include/onebit_hip.h declares, and
+rejects bad arguments before touching the GPU (no compute calls without a GPU)."""
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "onebit_hip.h"
+
+
+def _declared():
+    text = HEADER.read_text()
+    return re.findall(r"OB_API\s+[\w\s\*]+?\b(ob_\w+)\s*\(", text)
+
+
+def test_header_declares_expected_entry_points():
+    names = set(_declared())
+    assert {"ob_quant_pack", "ob_bitlinear_fwd", "ob_bitlinear_bwd_dx", "ob_bitlinear_bwd_dw",
+            "ob_quant_dequant", "ob_quant_ste_bwd", "ob_abi_version", "ob_status_string",
+            "ob_bitlinear_bwd_dw_workspace", "ob_quant_ste_bwd_workspace"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+    assert lib.ob_abi_version() == _lib.ABI_VERSION
+
+
+def test_status_strings():
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    assert lib.ob_status_string(0) == b"ok"
+    assert lib.ob_status_string(-3) == b"bitwidth must be one of {1,2,32}"
+    assert lib.ob_status_string(-99) == b"unknown status"
+
+
+def test_argument_validation_without_gpu():
+    """Every check below fails before any HIP call, so it is safe with no device."""
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    fake = 0x1000  # never dereferenced: validation rejects the call first
+    assert lib.ob_quant_pack(fake, fake, 1, 3, 4, 4, fake, fake, None) == -3  # bitwidth
+    assert lib.ob_quant_pack(fake, fake, 1, 0, 4, 4, fake, fake, None) == -3
+    assert lib.ob_quant_pack(fake, None, 1, 2, 4, 4, fake, fake, None) == -1  # null alpha
+    assert lib.ob_quant_pack(fake, fake, 1, 2, -1, 4, fake, fake, None) == -2  # shape
+    assert lib.ob_quant_pack(0x1001, fake, 1, 2, 4, 4, fake, fake, None) == -5  # align
+    assert lib.ob_bitlinear_fwd(fake, -1, 4, fake, fake, 1, None, 4, fake, None) == -2
+    assert lib.ob_bitlinear_fwd(None, 4, 4, fake, fake, 1, None, 4, fake, None) == -1
+    assert lib.ob_bitlinear_bwd_dx(fake, 4, 4, None, fake, 1, 4, fake, None) == -1
+    assert lib.ob_bitlinear_bwd_dw(fake, fake, 4, 4, 4, fake, fake, 1, 5, fake, fake, None, fake,
+                                   1 << 20, None) == -3
+    need = lib.ob_bitlinear_bwd_dw_workspace(7968, 576, 144)
+    assert need > 576 * 144 * 4  # at least one partial slab
+    assert lib.ob_bitlinear_bwd_dw(fake, fake, 7968, 576, 144, fake, fake, 1, 2, fake, fake, None,
+                                   fake, need - 1, None) == -4
+    assert lib.ob_quant_ste_bwd(fake, fake, fake, 0, 2, 16, fake, fake, fake, 0, None) == -4
+    assert lib.ob_quant_ste_bwd_workspace(-1) == 0
+
+
+def test_bitlinear_python_surface_on_cpu():
+    """The module keeps the reference surface; bitwidth 1/2 has no CPU fallback."""
+    import torch
+
+    from onebit_asr.quant import BitLinear, QuantizedLinear
+
+    assert BitLinear is QuantizedLinear
+    m = QuantizedLinear(12, 5)
+    assert set(dict(m.named_parameters())) == {"weight", "alpha", "bias"}
+    assert m.alpha.shape == () and m.weight.shape == (5, 12)
+    assert float(m.weight.abs().max()) <= 2 / 12 ** 0.5 + 1e-6
+    assert torch.isclose(m.alpha, m.weight.abs().mean())
+    x = torch.randn(3, 12)
+    assert torch.allclose(m(x, 32), torch.nn.functional.linear(x, m.weight, m.bias))
+    with pytest.raises(ValueError, match=r"bitwidth must be one of \{1,2,32\}"):
+        m(x, 4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m(x, 2)
+    assert QuantizedLinear(4, 4, bias=False).bias is None

@@ -1,0 +1,97 @@
+"""CPU, world_size 2 (gloo): the product's DDP step wiring -- one OneBitStep forward per
+backward, identical SP masks on every rank, gradient all-reduce = mean of per-shard
+gradients, replicas identical after the optimizer step. The model is the CPU oracle (the
+product BitLinear has no CPU path); the step module and train_step are the product's."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+TINY = dict(enc_d_model=32, enc_layers=2, enc_heads=2, enc_d_ff=64, enc_conv_kernel=7,
+            enc_dropout=0.0, dec_layers=1, dec_heads=2, dec_d_ff=64, dec_dropout=0.0)
+TINY_ORACLE = dict(input_dim=40, vocab_size=48, d_model=32, n_layers=2, n_heads=2, d_ff=64,
+                   conv_kernel=7, dec_layers=1, dec_heads=2, dec_d_ff=64, dropout=0.0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _model():
+    from onebit_asr.conformer import ConformerASR
+    from oracle.conformer_oracle import OracleConformer
+
+    torch.manual_seed(0)
+    prod = ConformerASR(40, 48, **TINY)
+    return OracleConformer(prod.state_dict(), **TINY_ORACLE)
+
+
+def _batch(rank):
+    from onebit_asr.data import synthetic_batch
+
+    return synthetic_batch([120, 97], [5, 3], n_mels=40, vocab=48, seed=100 + rank)
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "cmu-11785-idl-1.58bit-asr_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from onebit_asr.train_step import OneBitStep, make_optimizer, sample_sp_mask, train_step
+
+    model = _model()
+    step = DDP(OneBitStep(model, n_layers=2), broadcast_buffers=False)
+    gen = torch.Generator().manual_seed(7)
+    sp_mask = sample_sp_mask(2, generator=gen)
+    loss, _ = step(_batch(rank), sp_mask)
+    loss.backward()
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+    # one full product train_step (clip + AdamW) on top, to check replicas stay identical
+    opt = make_optimizer(model.parameters())
+    train_step(step, opt, None, _batch(rank), sp_mask)
+    params = {k: p.detach().clone() for k, p in model.named_parameters()}
+    torch.save({"sp_mask": sp_mask, "grads": grads, "params": params, "loss": loss.item()},
+               os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_ddp_two_ranks_gloo(tmp_path):
+    from onebit_asr.train_step import OneBitStep, sample_sp_mask
+
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    assert res[0]["sp_mask"] == res[1]["sp_mask"]
+    # reference: mean over shards of single-process gradients
+    sp_mask = sample_sp_mask(2, generator=torch.Generator().manual_seed(7))
+    assert sp_mask == res[0]["sp_mask"]
+    per_rank = []
+    for r in range(world):
+        m = _model()
+        loss, _ = OneBitStep(m, n_layers=2)(_batch(r), sp_mask)
+        loss.backward()
+        per_rank.append({k: p.grad for k, p in m.named_parameters()})
+    for k in per_rank[0]:
+        ref = (per_rank[0][k] + per_rank[1][k]) / 2
+        # shard gradients can cancel in the mean: bound the error by the shards' magnitude
+        scale = max(per_rank[0][k].abs().max().item(), per_rank[1][k].abs().max().item())
+        for r in range(world):
+            err = (res[r]["grads"][k] - ref).abs().max().item()
+            assert err <= 1e-5 * scale + 1e-6, (k, err, scale)  # dw.bias grad is ~0 (BN follows)
+    for k in res[0]["params"]:
+        assert torch.equal(res[0]["params"][k], res[1]["params"][k]), k
