@@ -2,9 +2,20 @@
 //   part[c] = dY[rows of chunk c]^T . X[rows of chunk c]      (autograd of quant.py:126)
 // finished by ste_reduce (quant.hip), which applies quant.py:80-91.
 //
-// fp32 v_mfma_f32_16x16x4_f32 (exact fp32 fma chain). Fragment map (lane l, r = l&15,
-// g = l>>4): A[i=r][kk=g], B[kk=g][j=r], D[row=4g+reg][col=r]; kk is free to permute as
-// long as A and B agree, so every lane loads 4 contiguous fp32 (one dwordx4) of a row.
+// Default kernel: bf16x6 split MFMA. Both operands are dense fp32; each is split exactly
+// into hi + mid + lo bf16 parts and the six products with combined weight >= 2^-16
+// (hh, hm, mh, hl, lh, mm; each exact in fp32) are accumulated by
+// v_mfma_f32_16x16x32_bf16 in fp32. The dropped terms (ml, lm, ll) are below 2^-24
+// relative, so G matches an fp32 GEMM to fp32 rounding, at 6/16 of the fp32-MFMA cost.
+// No LDS in the main loop: lane (r, g) loads VW consecutive columns of rows 8g..8g+7 of
+// a 32-row step for both operands; element e of the VW columns is the operand of n-tile
+// (or k-tile) e, so a 16*VW-wide tile needs no transpose (VW = 3: 48-wide tiles, which
+// divide the Conformer widths 144 / 576; VW = 4: 64-wide).
+// Fragment map of v_mfma_f32_16x16x32_bf16 (lane l, r = l&15, g = l>>4):
+//   A[i=r][kk=8g+j], B[kk=8g+j][col=r], D[row=4g+reg][col=r].
+//
+// OB_GEMM=f32 selects the fp32 kernel (v_mfma_f32_16x16x4_f32, exact fp32 fma chain):
+// A[i=r][kk=g], B[kk=g][j=r]; every lane loads 4 contiguous fp32 (one dwordx4) of a row.
 #include <cstdlib>
 
 #include "ob_launch.h"
@@ -19,7 +30,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;  // 4 waves
-constexpr int kGemmRows = 64;  // rows of X per block (16 per wave)
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -187,19 +197,224 @@ __global__ __launch_bounds__(kThreads) void dw_partial_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// dW partial, bf16x6: part[c][n][k] = sum_{m in chunk c} dY[m][n] * X[m][k].
+// Block = one (16VW x 16VW) output tile x one M chunk of 4*S*32 rows; wave w takes the
+// 32-row steps w, w+4, ...; the 4 wave tiles are summed in wave order through LDS.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Buffer descriptor over [base, base + bytes): loads past the end return 0 (hardware
+// range check), which zero-fills the rows past M without any per-lane test.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, int64_t bytes) {
+  const uint32_t nrec = bytes > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)nrec,
+                                           0x00020000);
+}
+
+// 4 fp32 -> 8-lane bf16 fragments, split exactly: x = hi + mid + lo.
+template <int VW>
+__device__ __forceinline__ void split_col(const f32x4 (&rows)[8], int e, bf16x8& hi, bf16x8& mid,
+                                          bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = rows[j][e];
+    const __bf16 h = (__bf16)x;
+    const float r1 = x - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    hi[j] = h;
+    mid[j] = m;
+    lo[j] = (__bf16)r2;
+  }
+}
+
+// Requires N % 4 == 0, K % 4 == 0 (dwordx4 rows); other shapes take the fp32 kernel.
+// Lane (r, g) loads columns n0+4r..4r+3 (dY) and k0+4r..4r+3 (X) of rows 8g..8g+7 of a
+// 32-row step: element e is the operand of n-tile (k-tile) e. Out-of-range rows read 0
+// from the buffer descriptor; out-of-range columns only feed outputs that are never
+// stored, so the main loop has no masks. Row and step offsets are scalar (soffset).
+template <int S>
+__global__ __launch_bounds__(kThreads) void dw_bf16x6_kernel(
+    const float* __restrict__ dY, const float* __restrict__ X, int64_t M, int N, int K,
+    int tiles_k, int64_t rows_per_chunk, float* __restrict__ part, float* __restrict__ part_db,
+    uint32_t* __restrict__ ticket) {
+  constexpr int VW = 4, T = 64;
+  __shared__ float red[2][T * T];
+  __shared__ float dbred[4][T];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int tn = blockIdx.x / tiles_k;
+  const int tk = blockIdx.x - tn * tiles_k;
+  const int n0 = tn * T, k0 = tk * T;
+  const int64_t chunk = blockIdx.y;
+  const int64_t m_begin = chunk * rows_per_chunk;
+  const bool do_db = (part_db != nullptr) && (tk == 0);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ticket = 0u;
+
+  // Descriptors start at the chunk's first row, so every offset fits 32 bits.
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(dY + m_begin * N, (M - m_begin) * N * 4);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + m_begin * K, (M - m_begin) * K * 4);
+  // Column offset clamped into the row (columns past N / K feed discarded outputs).
+  const int nb = n0 + 4 * r < N - 4 ? n0 + 4 * r : N - 4;
+  const int kb = k0 + 4 * r < K - 4 ? k0 + 4 * r : K - 4;
+  const int voff_y = (8 * g * N + nb) * 4;
+  const int voff_x = (8 * g * K + kb) * 4;
+
+  f32x4 acc[VW][VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e)
+#pragma unroll
+    for (int f = 0; f < VW; ++f) acc[e][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 dbacc = {0.f, 0.f, 0.f, 0.f};
+
+  struct Step {
+    f32x4 dy[8];
+    f32x4 x[8];
+  };
+  auto load = [&](int row0, Step& st) {  // row0: chunk-relative first row of the step
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st.dy[j] = __builtin_amdgcn_raw_buffer_load_b128(ry, voff_y, (row0 + j) * N * 4, 0);
+      st.x[j] = __builtin_amdgcn_raw_buffer_load_b128(rx, voff_x, (row0 + j) * K * 4, 0);
+    }
+  };
+  auto compute = [&](const Step& st) {
+    bf16x8 ah[VW], am[VW], al[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) split_col<VW>(st.dy, e, ah[e], am[e], al[e]);
+    if (do_db) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dbacc += st.dy[j];
+    }
+#pragma unroll
+    for (int f = 0; f < VW; ++f) {
+      bf16x8 bh, bm, bl;
+      split_col<VW>(st.x, f, bh, bm, bl);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        f32x4 c = acc[e][f];
+        c = mfma_bf16(am[e], bm, c);  // smallest terms first
+        c = mfma_bf16(al[e], bh, c);
+        c = mfma_bf16(ah[e], bl, c);
+        c = mfma_bf16(am[e], bh, c);
+        c = mfma_bf16(ah[e], bm, c);
+        c = mfma_bf16(ah[e], bh, c);
+        acc[e][f] = c;
+      }
+    }
+  };
+
+  // S steps per wave (wave w: steps w, w+4, ... of the chunk), one step in flight ahead.
+  const int r0 = 32 * wave;
+  Step bufA, bufB;
+  load(r0, bufA);
+#pragma unroll
+  for (int i = 0; i < S; i += 2) {
+    if (i + 1 < S) load(r0 + 128 * (i + 1), bufB);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(bufA);
+    if (i + 1 < S) {
+      if (i + 2 < S) load(r0 + 128 * (i + 2), bufA);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(bufB);
+    }
+  }
+
+  // Combine the 4 wave tiles in a fixed order: (w0 + w2) + (w1 + w3).
+  // Tile (e,f) D[row=4g+reg][col=r] -> G[n0 + 4*(4g+reg) + e][k0 + 4*r + f].
+  float* myred = red[wave & 1];
+  auto tile_index = [&](int e, int f, int reg) { return (VW * (4 * g + reg) + e) * T + VW * r + f; };
+  if (wave >= 2) {
+#pragma unroll
+    for (int e = 0; e < VW; ++e)
+#pragma unroll
+      for (int f = 0; f < VW; ++f)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) myred[tile_index(e, f, reg)] = acc[e][f][reg];
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int e = 0; e < VW; ++e)
+#pragma unroll
+      for (int f = 0; f < VW; ++f)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          float* p = &myred[tile_index(e, f, reg)];
+          *p = acc[e][f][reg] + *p;
+        }
+  }
+  if (do_db) {
+    // rows 8g..8g+7 of every step are in this lane's sums; add the 4 row groups in order
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      float v = dbacc[e];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      dbacc[e] = v;
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int e = 0; e < VW; ++e) dbred[wave][VW * r + e] = dbacc[e];
+    }
+  }
+  __syncthreads();
+
+  float* out = part + chunk * ((int64_t)N * K);
+  for (int idx = threadIdx.x; idx < T * T; idx += kThreads) {
+    const int nl = idx / T, kl = idx - nl * T;
+    const int n = n0 + nl, k = k0 + kl;
+    if (n < N && k < K) out[(int64_t)n * K + k] = red[0][idx] + red[1][idx];
+  }
+  if (do_db && threadIdx.x < T) {
+    const int n = n0 + threadIdx.x;
+    if (n < N) {
+      const int i = threadIdx.x;
+      part_db[chunk * N + n] = ((dbred[0][i] + dbred[1][i]) + dbred[2][i]) + dbred[3][i];
+    }
+  }
+}
+
+bool use_f32_dw() {
+  static const int v = [] {
+    const char* e = getenv("OB_GEMM");
+    return (e && e[0] == 'f') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 }  // namespace
 
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   DwPlan p;
-  // At least one tile each way so that K = 0 still produces the bias partials.
-  p.tiles_n = N > 0 ? ceil_div(N, kDwTile) : 1;
-  p.tiles_k = K > 0 ? ceil_div(K, kDwTile) : 1;
-  const int64_t tiles = p.tiles_n * p.tiles_k;
-  // Chunk = S steps x 16 rows, S in {8, 16, 32}: the longest chunk that still gives
-  // >= 256 blocks (one per CU), so the partial slabs stay few.
-  int64_t steps = 32;
-  while (steps > 8 && tiles * ceil_div(M, 16 * steps) < 256) steps /= 2;
-  p.rows_per_chunk = 16 * steps;
+  if (use_f32_dw() || N % 4 != 0 || K % 4 != 0 || N < 4 || K < 4) {
+    p.variant = 0;
+    p.tiles_n = N > 0 ? ceil_div(N, kDwTile) : 1;  // >= 1 so K = 0 still yields db
+    p.tiles_k = K > 0 ? ceil_div(K, kDwTile) : 1;
+    const int64_t tiles = p.tiles_n * p.tiles_k;
+    int64_t steps = 32;  // chunk = S steps x 16 rows
+    while (steps > 8 && tiles * ceil_div(M, 16 * steps) < 256) steps /= 2;
+    p.rows_per_chunk = 16 * steps;
+  } else {
+    // 64-wide tiles (one dwordx4 per lane per row). 48-wide tiles (which divide 144 / 576
+    // without waste) measured slower: three strided dword loads per row.
+    p.variant = 4;
+    const int64_t t = 16 * p.variant;
+    p.tiles_n = N > 0 ? ceil_div(N, t) : 1;
+    p.tiles_k = K > 0 ? ceil_div(K, t) : 1;
+    const int64_t tiles = p.tiles_n * p.tiles_k;
+    // Chunk = 4 waves x S steps x 32 rows, S in {2, 4, 8}: the longest chunk that still
+    // gives >= 256 blocks (one per CU), so the partial slabs stay few.
+    int64_t steps = 8;
+    while (steps > 2 && tiles * ceil_div(M, 128 * steps) < 256) steps /= 2;
+    p.rows_per_chunk = 128 * steps;
+  }
   p.chunks = M > 0 ? ceil_div(M, p.rows_per_chunk) : 1;
   return p;
 }
@@ -215,6 +430,16 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
 #define OB_DW(V, S)                                                                        \
   hipLaunchKernelGGL((dw_partial_kernel<V, S>), grid, dim3(kThreads), 0, s, dY, X, M, N, K,   \
                      p.tiles_k, p.rows_per_chunk, part, part_db, ticket)
+#define OB_DW6(S)                                                                          \
+  hipLaunchKernelGGL((dw_bf16x6_kernel<S>), grid, dim3(kThreads), 0, s, dY, X, M, (int)N,     \
+                     (int)K, (int)p.tiles_k, p.rows_per_chunk, part, part_db, ticket)
+  if (p.variant != 0) {
+    const int64_t steps = p.rows_per_chunk / 128;
+    if (steps == 8) OB_DW6(8);
+    else if (steps == 4) OB_DW6(4);
+    else OB_DW6(2);
+    return;
+  }
   const int64_t steps = p.rows_per_chunk / 16;
   if (vec) {
     if (steps == 32) OB_DW(true, 32);
@@ -225,6 +450,7 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
     else if (steps == 16) OB_DW(false, 16);
     else OB_DW(false, 8);
   }
+#undef OB_DW6
 #undef OB_DW
 }
 

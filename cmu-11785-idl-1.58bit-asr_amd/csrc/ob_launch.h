@@ -36,6 +36,7 @@ void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* c
 // Split-M partial of G = dY^T . X: part[c][N*K] for chunk c, part_db[c][N] (optional).
 struct DwPlan {
   int64_t tiles_n, tiles_k, chunks, rows_per_chunk;
+  int variant;  // 0: fp32 MFMA (OB_GEMM=f32); 3 / 4: bf16x6 with 48- / 64-wide tiles
 };
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
 // Also zeroes *ticket (for the ste_reduce launch that follows on the same stream).

@@ -70,54 +70,58 @@ __global__ __launch_bounds__(kThreads) void quant_dequant_kernel(const float* __
 }
 
 // quant.py:80-91 applied to the fixed-order sum of `chunks` partial slabs.
-// Block = 64 elements x 4 chunk groups: group q sums chunks q, q+4, q+8, ... (independent,
-// coalesced loads), the 4 group sums are added in group order through LDS, then wave 0
-// applies the STE mask / alpha term and reduces its alpha partial. Deterministic.
-constexpr int kReduceElems = 64;
+// Block = 1024 elements (4 per thread, strided by 256 for coalescing); each thread sums its
+// elements' chunks in chunk order with all loads independent. Few, wide blocks keep the
+// number of ticket atomics on the one completion counter small (each costs ~12 ns
+// serialised; 1300 blocks cost 16 us at Conformer-S). Deterministic.
+constexpr int kReduceEPT = 4;
+constexpr int kReduceElems = kThreads * kReduceEPT;
 
 __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
     const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
     int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
     int bits, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ apart,
     uint32_t* __restrict__ ticket, float* __restrict__ dalpha) {
-  __shared__ float grp_sum[4][kReduceElems];
+  __shared__ float wsum[kThreads / 64];
   const int lane = threadIdx.x & 63;
-  const int grp = threadIdx.x >> 6;
-  const int64_t e = blockIdx.x * (int64_t)kReduceElems + lane;
-  const bool is_w = e < nk;
-  const bool is_b = !is_w && e < nk + n_db;
-  const float* src = is_w ? part + e : (is_b ? part_db + (e - nk) : nullptr);
-  const int64_t stride = is_w ? nk : n_db;
-  float s = 0.0f;
-  if (src) {
-    int c = grp;
-    for (; c + 12 < chunks; c += 16) {
-      const float v0 = src[(int64_t)c * stride];
-      const float v1 = src[(int64_t)(c + 4) * stride];
-      const float v2 = src[(int64_t)(c + 8) * stride];
-      const float v3 = src[(int64_t)(c + 12) * stride];
-      s += v0;
-      s += v1;
-      s += v2;
-      s += v3;
-    }
-    for (; c < chunks; c += 4) s += src[(int64_t)c * stride];
-  }
-  grp_sum[grp][lane] = s;
-  __syncthreads();
-  if (grp != 0) return;
-  const float g = ((grp_sum[0][lane] + grp_sum[1][lane]) + grp_sum[2][lane]) + grp_sum[3][lane];
+  const int wave = threadIdx.x >> 6;
+  const float a = effective_alpha(alpha, alpha_raw);
   float prod = 0.0f;
-  if (is_w) {
-    const float a = effective_alpha(alpha, alpha_raw);
-    const float wa = W[e] / a;
-    dW[e] = g * ste_indicator(wa);  // quant.py:81-82 (multiply: inf*0 -> NaN as in torch)
-    prod = g * alpha_term(wa, bits);  // quant.py:91 grad_out * term
-  } else if (is_b) {
-    db[e - nk] = g;
+#pragma unroll
+  for (int i = 0; i < kReduceEPT; ++i) {
+    const int64_t e = blockIdx.x * (int64_t)kReduceElems + i * kThreads + threadIdx.x;
+    const bool is_w = e < nk;
+    const bool is_b = !is_w && e < nk + n_db;
+    if (!is_w && !is_b) continue;
+    const float* src = is_w ? part + e : part_db + (e - nk);
+    const int64_t stride = is_w ? nk : n_db;
+    float g = 0.0f;
+    int c = 0;
+    for (; c + 4 <= chunks; c += 4) {
+      const float v0 = src[(int64_t)c * stride];
+      const float v1 = src[(int64_t)(c + 1) * stride];
+      const float v2 = src[(int64_t)(c + 2) * stride];
+      const float v3 = src[(int64_t)(c + 3) * stride];
+      g += v0;
+      g += v1;
+      g += v2;
+      g += v3;
+    }
+    for (; c < chunks; ++c) g += src[(int64_t)c * stride];
+    if (is_w) {
+      const float wa = W[e] / a;
+      dW[e] = g * ste_indicator(wa);  // quant.py:81-82 (multiply: inf*0 -> NaN as in torch)
+      prod += g * alpha_term(wa, bits);  // quant.py:91 grad_out * term
+    } else {
+      db[e - nk] = g;
+    }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
+  if (lane == 0) wsum[wave] = prod;
+  __syncthreads();
+  if (wave != 0) return;
+  prod = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
 
   // Last-arriver finish of quant.py:91 .sum() (Guideline 16, write-through form, no
   // fences): the partial is stored sc1 (agent-scope relaxed atomic store = write-through),

@@ -101,10 +101,13 @@ __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
   const int n0 = ct * (16 * NT);
 
   // Decode this block's Q rows: one code word -> 16 bf16 (two 16-byte LDS stores).
-  for (int idx = threadIdx.x; idx < 16 * NT * kwp; idx += kThreads) {
+  // Consecutive threads take consecutive words of the block's (contiguous) code rows, and
+  // every word of the thread is loaded before any is decoded, so the prologue pays one
+  // L2 latency instead of one per word.
+  const int nwords = 16 * NT * kwp;
+  auto decode_store = [&](int idx, uint32_t word) {
     const int nl = idx / kwp, w = idx - nl * kwp;
-    const int n = n0 + nl;
-    const uint32_t word = (n < N && w < KW) ? codes[(int64_t)n * KW + w] : 0u;
+    word = (n0 + nl < N && w < KW && idx < nwords) ? word : 0u;
     u32x4 lo4, hi4;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -112,9 +115,29 @@ __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
       hi4[p] = code_bf16((word >> (4 * p + 16)) & 3u) |
                (code_bf16((word >> (4 * p + 18)) & 3u) << 16);
     }
-    u32x4* dst = reinterpret_cast<u32x4*>(bimg + nl * stride + 16 * w);
-    dst[0] = lo4;
-    dst[1] = hi4;
+    if (idx < nwords) {
+      u32x4* dst = reinterpret_cast<u32x4*>(bimg + nl * stride + 16 * w);
+      dst[0] = lo4;
+      dst[1] = hi4;
+    }
+  };
+  auto word_at = [&](int idx) -> uint32_t {
+    const int nl = idx / kwp, w = idx - nl * kwp;
+    int64_t n = n0 + nl;
+    n = n < N ? n : N - 1;
+    const int wc = w < KW ? w : KW - 1;
+    return codes[n * KW + wc];  // clamped, always valid; out-of-range words are zeroed above
+  };
+  if constexpr (NCH > 0) {
+    constexpr int kWpt = (16 * NT * 2 * NCH + kThreads - 1) / kThreads;
+    uint32_t wv[kWpt];
+#pragma unroll
+    for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThreads);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThreads, wv[i]);
+  } else {
+    for (int idx = threadIdx.x; idx < nwords; idx += kThreads) decode_store(idx, word_at(idx));
   }
   __syncthreads();
 
