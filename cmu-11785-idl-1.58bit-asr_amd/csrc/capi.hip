@@ -160,4 +160,33 @@ int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, i
   return launched();
 }
 
+int ob_dwconv1d_fwd(const float* x, const float* w, const float* bias, int64_t B, int64_t C,
+                    int64_t T, int64_t KT, float* y, void* stream) {
+  if (B < 0 || C < 0 || T < 0 || KT < 1 || KT % 2 == 0 || !dwconv_supported((int)KT))
+    return OB_ERR_SHAPE;
+  if (B * C * T > 0 && (!x || !y || !w)) return OB_ERR_NULL;
+  if (!aligned4(x) || !aligned4(y) || !aligned4(w) || !aligned4(bias)) return OB_ERR_ALIGN;
+  launch_dwconv_fwd(x, w, bias, B, C, T, KT, y, as_stream(stream));
+  return launched();
+}
+
+size_t ob_dwconv1d_bwd_workspace(int64_t B, int64_t C, int64_t KT) {
+  if (B < 0 || C < 0 || KT < 1) return 0;
+  return align_up(dwconv_bwd_workspace(B, C, KT));
+}
+
+int ob_dwconv1d_bwd(const float* x, const float* dy, const float* w, int64_t B, int64_t C,
+                    int64_t T, int64_t KT, float* dx, float* dw, float* db, void* ws,
+                    size_t ws_bytes, void* stream) {
+  if (B < 0 || C < 0 || T < 0 || KT < 1 || KT % 2 == 0 || !dwconv_supported((int)KT))
+    return OB_ERR_SHAPE;
+  if (!dw || !w || !ws || (B * C * T > 0 && (!x || !dy))) return OB_ERR_NULL;
+  if (!aligned4(x) || !aligned4(dy) || !aligned4(dx) || !aligned4(dw) || !aligned4(db))
+    return OB_ERR_ALIGN;
+  if (ws_bytes < ob_dwconv1d_bwd_workspace(B, C, KT)) return OB_ERR_WORKSPACE;
+  launch_dwconv_bwd(x, dy, w, B, C, T, KT, dx, dw, db, static_cast<float*>(ws),
+                    as_stream(stream));
+  return launched();
+}
+
 }  // extern "C"

@@ -44,4 +44,13 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
                        hipStream_t s);
 
+// dwconv.hip (depthwise Conv1d of the conv module, odd kernel width, 'same' padding)
+bool dwconv_supported(int KT);
+void launch_dwconv_fwd(const float* x, const float* w, const float* bias, int64_t B, int64_t C,
+                       int64_t T, int64_t KT, float* y, hipStream_t s);
+size_t dwconv_bwd_workspace(int64_t B, int64_t C, int64_t KT);
+void launch_dwconv_bwd(const float* x, const float* dy, const float* w, int64_t B, int64_t C,
+                       int64_t T, int64_t KT, float* dx, float* dw, float* db, float* part,
+                       hipStream_t s);
+
 }  // namespace ob

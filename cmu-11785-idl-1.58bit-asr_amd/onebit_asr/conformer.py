@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .conv import depthwise_conv1d
 from .quant import QuantizedLinear
 
 __all__ = [
@@ -181,7 +182,7 @@ class ConvModule(nn.Module):
 
     def forward(self, x, mask=None):
         h = self.glu(self.pw1(self.ln(x).transpose(1, 2)))
-        h = self.pw2(swish(self.bn(self.dw(h))))
+        h = self.pw2(swish(self.bn(depthwise_conv1d(h, self.dw))))
         h = self.dropout(h).transpose(1, 2)
         return x + _pad_rows(h, mask)
 

@@ -115,6 +115,20 @@ OB_API int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64
                                float* dW, float* dalpha, float* db, void* ws, size_t ws_bytes,
                                void* stream);
 
+/*
+ * Conv-module depthwise Conv1d (reference conformer.py:147
+ * nn.Conv1d(C, C, KT, padding=KT//2, groups=C), applied at conformer.py:157).
+ * x, y: [B][C][T]; w: [C][KT] (the Conv1d weight [C,1,KT]); bias [C] or NULL; KT odd, <= 64.
+ *   y[b,c,t] = bias[c] + sum_j w[c,j] * x[b,c,t+j-KT/2]   (zero padding)
+ * Backward: dx (may be NULL), dw [C][KT], db [C] (may be NULL); deterministic.
+ */
+OB_API int ob_dwconv1d_fwd(const float* x, const float* w, const float* bias, int64_t B,
+                           int64_t C, int64_t T, int64_t KT, float* y, void* stream);
+OB_API size_t ob_dwconv1d_bwd_workspace(int64_t B, int64_t C, int64_t KT);
+OB_API int ob_dwconv1d_bwd(const float* x, const float* dy, const float* w, int64_t B, int64_t C,
+                           int64_t T, int64_t KT, float* dx, float* dw, float* db, void* ws,
+                           size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
