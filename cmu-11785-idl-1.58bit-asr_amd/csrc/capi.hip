@@ -189,4 +189,36 @@ int ob_dwconv1d_bwd(const float* x, const float* dy, const float* w, int64_t B, 
   return launched();
 }
 
+size_t ob_ctc_loss_workspace(int64_t B, int64_t T, int64_t S) {
+  if (B < 0 || T < 0 || S < 0) return 0;
+  return align_up(ctc_workspace(B, T, S));
+}
+
+int ob_ctc_loss_fwd(const float* log_probs, const int64_t* targets, const int64_t* input_lengths,
+                    const int64_t* target_lengths, int64_t B, int64_t T, int64_t V, int64_t S,
+                    int blank, float* loss, void* ws, size_t ws_bytes, void* stream) {
+  if (B < 1 || T < 0 || V < 1 || S < 0 || blank < 0 || blank >= V || !ctc_supported(S))
+    return OB_ERR_SHAPE;
+  if (!log_probs || !input_lengths || !target_lengths || !loss || !ws || (S > 0 && !targets))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
+  launch_ctc_fwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, loss,
+                 static_cast<float*>(ws), as_stream(stream));
+  return launched();
+}
+
+int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets, const int64_t* input_lengths,
+                    const int64_t* target_lengths, int64_t B, int64_t T, int64_t V, int64_t S,
+                    int blank, const float* grad_out, float* grad, void* ws, size_t ws_bytes,
+                    void* stream) {
+  if (B < 1 || T < 0 || V < 1 || S < 0 || blank < 0 || blank >= V || !ctc_supported(S))
+    return OB_ERR_SHAPE;
+  if (!log_probs || !input_lengths || !target_lengths || !grad || !ws || (S > 0 && !targets))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
+  launch_ctc_bwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, grad_out,
+                 grad, static_cast<float*>(ws), as_stream(stream));
+  return launched();
+}
+
 }  // extern "C"

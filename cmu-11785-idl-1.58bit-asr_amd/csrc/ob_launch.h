@@ -53,4 +53,14 @@ void launch_dwconv_bwd(const float* x, const float* dy, const float* w, int64_t 
                        int64_t T, int64_t KT, float* dx, float* dw, float* db, float* part,
                        hipStream_t s);
 
+// ctc.hip (CTC loss with device-side lengths; log_probs [B][T][V])
+size_t ctc_workspace(int64_t B, int64_t T, int64_t S);
+bool ctc_supported(int64_t S);
+void launch_ctc_fwd(const float* lp, const int64_t* targets, const int64_t* in_len,
+                    const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                    float* loss, float* ws, hipStream_t s);
+void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_len,
+                    const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                    const float* grad_out, float* grad, float* ws, hipStream_t s);
+
 }  // namespace ob

@@ -47,6 +47,11 @@ SIGNATURES = {
     "ob_dwconv1d_bwd_workspace": (_sz, [_i64, _i64, _i64]),
     "ob_dwconv1d_bwd": (
         _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_ctc_loss_workspace": (_sz, [_i64, _i64, _i64]),
+    "ob_ctc_loss_fwd": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _sz, _c_f]),
+    "ob_ctc_loss_bwd": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _sz, _c_f]),
 }
 
 ABI_VERSION = 1

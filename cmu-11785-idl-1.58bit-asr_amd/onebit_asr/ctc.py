@@ -1,0 +1,54 @@
+"""CTC loss on the HIP kernel (reference losses.py:41-47 semantics), with device-side lengths.
+
+torch's CUDA CTC copies its length tensors to the host (a device->host sync per call), which
+also makes the step uncapturable in a HIP graph. ``ctc_loss_mean`` computes the same loss
+(blank, zero_infinity=True, reduction 'mean': per-sample nll / max(target_len, 1), then the
+batch mean) and torch's gradient, reading lengths on device. Inputs: log-probs [B, T, V]
+(batch-major), targets [B, S] int64 (padded), lengths int64 [B] on the same device.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+__all__ = ["ctc_loss_mean"]
+
+
+class _CTCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, log_probs, targets, input_lengths, target_lengths, blank):
+        b, t, v = log_probs.shape
+        s = targets.shape[1]
+        lp = log_probs.contiguous()
+        tg = targets.contiguous().to(torch.int64)
+        il = input_lengths.contiguous().to(torch.int64)
+        tl = target_lengths.contiguous().to(torch.int64)
+        lib = _lib.load()
+        wsb = lib.ob_ctc_loss_workspace(b, t, s)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=lp.device)
+        loss = torch.empty((), dtype=torch.float32, device=lp.device)
+        _lib.check(lib.ob_ctc_loss_fwd(lp.data_ptr(), tg.data_ptr(), il.data_ptr(), tl.data_ptr(),
+                                       b, t, v, s, blank, loss.data_ptr(), ws.data_ptr(), wsb,
+                                       _lib.stream_of(lp)), "ob_ctc_loss_fwd")
+        ctx.save_for_backward(lp, tg, il, tl, ws)
+        ctx.blank = blank
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        lp, tg, il, tl, ws = ctx.saved_tensors
+        b, t, v = lp.shape
+        s = tg.shape[1]
+        grad = torch.empty_like(lp)
+        gout = gout.contiguous().to(torch.float32)
+        lib = _lib.load()
+        _lib.check(lib.ob_ctc_loss_bwd(lp.data_ptr(), tg.data_ptr(), il.data_ptr(), tl.data_ptr(),
+                                       b, t, v, s, ctx.blank, gout.data_ptr(), grad.data_ptr(),
+                                       ws.data_ptr(), ws.numel(), _lib.stream_of(lp)),
+                   "ob_ctc_loss_bwd")
+        return grad, None, None, None, None
+
+
+def ctc_loss_mean(log_probs_btv, targets, input_lengths, target_lengths, blank: int):
+    return _CTCFn.apply(log_probs_btv, targets, input_lengths, target_lengths, blank)

@@ -129,6 +129,23 @@ OB_API int ob_dwconv1d_bwd(const float* x, const float* dy, const float* w, int6
                            int64_t T, int64_t KT, float* dx, float* dw, float* db, void* ws,
                            size_t ws_bytes, void* stream);
 
+/*
+ * CTC loss (reference losses.py:41-47: nn.CTCLoss(blank, zero_infinity=True), 'mean'),
+ * with the lengths read on device so a training step can be captured in a HIP graph.
+ * log_probs [B][T][V] (log_softmax output), targets [B][S] int64 padded, lengths int64 [B].
+ * fwd writes loss[0] and fills ws (alpha, per-sample nll); bwd needs the same ws and writes
+ * grad [B][T][V] with torch's CTC gradient formula, scaled by grad_out[0] (NULL -> 1).
+ */
+OB_API size_t ob_ctc_loss_workspace(int64_t B, int64_t T, int64_t S);
+OB_API int ob_ctc_loss_fwd(const float* log_probs, const int64_t* targets,
+                           const int64_t* input_lengths, const int64_t* target_lengths, int64_t B,
+                           int64_t T, int64_t V, int64_t S, int blank, float* loss, void* ws,
+                           size_t ws_bytes, void* stream);
+OB_API int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets,
+                           const int64_t* input_lengths, const int64_t* target_lengths, int64_t B,
+                           int64_t T, int64_t V, int64_t S, int blank, const float* grad_out,
+                           float* grad, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,49 @@
+"""GPU parity of the HIP CTC loss (device-side lengths) against torch's nn.CTCLoss on CPU
+(reference losses.py:41-47: blank 3, zero_infinity, 'mean'). Bars: loss rel <= 1e-5,
+logits-gradient (through log_softmax) max|err| <= 1e-5 * max|ref| + 1e-7; deterministic."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(B, T, V, in_lens, tg_lens, seed, repeat=False):
+    g = torch.Generator().manual_seed(seed)
+    logits = torch.randn(B, T, V, generator=g) * 2
+    S = max(max(tg_lens), 1)
+    tg = torch.zeros(B, S, dtype=torch.long)
+    for b, L in enumerate(tg_lens):
+        if L:
+            vals = torch.randint(4, V, (L,), generator=g)
+            if repeat:
+                vals[1::2] = vals[0::2][: len(vals[1::2])]  # adjacent repeats
+            tg[b, :L] = vals
+    return logits, tg, torch.tensor(in_lens), torch.tensor(tg_lens)
+
+
+@pytest.mark.parametrize("case", [
+    dict(B=2, T=50, V=30, in_lens=[50, 37], tg_lens=[10, 4], seed=0),
+    dict(B=3, T=40, V=20, in_lens=[40, 40, 30], tg_lens=[6, 8, 5], seed=1, repeat=True),
+    dict(B=2, T=12, V=10, in_lens=[12, 5], tg_lens=[4, 9], seed=2),           # sample 1 infeasible
+    dict(B=2, T=20, V=10, in_lens=[20, 20], tg_lens=[0, 3], seed=3),          # empty target
+    dict(B=4, T=249, V=5004, in_lens=[249, 249, 200, 100], tg_lens=[40, 27, 12, 40], seed=4),
+])
+def test_ctc_matches_torch(gpu, case):
+    from onebit_asr.ctc import ctc_loss_mean
+
+    logits, tg, il, tl = _case(**case)
+    lr = logits.clone().requires_grad_()
+    ref = torch.nn.CTCLoss(blank=3, zero_infinity=True)(
+        F.log_softmax(lr, -1).transpose(0, 1), tg, il, tl)
+    ref.backward()
+    lg = logits.to(gpu).requires_grad_()
+    out = ctc_loss_mean(F.log_softmax(lg, -1), tg.to(gpu), il.to(gpu), tl.to(gpu), 3)
+    out.backward()
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item()) + 1e-6, (out.item(), ref.item())
+    err = (lg.grad.cpu() - lr.grad).abs().max().item()
+    assert err <= 1e-5 * lr.grad.abs().max().item() + 1e-7, err
+    g1 = lg.grad.clone()
+    lg.grad = None
+    ctc_loss_mean(F.log_softmax(lg, -1), tg.to(gpu), il.to(gpu), tl.to(gpu), 3).backward()
+    assert torch.equal(g1, lg.grad)
