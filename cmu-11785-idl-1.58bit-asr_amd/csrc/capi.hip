@@ -61,7 +61,17 @@ int ob_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits, i
   if (N < 0 || K < 0) return OB_ERR_SHAPE;
   if (!alpha || (N * K > 0 && !W)) return OB_ERR_NULL;
   if (!aligned4(W) || !aligned4(codes) || !aligned4(codes_t)) return OB_ERR_ALIGN;
-  launch_quant_pack(W, alpha, alpha_raw, bits, N, K, codes, codes_t, as_stream(stream));
+  launch_quant_pack(W, alpha, alpha_raw, bits, nullptr, N, K, codes, codes_t, as_stream(stream));
+  return launched();
+}
+
+int ob_quant_pack_dyn(const float* W, const float* alpha, int alpha_raw, const int32_t* bits_dev,
+                      int64_t N, int64_t K, uint32_t* codes, uint32_t* codes_t, void* stream) {
+  if (N < 0 || K < 0) return OB_ERR_SHAPE;
+  if (!alpha || !bits_dev || (N * K > 0 && !W)) return OB_ERR_NULL;
+  if (!aligned4(W) || !aligned4(codes) || !aligned4(codes_t) || !aligned4(bits_dev))
+    return OB_ERR_ALIGN;
+  launch_quant_pack(W, alpha, alpha_raw, 2, bits_dev, N, K, codes, codes_t, as_stream(stream));
   return launched();
 }
 
@@ -93,8 +103,8 @@ int ob_quant_ste_bwd(const float* grad_W_hat, const float* W, const float* alpha
   float* apart = reinterpret_cast<float*>(static_cast<char*>(ws) + 16);
   if (hipMemsetAsync(ticket, 0, sizeof(uint32_t), as_stream(stream)) != hipSuccess)
     return OB_ERR_HIP;
-  launch_ste_reduce(grad_W_hat, 1, n, nullptr, 0, W, alpha, alpha_raw, bits, grad_W, nullptr,
-                    apart, ticket, grad_alpha, as_stream(stream));
+  launch_ste_reduce(grad_W_hat, 1, n, nullptr, 0, W, alpha, alpha_raw, bits, nullptr, grad_W,
+                    nullptr, apart, ticket, grad_alpha, as_stream(stream));
   return launched();
 }
 
@@ -125,14 +135,16 @@ size_t ob_bitlinear_bwd_dw_workspace(int64_t M, int64_t N, int64_t K) {
   return dw_layout(M, N, K).total;
 }
 
-int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
-                        const float* W, const float* alpha, int alpha_raw, int bits, float* dW,
-                        float* dalpha, float* db, void* ws, size_t ws_bytes, void* stream) {
-  if (int st = check_bits(bits)) return st;
+namespace {
+
+int bwd_dw_impl(const float* dY, const float* X, int64_t M, int64_t N, int64_t K, const float* W,
+                const float* alpha, int alpha_raw, int bits, const int32_t* bits_dev, float* dW,
+                float* dalpha, float* db, void* ws, size_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0) return OB_ERR_SHAPE;
   if (!alpha || !dalpha || !ws || (N * K > 0 && (!W || !dW)) || (M > 0 && (!dY || (K > 0 && !X))))
     return OB_ERR_NULL;
-  if (!aligned4(dY) || !aligned4(X) || !aligned4(dW) || !aligned4(db)) return OB_ERR_ALIGN;
+  if (!aligned4(dY) || !aligned4(X) || !aligned4(dW) || !aligned4(db) || !aligned4(bits_dev))
+    return OB_ERR_ALIGN;
   const DwWorkspace L = dw_layout(M, N, K);
   if (ws_bytes < L.total) return OB_ERR_WORKSPACE;
   const DwPlan p = plan_dw(M, N, K);
@@ -155,9 +167,28 @@ int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, i
   } else {
     launch_dw_partial(dY, X, M, N, K, p, part, part_db, ticket, s);
   }
-  launch_ste_reduce(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, bits, dW, db,
-                    apart, ticket, dalpha, s);
+  launch_ste_reduce(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, bits,
+                    reinterpret_cast<const int*>(bits_dev), dW, db, apart, ticket, dalpha, s);
   return launched();
+}
+
+}  // namespace
+
+int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                        const float* W, const float* alpha, int alpha_raw, int bits, float* dW,
+                        float* dalpha, float* db, void* ws, size_t ws_bytes, void* stream) {
+  if (int st = check_bits(bits)) return st;
+  return bwd_dw_impl(dY, X, M, N, K, W, alpha, alpha_raw, bits, nullptr, dW, dalpha, db, ws,
+                     ws_bytes, stream);
+}
+
+int ob_bitlinear_bwd_dw_dyn(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                            const float* W, const float* alpha, int alpha_raw,
+                            const int32_t* bits_dev, float* dW, float* dalpha, float* db, void* ws,
+                            size_t ws_bytes, void* stream) {
+  if (!bits_dev) return OB_ERR_NULL;
+  return bwd_dw_impl(dY, X, M, N, K, W, alpha, alpha_raw, 2, bits_dev, dW, dalpha, db, ws,
+                     ws_bytes, stream);
 }
 
 int ob_dwconv1d_fwd(const float* x, const float* w, const float* bias, int64_t B, int64_t C,

@@ -11,8 +11,10 @@ namespace ob {
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // quant.hip
-void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits, int64_t N,
-                       int64_t K, uint32_t* codes, uint32_t* codes_t, hipStream_t s);
+// bits_dev (may be NULL): when set, the bitwidth is read on device (graph mode).
+void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits,
+                       const int* bits_dev, int64_t N, int64_t K, uint32_t* codes,
+                       uint32_t* codes_t, hipStream_t s);
 void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
                           float* W_hat, hipStream_t s);
 
@@ -24,8 +26,8 @@ void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int
 int64_t ste_reduce_blocks(int64_t total);
 void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* part_db,
                        int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,
-                       float* dW, float* db, float* apart, uint32_t* ticket, float* dalpha,
-                       hipStream_t s);
+                       const int* bits_dev, float* dW, float* db, float* apart, uint32_t* ticket,
+                       float* dalpha, hipStream_t s);
 
 // gemm.hip
 // C[M][N] = a * (A[M][K] . Q^T) + bias, Q given as 2-bit codes [N][ceil(K/16)].

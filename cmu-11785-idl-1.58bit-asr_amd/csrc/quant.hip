@@ -29,8 +29,9 @@ __device__ __forceinline__ uint32_t or16(uint32_t v) {
 
 __global__ __launch_bounds__(kThreads) void quant_pack_kernel(
     const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw, int bits,
-    int64_t N, int64_t K, int64_t KW, int64_t NW, uint32_t* __restrict__ codes,
-    uint32_t* __restrict__ codes_t) {
+    const int* __restrict__ bits_dev, int64_t N, int64_t K, int64_t KW, int64_t NW,
+    uint32_t* __restrict__ codes, uint32_t* __restrict__ codes_t) {
+  if (bits_dev) bits = *bits_dev;  // graph mode: per-call bitwidth read on device
   const float a = effective_alpha(alpha, alpha_raw);
   const int64_t t = blockIdx.x * (int64_t)kThreads + threadIdx.x;
   const int j = threadIdx.x & 15;
@@ -80,8 +81,9 @@ constexpr int kReduceElems = kThreads * kReduceEPT;
 __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
     const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
     int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
-    int bits, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ apart,
-    uint32_t* __restrict__ ticket, float* __restrict__ dalpha) {
+    int bits, const int* __restrict__ bits_dev, float* __restrict__ dW, float* __restrict__ db,
+    float* __restrict__ apart, uint32_t* __restrict__ ticket, float* __restrict__ dalpha) {
+  if (bits_dev) bits = *bits_dev;  // graph mode: per-call bitwidth read on device
   __shared__ float wsum[kThreads / 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -154,14 +156,15 @@ __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
 
 }  // namespace
 
-void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits, int64_t N,
-                       int64_t K, uint32_t* codes, uint32_t* codes_t, hipStream_t s) {
+void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits,
+                       const int* bits_dev, int64_t N, int64_t K, uint32_t* codes,
+                       uint32_t* codes_t, hipStream_t s) {
   const int64_t KW = ceil_div(K, 16), NW = ceil_div(N, 16);
   const int64_t total = 16 * ((codes ? N * KW : 0) + (codes_t ? K * NW : 0));
   if (total == 0) return;
   const int64_t blocks = ceil_div(total, kThreads);
   hipLaunchKernelGGL(quant_pack_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, W, alpha,
-                     alpha_raw, bits, N, K, KW, NW, codes, codes_t);
+                     alpha_raw, bits, bits_dev, N, K, KW, NW, codes, codes_t);
 }
 
 void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
@@ -177,12 +180,13 @@ int64_t ste_reduce_blocks(int64_t total) { return ceil_div(total, kReduceElems);
 
 void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* part_db,
                        int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,
-                       float* dW, float* db, float* apart, uint32_t* ticket, float* dalpha,
-                       hipStream_t s) {
+                       const int* bits_dev, float* dW, float* db, float* apart, uint32_t* ticket,
+                       float* dalpha, hipStream_t s) {
   int64_t nb = ste_reduce_blocks(nk + n_db);
   if (nb == 0) nb = 1;  // an empty tensor still writes dalpha = 0
   hipLaunchKernelGGL(ste_reduce_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, chunks,
-                     nk, part_db, n_db, W, alpha, alpha_raw, bits, dW, db, apart, ticket, dalpha);
+                     nk, part_db, n_db, W, alpha, alpha_raw, bits, bits_dev, dW, db, apart, ticket,
+                     dalpha);
 }
 
 }  // namespace ob

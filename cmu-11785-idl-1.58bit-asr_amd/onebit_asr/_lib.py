@@ -43,6 +43,11 @@ SIGNATURES = {
         _int,
         [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _int, _int, _c_f, _c_f, _c_f, _c_f, _sz, _c_f],
     ),
+    "ob_quant_pack_dyn": (_int, [_c_f, _c_f, _int, _c_f, _i64, _i64, _c_f, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dw_dyn": (
+        _int,
+        [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f],
+    ),
     "ob_dwconv1d_fwd": (_int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f]),
     "ob_dwconv1d_bwd_workspace": (_sz, [_i64, _i64, _i64]),
     "ob_dwconv1d_bwd": (

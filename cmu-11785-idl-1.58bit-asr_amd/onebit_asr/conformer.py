@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .conv import depthwise_conv1d
-from .quant import QuantizedLinear
+from .quant import DeviceBits, QuantizedLinear
 
 __all__ = [
     "LayerNorm", "FeedForwardModule", "RelPositionalEncoding", "MHSA", "ConvModule",
@@ -241,6 +241,8 @@ class ConformerBlock(nn.Module):
 def block_bitwidths(n_layers: int, precision: int, sp_mask: Optional[Sequence[int]]) -> List[int]:
     """Per-block BitLinear bitwidth (conformer.py:265-269): ``precision`` everywhere, or with
     an SP mask 1 where sp_mask[i] == 1 else 2; anything outside {1, 2} runs at 32."""
+    if isinstance(sp_mask, DeviceBits):  # graph mode: per-block bitwidths read on device
+        return [sp_mask[i] for i in range(n_layers)]
     out = []
     for i in range(n_layers):
         bw = precision if sp_mask is None else (1 if sp_mask[i] == 1 else 2)
@@ -292,9 +294,12 @@ class TransformerDecoder(nn.Module):
         tt = tgt_inp.size(1)
         future = torch.ones(tt, tt, device=tgt_inp.device).triu(diagonal=1).bool()
         causal = torch.zeros(tt, tt, device=tgt_inp.device).masked_fill(future, float("-inf"))
+        # tgt_is_causal=True is what torch's _detect_is_causal_mask concludes for this mask in
+        # the reference call; passing it skips that check's device->host sync (the
+        # attention math is unchanged: the explicit mask is still used).
         y = self.dec(self.emb(tgt_inp), memory, tgt_mask=causal,
                      memory_key_padding_mask=(memory_mask == 0),
-                     tgt_key_padding_mask=tgt_key_padding_mask)
+                     tgt_key_padding_mask=tgt_key_padding_mask, tgt_is_causal=True)
         return self.out(self.ln(y))
 
 

@@ -33,12 +33,53 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes"]
+__all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "DeviceBits",
+           "DynamicBitwidth"]
 
 _VALID = (1, 2, 32)
 
 
-def _check_bitwidth(bitwidth: int) -> int:
+class DynamicBitwidth:
+    """A BitLinear bitwidth (1 or 2) that lives on the device: slot `index` of an int32
+    tensor. Used for the stochastic-precision pass under HIP-graph capture, where the
+    per-block bitwidths change every step but the captured graph must not
+    (reference train.py:102-103, conformer.py:265-269)."""
+
+    __slots__ = ("tensor", "index")
+
+    def __init__(self, tensor: torch.Tensor, index: int):
+        self.tensor = tensor
+        self.index = index
+
+    def ptr(self) -> int:
+        return self.tensor.data_ptr() + 4 * self.index
+
+
+class DeviceBits:
+    """Per-block SP bitwidths on device. ``set(sp_mask)`` stages a new mask (1 -> 1-bit,
+    else 2-bit, as conformer.py:268) with an async H2D copy; ``[i]`` is block i's
+    DynamicBitwidth. It stands in for the reference's ``sp_mask`` list."""
+
+    def __init__(self, n_layers: int, device):
+        self.n_layers = n_layers
+        self.tensor = torch.full((n_layers,), 2, dtype=torch.int32, device=device)
+
+    def set(self, sp_mask) -> None:
+        host = torch.tensor([1 if m == 1 else 2 for m in sp_mask], dtype=torch.int32)
+        if self.tensor.is_cuda:
+            host = host.pin_memory()
+        self.tensor.copy_(host, non_blocking=True)
+
+    def __getitem__(self, i: int) -> DynamicBitwidth:
+        return DynamicBitwidth(self.tensor, i)
+
+    def __len__(self) -> int:
+        return self.n_layers
+
+
+def _check_bitwidth(bitwidth) -> int:
+    if isinstance(bitwidth, DynamicBitwidth):
+        return 0
     if bitwidth not in _VALID:
         raise ValueError("bitwidth must be one of {1,2,32}")
     return int(bitwidth)
@@ -55,20 +96,23 @@ def _require_device(*tensors: torch.Tensor) -> None:
             raise TypeError(f"BitLinear parity path computes in fp32, got {t.dtype}")
 
 
-def pack_codes(weight: torch.Tensor, alpha: torch.Tensor, bits: int, alpha_raw: bool = True):
+def pack_codes(weight: torch.Tensor, alpha: torch.Tensor, bits, alpha_raw: bool = True):
     """2-bit codes of Q(W / a): ``codes [N, ceil(K/16)]`` and ``codes_t [K, ceil(N/16)]``
-    (int32 views of the uint32 words described in include/onebit_hip.h)."""
+    (int32 views of the uint32 words described in include/onebit_hip.h). ``bits`` is 1, 2 or
+    a DynamicBitwidth (read on device)."""
     _require_device(weight, alpha)
     n, k = weight.shape
     w = weight.detach().contiguous()
     codes = torch.empty((n, (k + 15) // 16), dtype=torch.int32, device=w.device)
     codes_t = torch.empty((k, (n + 15) // 16), dtype=torch.int32, device=w.device)
     lib = _lib.load()
-    _lib.check(
-        lib.ob_quant_pack(w.data_ptr(), alpha.data_ptr(), int(alpha_raw), bits, n, k,
-                          codes.data_ptr(), codes_t.data_ptr(), _lib.stream_of(w)),
-        "ob_quant_pack",
-    )
+    if isinstance(bits, DynamicBitwidth):
+        st = lib.ob_quant_pack_dyn(w.data_ptr(), alpha.data_ptr(), int(alpha_raw), bits.ptr(), n, k,
+                                   codes.data_ptr(), codes_t.data_ptr(), _lib.stream_of(w))
+    else:
+        st = lib.ob_quant_pack(w.data_ptr(), alpha.data_ptr(), int(alpha_raw), bits, n, k,
+                               codes.data_ptr(), codes_t.data_ptr(), _lib.stream_of(w))
+    _lib.check(st, "ob_quant_pack")
     return codes, codes_t
 
 
@@ -113,13 +157,17 @@ class _BitLinearFn(torch.autograd.Function):
             gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
             ws_bytes = lib.ob_bitlinear_bwd_dw_workspace(m, n, k)
             ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
-            _lib.check(
-                lib.ob_bitlinear_bwd_dw(gy.data_ptr(), x2d.data_ptr(), m, n, k,
-                                        weight.data_ptr(), alpha.data_ptr(), 1, ctx.bits,
-                                        gw.data_ptr(), galpha.data_ptr(), _lib.ptr(gb),
-                                        ws.data_ptr(), ws_bytes, stream),
-                "ob_bitlinear_bwd_dw",
-            )
+            if isinstance(ctx.bits, DynamicBitwidth):
+                st = lib.ob_bitlinear_bwd_dw_dyn(gy.data_ptr(), x2d.data_ptr(), m, n, k,
+                                                 weight.data_ptr(), alpha.data_ptr(), 1,
+                                                 ctx.bits.ptr(), gw.data_ptr(), galpha.data_ptr(),
+                                                 _lib.ptr(gb), ws.data_ptr(), ws_bytes, stream)
+            else:
+                st = lib.ob_bitlinear_bwd_dw(gy.data_ptr(), x2d.data_ptr(), m, n, k,
+                                             weight.data_ptr(), alpha.data_ptr(), 1, ctx.bits,
+                                             gw.data_ptr(), galpha.data_ptr(), _lib.ptr(gb),
+                                             ws.data_ptr(), ws_bytes, stream)
+            _lib.check(st, "ob_bitlinear_bwd_dw")
             if not ctx.needs_input_grad[1]:
                 gw = None
             if not ctx.needs_input_grad[2]:
@@ -211,16 +259,20 @@ class QuantizedLinear(nn.Module):
         return codes, codes_t
 
     def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
-        bitwidth = _check_bitwidth(bitwidth)
-        if bitwidth == 32:  # quant.py:121-122
+        bits = _check_bitwidth(bitwidth)
+        if bits == 32:  # quant.py:121-122
             return F.linear(x, self.weight, self.bias)
         _require_device(x, self.weight)
         lead = x.shape[:-1]
         x2d = x.reshape(-1, self.in_features)
         if not x2d.is_contiguous():
             x2d = x2d.contiguous()
-        codes, codes_t = self._codes(bitwidth)
-        y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bitwidth, codes, codes_t)
+        if bits == 0:  # DynamicBitwidth: codes depend on a device value, never cached
+            codes, codes_t = pack_codes(self.weight, self.alpha, bitwidth, alpha_raw=True)
+            bits = bitwidth
+        else:
+            codes, codes_t = self._codes(bits)
+        y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bits, codes, codes_t)
         return y.view(*lead, self.out_features)
 
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate cached codes

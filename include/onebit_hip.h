@@ -116,6 +116,20 @@ OB_API int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64
                                void* stream);
 
 /*
+ * Graph-mode variants: the bitwidth is read on device from *bits_dev (int32, 1 or 2) when
+ * the kernel runs, so one captured HIP graph serves the stochastic-precision pass whose
+ * per-block bitwidths change every step (reference train.py:102-103, conformer.py:265-269).
+ * Same semantics as ob_quant_pack / ob_bitlinear_bwd_dw otherwise.
+ */
+OB_API int ob_quant_pack_dyn(const float* W, const float* alpha, int alpha_raw,
+                             const int32_t* bits_dev, int64_t N, int64_t K, uint32_t* codes,
+                             uint32_t* codes_t, void* stream);
+OB_API int ob_bitlinear_bwd_dw_dyn(const float* dY, const float* X, int64_t M, int64_t N,
+                                   int64_t K, const float* W, const float* alpha, int alpha_raw,
+                                   const int32_t* bits_dev, float* dW, float* dalpha, float* db,
+                                   void* ws, size_t ws_bytes, void* stream);
+
+/*
  * Conv-module depthwise Conv1d (reference conformer.py:147
  * nn.Conv1d(C, C, KT, padding=KT//2, groups=C), applied at conformer.py:157).
  * x, y: [B][C][T]; w: [C][KT] (the Conv1d weight [C,1,KT]); bias [C] or NULL; KT odd, <= 64.
