@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--tokens", type=int, default=40)
+    ap.add_argument("--eager", action="store_true",
+                    help="run the step eagerly (DDP for N>1) instead of the captured HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -239,24 +241,39 @@ def main():
     from onebit_asr.data import CONFORMER_S, synthetic_batch
     from onebit_asr.train_step import OneBitStep, WarmupCosine, make_optimizer, sample_sp_mask, train_step
 
-    torch.manual_seed(1234)  # identical init on every rank (DDP also broadcasts)
+    torch.manual_seed(1234)  # identical init on every rank (DDP / the graph path broadcast)
     model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S).to(dev)
-    step_mod = OneBitStep(model, n_layers=CONFORMER_S["enc_layers"])
-    if distributed:
-        from torch.nn.parallel import DistributedDataParallel as DDP
-
-        step_mod = DDP(step_mod, device_ids=[local], broadcast_buffers=False,
-                       gradient_as_bucket_view=True)
-    opt = make_optimizer(model.parameters())
-    sched = WarmupCosine(opt, warmup_steps=4000, total_steps=100000)
+    n_layers = CONFORMER_S["enc_layers"]
+    step_mod = OneBitStep(model, n_layers=n_layers)
     batch = synthetic_batch([args.frames] * args.batch, [args.tokens] * args.batch,
                             seed=1234 + rank, device=dev)
     sp_gen = torch.Generator().manual_seed(4321)  # same SP masks on every rank
+    if distributed:
+        for p in model.parameters():  # replicas start identical (DDP does the same)
+            dist.broadcast(p.data, 0)
 
-    def step():
-        return train_step(step_mod, opt, sched, batch, sample_sp_mask(CONFORMER_S["enc_layers"], generator=sp_gen))
+    if args.eager:
+        if distributed:
+            from torch.nn.parallel import DistributedDataParallel as DDP
 
-    for _ in range(args.warmup):
+            step_mod = DDP(step_mod, device_ids=[local], broadcast_buffers=False,
+                           gradient_as_bucket_view=True)
+        opt = make_optimizer(model.parameters())
+        sched = WarmupCosine(opt, warmup_steps=4000, total_steps=100000)
+
+        def step():
+            return train_step(step_mod, opt, sched, batch, sample_sp_mask(n_layers, generator=sp_gen))
+    else:
+        from onebit_asr.graph_step import GraphedTrainStep
+
+        gs = GraphedTrainStep(step_mod, n_layers, warmup_steps=4000, total_steps=100000,
+                              process_group=dist.group.WORLD if distributed else None,
+                              warmup_iters=2)
+
+        def step():
+            return gs.step(batch, sample_sp_mask(n_layers, generator=sp_gen))
+
+    for _ in range(max(args.warmup, 1)):  # graph mode: the first call captures
         loss, _ = step()
     torch.cuda.synchronize()
     if distributed:
@@ -292,6 +309,7 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (N(0,1) 80-mel x 1000-frame padded batches, random-init weights)",
         "config": {"workload": "conformer-s-1.58bit-train-step", "global_batch": args.batch * world,
+                   "execution": "eager" if args.eager else "hip-graph",
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
                    "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
                    "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP"},

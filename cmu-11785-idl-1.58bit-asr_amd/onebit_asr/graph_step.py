@@ -1,0 +1,185 @@
+"""The training step (reference onebit_asr/train.py:82-120) captured as HIP graphs.
+
+An eager step of the 3-pass Conformer-S body issues ~4000 kernel launches from Python;
+at B=32 x 1000 frames the GPU work is short enough that host launch overhead is a large
+part of the step. Once nothing in the step synchronises with the host (bitwidths as Python
+ints or device values, the HIP CTC with device-side lengths, the decoder's causal hint,
+AdamW with a device lr) the whole body is captured once and replayed:
+
+* graph A: zero the flat gradient buffer, the three passes, their losses, backward;
+* [N > 1: one all-reduce (SUM) of the flat gradient buffer over RCCL, outside the graph;]
+* graph B (merged into A when N == 1): average over ranks, clip_grad_norm_(5.0), AdamW.
+
+What changes per step without re-capture:
+* the stochastic-precision mask: ``DeviceBits.set`` copies the new per-block bitwidths
+  into the device slots the captured BitLinear kernels read (quant.py DynamicBitwidth);
+* the learning rate: ``WarmupCosine`` fills the device lr tensor AdamW reads
+  (capturable=True);
+* the batch: copied into the captured input tensors (same shapes; a different padded
+  shape needs another ``GraphedTrainStep``);
+* dropout masks: torch's philox offsets advance per replay.
+
+Gradients live in one flat fp32 buffer (parameter order) so the N > 1 exchange is a
+single large all-reduce -- the bucket size xGMI ring all-reduce wants -- with no
+flatten/unflatten copies. Parameters that receive no gradient in the step are excluded
+from the optimizer exactly like the reference (AdamW skips grad=None).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .quant import DeviceBits, QuantizedLinear
+from .train_step import WarmupCosine
+
+__all__ = ["GraphedTrainStep"]
+
+
+class GraphedTrainStep:
+    def __init__(self, step_module, n_layers: int, lr: float = 5e-4, warmup_steps: int = 4000,
+                 total_steps: int = 100000, max_norm: float = 5.0,
+                 process_group: Optional[dist.ProcessGroup] = None, warmup_iters: int = 2,
+                 use_graph: bool = True):
+        self.step_module = step_module
+        self.n_layers = n_layers
+        self.lr0 = lr
+        self.warmup_steps = warmup_steps
+        self.total_steps = total_steps
+        self.max_norm = max_norm
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if process_group is not None else 1
+        self.warmup_iters = warmup_iters
+        self.use_graph = use_graph
+        self.device = next(step_module.parameters()).device
+        self.bits = DeviceBits(n_layers, self.device)
+        self.batch: Optional[Dict[str, torch.Tensor]] = None
+        self.params: List[torch.nn.Parameter] = []
+        self.flat: Optional[torch.Tensor] = None
+        self.opt = None
+        self.sched = None
+        self.graph_a = self.graph_b = None
+        self.loss = self.parts = None
+        self.steps_done = 0
+
+    # ------------------------------------------------------------------ setup
+    def _set_batch(self, batch):
+        if self.batch is None:
+            self.batch = {k: v.clone() for k, v in batch.items()}
+            return
+        for k, v in batch.items():
+            dst = self.batch[k]
+            if dst.shape != v.shape:
+                raise ValueError(f"batch[{k!r}] shape {tuple(v.shape)} != captured {tuple(dst.shape)}")
+            if dst.data_ptr() != v.data_ptr():
+                dst.copy_(v, non_blocking=True)
+
+    def _discover_params(self):
+        """One forward+backward (no update) to find the parameters the step differentiates."""
+        for p in self.step_module.parameters():
+            p.grad = None
+        loss, _ = self.step_module(self.batch, self.bits)
+        loss.backward()
+        self.params = [p for p in self.step_module.parameters() if p.grad is not None]
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
+        off = 0
+        for p in self.step_module.parameters():
+            p.grad = None
+        for p in self.params:
+            n = p.numel()
+            p.grad = self.flat[off:off + n].view_as(p)
+            off += n
+        cap = self.device.type == "cuda"
+        lr = torch.tensor(self.lr0, dtype=torch.float32, device=self.device) if cap else self.lr0
+        self.opt = torch.optim.AdamW(self.params, lr=lr, betas=(0.9, 0.98), weight_decay=1e-2,
+                                     capturable=cap, foreach=True)
+        self.sched = WarmupCosine(self.opt, self.warmup_steps, self.total_steps)
+
+    def _fwd_bwd(self):
+        self.flat.zero_()
+        loss, parts = self.step_module(self.batch, self.bits)
+        loss.backward()
+        return loss.detach(), parts
+
+    def _update(self):
+        if self.world > 1:
+            self.flat.div_(self.world)
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, foreach=True)
+        self.opt.step()
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat, group=self.pg)
+
+    def _eager(self):
+        loss, parts = self._fwd_bwd()
+        self._allreduce()
+        self._update()
+        return loss, parts
+
+    def _warm(self):
+        for _ in range(self.warmup_iters):
+            self.loss, self.parts = self._eager()
+            self.sched.step()
+            self.steps_done += 1
+
+    @staticmethod
+    def _drop_code_caches(module):
+        for m in module.modules():
+            if isinstance(m, QuantizedLinear):
+                m._codes_cache = {}
+
+    def prime(self, batch, sp_mask):
+        """Static inputs, flat grads, optimizer; ``warmup_iters`` real (eager) steps on a side
+        stream; then capture. The warm-up steps are training steps: they update the model
+        and advance the schedule like any other step."""
+        self._set_batch(batch)
+        self.bits.set(sp_mask)
+        if self.device.type != "cuda":  # host path (gloo tests of the exchange logic)
+            self.use_graph = False
+            self._discover_params()
+            self._warm()
+            return
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self._discover_params()
+            self._warm()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        if not self.use_graph:
+            return
+        torch.cuda.synchronize(self.device)
+        self._drop_code_caches(self.step_module)
+        self.graph_a = torch.cuda.CUDAGraph()
+        pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(self.graph_a, pool=pool):
+            self.loss, self.parts = self._fwd_bwd()
+            if self.world == 1:
+                self._update()
+        if self.world > 1:
+            self.graph_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_b, pool=pool):
+                self._update()
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ step
+    def step(self, batch, sp_mask):
+        """One training step (train.py:82-120). Returns device (loss, parts); no host sync.
+        The first call primes and captures (and runs ``warmup_iters`` steps)."""
+        if self.opt is None:
+            self.prime(batch, sp_mask)
+            return self.loss, self.parts
+        self._set_batch(batch)
+        self.bits.set(sp_mask)
+        if self.graph_a is None:
+            self.loss, self.parts = self._eager()
+        else:
+            self.graph_a.replay()
+            if self.world > 1:
+                self._allreduce()
+                self.graph_b.replay()
+        self.sched.step()
+        self.steps_done += 1
+        return self.loss, self.parts

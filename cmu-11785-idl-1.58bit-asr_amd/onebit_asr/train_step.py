@@ -47,7 +47,8 @@ class WarmupCosine:
         self.min_lr_ratio = min_lr_ratio
         self.step_num = 0
         for group in optimizer.param_groups:
-            group.setdefault("initial_lr", group.get("lr", 1e-3))
+            if "initial_lr" not in group:
+                group["initial_lr"] = float(group.get("lr", 1e-3))
 
     def scale(self, step: int) -> float:
         if step < self.warmup_steps:
@@ -60,7 +61,10 @@ class WarmupCosine:
         self.step_num += 1
         s = self.scale(self.step_num)
         for group in self.optimizer.param_groups:
-            group["lr"] = group["initial_lr"] * s
+            if isinstance(group["lr"], torch.Tensor):  # capturable AdamW: lr read on device
+                group["lr"].fill_(group["initial_lr"] * s)
+            else:
+                group["lr"] = group["initial_lr"] * s
 
 
 def make_optimizer(params, lr: float = 5e-4) -> torch.optim.Optimizer:
@@ -93,7 +97,8 @@ class OneBitStep(nn.Module):
         l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
         return logits, l_int, l_ctc
 
-    def forward(self, batch: Dict[str, torch.Tensor], sp_mask: List[int]):
+    def forward(self, batch: Dict[str, torch.Tensor], sp_mask):
+        """``sp_mask``: the reference's per-block list, or a ``DeviceBits`` (graph mode)."""
         sp = self.special
         t_inp, t_out, t_pad = make_att_targets(batch["tokens"], sp["bos_id"], sp["eos_id"], sp["pad_id"])
         logits2, lint2, lctc2 = self._pass(batch, t_inp, t_out, t_pad, 2)          # teacher

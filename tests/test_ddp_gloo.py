@@ -95,3 +95,81 @@ def test_ddp_two_ranks_gloo(tmp_path):
             assert err <= 1e-5 * scale + 1e-6, (k, err, scale)  # dw.bias grad is ~0 (BN follows)
     for k in res[0]["params"]:
         assert torch.equal(res[0]["params"][k], res[1]["params"][k]), k
+
+
+class _HostBitsStep(torch.nn.Module):
+    """OneBitStep over the CPU oracle, reading the DeviceBits slots back as the reference's
+    per-block list (the oracle has no device-bits path)."""
+
+    def __init__(self, model):
+        super().__init__()
+        from onebit_asr.train_step import OneBitStep
+
+        self.inner = OneBitStep(model, n_layers=2)
+
+    def forward(self, batch, bits):
+        return self.inner(batch, [1 if v == 1 else 0 for v in bits.tensor.tolist()])
+
+
+def _graph_step_worker(rank, world, port, out_dir):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "cmu-11785-idl-1.58bit-asr_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from onebit_asr.graph_step import GraphedTrainStep
+
+    model = _model()
+    gs = GraphedTrainStep(_HostBitsStep(model), n_layers=2, process_group=dist.group.WORLD,
+                          warmup_iters=1, warmup_steps=4, total_steps=10)
+    losses = []
+    for mask in ([1, 0], [0, 1], [1, 1]):
+        loss, _ = gs.step(_batch(rank), mask)
+        losses.append(loss.item())
+    params = {k: p.detach().clone() for k, p in model.named_parameters()}
+    torch.save({"params": params, "losses": losses}, os.path.join(out_dir, f"g{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_graph_step_flat_allreduce_gloo(tmp_path):
+    """GraphedTrainStep's N>1 exchange (flat-buffer SUM all-reduce, /world, clip, AdamW,
+    warmup-cosine) equals single-process training on the mean of the shard gradients."""
+    from onebit_asr.train_step import OneBitStep, WarmupCosine, make_optimizer
+
+    world = 2
+    mp.spawn(_graph_step_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(world)]
+    model = _model()
+    step = OneBitStep(model, n_layers=2)
+    opt = make_optimizer(model.parameters())
+    sched = WarmupCosine(opt, 4, 10)
+    for mask in ([1, 0], [0, 1], [1, 1]):
+        shard = []
+        for r in range(world):
+            model.zero_grad(set_to_none=True)
+            loss, _ = step(_batch(r), mask)
+            loss.backward()
+            shard.append({k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+        for k, p in model.named_parameters():
+            p.grad = (shard[0][k] + shard[1][k]) / 2 if k in shard[0] else None
+        torch.nn.utils.clip_grad_norm_([p for p in model.parameters() if p.grad is not None], 5.0)
+        opt.step()
+        sched.step()
+    # k_proj.bias (softmax shift; also inside the decoder in_proj_bias) and the depthwise-conv bias (BatchNorm follows) have a
+    # mathematically zero gradient: Adam turns its rounding noise into +-lr steps, so those
+    # two only get a bound of the summed learning rates.
+    noise_only = ("k_proj__bias", "dw__bias", "in_proj_bias")  # in_proj_bias holds the k bias
+    for k, p in model.named_parameters():
+        for r in range(world):
+            err = (res[r]["params"][k] - p.detach()).abs().max().item()
+            if any(n in k for n in noise_only):
+                assert err <= 1e-3, (k, r, err)
+            else:
+                assert err <= 1e-5 * p.detach().abs().max().item() + 1e-7, (k, r, err)
+    for k in res[0]["params"]:
+        assert torch.equal(res[0]["params"][k], res[1]["params"][k]), k
