@@ -252,4 +252,31 @@ int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets, const int64_
   return launched();
 }
 
+int64_t ob_adamw_plan(const int64_t* numels, int64_t n_tensors, int64_t* chunk_map) {
+  if (!numels || n_tensors < 1) return OB_ERR_SHAPE;
+  for (int64_t t = 0; t < n_tensors; ++t)
+    if (numels[t] < 1) return OB_ERR_SHAPE;
+  return adamw_plan(numels, n_tensors, chunk_map);
+}
+
+size_t ob_adamw_workspace(int64_t n_blocks) {
+  if (n_blocks < 1) return 0;
+  return align_up(adamw_workspace(n_blocks));
+}
+
+int ob_adamw_clip_step(const ob_adamw_tensor* table, int64_t n_tensors, const int64_t* chunk_map,
+                       int64_t n_blocks, const float* lr, float* step, float grad_scale,
+                       double beta1, double beta2, double eps, double weight_decay,
+                       double max_norm, float* total_norm,
+                       void* ws, size_t ws_bytes, void* stream) {
+  static_assert(sizeof(ob_adamw_tensor) == sizeof(AdamwTensor), "table layout");
+  if (n_tensors < 1 || n_blocks < 1 || n_blocks > 0x7fffffff) return OB_ERR_SHAPE;
+  if (!table || !chunk_map || !lr || !step || !ws) return OB_ERR_NULL;
+  if (ws_bytes < ob_adamw_workspace(n_blocks)) return OB_ERR_WORKSPACE;
+  launch_adamw(reinterpret_cast<const AdamwTensor*>(table), chunk_map, n_blocks, lr, step,
+               grad_scale, beta1, beta2, eps, weight_decay, max_norm, total_norm, ws,
+               as_stream(stream));
+  return launched();
+}
+
 }  // extern "C"

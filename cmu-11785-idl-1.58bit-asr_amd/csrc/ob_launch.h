@@ -65,4 +65,19 @@ void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_l
                     const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
                     const float* grad_out, float* grad, float* ws, hipStream_t s);
 
+// adamw.hip (clip_grad_norm_ + AdamW over a tensor table; layout = ob_adamw_tensor)
+struct AdamwTensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+};
+int64_t adamw_plan(const int64_t* numels, int64_t n, int64_t* map);
+size_t adamw_workspace(int64_t n_blocks);
+void launch_adamw(const AdamwTensor* tab, const int64_t* map, int64_t nb, const float* lr,
+                  float* step, float grad_scale, double beta1, double beta2, double eps,
+                  double weight_decay, double max_norm, float* total_norm_out, void* ws,
+                  hipStream_t s);
+
 }  // namespace ob

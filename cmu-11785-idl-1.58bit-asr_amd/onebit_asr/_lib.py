@@ -27,6 +27,8 @@ _c_f = ctypes.c_void_p  # device pointers are passed as raw addresses
 _i64 = ctypes.c_int64
 _int = ctypes.c_int
 _sz = ctypes.c_size_t
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
 
 # name -> (restype, argtypes); mirrors include/onebit_hip.h one-to-one.
 SIGNATURES = {
@@ -57,6 +59,11 @@ SIGNATURES = {
         _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _sz, _c_f]),
     "ob_ctc_loss_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_adamw_plan": (_i64, [_c_f, _i64, _c_f]),
+    "ob_adamw_workspace": (_sz, [_i64]),
+    "ob_adamw_clip_step": (
+        _int, [_c_f, _i64, _c_f, _i64, _c_f, _c_f, _f32, _f64, _f64, _f64, _f64, _f64, _c_f, _c_f,
+               _sz, _c_f]),
 }
 
 ABI_VERSION = 1

@@ -8,7 +8,8 @@ AdamW with a device lr) the whole body is captured once and replayed:
 
 * graph A: zero the flat gradient buffer, the three passes, their losses, backward;
 * [N > 1: one all-reduce (SUM) of the flat gradient buffer over RCCL, outside the graph;]
-* graph B (merged into A when N == 1): average over ranks, clip_grad_norm_(5.0), AdamW.
+* graph B (merged into A when N == 1): clip_grad_norm_(5.0) + AdamW as the three-launch
+  ``FusedAdamW`` (the 1/world average is folded into its gradient scale).
 
 What changes per step without re-capture:
 * the stochastic-precision mask: ``DeviceBits.set`` copies the new per-block bitwidths
@@ -19,10 +20,12 @@ What changes per step without re-capture:
   shape needs another ``GraphedTrainStep``);
 * dropout masks: torch's philox offsets advance per replay.
 
-Gradients live in one flat fp32 buffer (parameter order) so the N > 1 exchange is a
+With N > 1 gradients live in one flat fp32 buffer (parameter order) so the exchange is a
 single large all-reduce -- the bucket size xGMI ring all-reduce wants -- with no
-flatten/unflatten copies. Parameters that receive no gradient in the step are excluded
-from the optimizer exactly like the reference (AdamW skips grad=None).
+flatten/unflatten copies. With N == 1 autograd's own gradient buffers are used as they
+are (``p.grad = None`` before backward, so no accumulate kernels). Parameters that receive
+no gradient in the step are excluded from the optimizer exactly like the reference (AdamW
+skips grad=None).
 """
 from __future__ import annotations
 
@@ -31,6 +34,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from .optim import FusedAdamW
 from .quant import DeviceBits, QuantizedLinear
 from .train_step import WarmupCosine
 
@@ -58,6 +62,7 @@ class GraphedTrainStep:
         self.params: List[torch.nn.Parameter] = []
         self.flat: Optional[torch.Tensor] = None
         self.opt = None
+        self.fused = False
         self.sched = None
         self.graph_a = self.graph_b = None
         self.loss = self.parts = None
@@ -82,28 +87,42 @@ class GraphedTrainStep:
         loss, _ = self.step_module(self.batch, self.bits)
         loss.backward()
         self.params = [p for p in self.step_module.parameters() if p.grad is not None]
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
-        off = 0
         for p in self.step_module.parameters():
             p.grad = None
-        for p in self.params:
-            n = p.numel()
-            p.grad = self.flat[off:off + n].view_as(p)
-            off += n
-        cap = self.device.type == "cuda"
-        lr = torch.tensor(self.lr0, dtype=torch.float32, device=self.device) if cap else self.lr0
-        self.opt = torch.optim.AdamW(self.params, lr=lr, betas=(0.9, 0.98), weight_decay=1e-2,
-                                     capturable=cap, foreach=True)
+        if self.world > 1:
+            # one flat gradient buffer: the all-reduce is a single large RCCL call
+            total = sum(p.numel() for p in self.params)
+            self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
+            off = 0
+            for p in self.params:
+                n = p.numel()
+                p.grad = self.flat[off:off + n].view_as(p)
+                off += n
+        if self.device.type == "cuda":
+            self.fused = True
+            self.opt = FusedAdamW(self.params, lr=self.lr0, betas=(0.9, 0.98), eps=1e-8,
+                                  weight_decay=1e-2, max_norm=self.max_norm)
+            self.opt.grad_scale = 1.0 / self.world
+        else:  # host path (gloo tests of the exchange logic): torch AdamW + clip
+            self.fused = False
+            self.opt = torch.optim.AdamW(self.params, lr=self.lr0, betas=(0.9, 0.98),
+                                         weight_decay=1e-2, foreach=True)
         self.sched = WarmupCosine(self.opt, self.warmup_steps, self.total_steps)
 
     def _fwd_bwd(self):
-        self.flat.zero_()
+        if self.flat is not None:
+            self.flat.zero_()
+        else:  # N == 1: autograd hands its gradient buffers over (no accumulate kernels)
+            for p in self.params:
+                p.grad = None
         loss, parts = self.step_module(self.batch, self.bits)
         loss.backward()
         return loss.detach(), parts
 
     def _update(self):
+        if self.fused:  # clip + AdamW in three launches (grad_scale = 1/world)
+            self.opt.step()
+            return
         if self.world > 1:
             self.flat.div_(self.world)
         torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, foreach=True)

@@ -1,0 +1,115 @@
+"""The optimizer tail of the training step on the HIP library: clip_grad_norm_ + AdamW.
+
+Reference: onebit_asr/train.py:116-118 (``clip_grad_norm_(model.parameters(), 5.0)``,
+``optimizer.step()``) with ``AdamW(lr, betas=(0.9, 0.98), weight_decay=1e-2)``
+(train.py:259). ``FusedAdamW.step()`` is three launches (``ob_adamw_clip_step``) over a
+device table of (param, grad, exp_avg, exp_avg_sq) pointers instead of torch's per-tensor
+norm / scale / update kernels for every parameter tensor. lr and the step counter are
+device scalars, so a captured step replays with the schedule's current lr
+(``WarmupCosine`` fills ``param_groups[0]["lr"]``).
+
+Semantics follow torch: parameters without a gradient are skipped (they are left out of
+the table, which is re-planned when the set changes); the global norm covers exactly the
+parameters in the table; gradients are clipped in registers (``p.grad`` is not rescaled
+in place, unlike ``clip_grad_norm_``). There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, List
+
+import torch
+
+from . import _lib
+
+__all__ = ["FusedAdamW"]
+
+
+class FusedAdamW:
+    def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 5e-4,
+                 betas=(0.9, 0.98), eps: float = 1e-8, weight_decay: float = 1e-2,
+                 max_norm: float = 5.0):
+        self.params: List[torch.nn.Parameter] = list(params)
+        if not self.params:
+            raise ValueError("FusedAdamW got an empty parameter list")
+        dev = self.params[0].device
+        if dev.type != "cuda":
+            raise RuntimeError("FusedAdamW runs only on a ROCm device (HIP kernels, no CPU fallback)")
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise TypeError("FusedAdamW needs contiguous fp32 parameters")
+        self.device = dev
+        self.betas = (float(betas[0]), float(betas[1]))
+        self.eps = float(eps)
+        self.weight_decay = float(weight_decay)
+        self.max_norm = float(max_norm)
+        self.grad_scale = 1.0
+        self.lr = torch.tensor(float(lr), dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.total_norm = torch.zeros((), dtype=torch.float32, device=dev)
+        self.exp_avg = [torch.zeros_like(p) for p in self.params]
+        self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
+        # torch.optim-like surface for WarmupCosine
+        self.param_groups = [{"lr": self.lr, "initial_lr": float(lr), "params": self.params}]
+        self._members = None
+        self._ptrs = None
+        self._host_tables = []  # pinned host tables stay alive (a captured copy reads them)
+
+    # ------------------------------------------------------------------ table
+    def _plan(self, members):
+        lib = _lib.load()
+        numels = (ctypes.c_int64 * len(members))(*[self.params[i].numel() for i in members])
+        nb = lib.ob_adamw_plan(ctypes.addressof(numels), len(members), None)
+        _lib.check(0 if nb > 0 else int(nb), "ob_adamw_plan")
+        cmap = (ctypes.c_int64 * (2 * nb))()
+        lib.ob_adamw_plan(ctypes.addressof(numels), len(members), ctypes.addressof(cmap))
+        self.map = torch.tensor(list(cmap), dtype=torch.int64).to(self.device)
+        self.n_blocks = int(nb)
+        self.ws_bytes = lib.ob_adamw_workspace(nb)
+        self.ws = torch.empty((self.ws_bytes,), dtype=torch.uint8, device=self.device)
+        self.table = torch.empty((len(members), 5), dtype=torch.int64, device=self.device)
+        self._members = members
+        self._ptrs = None
+
+    def _refresh(self):
+        members = tuple(i for i, p in enumerate(self.params) if p.grad is not None)
+        if not members:
+            return False
+        if members != self._members:
+            self._plan(members)
+        ptrs = []
+        for i in members:
+            p = self.params[i]
+            g = p.grad
+            if g.dtype != torch.float32 or not g.is_contiguous() or g.shape != p.shape:
+                raise TypeError("FusedAdamW needs contiguous fp32 gradients shaped like the parameter")
+            ptrs.append((p.data_ptr(), g.data_ptr(), self.exp_avg[i].data_ptr(),
+                         self.exp_avg_sq[i].data_ptr(), p.numel()))
+        if ptrs != self._ptrs:
+            host = torch.tensor(ptrs, dtype=torch.int64).pin_memory()
+            self._host_tables.append(host)
+            if len(self._host_tables) > 8:  # keep the recent ones (graphs captured from them)
+                self._host_tables = self._host_tables[-8:]
+            self.table.copy_(host, non_blocking=True)
+            self._ptrs = ptrs
+        return True
+
+    # ------------------------------------------------------------------ step
+    @torch.no_grad()
+    def step(self):
+        if not self._refresh():
+            return
+        lib = _lib.load()
+        st = lib.ob_adamw_clip_step(
+            self.table.data_ptr(), len(self._members), self.map.data_ptr(), self.n_blocks,
+            self.lr.data_ptr(), self.step_t.data_ptr(), self.grad_scale, self.betas[0],
+            self.betas[1], self.eps, self.weight_decay, self.max_norm, self.total_norm.data_ptr(),
+            self.ws.data_ptr(), self.ws_bytes, torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(st, "ob_adamw_clip_step")
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()

@@ -160,6 +160,41 @@ OB_API int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets,
                            int64_t T, int64_t V, int64_t S, int blank, const float* grad_out,
                            float* grad, void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Optimizer tail of the training step: clip_grad_norm_(params, max_norm) followed by
+ * AdamW.step() (reference onebit_asr/train.py:116-118 with the optimizer of train.py:259:
+ * betas (0.9, 0.98), eps 1e-8, weight_decay 1e-2). torch issues per-tensor launches for
+ * the ~800 parameter tensors; this is three launches over a table of tensors.
+ *
+ * table     : DEVICE array of n_tensors descriptors (param, grad, exp_avg, exp_avg_sq are
+ *             device fp32 buffers of numel elements; exp_avg / exp_avg_sq start at 0)
+ * chunk_map : DEVICE int64 [2 * n_blocks] from ob_adamw_plan (host) for the same numels
+ * lr        : DEVICE fp32 learning rate (the warmup-cosine schedule writes it)
+ * step      : DEVICE fp32 step counter shared by all tensors; incremented by the call
+ * grad_scale: every gradient is multiplied by it first (1/world after a SUM all-reduce)
+ * max_norm  : <= 0 disables clipping. total_norm (optional DEVICE fp32) receives the
+ *             pre-clip global L2 norm, as clip_grad_norm_ returns it.
+ * Gradients are clipped in registers (the grad buffers are not modified).
+ * ------------------------------------------------------------------------------------ */
+typedef struct ob_adamw_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} ob_adamw_tensor;
+
+/* Host-only. Number of blocks for these tensor sizes; fills chunk_map (HOST int64
+ * [2 * n_blocks]) when non-NULL. Negative status for an empty table or numel < 1. */
+OB_API int64_t ob_adamw_plan(const int64_t* numels, int64_t n_tensors, int64_t* chunk_map);
+OB_API size_t ob_adamw_workspace(int64_t n_blocks);
+OB_API int ob_adamw_clip_step(const ob_adamw_tensor* table, int64_t n_tensors,
+                              const int64_t* chunk_map, int64_t n_blocks, const float* lr,
+                              float* step, float grad_scale, double beta1, double beta2,
+                              double eps, double weight_decay, double max_norm,
+                              float* total_norm, void* ws,
+                              size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,8 @@
 """GPU parity of the HIP CTC loss (device-side lengths) against torch's nn.CTCLoss on CPU
-(reference losses.py:41-47: blank 3, zero_infinity, 'mean'). Bars: loss rel <= 1e-5,
-logits-gradient (through log_softmax) max|err| <= 1e-5 * max|ref| + 1e-7; deterministic."""
+(reference losses.py:41-47: blank 3, zero_infinity, 'mean'). The reference value is torch's
+CTC in float64 (torch's fp32 CTC itself is off by ~1e-5 of max|grad| over T=249 steps).
+Bars: loss rel <= 1e-5, logits-gradient (through log_softmax) max|err| <= 2e-5 * max|ref| +
+1e-7 and no worse than 2x torch-fp32's own error; deterministic."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -33,16 +35,21 @@ def test_ctc_matches_torch(gpu, case):
     from onebit_asr.ctc import ctc_loss_mean
 
     logits, tg, il, tl = _case(**case)
-    lr = logits.clone().requires_grad_()
+    lr = logits.clone().double().requires_grad_()
     ref = torch.nn.CTCLoss(blank=3, zero_infinity=True)(
         F.log_softmax(lr, -1).transpose(0, 1), tg, il, tl)
     ref.backward()
+    l32 = logits.clone().requires_grad_()
+    torch.nn.CTCLoss(blank=3, zero_infinity=True)(
+        F.log_softmax(l32, -1).transpose(0, 1), tg, il, tl).backward()
+    err32 = (l32.grad.double() - lr.grad).abs().max().item()
     lg = logits.to(gpu).requires_grad_()
     out = ctc_loss_mean(F.log_softmax(lg, -1), tg.to(gpu), il.to(gpu), tl.to(gpu), 3)
     out.backward()
     assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item()) + 1e-6, (out.item(), ref.item())
-    err = (lg.grad.cpu() - lr.grad).abs().max().item()
-    assert err <= 1e-5 * lr.grad.abs().max().item() + 1e-7, err
+    err = (lg.grad.cpu().double() - lr.grad).abs().max().item()
+    assert err <= 2e-5 * lr.grad.abs().max().item() + 1e-7, (err, err32)
+    assert err <= 2 * err32 + 1e-7, (err, err32)
     g1 = lg.grad.clone()
     lg.grad = None
     ctc_loss_mean(F.log_softmax(lg, -1), tg.to(gpu), il.to(gpu), tl.to(gpu), 3).backward()
