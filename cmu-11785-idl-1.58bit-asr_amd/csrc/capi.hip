@@ -26,8 +26,8 @@ struct DwWorkspace {
   size_t part, part_db, apart, total;
 };
 
-DwWorkspace dw_layout(int64_t M, int64_t N, int64_t K) {
-  const DwPlan p = plan_dw(M, N, K);
+DwWorkspace dw_layout(int64_t P, int64_t M, int64_t N, int64_t K) {
+  const DwPlan p = plan_dw_passes(P, M, N, K);
   DwWorkspace w;
   w.part = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N * (size_t)K);
   w.part_db = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N);
@@ -132,22 +132,26 @@ int ob_bitlinear_bwd_dx(const float* dY, int64_t M, int64_t N, const uint32_t* c
 
 size_t ob_bitlinear_bwd_dw_workspace(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return 0;
-  return dw_layout(M, N, K).total;
+  return dw_layout(1, M, N, K).total;
 }
 
 namespace {
 
-int bwd_dw_impl(const float* dY, const float* X, int64_t M, int64_t N, int64_t K, const float* W,
-                const float* alpha, int alpha_raw, int bits, const int32_t* bits_dev, float* dW,
-                float* dalpha, float* db, void* ws, size_t ws_bytes, void* stream) {
-  if (M < 0 || N < 0 || K < 0) return OB_ERR_SHAPE;
+// P stacked passes of M rows each (P = 1: the single-call entries). Pass bitwidths come
+// from pass_bits (device [P]) when given, else from bits / bits_dev for the one pass.
+int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N, int64_t K,
+                const float* W, const float* alpha, int alpha_raw, int bits,
+                const int32_t* bits_dev, const int32_t* pass_bits, float* dW, float* dalpha,
+                float* db, void* ws, size_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || P < 1 || P > kMaxPasses) return OB_ERR_SHAPE;
   if (!alpha || !dalpha || !ws || (N * K > 0 && (!W || !dW)) || (M > 0 && (!dY || (K > 0 && !X))))
     return OB_ERR_NULL;
-  if (!aligned4(dY) || !aligned4(X) || !aligned4(dW) || !aligned4(db) || !aligned4(bits_dev))
+  if (!aligned4(dY) || !aligned4(X) || !aligned4(dW) || !aligned4(db) || !aligned4(bits_dev) ||
+      !aligned4(pass_bits))
     return OB_ERR_ALIGN;
-  const DwWorkspace L = dw_layout(M, N, K);
+  const DwWorkspace L = dw_layout(P, M, N, K);
   if (ws_bytes < L.total) return OB_ERR_WORKSPACE;
-  const DwPlan p = plan_dw(M, N, K);
+  const DwPlan p = plan_dw_passes(P, M, N, K);
   char* base = static_cast<char*>(ws);
   float* part = reinterpret_cast<float*>(base);
   float* part_db = db ? reinterpret_cast<float*>(base + L.part) : nullptr;
@@ -156,6 +160,7 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t M, int64_t N, int64_t K
   float* apart = reinterpret_cast<float*>(base + L.part + L.part_db + 16);
   hipStream_t s = as_stream(stream);
   int chunks = (int)p.chunks;
+  int cpp = (int)p.chunks_per_pass;
   if (M == 0 || N == 0) {
     // No rows: every gradient is zero. Zero the first slab and reduce one chunk.
     if (N * K > 0 && hipMemsetAsync(part, 0, sizeof(float) * N * K, s) != hipSuccess)
@@ -164,11 +169,18 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t M, int64_t N, int64_t K
       return OB_ERR_HIP;
     if (hipMemsetAsync(ticket, 0, sizeof(uint32_t), s) != hipSuccess) return OB_ERR_HIP;
     chunks = 1;
+    cpp = 1;
+    P = 1;
   } else {
-    launch_dw_partial(dY, X, M, N, K, p, part, part_db, ticket, s);
+    launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s);
   }
-  launch_ste_reduce(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, bits,
-                    reinterpret_cast<const int*>(bits_dev), dW, db, apart, ticket, dalpha, s);
+  if (pass_bits)
+    launch_ste_reduce_passes(part, (int)P, cpp, N * K, part_db, db ? N : 0, W, alpha, alpha_raw,
+                             reinterpret_cast<const int*>(pass_bits), dW, db, apart, ticket,
+                             dalpha, s);
+  else
+    launch_ste_reduce(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, bits,
+                      reinterpret_cast<const int*>(bits_dev), dW, db, apart, ticket, dalpha, s);
   return launched();
 }
 
@@ -178,8 +190,8 @@ int ob_bitlinear_bwd_dw(const float* dY, const float* X, int64_t M, int64_t N, i
                         const float* W, const float* alpha, int alpha_raw, int bits, float* dW,
                         float* dalpha, float* db, void* ws, size_t ws_bytes, void* stream) {
   if (int st = check_bits(bits)) return st;
-  return bwd_dw_impl(dY, X, M, N, K, W, alpha, alpha_raw, bits, nullptr, dW, dalpha, db, ws,
-                     ws_bytes, stream);
+  return bwd_dw_impl(dY, X, 1, M, N, K, W, alpha, alpha_raw, bits, nullptr, nullptr, dW, dalpha,
+                     db, ws, ws_bytes, stream);
 }
 
 int ob_bitlinear_bwd_dw_dyn(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
@@ -187,8 +199,51 @@ int ob_bitlinear_bwd_dw_dyn(const float* dY, const float* X, int64_t M, int64_t 
                             const int32_t* bits_dev, float* dW, float* dalpha, float* db, void* ws,
                             size_t ws_bytes, void* stream) {
   if (!bits_dev) return OB_ERR_NULL;
-  return bwd_dw_impl(dY, X, M, N, K, W, alpha, alpha_raw, 2, bits_dev, dW, dalpha, db, ws,
-                     ws_bytes, stream);
+  return bwd_dw_impl(dY, X, 1, M, N, K, W, alpha, alpha_raw, 2, bits_dev, nullptr, dW, dalpha,
+                     db, ws, ws_bytes, stream);
+}
+
+int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t K,
+                            const uint32_t* codes2, const uint32_t* codes1,
+                            const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                            const float* bias, int64_t N, float* Y, void* stream) {
+  if (M < 0 || K < 0 || N < 0 || P < 1 || P > 65535) return OB_ERR_SHAPE;
+  if (!alpha || !pass_bits || (M * N > 0 && !Y) || (M * K > 0 && !X) ||
+      (N * K > 0 && (!codes2 || !codes1)))
+    return OB_ERR_NULL;
+  if (!aligned4(X) || !aligned4(Y) || !aligned4(bias) || !aligned4(pass_bits)) return OB_ERR_ALIGN;
+  launch_ternary_gemm_passes(X, (int)P, M, K, codes2, codes1, reinterpret_cast<const int*>(pass_bits),
+                             N, alpha, alpha_raw, bias, Y, as_stream(stream));
+  return launched();
+}
+
+int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
+                               const uint32_t* codes2_t, const uint32_t* codes1_t,
+                               const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                               int64_t K, float* dX, void* stream) {
+  if (M < 0 || K < 0 || N < 0 || P < 1 || P > 65535) return OB_ERR_SHAPE;
+  if (!alpha || !pass_bits || (M * K > 0 && !dX) || (M * N > 0 && !dY) ||
+      (N * K > 0 && (!codes2_t || !codes1_t)))
+    return OB_ERR_NULL;
+  if (!aligned4(dY) || !aligned4(dX) || !aligned4(pass_bits)) return OB_ERR_ALIGN;
+  launch_ternary_gemm_passes(dY, (int)P, M, N, codes2_t, codes1_t,
+                             reinterpret_cast<const int*>(pass_bits), K, alpha, alpha_raw, nullptr,
+                             dX, as_stream(stream));
+  return launched();
+}
+
+size_t ob_bitlinear_bwd_dw_passes_workspace(int64_t P, int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0 || P < 1 || P > kMaxPasses) return 0;
+  return dw_layout(P, M, N, K).total;
+}
+
+int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P, int64_t M, int64_t N,
+                               int64_t K, const float* W, const float* alpha, int alpha_raw,
+                               const int32_t* pass_bits, float* dW, float* dalpha, float* db,
+                               void* ws, size_t ws_bytes, void* stream) {
+  if (!pass_bits) return OB_ERR_NULL;
+  return bwd_dw_impl(dY, X, P, M, N, K, W, alpha, alpha_raw, 2, nullptr, pass_bits, dW, dalpha,
+                     db, ws, ws_bytes, stream);
 }
 
 int ob_dwconv1d_fwd(const float* x, const float* w, const float* bias, int64_t B, int64_t C,

@@ -50,7 +50,7 @@ constexpr int kDwTile = 64;
 template <bool VEC, int S>
 __global__ __launch_bounds__(kThreads) void dw_partial_kernel(
     const float* __restrict__ dY, const float* __restrict__ X, int64_t M, int64_t N, int64_t K,
-    int64_t tiles_k, int64_t rows_per_chunk, float* __restrict__ part,
+    int64_t tiles_k, int64_t rows_per_chunk, int64_t cpp, float* __restrict__ part,
     float* __restrict__ part_db, uint32_t* __restrict__ ticket) {
   __shared__ float red[2][kDwTile * kDwTile];  // 32 KB: waves pair up (0+2, 1+3)
   __shared__ float dbred[4][kDwTile];
@@ -62,9 +62,12 @@ __global__ __launch_bounds__(kThreads) void dw_partial_kernel(
   const int64_t tn = blockIdx.x / tiles_k;
   const int64_t tk = blockIdx.x - tn * tiles_k;
   const int64_t n0 = tn * kDwTile, k0 = tk * kDwTile;
+  // chunk -> (pass, chunk of the pass); M is the row count of one pass
   const int64_t chunk = blockIdx.y;
-  const int64_t m_begin = chunk * rows_per_chunk;
-  const int64_t m_end = (m_begin + rows_per_chunk < M) ? m_begin + rows_per_chunk : M;
+  const int64_t pass = chunk / cpp;
+  const int64_t m_lim = (pass + 1) * M;
+  const int64_t m_begin = pass * M + (chunk - pass * cpp) * rows_per_chunk;
+  const int64_t m_end = (m_begin + rows_per_chunk < m_lim) ? m_begin + rows_per_chunk : m_lim;
   const int64_t ncol = n0 + 4 * r;
   const int64_t kcol = k0 + 4 * r;
   const bool do_db = (part_db != nullptr) && (tk == 0);
@@ -239,8 +242,8 @@ __device__ __forceinline__ void split_col(const f32x4 (&rows)[8], int e, bf16x8&
 template <int S>
 __global__ __launch_bounds__(kThreads) void dw_bf16x6_kernel(
     const float* __restrict__ dY, const float* __restrict__ X, int64_t M, int N, int K,
-    int tiles_k, int64_t rows_per_chunk, float* __restrict__ part, float* __restrict__ part_db,
-    uint32_t* __restrict__ ticket) {
+    int tiles_k, int64_t rows_per_chunk, int64_t cpp, float* __restrict__ part,
+    float* __restrict__ part_db, uint32_t* __restrict__ ticket) {
   constexpr int VW = 4, T = 64;
   __shared__ float red[2][T * T];
   __shared__ float dbred[4][T];
@@ -252,14 +255,18 @@ __global__ __launch_bounds__(kThreads) void dw_bf16x6_kernel(
   const int tn = blockIdx.x / tiles_k;
   const int tk = blockIdx.x - tn * tiles_k;
   const int n0 = tn * T, k0 = tk * T;
+  // chunk -> (pass, chunk of the pass); M is the row count of one pass
   const int64_t chunk = blockIdx.y;
-  const int64_t m_begin = chunk * rows_per_chunk;
+  const int64_t pass = chunk / cpp;
+  const int64_t m_lim = (pass + 1) * M;
+  const int64_t m_begin = pass * M + (chunk - pass * cpp) * rows_per_chunk;
   const bool do_db = (part_db != nullptr) && (tk == 0);
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ticket = 0u;
 
-  // Descriptors start at the chunk's first row, so every offset fits 32 bits.
-  const __amdgpu_buffer_rsrc_t ry = make_rsrc(dY + m_begin * N, (M - m_begin) * N * 4);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + m_begin * K, (M - m_begin) * K * 4);
+  // Descriptors start at the chunk's first row and end at its pass's last row (rows past
+  // it read 0), so every offset fits 32 bits.
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(dY + m_begin * N, (m_lim - m_begin) * N * 4);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + m_begin * K, (m_lim - m_begin) * K * 4);
   // Column offset clamped into the row (columns past N / K feed discarded outputs).
   const int nb = n0 + 4 * r < N - 4 ? n0 + 4 * r : N - 4;
   const int kb = k0 + 4 * r < K - 4 ? k0 + 4 * r : K - 4;
@@ -391,8 +398,11 @@ bool use_f32_dw() {
 
 }  // namespace
 
-DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
+DwPlan plan_dw(int64_t M, int64_t N, int64_t K) { return plan_dw_passes(1, M, N, K); }
+
+DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
   DwPlan p;
+  const int64_t M = P * Mp;  // chunk length is chosen for the whole stacked M
   if (use_f32_dw() || N % 4 != 0 || K % 4 != 0 || N < 4 || K < 4) {
     p.variant = 0;
     p.tiles_n = N > 0 ? ceil_div(N, kDwTile) : 1;  // >= 1 so K = 0 still yields db
@@ -415,24 +425,29 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
     while (steps > 2 && tiles * ceil_div(M, 128 * steps) < 256) steps /= 2;
     p.rows_per_chunk = 128 * steps;
   }
-  p.chunks = M > 0 ? ceil_div(M, p.rows_per_chunk) : 1;
+  p.passes = P;
+  p.rows_per_pass = Mp;
+  p.chunks_per_pass = Mp > 0 ? ceil_div(Mp, p.rows_per_chunk) : 1;
+  p.chunks = P * p.chunks_per_pass;
   return p;
 }
 
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
                        hipStream_t s) {
-  if (M == 0 || N == 0) return;
+  if (p.rows_per_pass == 0 || N == 0) return;
+  M = p.rows_per_pass;  // kernels index rows per pass (M given = passes * rows_per_pass)
   dim3 grid((unsigned)(p.tiles_n * p.tiles_k), (unsigned)p.chunks);
   const bool vec = (N % 4 == 0) && (K % 4 == 0) && N >= 4 && K >= 4 &&
                    ((reinterpret_cast<uintptr_t>(dY) & 15) == 0) &&
                    ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
 #define OB_DW(V, S)                                                                        \
   hipLaunchKernelGGL((dw_partial_kernel<V, S>), grid, dim3(kThreads), 0, s, dY, X, M, N, K,   \
-                     p.tiles_k, p.rows_per_chunk, part, part_db, ticket)
+                     p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db, ticket)
 #define OB_DW6(S)                                                                          \
   hipLaunchKernelGGL((dw_bf16x6_kernel<S>), grid, dim3(kThreads), 0, s, dY, X, M, (int)N,     \
-                     (int)K, (int)p.tiles_k, p.rows_per_chunk, part, part_db, ticket)
+                     (int)K, (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db,   \
+                     ticket)
   if (p.variant != 0) {
     const int64_t steps = p.rows_per_chunk / 128;
     if (steps == 8) OB_DW6(8);

@@ -28,6 +28,13 @@ void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* p
                        int64_t n_db, const float* W, const float* alpha, int alpha_raw, int bits,
                        const int* bits_dev, float* dW, float* db, float* apart, uint32_t* ticket,
                        float* dalpha, hipStream_t s);
+// Stacked passes: chunks = P * cpp, chunk c of pass c / cpp; pass p's STE/alpha term uses
+// bitwidth pass_bits[p] (DEVICE int32 [P], 1 or 2). P <= kMaxPasses.
+constexpr int kMaxPasses = 4;
+void launch_ste_reduce_passes(const float* part, int P, int cpp, int64_t nk, const float* part_db,
+                              int64_t n_db, const float* W, const float* alpha, int alpha_raw,
+                              const int* pass_bits, float* dW, float* db, float* apart,
+                              uint32_t* ticket, float* dalpha, hipStream_t s);
 
 // gemm.hip
 // C[M][N] = a * (A[M][K] . Q^T) + bias, Q given as 2-bit codes [N][ceil(K/16)].
@@ -35,12 +42,23 @@ void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* c
                          const float* alpha, int alpha_raw, const float* bias, float* C,
                          hipStream_t s);
 
+// P stacked passes of one layer (rows p*M .. p*M+M of A and C): pass p multiplies by the
+// codes1 operand when pass_bits[p] (DEVICE int32 [P]) == 1, else by `codes`.
+void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
+                                const uint32_t* codes, const uint32_t* codes1,
+                                const int* pass_bits, int64_t N, const float* alpha,
+                                int alpha_raw, const float* bias, float* C, hipStream_t s);
+
 // Split-M partial of G = dY^T . X: part[c][N*K] for chunk c, part_db[c][N] (optional).
+// With P stacked passes the chunks never straddle a pass: chunk c belongs to pass
+// c / chunks_per_pass (so the reduction can weight each pass by its own bitwidth).
 struct DwPlan {
   int64_t tiles_n, tiles_k, chunks, rows_per_chunk;
-  int variant;  // 0: fp32 MFMA (OB_GEMM=f32); 3 / 4: bf16x6 with 48- / 64-wide tiles
+  int64_t passes, rows_per_pass, chunks_per_pass;
+  int variant;  // 0: fp32 MFMA (OB_GEMM=f32); 4: bf16x6 with 64-wide tiles
 };
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
+DwPlan plan_dw_passes(int64_t P, int64_t M_per_pass, int64_t N, int64_t K);
 // Also zeroes *ticket (for the ste_reduce launch that follows on the same stream).
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,

@@ -79,11 +79,26 @@ constexpr int kReduceEPT = 4;
 constexpr int kReduceElems = kThreads * kReduceEPT;
 
 __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
-    const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
+    const float* __restrict__ part, int P, int cpp, int64_t nk, const float* __restrict__ part_db,
     int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
-    int bits, const int* __restrict__ bits_dev, float* __restrict__ dW, float* __restrict__ db,
-    float* __restrict__ apart, uint32_t* __restrict__ ticket, float* __restrict__ dalpha) {
-  if (bits_dev) bits = *bits_dev;  // graph mode: per-call bitwidth read on device
+    int bits, const int* __restrict__ bits_dev, const int* __restrict__ pass_bits,
+    float* __restrict__ dW, float* __restrict__ db, float* __restrict__ apart,
+    uint32_t* __restrict__ ticket, float* __restrict__ dalpha) {
+  // Per-pass bitwidth: pass_bits[p] (stacked passes), else one bitwidth (bits_dev: read on
+  // device in graph mode). Passes of equal bitwidth share one alpha term (quant.py:86-90),
+  // so the partial sums are kept per bitwidth: g1 (1-bit passes) and g2 (2-bit passes).
+  if (bits_dev) bits = *bits_dev;
+  int pb[kMaxPasses];
+  bool has1 = false, has2 = false;
+#pragma unroll
+  for (int p = 0; p < kMaxPasses; ++p) {
+    const int b = p < P ? (pass_bits ? pass_bits[p] : bits) : 2;
+    pb[p] = b == 1 ? 1 : 2;
+    if (p < P) {
+      has1 |= pb[p] == 1;
+      has2 |= pb[p] == 2;
+    }
+  }
   __shared__ float wsum[kThreads / 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -97,23 +112,35 @@ __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
     if (!is_w && !is_b) continue;
     const float* src = is_w ? part + e : part_db + (e - nk);
     const int64_t stride = is_w ? nk : n_db;
-    float g = 0.0f;
-    int c = 0;
-    for (; c + 4 <= chunks; c += 4) {
-      const float v0 = src[(int64_t)c * stride];
-      const float v1 = src[(int64_t)(c + 1) * stride];
-      const float v2 = src[(int64_t)(c + 2) * stride];
-      const float v3 = src[(int64_t)(c + 3) * stride];
-      g += v0;
-      g += v1;
-      g += v2;
-      g += v3;
+    float g1 = 0.0f, g2 = 0.0f;
+#pragma unroll
+    for (int p = 0; p < kMaxPasses; ++p) {
+      if (p >= P) break;
+      const float* sp = src + (int64_t)p * cpp * stride;
+      float gp = 0.0f;
+      int c = 0;
+      for (; c + 4 <= cpp; c += 4) {
+        const float v0 = sp[(int64_t)c * stride];
+        const float v1 = sp[(int64_t)(c + 1) * stride];
+        const float v2 = sp[(int64_t)(c + 2) * stride];
+        const float v3 = sp[(int64_t)(c + 3) * stride];
+        gp += v0;
+        gp += v1;
+        gp += v2;
+        gp += v3;
+      }
+      for (; c < cpp; ++c) gp += sp[(int64_t)c * stride];
+      if (pb[p] == 1) g1 += gp;
+      else g2 += gp;
     }
-    for (; c < chunks; ++c) g += src[(int64_t)c * stride];
+    const float g = g2 + g1;
     if (is_w) {
       const float wa = W[e] / a;
       dW[e] = g * ste_indicator(wa);  // quant.py:81-82 (multiply: inf*0 -> NaN as in torch)
-      prod += g * alpha_term(wa, bits);  // quant.py:91 grad_out * term
+      float t = 0.0f;                 // quant.py:91 grad_out * term, per bitwidth
+      if (has2) t += g2 * alpha_term(wa, 2);
+      if (has1) t += g1 * alpha_term(wa, 1);
+      prod += t;
     } else {
       db[e - nk] = g;
     }
@@ -184,9 +211,20 @@ void launch_ste_reduce(const float* part, int chunks, int64_t nk, const float* p
                        float* dalpha, hipStream_t s) {
   int64_t nb = ste_reduce_blocks(nk + n_db);
   if (nb == 0) nb = 1;  // an empty tensor still writes dalpha = 0
-  hipLaunchKernelGGL(ste_reduce_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, chunks,
-                     nk, part_db, n_db, W, alpha, alpha_raw, bits, bits_dev, dW, db, apart, ticket,
-                     dalpha);
+  hipLaunchKernelGGL(ste_reduce_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, 1, chunks,
+                     nk, part_db, n_db, W, alpha, alpha_raw, bits, bits_dev, (const int*)nullptr,
+                     dW, db, apart, ticket, dalpha);
+}
+
+void launch_ste_reduce_passes(const float* part, int P, int cpp, int64_t nk, const float* part_db,
+                              int64_t n_db, const float* W, const float* alpha, int alpha_raw,
+                              const int* pass_bits, float* dW, float* db, float* apart,
+                              uint32_t* ticket, float* dalpha, hipStream_t s) {
+  int64_t nb = ste_reduce_blocks(nk + n_db);
+  if (nb == 0) nb = 1;
+  hipLaunchKernelGGL(ste_reduce_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, P, cpp,
+                     nk, part_db, n_db, W, alpha, alpha_raw, 2, (const int*)nullptr, pass_bits,
+                     dW, db, apart, ticket, dalpha);
 }
 
 }  // namespace ob

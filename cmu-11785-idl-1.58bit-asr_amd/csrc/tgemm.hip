@@ -84,11 +84,26 @@ __device__ __forceinline__ void load8(const float* __restrict__ arow, int k, int
   b = *reinterpret_cast<const f32x4*>(arow + kb);
 }
 
+// Stacked passes (pass_bits != nullptr): blockIdx.y = pass p; the pass's rows are
+// A[p*M .. p*M+M) / C[p*M ..), and its codes are codes1 when pass_bits[p] == 1, else codes.
+__device__ __forceinline__ void select_pass(const float* __restrict__& A, float* __restrict__& C,
+                                            const uint32_t* __restrict__& codes,
+                                            const uint32_t* codes1, const int* pass_bits,
+                                            int64_t M, int K, int N) {
+  if (!pass_bits) return;
+  const int p = blockIdx.y;
+  if (pass_bits[p] == 1) codes = codes1;
+  A += (int64_t)p * M * K;
+  C += (int64_t)p * M * N;
+}
+
 template <int NT, int NCH>
 __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
-    const float* __restrict__ bias, float* __restrict__ C) {
+    const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
+    const int* __restrict__ pass_bits) {
+  select_pass(A, C, codes, codes1, pass_bits, M, K, N);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
   const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
@@ -235,7 +250,14 @@ constexpr int kF32NT = 3;
 __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
     const float* __restrict__ A, int64_t M, int64_t K, const uint32_t* __restrict__ codes,
     int64_t KW, int64_t N, const float* __restrict__ alpha, int alpha_raw,
-    const float* __restrict__ bias, float* __restrict__ C) {
+    const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
+    const int* __restrict__ pass_bits) {
+  if (pass_bits) {  // stacked passes: blockIdx.z = pass
+    const int p = blockIdx.z;
+    if (pass_bits[p] == 1) codes = codes1;
+    A += (int64_t)p * M * K;
+    C += (int64_t)p * M * N;
+  }
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15;
@@ -304,18 +326,20 @@ int pick_nt(int64_t N, int64_t K) {
 
 template <int NT>
 void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
-                   const float* alpha, int alpha_raw, const float* bias, float* C, hipStream_t s) {
+                   const float* alpha, int alpha_raw, const float* bias, float* C,
+                   const uint32_t* codes1, const int* pass_bits, int P, hipStream_t s) {
   const int n_ct = (int)ceil_div(N, 16 * NT);
   const int n_rt = (int)ceil_div(M, kRows);
-  int rgroups = kTargetBlocks / n_ct;
+  int rgroups = kTargetBlocks / (n_ct * P);
   if (rgroups < 1) rgroups = 1;
   if (rgroups > n_rt) rgroups = n_rt;
-  const dim3 grid((unsigned)(rgroups * n_ct));
+  const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
   const size_t lds = bimg_bytes(NT, K);
   const int KW = (int)ceil_div(K, 16);
 #define OB_TGEMM(NCH)                                                                        \
   hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH>), grid, dim3(kThreads), lds, s, A, M, (int)K, \
-                     codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C)
+                     codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C, codes1, \
+                     pass_bits)
   switch ((K + 31) / 32) {  // Conformer widths: 64, 144, 256, 576
     case 2: OB_TGEMM(2); break;
     case 5: OB_TGEMM(5); break;
@@ -328,26 +352,38 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
 
 }  // namespace
 
+void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
+                                const uint32_t* codes, const uint32_t* codes1,
+                                const int* pass_bits, int64_t N, const float* alpha,
+                                int alpha_raw, const float* bias, float* C, hipStream_t s) {
+  if (M == 0 || N == 0 || P == 0) return;
+  const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const int nt = vec && !use_f32_gemm() ? pick_nt(N, K) : 0;
+#define OB_NT(V)                                                                            \
+  case V:                                                                                   \
+    launch_bf16x3<V>(A, M, K, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, s); \
+    return;
+  switch (nt) {
+    OB_NT(12)
+    OB_NT(9)
+    OB_NT(6)
+    OB_NT(4)
+    OB_NT(3)
+    OB_NT(2)
+    OB_NT(1)
+    default: break;
+  }
+#undef OB_NT
+  // fp32 path (K == 0 included: its k-loop is empty and never reads A).
+  const dim3 grid((unsigned)ceil_div(M, kRows), (unsigned)ceil_div(N, 16 * kF32NT), (unsigned)P);
+  hipLaunchKernelGGL(tgemm_f32_kernel, grid, dim3(kThreads), 0, s, A, M, K, codes,
+                     ceil_div(K, 16), N, alpha, alpha_raw, bias, C, codes1, pass_bits);
+}
+
 void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
                          const float* alpha, int alpha_raw, const float* bias, float* C,
                          hipStream_t s) {
-  if (M == 0 || N == 0) return;
-  const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-  const int nt = vec && !use_f32_gemm() ? pick_nt(N, K) : 0;
-  switch (nt) {
-    case 12: launch_bf16x3<12>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    case 9: launch_bf16x3<9>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    case 6: launch_bf16x3<6>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    case 4: launch_bf16x3<4>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    case 3: launch_bf16x3<3>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    case 2: launch_bf16x3<2>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    case 1: launch_bf16x3<1>(A, M, K, codes, N, alpha, alpha_raw, bias, C, s); return;
-    default: break;
-  }
-  // fp32 path (K == 0 included: its k-loop is empty and never reads A).
-  const dim3 grid((unsigned)ceil_div(M, kRows), (unsigned)ceil_div(N, 16 * kF32NT));
-  hipLaunchKernelGGL(tgemm_f32_kernel, grid, dim3(kThreads), 0, s, A, M, K, codes,
-                     ceil_div(K, 16), N, alpha, alpha_raw, bias, C);
+  launch_ternary_gemm_passes(A, 1, M, K, codes, codes, nullptr, N, alpha, alpha_raw, bias, C, s);
 }
 
 }  // namespace ob

@@ -59,6 +59,14 @@ SIGNATURES = {
         _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _sz, _c_f]),
     "ob_ctc_loss_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_bitlinear_fwd_passes": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dx_passes": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _i64, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dw_passes_workspace": (_sz, [_i64, _i64, _i64, _i64]),
+    "ob_bitlinear_bwd_dw_passes": (
+        _int, [_c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f, _c_f,
+               _sz, _c_f]),
     "ob_adamw_plan": (_i64, [_c_f, _i64, _c_f]),
     "ob_adamw_workspace": (_sz, [_i64]),
     "ob_adamw_clip_step": (

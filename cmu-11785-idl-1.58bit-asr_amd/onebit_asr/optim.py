@@ -53,7 +53,16 @@ class FusedAdamW:
         self.param_groups = [{"lr": self.lr, "initial_lr": float(lr), "params": self.params}]
         self._members = None
         self._ptrs = None
-        self._host_tables = []  # pinned host tables stay alive (a captured copy reads them)
+        # Pinned staging for the table's H2D copy, allocated here because pinning host
+        # memory is not allowed while a stream is being captured. A buffer used during
+        # capture is never written again (the graph's copy node re-reads it on replay).
+        rows = len(self.params)
+        self._ring = [torch.empty((rows, 5), dtype=torch.int64).pin_memory() for _ in range(2)]
+        self._ring_ev = [None, None]
+        self._rr = 0
+        self._capture_bufs = [torch.empty((rows, 5), dtype=torch.int64).pin_memory()
+                              for _ in range(2)]
+        self._frozen = []
 
     # ------------------------------------------------------------------ table
     def _plan(self, members):
@@ -86,13 +95,31 @@ class FusedAdamW:
             ptrs.append((p.data_ptr(), g.data_ptr(), self.exp_avg[i].data_ptr(),
                          self.exp_avg_sq[i].data_ptr(), p.numel()))
         if ptrs != self._ptrs:
-            host = torch.tensor(ptrs, dtype=torch.int64).pin_memory()
-            self._host_tables.append(host)
-            if len(self._host_tables) > 8:  # keep the recent ones (graphs captured from them)
-                self._host_tables = self._host_tables[-8:]
-            self.table.copy_(host, non_blocking=True)
+            self._stage(ptrs)
             self._ptrs = ptrs
         return True
+
+    def _stage(self, ptrs):
+        n = len(ptrs)
+        src = torch.tensor(ptrs, dtype=torch.int64)
+        if torch.cuda.is_current_stream_capturing():
+            if not self._capture_bufs:
+                raise RuntimeError("FusedAdamW: no pinned staging buffer left for capture")
+            buf = self._capture_bufs.pop()
+            self._frozen.append(buf)
+            buf[:n].copy_(src)
+            self.table.copy_(buf[:n], non_blocking=True)
+            return
+        i = self._rr % len(self._ring)
+        self._rr += 1
+        if self._ring_ev[i] is not None:
+            self._ring_ev[i].synchronize()  # its previous copy has been consumed
+        buf = self._ring[i]
+        buf[:n].copy_(src)
+        self.table.copy_(buf[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._ring_ev[i] = ev
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()

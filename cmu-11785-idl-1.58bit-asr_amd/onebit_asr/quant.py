@@ -34,7 +34,7 @@ import torch.nn.functional as F
 from . import _lib
 
 __all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "DeviceBits",
-           "DynamicBitwidth"]
+           "DynamicBitwidth", "PassBits"]
 
 _VALID = (1, 2, 32)
 
@@ -75,6 +75,25 @@ class DeviceBits:
 
     def __len__(self) -> int:
         return self.n_layers
+
+
+class PassBits:
+    """Bitwidths of P stacked passes of one layer call: the reference's teacher (2-bit),
+    student (1-bit) and stochastic-precision passes (train.py:82-105) run as ONE call on
+    inputs stacked along the batch, pass p at bitwidth ``tensor[p]`` (DEVICE int32 [P],
+    1 or 2). The layer then needs one launch per kernel instead of one per pass, and its
+    parameter gradients are summed inside the kernels rather than by autograd."""
+
+    __slots__ = ("tensor",)
+
+    def __init__(self, tensor: torch.Tensor):
+        if tensor.dtype != torch.int32 or tensor.dim() != 1:
+            raise TypeError("PassBits wants a 1-D int32 device tensor")
+        self.tensor = tensor
+
+    @property
+    def passes(self) -> int:
+        return self.tensor.numel()
 
 
 def _check_bitwidth(bitwidth) -> int:
@@ -175,6 +194,64 @@ class _BitLinearFn(torch.autograd.Function):
         return gx, gw, galpha, gb, None, None, None
 
 
+class _BitLinearPassesFn(torch.autograd.Function):
+    """P stacked passes (rows p*M .. p*M+M at bitwidth pass_bits[p]) in one call each for
+    fwd, dX and dW (include/onebit_hip.h, "Stacked passes")."""
+
+    @staticmethod
+    def forward(ctx, x2d, weight, alpha, bias, pass_bits, P, codes2, codes2_t, codes1, codes1_t):
+        rows, k = x2d.shape
+        m = rows // P
+        n = weight.shape[0]
+        y = torch.empty((rows, n), dtype=torch.float32, device=x2d.device)
+        lib = _lib.load()
+        _lib.check(
+            lib.ob_bitlinear_fwd_passes(x2d.data_ptr(), P, m, k, codes2.data_ptr(), codes1.data_ptr(),
+                                        pass_bits.data_ptr(), alpha.data_ptr(), 1, _lib.ptr(bias), n,
+                                        y.data_ptr(), _lib.stream_of(x2d)),
+            "ob_bitlinear_fwd_passes",
+        )
+        ctx.P = P
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x2d, weight, alpha, pass_bits, codes2_t, codes1_t)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2d, weight, alpha, pass_bits, codes2_t, codes1_t = ctx.saved_tensors
+        gy = gy.contiguous()
+        rows, k = x2d.shape
+        P = ctx.P
+        m = rows // P
+        n = weight.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(gy)
+        gx = gw = galpha = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty((rows, k), dtype=torch.float32, device=gy.device)
+            _lib.check(
+                lib.ob_bitlinear_bwd_dx_passes(gy.data_ptr(), P, m, n, codes2_t.data_ptr(),
+                                               codes1_t.data_ptr(), pass_bits.data_ptr(),
+                                               alpha.data_ptr(), 1, k, gx.data_ptr(), stream),
+                "ob_bitlinear_bwd_dx_passes",
+            )
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            gw = torch.empty_like(weight)
+            galpha = torch.empty((), dtype=torch.float32, device=gy.device)
+            gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            ws_bytes = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
+            ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
+            _lib.check(
+                lib.ob_bitlinear_bwd_dw_passes(gy.data_ptr(), x2d.data_ptr(), P, m, n, k,
+                                               weight.data_ptr(), alpha.data_ptr(), 1,
+                                               pass_bits.data_ptr(), gw.data_ptr(),
+                                               galpha.data_ptr(), _lib.ptr(gb), ws.data_ptr(),
+                                               ws_bytes, stream),
+                "ob_bitlinear_bwd_dw_passes",
+            )
+        return gx, gw, galpha, gb, None, None, None, None, None, None
+
+
 class _QuantizeSTE(torch.autograd.Function):
     """quantize_weight's autograd function (quant.py:38-92): W_hat = a * Q(W/a) with the
     STE / LSQ-style alpha gradient. ``alpha`` is used as given (no abs/eps), as in the
@@ -259,6 +336,8 @@ class QuantizedLinear(nn.Module):
         return codes, codes_t
 
     def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
+        if isinstance(bitwidth, PassBits):
+            return self._forward_passes(x, bitwidth)
         bits = _check_bitwidth(bitwidth)
         if bits == 32:  # quant.py:121-122
             return F.linear(x, self.weight, self.bias)
@@ -273,6 +352,22 @@ class QuantizedLinear(nn.Module):
         else:
             codes, codes_t = self._codes(bits)
         y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bits, codes, codes_t)
+        return y.view(*lead, self.out_features)
+
+    def _forward_passes(self, x: torch.Tensor, pb: PassBits) -> torch.Tensor:
+        """x: the P passes stacked on the leading dim ([P*B, ..., K] or [P*M, K])."""
+        _require_device(x, self.weight)
+        P = pb.passes
+        lead = x.shape[:-1]
+        x2d = x.reshape(-1, self.in_features)
+        if x2d.shape[0] % P:
+            raise ValueError(f"{x2d.shape[0]} rows do not split into {P} passes")
+        if not x2d.is_contiguous():
+            x2d = x2d.contiguous()
+        codes2, codes2_t = self._codes(2)
+        codes1, codes1_t = self._codes(1)
+        y = _BitLinearPassesFn.apply(x2d, self.weight, self.alpha, self.bias, pb.tensor, P,
+                                     codes2, codes2_t, codes1, codes1_t)
         return y.view(*lead, self.out_features)
 
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate cached codes

@@ -161,6 +161,38 @@ OB_API int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets,
                            float* grad, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Stacked passes. The reference's training step runs every BitLinear three times per
+ * batch -- 2-bit teacher, 1-bit student and the stochastic-precision pass
+ * (onebit_asr/train.py:82-105) -- each a separate QuantizedLinear.forward
+ * (quant.py:120-127) whose autograd gradients torch then sums. These entries take the P
+ * passes of one layer stacked along rows: X is [P][M][K] (P*M rows), pass p runs at
+ * bitwidth pass_bits[p] (DEVICE int32 [P]; 1 selects the 1-bit codes, anything else the
+ * 2-bit codes), so the per-step SP mask can change without re-launch decisions on the
+ * host. codes2 / codes1 are the ob_quant_pack outputs of the same (W, alpha) for
+ * bits 2 and 1.
+ *   fwd : Y[p] = a * X[p] . Q_{bits_p}^T + bias
+ *   dX  : dX[p] = a * dY[p] . Q_{bits_p}
+ *   dW  : dW = 1[|W/a| <= 1] * sum_p dY[p]^T X[p]; dalpha = sum_p sum(G_p * term_{bits_p})
+ *         * d|alpha|; db = sum over all P*M rows of dY -- the sum over passes the
+ *         reference's autograd forms (the STE mask does not depend on the bitwidth).
+ * P <= 4 for dW (ob_bitlinear_bwd_dw_passes_workspace returns 0 otherwise).
+ * ------------------------------------------------------------------------------------ */
+OB_API int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t K,
+                                   const uint32_t* codes2, const uint32_t* codes1,
+                                   const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                   const float* bias, int64_t N, float* Y, void* stream);
+OB_API int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
+                                      const uint32_t* codes2_t, const uint32_t* codes1_t,
+                                      const int32_t* pass_bits, const float* alpha,
+                                      int alpha_raw, int64_t K, float* dX, void* stream);
+OB_API size_t ob_bitlinear_bwd_dw_passes_workspace(int64_t P, int64_t M, int64_t N, int64_t K);
+OB_API int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P, int64_t M,
+                                      int64_t N, int64_t K, const float* W, const float* alpha,
+                                      int alpha_raw, const int32_t* pass_bits, float* dW,
+                                      float* dalpha, float* db, void* ws, size_t ws_bytes,
+                                      void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Optimizer tail of the training step: clip_grad_norm_(params, max_norm) followed by
  * AdamW.step() (reference onebit_asr/train.py:116-118 with the optimizer of train.py:259:
  * betas (0.9, 0.98), eps 1e-8, weight_decay 1e-2). torch issues per-tensor launches for
