@@ -64,74 +64,95 @@ def parse():
 
 # ------------------------------------------------------------------------- roofline
 def ql_shapes(batch: int, frames: int, d: int = 144, d_ff: int = 576, layers: int = 16):
-    """(name, M, K, N, count_per_step) of every BitLinear call in one step (3 passes)."""
+    """(name, M per pass, K, N, launches per step) of every BitLinear call in one step. The
+    step runs the three passes stacked (OneBitStep stacked=True): one launch per kernel
+    covers P = 3 passes, i.e. 3*M rows."""
     from onebit_asr.conformer import subsampled_length
 
     t = subsampled_length(frames)
     m = batch * t
-    per_pass = [("lin1", m, d, d_ff, 2), ("lin2", m, d_ff, d, 2), ("qkvo", m, d, d, 4),
-                ("pos", t, d, d, 1)]
-    return [(n, M, K, N, c * layers * 3) for (n, M, K, N, c) in per_pass]
+    per_block = [("lin1", m, d, d_ff, 2), ("lin2", m, d_ff, d, 2), ("qkvo", m, d, d, 4),
+                 ("pos", t, d, d, 1)]
+    return [(n, M, K, N, c * layers) for (n, M, K, N, c) in per_block]
+
+
+PASSES = 3
+PASS_BITS = [2, 1, 1]  # teacher, student, an SP pass at 1 bit
 
 
 def roofline(batch, frames, dev, reps=20):
-    """Time each BitLinear kernel family at the step's shapes with HIP events on the current
-    stream; the dominant family (largest time per step) is reported against its roof."""
+    """Time each BitLinear kernel family at the step's stacked shapes with HIP events on the
+    launch stream (kernels captured in a HIP graph and replayed, so the events bracket
+    device time, not Python launch gaps); the dominant family (largest time per step) is
+    reported against its roof. Algorithmic bytes / FLOPs per launch are counted for the P
+    passes one launch covers."""
     from onebit_asr import _lib
     from onebit_asr.quant import pack_codes
 
     lib = _lib.load()
-    stream = torch.cuda.current_stream(dev)
-    s = stream.cuda_stream
+    P = PASSES
     fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0], "dw_partial+ste_reduce": [0.0, 0.0, 0.0, 0]}
     # fam value: [total_time_us_per_step, total_bytes_per_step, total_flops_per_step, launches]
     detail = []
+    side = torch.cuda.Stream(dev)
+    bits_t = torch.tensor(PASS_BITS, dtype=torch.int32, device=dev)
     for name, M, K, N, count in ql_shapes(batch, frames):
         g = torch.Generator(device=dev).manual_seed(M + K + N)
-        X = torch.randn(M, K, device=dev, generator=g)
-        dY = torch.randn(M, N, device=dev, generator=g)
+        X = torch.randn(P * M, K, device=dev, generator=g)
+        dY = torch.randn(P * M, N, device=dev, generator=g)
         W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
         alpha = W.abs().mean()
         b = torch.zeros(N, device=dev)
-        codes, codes_t = pack_codes(W, alpha, 2)
-        Y = torch.empty(M, N, device=dev)
-        dX = torch.empty(M, K, device=dev)
+        c2, c2t = pack_codes(W, alpha, 2)
+        c1, c1t = pack_codes(W, alpha, 1)
+        Y = torch.empty(P * M, N, device=dev)
+        dX = torch.empty(P * M, K, device=dev)
         dW = torch.empty(N, K, device=dev)
         da = torch.empty((), device=dev)
         db = torch.empty(N, device=dev)
-        wsb = lib.ob_bitlinear_bwd_dw_workspace(M, N, K)
+        wsb = lib.ob_bitlinear_bwd_dw_passes_workspace(P, M, N, K)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
-        def fwd():
-            lib.ob_bitlinear_fwd(X.data_ptr(), M, K, codes.data_ptr(), alpha.data_ptr(), 1,
-                                 b.data_ptr(), N, Y.data_ptr(), s)
+        def fwd(s):
+            return lib.ob_bitlinear_fwd_passes(X.data_ptr(), P, M, K, c2.data_ptr(), c1.data_ptr(),
+                                               bits_t.data_ptr(), alpha.data_ptr(), 1, b.data_ptr(),
+                                               N, Y.data_ptr(), s)
 
-        def bdx():
-            lib.ob_bitlinear_bwd_dx(dY.data_ptr(), M, N, codes_t.data_ptr(), alpha.data_ptr(), 1,
-                                    K, dX.data_ptr(), s)
+        def bdx(s):
+            return lib.ob_bitlinear_bwd_dx_passes(dY.data_ptr(), P, M, N, c2t.data_ptr(),
+                                                  c1t.data_ptr(), bits_t.data_ptr(),
+                                                  alpha.data_ptr(), 1, K, dX.data_ptr(), s)
 
-        def bdw():
-            lib.ob_bitlinear_bwd_dw(dY.data_ptr(), X.data_ptr(), M, N, K, W.data_ptr(),
-                                    alpha.data_ptr(), 1, 2, dW.data_ptr(), da.data_ptr(),
-                                    db.data_ptr(), ws.data_ptr(), wsb, s)
+        def bdw(s):
+            return lib.ob_bitlinear_bwd_dw_passes(dY.data_ptr(), X.data_ptr(), P, M, N, K,
+                                                  W.data_ptr(), alpha.data_ptr(), 1,
+                                                  bits_t.data_ptr(), dW.data_ptr(), da.data_ptr(),
+                                                  db.data_ptr(), ws.data_ptr(), wsb, s)
 
         def timed(fn):
-            for _ in range(3):
-                fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
-                fn()
-            e1.record(stream)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    _lib.check(fn(side.cuda_stream), "roofline warm-up")
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=side):
+                    for _ in range(reps):
+                        fn(torch.cuda.current_stream(dev).cuda_stream)
+                graph.replay()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+                graph.replay()
+                e1.record(side)
             e1.synchronize()
             return e0.elapsed_time(e1) * 1e3 / reps  # us per launch
 
         t_f, t_dx, t_dw = timed(fwd), timed(bdx), timed(bdw)
         cw = 4 * N * ((K + 15) // 16)
-        by_f = 4 * (M * K + M * N + N) + cw           # X, Y, bias, codes
-        by_dx = 4 * (M * N + M * K) + cw               # dY, dX, codes_t
-        by_dw = 4 * (M * N + M * K + 2 * N * K + N)    # dY, X, W, dW, db
-        fl = 2.0 * M * K * N
+        rows = P * M
+        by_f = 4 * (rows * K + rows * N + N) + 2 * cw      # X, Y, bias, codes (2 bitwidths)
+        by_dx = 4 * (rows * N + rows * K) + 2 * cw          # dY, dX, codes_t
+        by_dw = 4 * (rows * N + rows * K + 2 * N * K + N)   # dY, X, W, dW, db
+        fl = 2.0 * rows * K * N
         n_dx = 0 if name == "pos" else count  # pos_emb needs no input gradient
         f = fam["ternary_gemm"]
         f[0] += count * t_f + n_dx * t_dx
@@ -143,14 +164,15 @@ def roofline(batch, frames, dev, reps=20):
         f[1] += count * by_dw
         f[2] += count * fl
         f[3] += count
-        detail.append({"layer": name, "M": M, "K": K, "N": N, "per_step": count,
-                       "fwd_us": round(t_f, 2), "dx_us": round(t_dx, 2), "dw_us": round(t_dw, 2)})
+        detail.append({"layer": name, "M_per_pass": M, "passes": P, "K": K, "N": N,
+                       "launches_per_step": count, "fwd_us": round(t_f, 2),
+                       "dx_us": round(t_dx, 2), "dw_us": round(t_dw, 2)})
     dom = max(fam, key=lambda k: fam[k][0])
     t_us, by, fl, n = fam[dom]
     avg_t = t_us / n
     gbs = (by / n) / (avg_t * 1e-6) / 1e9
     tfs = (fl / n) / (avg_t * 1e-6) / 1e12
-    # fp32-MFMA kernels: the binding roof is whichever takes longer at peak
+    # fp32-MFMA-equivalent kernels: the binding roof is whichever takes longer at peak
     bound_mfma = (fl / PEAK_FP32_MFMA_TFLOPS / 1e12) > (by / PEAK_HBM_GBS / 1e9)
     if bound_mfma:
         roof = {"bound": "mfma", "achieved": round(tfs, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
