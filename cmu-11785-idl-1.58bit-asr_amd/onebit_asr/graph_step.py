@@ -181,6 +181,13 @@ class GraphedTrainStep:
         torch.cuda.current_stream(self.device).wait_stream(side)
         if not self.use_graph:
             return
+        use_stacked = getattr(self.step_module, "_use_stacked", None)
+        if use_stacked is not None and not use_stacked():
+            # Measured: replaying the literal three-forward step corrupts the gradients of
+            # parameters that receive three broadcast-reduced contributions (pos_bias_u/v)
+            # at Conformer-S; the stacked step gives each parameter one contribution.
+            raise ValueError("HIP-graph capture needs OneBitStep(stacked=True); run the "
+                             "literal three-pass step with use_graph=False")
         warm_loss, warm_parts = self.loss.clone(), self.parts.clone()
         torch.cuda.synchronize(self.device)
         self._drop_code_caches(self.step_module)

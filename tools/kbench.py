@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--shape", default=None, help="only this layer (lin1|lin2|qkvo|pos)")
     ap.add_argument("--op", default=None, help="only this op (pack|fwd|dx|dw)")
+    ap.add_argument("--passes", type=int, default=3,
+                    help="stacked passes per launch (the training step runs 3; 0 = single-pass entries)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = _lib.load()
@@ -64,18 +66,21 @@ def main():
     for name, M, K, N in SHAPES:
         if args.shape and name != args.shape:
             continue
-        X = torch.randn(M, K, device=dev)
-        dY = torch.randn(M, N, device=dev)
+        P = max(args.passes, 1)
+        X = torch.randn(P * M, K, device=dev)
+        dY = torch.randn(P * M, N, device=dev)
         W = (torch.rand(N, K, device=dev) * 2 - 1) * (2 / math.sqrt(K))
         alpha = W.abs().mean()
         b = torch.zeros(N, device=dev)
         codes, codes_t = pack_codes(W, alpha, 2)
-        Y = torch.empty(M, N, device=dev)
-        dX = torch.empty(M, K, device=dev)
+        c1, c1t = pack_codes(W, alpha, 1)
+        pbits = torch.tensor([2, 1, 1, 2][:P], dtype=torch.int32, device=dev)
+        Y = torch.empty(P * M, N, device=dev)
+        dX = torch.empty(P * M, K, device=dev)
         dW = torch.empty(N, K, device=dev)
         da = torch.empty((), device=dev)
         db = torch.empty(N, device=dev)
-        wsb = lib.ob_bitlinear_bwd_dw_workspace(M, N, K)
+        wsb = lib.ob_bitlinear_bwd_dw_passes_workspace(P, M, N, K)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         fns = {
             "pack": lambda cs=s: lib.ob_quant_pack(W.data_ptr(), alpha.data_ptr(), 1, 2, N, K,
@@ -88,11 +93,24 @@ def main():
                                                   alpha.data_ptr(), 1, 2, dW.data_ptr(), da.data_ptr(),
                                                   db.data_ptr(), ws.data_ptr(), wsb, cs),
         }
+        if args.passes > 0:
+            fns.update({
+                "fwd": lambda cs=s: lib.ob_bitlinear_fwd_passes(
+                    X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, b.data_ptr(), N, Y.data_ptr(), cs),
+                "dx": lambda cs=s: lib.ob_bitlinear_bwd_dx_passes(
+                    dY.data_ptr(), P, M, N, codes_t.data_ptr(), c1t.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, K, dX.data_ptr(), cs),
+                "dw": lambda cs=s: lib.ob_bitlinear_bwd_dw_passes(
+                    dY.data_ptr(), X.data_ptr(), P, M, N, K, W.data_ptr(), alpha.data_ptr(), 1,
+                    pbits.data_ptr(), dW.data_ptr(), da.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                    wsb, cs),
+            })
         res = {}
         for k, fn in fns.items():
             res[k] = timed(fn, args.reps, args.graph) if (not args.op or k == args.op) else float("nan")
-        gb_f = 4 * (M * K + M * N) / res["fwd"] / 1e3
-        gb_w = 4 * (M * K + M * N) / res["dw"] / 1e3
+        gb_f = 4 * P * (M * K + M * N) / res["fwd"] / 1e3
+        gb_w = 4 * P * (M * K + M * N) / res["dw"] / 1e3
         print(f"{name:6s} {M:5d} {K:4d} {N:4d} | {res['pack']:7.2f} {res['fwd']:7.2f} {res['dx']:7.2f} {res['dw']:7.2f} us | {gb_f:8.0f} {gb_w:8.0f}")
 
 
