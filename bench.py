@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    ap.add_argument("--roofline-only", action="store_true", help="skip the step timing")
+    ap.add_argument("--progress", action="store_true", help="progress lines on stderr")
     return ap.parse_args()
 
 
@@ -80,7 +82,7 @@ PASSES = 3
 PASS_BITS = [2, 1, 1]  # teacher, student, an SP pass at 1 bit
 
 
-def roofline(batch, frames, dev, reps=20):
+def roofline(batch, frames, dev, reps=20, log=lambda m: None):
     """Time each BitLinear kernel family at the step's stacked shapes with HIP events on the
     launch stream (kernels captured in a HIP graph and replayed, so the events bracket
     device time, not Python launch gaps); the dominant family (largest time per step) is
@@ -146,7 +148,12 @@ def roofline(batch, frames, dev, reps=20):
             e1.synchronize()
             return e0.elapsed_time(e1) * 1e3 / reps  # us per launch
 
-        t_f, t_dx, t_dw = timed(fwd), timed(bdx), timed(bdw)
+        log(f"roofline {name}: fwd")
+        t_f = timed(fwd)
+        log(f"roofline {name}: dx")
+        t_dx = timed(bdx)
+        log(f"roofline {name}: dw")
+        t_dw = timed(bdw)
         cw = 4 * N * ((K + 15) // 16)
         rows = P * M
         by_f = 4 * (rows * K + rows * N + N) + 2 * cw      # X, Y, bias, codes (2 bitwidths)
@@ -248,6 +255,11 @@ def cpu_baseline(seconds: float):
 
 
 # ------------------------------------------------------------------------- main
+def log(args, msg):
+    if args.progress:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -295,8 +307,15 @@ def main():
         def step():
             return gs.step(batch, sample_sp_mask(n_layers, generator=sp_gen))
 
-    for _ in range(max(args.warmup, 1)):  # graph mode: the first call captures
+    if args.roofline_only:
+        roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
+        print(json.dumps({"roofline": roof}), flush=True)
+        return
+    log(args, "model built; first step (graph mode: warm-up steps + capture)")
+    for i in range(max(args.warmup, 1)):  # graph mode: the first call captures
         loss, _ = step()
+        torch.cuda.synchronize()
+        log(args, f"warm-up step {i} done, loss {loss.item():.4f}")
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -305,6 +324,7 @@ def main():
     for _ in range(args.steps):
         loss, _ = step()
     torch.cuda.synchronize()
+    log(args, "timed steps done")
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -338,7 +358,7 @@ def main():
         "final_loss": round(loss_val, 4),
     }
     if rank == 0 and world == 1 and not args.no_roofline:
-        roof = roofline(args.batch, args.frames, dev)
+        roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
         roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
         out["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
