@@ -307,6 +307,56 @@ int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets, const int64_
   return launched();
 }
 
+namespace {
+int relattn_check(int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop) {
+  if (Bt < 1 || P < 1 || Bt % P != 0 || H < 1 || !relattn_supported(T, d)) return OB_ERR_SHAPE;
+  if (Bt > 65535 || H > 65535 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+  return OB_OK;
+}
+}  // namespace
+
+int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
+                   const float* u, const float* vb, const int32_t* lens, int64_t Bt, int64_t P,
+                   int64_t T, int64_t H, int64_t d, float p_drop, const int64_t* rng,
+                   float* probs, float* ctx, void* stream) {
+  if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
+  if (!q || !k || !v || !pos || !u || !vb || !lens || !ctx || (p_drop > 0.0f && !rng))
+    return OB_ERR_NULL;
+  launch_relattn_fwd(q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop,
+                     reinterpret_cast<const uint64_t*>(rng), probs, ctx, as_stream(stream));
+  return launched();
+}
+
+size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
+  if (Bt < 1 || H < 1 || !relattn_supported(T, d)) return 0;
+  return align_up(relattn_bwd_workspace(Bt, T, H, d));
+}
+
+int ob_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
+                   const float* pos, const float* u, const float* vb, const int32_t* lens,
+                   int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
+                   const int64_t* rng, const float* probs, float* dq, float* dk, float* dv,
+                   float* dpos, float* du, float* dvb, void* ws, size_t ws_bytes, void* stream) {
+  if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
+  if (!dctx || !q || !k || !v || !pos || !u || !vb || !lens || !probs || !dq || !dk || !dv ||
+      !dpos || !du || !dvb || !ws || (p_drop > 0.0f && !rng))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_relattn_bwd_workspace(Bt, T, H, d)) return OB_ERR_WORKSPACE;
+  launch_relattn_bwd(dctx, q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop,
+                     reinterpret_cast<const uint64_t*>(rng), probs, dq, dk, dv, dpos, du, dvb, ws,
+                     as_stream(stream));
+  return launched();
+}
+
+int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, uint8_t* out,
+                            void* stream) {
+  if (n < 0 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+  if ((n > 0 && !out) || (p_drop > 0.0f && !rng)) return OB_ERR_NULL;
+  launch_relattn_dropout_mask(n, p_drop, reinterpret_cast<const uint64_t*>(rng), out,
+                              as_stream(stream));
+  return launched();
+}
+
 int64_t ob_adamw_plan(const int64_t* numels, int64_t n_tensors, int64_t* chunk_map) {
   if (!numels || n_tensors < 1) return OB_ERR_SHAPE;
   for (int64_t t = 0; t < n_tensors; ++t)

@@ -98,4 +98,19 @@ void launch_adamw(const AdamwTensor* tab, const int64_t* map, int64_t nb, const 
                   double weight_decay, double max_norm, float* total_norm_out, void* ws,
                   hipStream_t s);
 
+// relattn.hip (fused relative-position attention core of MHSA)
+bool relattn_supported(int64_t T, int64_t d);
+size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
+void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
+                        const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
+                        int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
+                        float* probs, float* ctx, hipStream_t s);
+void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
+                        const float* pos, const float* u, const float* vb, const int* lens,
+                        int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
+                        const uint64_t* rng, const float* probs, float* dq, float* dk, float* dv,
+                        float* dpos, float* du, float* dvb, void* ws, hipStream_t s);
+void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,
+                                 hipStream_t s);
+
 }  // namespace ob

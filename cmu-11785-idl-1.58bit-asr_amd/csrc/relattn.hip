@@ -1,0 +1,586 @@
+// relattn.hip — the relative-position attention core of MHSA, fused (forward + backward).
+//
+// Reference: onebit_asr/conformer.py:115-130 (MHSA.forward between the projections):
+//   ac = (q + u) k^T                    matrix_ac
+//   bd = rel_shift((q + v) p^T)         matrix_bd, rel_shift of :97-103
+//   S  = (ac + bd) / sqrt(d); S[i][j] = -inf where frame i or j is padding (mask :121-122)
+//   A  = nan_to_num(softmax(S))         fully masked rows -> 0 (:123-125)
+//   A  = dropout(A); ctx = A v          (:126-127)
+// torch materialises ac, bd (padded, shifted copies), S, A and the dropout mask as
+// [B,H,T,T] fp32 tensors, ~10 full passes per block per pass. Here the forward is one
+// kernel that keeps a query tile's scores in registers and writes only ctx and the
+// softmax probabilities (kept for the backward); the backward is one kernel plus a small
+// fixed-order reduction, writing dq, dk, dv, dpos, du, dv_bias.
+//
+// rel_shift as a gather: with X = (q + v) p^T,
+//   bd[i][j] = X[i][T-1-i+j]   (j <= i);   0   (j == i+1);   X[i+1][j-i-2]   (j >= i+2)
+// and its adjoint: dX[i][m] = dbd[i][m-T+1+i] (m >= T-1-i), else dbd[i-1][m+i+1] (i >= 1).
+//
+// Layout: q, k, v, ctx, dq, dk, dv [Bt][T][H*d]; pos, dpos [P][T][H*d] (batch row b uses
+// pass b / (Bt/P)); u, vb, du, dvb [H][d]; probs [Bt][H][T][T]; lens int32 [Bt].
+// Products on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, like torch's fp32 matmul).
+// Dropout keeps (i, j) when hash(seed, counter, index) >= p * 2^32 (a counter-based hash:
+// the backward regenerates the same mask; torch's own RNG stream is not reproduced).
+#include <math.h>
+
+#include "ob_launch.h"
+
+namespace ob {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kTile = 64;  // query rows per block (16 per wave)
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t ctr, uint64_t idx) {
+  uint64_t x = idx * 0x9E3779B97F4A7C15ull ^ (seed + ctr * 0xD1B54A32D192ED03ull);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)(x >> 32);
+}
+
+struct DropCfg {
+  uint32_t thresh;  // keep iff hash >= thresh
+  float scale;      // 1 / (1 - p)
+  int on;
+};
+
+// ------------------------------------------------------------------------------------
+// Forward: block = (query tile of 64, head, batch row). X rows i0 .. i0+64 live in LDS
+// (row 64 = the next tile's first query, needed by the j >= i+2 branch of rel_shift).
+// ------------------------------------------------------------------------------------
+template <int DQ, int NTT>
+__global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ pos, const float* __restrict__ u, const float* __restrict__ vbias,
+    const int* __restrict__ lens, int Bp, int T, int H, float sqrt_d, DropCfg dc,
+    const uint64_t* __restrict__ rng, float* __restrict__ probs, float* __restrict__ ctx) {
+  constexpr int D = 4 * DQ;
+  constexpr int CT = (D + 15) / 16;
+  extern __shared__ float xs[];
+  const int nt = (T + 15) >> 4;
+  const int ldx = 16 * nt + 1;
+  const int b = blockIdx.z, h = blockIdx.y, i0 = blockIdx.x * kTile;
+  const int pass = b / Bp;
+  const int C = H * D;
+  const int L = min(lens[b], T);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const float* qb = q + (size_t)b * T * C + h * D;
+  const float* kb = k + (size_t)b * T * C + h * D;
+  const float* vbp = v + (size_t)b * T * C + h * D;
+  const float* pb = pos + (size_t)pass * T * C + h * D;
+  const float* ub = u + h * D;
+  const float* vbb = vbias + h * D;
+
+  const int qi = i0 + 16 * w + r;  // this lane's query row (scores phase)
+  const int qic = min(qi, T - 1);
+  float qu[DQ], qv[DQ];
+#pragma unroll
+  for (int s = 0; s < DQ; ++s) {
+    const int c = g * DQ + s;
+    const float x = qb[(size_t)qic * C + c];
+    qu[s] = x + ub[c];
+    qv[s] = x + vbb[c];
+  }
+
+  // X = (q + v) p^T for the wave's 16 rows: D[m][query] with A = p rows, B = (q+v)
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* prow = pb + (size_t)min(16 * t + r, T - 1) * C + g * DQ;
+#pragma unroll
+    for (int s = 0; s < DQ; ++s) acc = mfma4(prow[s], qv[s], acc);
+    float* dst = xs + (16 * w + r) * ldx + 16 * t + 4 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = acc[j];
+  }
+  // row 64: the next tile's first query (fp32 fma chain on the VALU)
+  if (i0 + kTile < T) {
+    const float* qe = qb + (size_t)(i0 + kTile) * C;
+    for (int m = threadIdx.x; m < T; m += kThreads) {
+      const float* prow = pb + (size_t)m * C;
+      float a = 0.0f;
+      for (int c = 0; c < D; ++c) a = fmaf(qe[c] + vbb[c], prow[c], a);
+      xs[kTile * ldx + m] = a;
+    }
+  }
+  __syncthreads();
+
+  // scores for (query r, keys 16t+4g+j): ac by MFMA (A = k rows, B = q+u), bd gathered
+  float sreg[NTT][4];
+  float mx = -INFINITY;
+  const float* xrow = xs + (16 * w + r) * ldx;
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* krow = kb + (size_t)min(16 * t + r, T - 1) * C + g * DQ;
+#pragma unroll
+    for (int s = 0; s < DQ; ++s) acc = mfma4(krow[s], qu[s], acc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int jj = 16 * t + 4 * g + j;
+      float bd;
+      if (jj <= qi) bd = xrow[max(T - 1 - qi + jj, 0)];
+      else if (jj == qi + 1) bd = 0.0f;
+      else bd = xrow[ldx + (jj - qi - 2)];
+      const float sc = (acc[j] + bd) / sqrt_d;
+      const bool valid = qi < L && jj < L;
+      sreg[t][j] = valid ? sc : -INFINITY;
+      mx = fmaxf(mx, sreg[t][j]);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  float sum = 0.0f;
+  const bool row_live = mx != -INFINITY;  // all -inf -> softmax NaN -> nan_to_num 0
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float e = row_live ? expf(sreg[t][j] - mx) : 0.0f;
+      sreg[t][j] = e;
+      sum += e;
+    }
+  }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const uint64_t seed = dc.on ? rng[0] : 0, ctr = dc.on ? rng[1] : 0;
+  const size_t prow_off = (((size_t)b * H + h) * T + qic) * T;
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int jj = 16 * t + 4 * g + j;
+      const float pr = row_live ? sreg[t][j] / sum : 0.0f;
+      if (probs && qi < T && jj < T) probs[prow_off + jj] = pr;
+      float pd = pr;
+      if (dc.on) {
+        const bool keep = drop_hash(seed, ctr, prow_off + jj) >= dc.thresh;
+        pd = keep ? pr * dc.scale : 0.0f;
+      }
+      sreg[t][j] = pd;
+    }
+  }
+
+  // ctx = A v: A = the lane's probabilities (row r, k = 4g+j of tile t), B = v rows
+  f32x4 o[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = min(16 * t + 4 * g + j, T - 1);
+      const float* vrow = vbp + (size_t)key * C;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) o[ct] = mfma4(sreg[t][j], vrow[min(16 * ct + r, D - 1)], o[ct]);
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = 16 * ct + r;
+    if (col >= D) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = i0 + 16 * w + 4 * g + j;
+      if (row < T) ctx[((size_t)b * T + row) * C + h * D + col] = o[ct][j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Backward: block = (query tile, head, batch row). dq is final; dk, dv, dpos, du, dvb
+// are written as per-tile partials and summed by relattn_reduce_kernel in fixed order.
+// LDS holds dS' = dS / sqrt(d) for query rows i0-1 .. i0+63 (row 0 = i0-1, recomputed
+// here on the VALU) -- the rows the rel_shift adjoint of the tile needs.
+// ------------------------------------------------------------------------------------
+template <int DQ, int NTT>
+__global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
+    const float* __restrict__ dctx, const float* __restrict__ q, const float* __restrict__ k,
+    const float* __restrict__ v, const float* __restrict__ pos, const float* __restrict__ u,
+    const float* __restrict__ vbias, const int* __restrict__ lens, int Bp, int T, int H,
+    float sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, const float* __restrict__ probs,
+    float* __restrict__ dq, float* __restrict__ dk_part, float* __restrict__ dv_part,
+    float* __restrict__ dp_part, float* __restrict__ du_part, float* __restrict__ dvb_part) {
+  constexpr int D = 4 * DQ;
+  constexpr int CT = (D + 15) / 16;
+  extern __shared__ float ds[];
+  __shared__ float red[kThreads / 64][2][64];
+  __shared__ float rsum[kThreads / 64];
+  const int nt = (T + 15) >> 4;
+  const int ldx = 16 * nt + 1;
+  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x, i0 = qt * kTile;
+  const int nqt = gridDim.x;
+  const int Bt = gridDim.z;
+  const int pass = b / Bp;
+  const int C = H * D;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const size_t bo = (size_t)b * T * C + h * D;
+  const float* qb = q + bo;
+  const float* kb = k + bo;
+  const float* vbp = v + bo;
+  const float* dob = dctx + bo;
+  const float* pb = pos + (size_t)pass * T * C + h * D;
+  const float* ub = u + h * D;
+  const float* vbb = vbias + h * D;
+  const float* prb = probs + ((size_t)b * H + h) * T * T;
+  const uint64_t seed = dc.on ? rng[0] : 0, ctr = dc.on ? rng[1] : 0;
+  const size_t pbase = ((size_t)b * H + h) * T * T;
+  auto keep_scale = [&](int i, int j) -> float {
+    if (!dc.on) return 1.0f;
+    return drop_hash(seed, ctr, pbase + (size_t)i * T + j) >= dc.thresh ? dc.scale : 0.0f;
+  };
+
+  const int qi = i0 + 16 * w + r;
+  const int qic = min(qi, T - 1);
+  float dor[DQ];
+#pragma unroll
+  for (int s = 0; s < DQ; ++s) dor[s] = dob[(size_t)qic * C + g * DQ + s];
+
+  // dPd[query r][key] = dO . v (A = v rows, B = dO row), P from the forward
+  float dsr[NTT][4];
+  float rowdot = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* vrow = vbp + (size_t)min(16 * t + r, T - 1) * C + g * DQ;
+#pragma unroll
+    for (int s = 0; s < DQ; ++s) acc = mfma4(vrow[s], dor[s], acc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int jj = 16 * t + 4 * g + j;
+      const float p = (qi < T && jj < T) ? prb[(size_t)qi * T + jj] : 0.0f;
+      const float dp = acc[j] * keep_scale(qic, jj);  // dropout backward
+      dsr[t][j] = p;
+      acc[j] = dp;
+      rowdot += p * dp;
+    }
+    // dS needs the row sum first: park dP in this lane's own LDS cells meanwhile
+    float* dst = ds + (1 + 16 * w + r) * ldx + 16 * t + 4 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = acc[j];
+  }
+  rowdot += __shfl_xor(rowdot, 16);
+  rowdot += __shfl_xor(rowdot, 32);
+  // dS' = P (dP - rowdot) / sqrt(d)  (softmax backward, then the 1/sqrt(d) of :120)
+  const float* dprow = ds + (1 + 16 * w + r) * ldx;
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int jj = 16 * t + 4 * g + j;
+      const float dp = dprow[jj];
+      dsr[t][j] = (dsr[t][j] * (dp - rowdot)) / sqrt_d;
+    }
+  }
+  // (each lane rewrites exactly the LDS cells it wrote: no barrier needed in between)
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+    float* dst = ds + (1 + 16 * w + r) * ldx + 16 * t + 4 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = dsr[t][j];
+  }
+
+  // row i0-1 (LDS row 0) on the VALU, the same formula
+  if (i0 > 0) {
+    const int ip = i0 - 1;
+    float part = 0.0f;
+    for (int jj = threadIdx.x; jj < T; jj += kThreads) {
+      const float* vrow = vbp + (size_t)jj * C;
+      const float* drow = dob + (size_t)ip * C;
+      float a = 0.0f;
+      for (int c = 0; c < D; ++c) a = fmaf(vrow[c], drow[c], a);
+      const float dp = a * keep_scale(ip, jj);
+      const float p = prb[(size_t)ip * T + jj];
+      ds[jj] = dp;
+      part += p * dp;
+    }
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) rsum[w] = part;
+    __syncthreads();
+    const float rd = ((rsum[0] + rsum[1]) + rsum[2]) + rsum[3];
+    for (int jj = threadIdx.x; jj < T; jj += kThreads) {
+      const float p = prb[(size_t)ip * T + jj];
+      ds[jj] = (p * (ds[jj] - rd)) / sqrt_d;
+    }
+  }
+  __syncthreads();
+
+  // dQu = dS' k (A = dS' row r, k = 4g+j of tile t; B = k rows)
+  f32x4 oq[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) oq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NTT; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = min(16 * t + 4 * g + j, T - 1);
+      const float* krow = kb + (size_t)key * C;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) oq[ct] = mfma4(dsr[t][j], krow[min(16 * ct + r, D - 1)], oq[ct]);
+    }
+  }
+  // dQv = dX p, dX gathered from LDS by the rel_shift adjoint
+  f32x4 ov[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) ov[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* row_i = ds + (1 + 16 * w + r) * ldx;  // dS' row qi
+  const float* row_im1 = row_i - ldx;                 // dS' row qi-1
+  auto dX = [&](int i, const float* ri, const float* rim1, int m) -> float {
+    if (m >= T - 1 - i) return ri[m - T + 1 + i];
+    return i >= 1 ? rim1[m + i + 1] : 0.0f;
+  };
+  const int nk = (T + 3) >> 2;
+  for (int mk = 0; mk < nk; ++mk) {
+    const int m = 4 * mk + g;
+    const float a = (qi < T && m < T) ? dX(qi, row_i, row_im1, m) : 0.0f;
+    const float* prow = pb + (size_t)min(m, T - 1) * C;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) ov[ct] = mfma4(a, prow[min(16 * ct + r, D - 1)], ov[ct]);
+  }
+  // dq = dQu + dQv; per-tile column sums of dQu / dQv for du / dvb
+  float su[CT], sv[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = 16 * ct + r;
+    su[ct] = 0.0f;
+    sv[ct] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = i0 + 16 * w + 4 * g + j;
+      if (row < T) {
+        su[ct] += oq[ct][j];
+        sv[ct] += ov[ct][j];
+        if (col < D) dq[bo + (size_t)row * C + col] = oq[ct][j] + ov[ct][j];
+      }
+    }
+    su[ct] += __shfl_xor(su[ct], 16);
+    su[ct] += __shfl_xor(su[ct], 32);
+    sv[ct] += __shfl_xor(sv[ct], 16);
+    sv[ct] += __shfl_xor(sv[ct], 32);
+  }
+  const size_t tile_id = ((size_t)b * H + h) * nqt + qt;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = 16 * ct + r;
+    if (g == 0 && col < D) {
+      red[w][0][col] = su[ct];
+      red[w][1][col] = sv[ct];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < D) {
+    const int c = threadIdx.x;
+    du_part[tile_id * D + c] = ((red[0][0][c] + red[1][0][c]) + red[2][0][c]) + red[3][0][c];
+    dvb_part[tile_id * D + c] = ((red[0][1][c] + red[1][1][c]) + red[2][1][c]) + red[3][1][c];
+  }
+
+  // key-side partials over this tile's 64 queries; wave w takes key tiles t = w, w+4, ...
+  // dK = dS'^T (q+u), dV = Pd^T dO, dpos = dX^T (q+v)
+  const size_t part_base = ((size_t)qt * Bt + b) * H + h;  // [qt][b][h] then [T][D]
+  for (int t = w; t < nt; t += 4) {
+    f32x4 ak[CT], av[CT], ap[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      ak[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      av[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int key = 16 * t + r;  // A row = key (or position m) r of the tile
+    for (int qk = 0; qk < kTile / 4; ++qk) {
+      const int qrow = i0 + 4 * qk + g;  // k index = query
+      const bool qok = qrow < T;
+      const int qrc = min(qrow, T - 1);
+      const float* lrow = ds + (1 + 4 * qk + g) * ldx;  // dS' row qrow
+      const float a_k = (qok && key < T) ? lrow[key] : 0.0f;
+      const float pv = (qok && key < T) ? prb[(size_t)qrow * T + key] : 0.0f;
+      const float a_v = pv * keep_scale(qrc, min(key, T - 1));
+      const float a_p = (qok && key < T) ? dX(qrow, lrow, lrow - ldx, key) : 0.0f;
+      const float* qrowp = qb + (size_t)qrc * C;
+      const float* drowp = dob + (size_t)qrc * C;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c = min(16 * ct + r, D - 1);
+        const float qx = qrowp[c];
+        ak[ct] = mfma4(a_k, qx + ub[c], ak[ct]);
+        av[ct] = mfma4(a_v, drowp[c], av[ct]);
+        ap[ct] = mfma4(a_p, qx + vbb[c], ap[ct]);
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int col = 16 * ct + r;
+      if (col >= D) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = 16 * t + 4 * g + j;
+        if (kk >= T) continue;
+        const size_t o = (part_base * T + kk) * D + col;
+        dk_part[o] = ak[ct][j];
+        dv_part[o] = av[ct][j];
+        dp_part[o] = ap[ct][j];
+      }
+    }
+  }
+}
+
+// dk, dv [Bt][T][H*D]: sum over query tiles; dpos [P][T][H*D]: over the pass's rows and
+// tiles; du, dvb [H][D]: over rows and tiles. Thread per output element, fixed order.
+__global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
+    const float* __restrict__ dk_part, const float* __restrict__ dv_part,
+    const float* __restrict__ dp_part, const float* __restrict__ du_part,
+    const float* __restrict__ dvb_part, int Bt, int P, int T, int H, int D, int nqt,
+    float* __restrict__ dk, float* __restrict__ dv, float* __restrict__ dpos,
+    float* __restrict__ du, float* __restrict__ dvb) {
+  const int C = H * D;
+  const int64_t n_kv = (int64_t)Bt * T * C;
+  const int64_t n_p = (int64_t)P * T * C;
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int Bp = Bt / P;
+  if (e < n_kv) {
+    const int b = (int)(e / ((int64_t)T * C));
+    const int rem = (int)(e - (int64_t)b * T * C);
+    const int t = rem / C, hc = rem - t * C, h = hc / D, c = hc - h * D;
+    float sk = 0.0f, sv = 0.0f;
+    for (int qt = 0; qt < nqt; ++qt) {
+      const size_t o = (((((size_t)qt * Bt + b) * H + h) * T) + t) * D + c;
+      sk += dk_part[o];
+      sv += dv_part[o];
+    }
+    dk[e] = sk;
+    dv[e] = sv;
+  } else if (e < n_kv + n_p) {
+    const int64_t f = e - n_kv;
+    const int p = (int)(f / ((int64_t)T * C));
+    const int rem = (int)(f - (int64_t)p * T * C);
+    const int t = rem / C, hc = rem - t * C, h = hc / D, c = hc - h * D;
+    float s = 0.0f;
+    for (int b = p * Bp; b < (p + 1) * Bp; ++b)
+      for (int qt = 0; qt < nqt; ++qt)
+        s += dp_part[(((((size_t)qt * Bt + b) * H + h) * T) + t) * D + c];
+    dpos[f] = s;
+  } else if (e < n_kv + n_p + 2 * C) {
+    const int f = (int)(e - n_kv - n_p);
+    const int which = f / C, hc = f - which * C, h = hc / D, c = hc - h * D;
+    const float* src = which == 0 ? du_part : dvb_part;
+    float s = 0.0f;
+    for (int b = 0; b < Bt; ++b)
+      for (int qt = 0; qt < nqt; ++qt) s += src[(((size_t)b * H + h) * nqt + qt) * D + c];
+    (which == 0 ? du : dvb)[hc] = s;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropCfg dc,
+                                                                const uint64_t* __restrict__ rng,
+                                                                uint8_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= n) return;
+  out[e] = (!dc.on || drop_hash(rng[0], rng[1], (uint64_t)e) >= dc.thresh) ? 1 : 0;
+}
+
+DropCfg make_drop(float p_drop) {
+  DropCfg dc;
+  dc.on = p_drop > 0.0f ? 1 : 0;
+  double t = (double)p_drop * 4294967296.0;
+  if (t > 4294967295.0) t = 4294967295.0;
+  dc.thresh = (uint32_t)t;
+  dc.scale = p_drop > 0.0f ? (float)(1.0 / (1.0 - (double)p_drop)) : 1.0f;
+  return dc;
+}
+
+size_t lds_bytes(int T) { return sizeof(float) * (size_t)(kTile + 1) * (16 * ((T + 15) / 16) + 1); }
+
+}  // namespace
+
+bool relattn_supported(int64_t T, int64_t d) {
+  return T >= 1 && T <= 512 && (d == 16 || d == 32 || d == 36 || d == 64);
+}
+
+size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
+  const int64_t nqt = (T + kTile - 1) / kTile;
+  return sizeof(float) * (size_t)(3 * nqt * Bt * H * T * d + 2 * Bt * H * nqt * d + 64);
+}
+
+#define OB_RA_DISPATCH(KERNEL)                 \
+  do {                                         \
+    const bool big = T > 256;                  \
+    if (d == 16) {                             \
+      if (big) KERNEL(4, 32); else KERNEL(4, 16);   \
+    } else if (d == 32) {                      \
+      if (big) KERNEL(8, 32); else KERNEL(8, 16);   \
+    } else if (d == 36) {                      \
+      if (big) KERNEL(9, 32); else KERNEL(9, 16);   \
+    } else {                                   \
+      if (big) KERNEL(16, 32); else KERNEL(16, 16); \
+    }                                          \
+  } while (0)
+
+void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
+                        const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
+                        int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
+                        float* probs, float* ctx, hipStream_t s) {
+  const dim3 grid((unsigned)((T + kTile - 1) / kTile), (unsigned)H, (unsigned)Bt);
+  const DropCfg dc = make_drop(p_drop);
+  const float sqrt_d = (float)sqrt((double)d);
+  const size_t lds = lds_bytes((int)T);
+#define OB_RA_FWD(DQ, NTT)                                                                 \
+  hipLaunchKernelGGL((relattn_fwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, q, k, v, pos, \
+                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, sqrt_d, dc, rng, probs, ctx)
+  OB_RA_DISPATCH(OB_RA_FWD);
+#undef OB_RA_FWD
+}
+
+void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
+                        const float* pos, const float* u, const float* vb, const int* lens,
+                        int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
+                        const uint64_t* rng, const float* probs, float* dq, float* dk, float* dv,
+                        float* dpos, float* du, float* dvb, void* ws, hipStream_t s) {
+  const int nqt = (int)((T + kTile - 1) / kTile);
+  const dim3 grid((unsigned)nqt, (unsigned)H, (unsigned)Bt);
+  const DropCfg dc = make_drop(p_drop);
+  const float sqrt_d = (float)sqrt((double)d);
+  const size_t lds = lds_bytes((int)T);
+  float* dk_part = (float*)ws;
+  float* dv_part = dk_part + (size_t)nqt * Bt * H * T * d;
+  float* dp_part = dv_part + (size_t)nqt * Bt * H * T * d;
+  float* du_part = dp_part + (size_t)nqt * Bt * H * T * d;
+  float* dvb_part = du_part + (size_t)Bt * H * nqt * d;
+#define OB_RA_BWD(DQ, NTT)                                                                     \
+  hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, q, k, v,  \
+                     pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, sqrt_d, dc, rng, probs, dq, \
+                     dk_part, dv_part, dp_part, du_part, dvb_part)
+  OB_RA_DISPATCH(OB_RA_BWD);
+#undef OB_RA_BWD
+  const int64_t C = H * d;
+  const int64_t total = Bt * T * C + P * T * C + 2 * C;
+  hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, dk_part, dv_part, dp_part, du_part, dvb_part, (int)Bt,
+                     (int)P, (int)T, (int)H, (int)d, nqt, dk, dv, dpos, du, dvb);
+}
+
+void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,
+                                 hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(relattn_mask_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, n, make_drop(p_drop), rng, out);
+}
+
+}  // namespace ob

@@ -1,0 +1,117 @@
+"""Fused relative-position attention core of MHSA on the HIP library.
+
+Reference: onebit_asr/conformer.py:115-127 (between MHSA's projections and out_proj):
+``((q+u) k^T + rel_shift((q+v) p^T)) / sqrt(d)``, padding masked to -inf, softmax,
+``nan_to_num``, dropout, ``A v``. ``rel_pos_attention`` computes exactly that from the
+projection outputs in their natural [B, T, H*d] layout and returns the context in the
+layout out_proj consumes, with one forward kernel and one backward kernel (+ a small
+reduction); see csrc/relattn.hip. Gradients flow to q, k, v, pos, pos_bias_u, pos_bias_v.
+
+Dropout uses the kernels' counter-based hash (seed, counter) per device; the counter
+advances on the device each call, so a captured step draws a fresh mask on every replay.
+The mask is not torch's RNG stream (no reference-visible quantity depends on it).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict
+
+import torch
+
+from . import _lib
+
+__all__ = ["rel_pos_attention", "fused_attention_supported", "dropout_mask"]
+
+_RNG: Dict[torch.device, torch.Tensor] = {}
+
+
+def fused_attention_supported(q: torch.Tensor, d_head: int) -> bool:
+    if os.environ.get("OB_ATTN", "") == "torch":
+        return False
+    return (q.is_cuda and q.dtype == torch.float32 and 1 <= q.size(1) <= 512
+            and d_head in (16, 32, 36, 64))
+
+
+def _rng_state(device: torch.device) -> torch.Tensor:
+    st = _RNG.get(device)
+    if st is None:
+        seed = int(torch.initial_seed()) & ((1 << 62) - 1)
+        st = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+        _RNG[device] = st
+    return st
+
+
+class _RelAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, pos, u, vb, lens, n_heads, p_drop, rng):
+        bt, t, c = q.shape
+        P = pos.size(0)
+        d = c // n_heads
+        out = torch.empty_like(q)
+        need = any(ctx.needs_input_grad[:6])
+        probs = torch.empty((bt, n_heads, t, t), dtype=torch.float32, device=q.device) if need else None
+        lib = _lib.load()
+        _lib.check(
+            lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
+                               u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt, P, t, n_heads, d,
+                               p_drop, _lib.ptr(rng), _lib.ptr(probs), out.data_ptr(),
+                               _lib.stream_of(q)),
+            "ob_relattn_fwd",
+        )
+        ctx.meta = (n_heads, p_drop)
+        if need:
+            ctx.save_for_backward(q, k, v, pos, u, vb, lens, probs, rng)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, pos, u, vb, lens, probs, rng = ctx.saved_tensors
+        n_heads, p_drop = ctx.meta
+        g = g.contiguous()
+        bt, t, c = q.shape
+        P = pos.size(0)
+        d = c // n_heads
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        dpos = torch.empty_like(pos)
+        du, dvb = torch.empty_like(u), torch.empty_like(vb)
+        lib = _lib.load()
+        wsb = lib.ob_relattn_bwd_workspace(bt, t, n_heads, d)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=q.device)
+        _lib.check(
+            lib.ob_relattn_bwd(g.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                               pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt,
+                               P, t, n_heads, d, p_drop, _lib.ptr(rng), probs.data_ptr(),
+                               dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(),
+                               du.data_ptr(), dvb.data_ptr(), ws.data_ptr(), wsb,
+                               _lib.stream_of(g)),
+            "ob_relattn_bwd",
+        )
+        return dq, dk, dv, dpos, du, dvb, None, None, None, None
+
+
+def rel_pos_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos: torch.Tensor,
+                      pos_bias_u: torch.Tensor, pos_bias_v: torch.Tensor, lens: torch.Tensor,
+                      n_heads: int, dropout_p: float = 0.0) -> torch.Tensor:
+    """q, k, v [Bt, T, H*d]; pos [P, T, H*d] (Bt = P * B, batch row b uses pass b // B);
+    pos_bias_u/v [H, d]; lens int [Bt] valid frames. Returns the context [Bt, T, H*d]."""
+    q, k, v, pos = (x.contiguous() for x in (q, k, v, pos))
+    lens = lens.to(torch.int32).contiguous()
+    rng = None
+    if dropout_p > 0:
+        st = _rng_state(q.device)
+        st[1:].add_(1)          # a fresh mask per call (also on graph replay)
+        rng = st.clone()        # the backward regenerates this call's mask
+    return _RelAttnFn.apply(q, k, v, pos, pos_bias_u.contiguous(), pos_bias_v.contiguous(), lens,
+                            n_heads, float(dropout_p), rng)
+
+
+def dropout_mask(shape, p: float, rng: torch.Tensor) -> torch.Tensor:
+    """The keep-mask (uint8, 1 = kept) the kernels draw for probs of ``shape`` (tests)."""
+    n = 1
+    for s in shape:
+        n *= s
+    out = torch.empty(n, dtype=torch.uint8, device=rng.device)
+    lib = _lib.load()
+    _lib.check(lib.ob_relattn_dropout_mask(n, float(p), rng.data_ptr(), out.data_ptr(),
+                                           _lib.stream_of(rng)), "ob_relattn_dropout_mask")
+    return out.view(*shape)

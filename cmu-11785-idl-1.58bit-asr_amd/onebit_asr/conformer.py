@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .attention import fused_attention_supported, rel_pos_attention
 from .conv import depthwise_conv1d
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
@@ -143,10 +144,36 @@ class MHSA(nn.Module):
     def _heads(self, t: torch.Tensor, batch: int) -> torch.Tensor:
         return t.view(batch, -1, self.n_heads, self.d_head).transpose(1, 2)
 
+    def _fused(self, x, h, mask, bitwidth, pos_emb):
+        """The same computation with the attention core in one HIP kernel per direction
+        (onebit_asr/attention.py); used on a ROCm device for supported shapes."""
+        bsz, tlen, width = x.shape
+        qp = self.q_proj(h, bitwidth)
+        kp = self.k_proj(h, bitwidth)
+        vp = self.v_proj(h, bitwidth)
+        if isinstance(bitwidth, PassBits):
+            P = bitwidth.passes
+            pe = pos_emb.expand(P, tlen, width).reshape(P * tlen, width)
+            pp = self.pos_proj(pe, bitwidth).view(P, tlen, width)
+        else:
+            pp = self.pos_proj(pos_emb, bitwidth).view(1, tlen, width)
+        if mask is None:
+            lens = torch.full((bsz,), tlen, dtype=torch.int32, device=x.device)
+        else:
+            lens = getattr(mask, "_ob_lens", None)
+            if lens is None:  # prefix masks (valid_i & valid_j): row 0 column = valid frames
+                lens = mask[:, :, 0].sum(dim=1)
+        ctx = rel_pos_attention(qp, kp, vp, pp, self.pos_bias_u, self.pos_bias_v, lens,
+                                self.n_heads, self.dropout.p if self.training else 0.0)
+        out = self.dropout(self.out_proj(ctx, bitwidth))
+        return x + _pad_rows(out, mask)
+
     def forward(self, x, mask, bitwidth: int, pos_emb: torch.Tensor):
         bsz, tlen, width = x.shape
         assert width == self.d_model, f"Expected {self.d_model}, got {width}"
         h = self.ln(x)
+        if fused_attention_supported(h, self.d_head):
+            return self._fused(x, h, mask, bitwidth, pos_emb)
         q = self._heads(self.q_proj(h, bitwidth), bsz)
         k = self._heads(self.k_proj(h, bitwidth), bsz)
         v = self._heads(self.v_proj(h, bitwidth), bsz)
@@ -295,6 +322,8 @@ class ConformerEncoder(nn.Module):
         frames = torch.arange(tsub, device=feats.device).unsqueeze(0)
         key_mask = frames < (feat_lens // 4).unsqueeze(1)            # [B, T'] bool
         attn_mask = key_mask.unsqueeze(2) & key_mask.unsqueeze(1)     # [B, T', T']
+        # valid frames per utterance, for the fused attention kernels (prefix masks)
+        attn_mask._ob_lens = key_mask.sum(dim=1, dtype=torch.int32)
         for blk, bw in zip(self.blocks, block_bitwidths(len(self.blocks), precision, sp_mask)):
             x = blk(x, attn_mask, bw, pos_emb)
         return self.ln_out(x), key_mask

@@ -193,6 +193,38 @@ OB_API int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P
                                       void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Relative-position attention core of MHSA.forward (onebit_asr/conformer.py:115-127),
+ * fused: ac = (q+u) k^T, bd = rel_shift((q+v) pos^T) (:97-103), S = (ac + bd) / sqrt(d),
+ * frames i or j >= lens[b] masked to -inf (:121-122), A = nan_to_num(softmax(S))
+ * (:123-125), A = dropout(A) (:126), ctx = A v (:127).
+ *   q, k, v, ctx, dq, dk, dv : [Bt][T][H*d]   (heads side by side, as the projections
+ *                              produce them and out_proj consumes them)
+ *   pos, dpos : [P][T][H*d]    (pass p = b / (Bt/P) for stacked passes; P = 1 otherwise)
+ *   u, vb, du, dvb : [H][d]    (pos_bias_u / pos_bias_v)
+ *   lens : DEVICE int32 [Bt]   (valid frames; the encoder's prefix masks)
+ *   probs : [Bt][H][T][T]      softmax before dropout; written by fwd when non-NULL,
+ *                              required by bwd
+ *   rng : DEVICE int64 [2] (seed, counter); dropout keeps element e of probs when
+ *         hash(seed, counter, e) >= p_drop * 2^32 (fwd and bwd regenerate the same mask;
+ *         ob_relattn_dropout_mask writes it out). Unused when p_drop == 0.
+ * Supported: 1 <= T <= 512, d in {16, 32, 36, 64}.
+ * ------------------------------------------------------------------------------------ */
+OB_API int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
+                          const float* u, const float* vb, const int32_t* lens, int64_t Bt,
+                          int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
+                          const int64_t* rng, float* probs, float* ctx, void* stream);
+OB_API size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
+OB_API int ob_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
+                          const float* pos, const float* u, const float* vb,
+                          const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H,
+                          int64_t d, float p_drop, const int64_t* rng, const float* probs,
+                          float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb,
+                          void* ws, size_t ws_bytes, void* stream);
+/* The dropout keep-mask (1 = kept) the attention kernels use, for n elements of probs. */
+OB_API int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, uint8_t* out,
+                                   void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Optimizer tail of the training step: clip_grad_norm_(params, max_norm) followed by
  * AdamW.step() (reference onebit_asr/train.py:116-118 with the optimizer of train.py:259:
  * betas (0.9, 0.98), eps 1e-8, weight_decay 1e-2). torch issues per-tensor launches for

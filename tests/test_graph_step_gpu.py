@@ -1,7 +1,8 @@
 """GraphedTrainStep (the whole 3-pass step + clip + AdamW as one HIP graph) on cfg1.
 
 * graph replay == the same step run eagerly: per-step loss and parts rel <= 1e-5,
-  parameters max|err| <= 1e-5 * max|p| + 1e-5 (Adam-amplified rounding);
+  parameters max|err| <= 1e-5 * max|p| + 1e-4 (Adam turns rounding-level gradient
+  differences of near-zero gradients into up to lr-sized steps; lr <= 5e-4 here);
 * == the reference-order eager ``train_step`` (non-capturable AdamW, Python-list SP mask):
   losses rel <= 1e-4 (capturable AdamW rounds its bias corrections differently);
 * a new SP mask and a new batch (same shape) take effect on replay without re-capture.
@@ -60,7 +61,7 @@ def test_graph_replay_matches_eager(gpu):
     # gradient differences, which Adam turns into <= lr-sized parameter differences.
     for (k, a), (_, b) in zip(m_g.named_parameters(), m_e.named_parameters()):
         err = (a - b).abs().max().item()
-        assert err <= 1e-5 * b.abs().max().item() + 1e-5, (k, err)
+        assert err <= 1e-5 * b.abs().max().item() + 1e-4, (k, err)
 
 
 def test_graph_matches_reference_step_order(gpu):
