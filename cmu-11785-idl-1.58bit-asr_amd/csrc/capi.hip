@@ -357,6 +357,15 @@ int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, uint8_t
   return launched();
 }
 
+int ob_embedding_bwd(const int64_t* indices, int64_t N, const float* grad, int64_t C,
+                     int64_t V, int64_t padding_idx, float* grad_weight, void* stream) {
+  if (N < 0 || V < 0 || !embed_supported(C) || padding_idx >= V) return OB_ERR_SHAPE;
+  if ((N > 0 && (!indices || !grad)) || (V > 0 && !grad_weight)) return OB_ERR_NULL;
+  if (!aligned4(grad) || !aligned4(grad_weight)) return OB_ERR_ALIGN;
+  launch_embed_bwd(indices, N, grad, C, V, padding_idx, grad_weight, as_stream(stream));
+  return launched();
+}
+
 int64_t ob_adamw_plan(const int64_t* numels, int64_t n_tensors, int64_t* chunk_map) {
   if (!numels || n_tensors < 1) return OB_ERR_SHAPE;
   for (int64_t t = 0; t < n_tensors; ++t)

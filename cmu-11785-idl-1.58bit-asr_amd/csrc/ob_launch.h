@@ -98,6 +98,11 @@ void launch_adamw(const AdamwTensor* tab, const int64_t* map, int64_t nb, const 
                   double weight_decay, double max_norm, float* total_norm_out, void* ws,
                   hipStream_t s);
 
+// embed.hip (deterministic token-embedding backward; pad < 0: no padding row)
+bool embed_supported(int64_t C);
+void launch_embed_bwd(const int64_t* idx, int64_t N, const float* g, int64_t C, int64_t V,
+                      int64_t pad, float* dW, hipStream_t s);
+
 // relattn.hip (fused relative-position attention core of MHSA)
 bool relattn_supported(int64_t T, int64_t d);
 size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);

@@ -75,6 +75,7 @@ SIGNATURES = {
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32,
                _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_relattn_dropout_mask": (_int, [_i64, _f32, _c_f, _c_f, _c_f]),
+    "ob_embedding_bwd": (_int, [_c_f, _i64, _c_f, _i64, _i64, _i64, _c_f, _c_f]),
     "ob_adamw_plan": (_i64, [_c_f, _i64, _c_f]),
     "ob_adamw_workspace": (_sz, [_i64]),
     "ob_adamw_clip_step": (

@@ -30,6 +30,7 @@ import torch.nn.functional as F
 
 from .attention import fused_attention_supported, rel_pos_attention
 from .conv import depthwise_conv1d
+from .embedding import embedding
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
 __all__ = [
@@ -349,7 +350,8 @@ class TransformerDecoder(nn.Module):
         # tgt_is_causal=True is what torch's _detect_is_causal_mask concludes for this mask in
         # the reference call; passing it skips that check's device->host sync (the
         # attention math is unchanged: the explicit mask is still used).
-        y = self.dec(self.emb(tgt_inp), memory, tgt_mask=causal,
+        tok = embedding(tgt_inp, self.emb.weight, self.emb.padding_idx)
+        y = self.dec(tok, memory, tgt_mask=causal,
                      memory_key_padding_mask=(memory_mask == 0),
                      tgt_key_padding_mask=tgt_key_padding_mask, tgt_is_causal=True)
         return self.out(self.ln(y))

@@ -224,6 +224,13 @@ OB_API int ob_relattn_bwd(const float* dctx, const float* q, const float* k, con
 OB_API int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, uint8_t* out,
                                    void* stream);
 
+/* Token-embedding backward of the decoder (conformer.py:279-299, nn.Embedding with
+ * padding_idx): grad_weight[v] = sum over n ascending with indices[n] == v of grad[n]
+ * (deterministic, graph-safe); grad_weight[padding_idx] = 0 (padding_idx < 0: none).
+ * indices int64 [N] in [0, V); grad [N][C]; grad_weight [V][C]; C <= 1024. */
+OB_API int ob_embedding_bwd(const int64_t* indices, int64_t N, const float* grad, int64_t C,
+                            int64_t V, int64_t padding_idx, float* grad_weight, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Optimizer tail of the training step: clip_grad_norm_(params, max_norm) followed by
  * AdamW.step() (reference onebit_asr/train.py:116-118 with the optimizer of train.py:259:

@@ -61,6 +61,9 @@ def test_graph_replay_matches_eager(gpu):
     # gradient differences, which Adam turns into <= lr-sized parameter differences.
     for (k, a), (_, b) in zip(m_g.named_parameters(), m_e.named_parameters()):
         err = (a - b).abs().max().item()
+        if any(n in k for n in ("k_proj.bias", "conv.dw.bias", "in_proj_bias")):
+            assert err <= 5 * 5e-4, (k, err)  # zero-gradient params: Adam steps on noise
+            continue
         assert err <= 1e-5 * b.abs().max().item() + 1e-4, (k, err)
 
 

@@ -7,6 +7,10 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+# parameters whose gradient is mathematically zero (softmax shift / BatchNorm follows):
+# what the two step forms produce there is rounding noise of different summation orders
+NOISE_ONLY = ("k_proj.bias", "conv.dw.bias", "in_proj_bias")
+
 
 def _model(gpu):
     from onebit_asr.conformer import ConformerASR
@@ -33,8 +37,12 @@ def test_stacked_equals_literal(gpu, sp_mask):
     assert abs(l1 - l0) <= 1e-5 * abs(l0), (l1, l0)
     torch.testing.assert_close(p1, p0, rtol=1e-5, atol=1e-7)
     assert g0.keys() == g1.keys()
+    scale = max(g.abs().max().item() for g in g0.values())
     for k in g0:
         err = (g1[k] - g0[k]).abs().max().item()
+        if any(n in k for n in NOISE_ONLY):  # exact gradient 0: rounding noise only
+            assert err <= 1e-6 * scale, (k, err)
+            continue
         # scalar alpha gradients are cancellation-prone sums over N*K products
         rel = 1e-3 if k.endswith(".alpha") else 2e-4
         assert err <= rel * g0[k].abs().max().item() + 1e-7, (k, err)

@@ -32,6 +32,7 @@ def main():
     n = cfg["enc_layers"]
     step = OneBitStep(model, n_layers=n, stacked=False if a.literal else None)
     batch = synthetic_batch([1000] * a.batch, [40] * a.batch, seed=1234, device=dev)
+    print(f"mode {a.mode} batch {a.batch} steps {a.steps}", flush=True)
     gen = torch.Generator().manual_seed(4321)
     if a.mode == "eager":
         opt = make_optimizer(model.parameters())

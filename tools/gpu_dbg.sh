@@ -1,14 +1,9 @@
 #!/bin/bash
-# Debug session: graph-vs-eager loss traces (stacked / literal, fused / torch optimizer),
-# then the GPU test suite (no -x).
+# Debug session: new-kernel tests, then a long graph-mode run printing every step.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-dbg}
 mkdir -p $O
-timeout -k 10 200 python tools/debug_graph.py --mode graph > $O/graph.log 2>&1 || exit 1
-timeout -k 10 200 python tools/debug_graph.py --mode graph --literal > $O/graph_literal.log 2>&1 || exit 1
-timeout -k 10 200 python tools/debug_graph.py --mode graph --literal --torch-opt > $O/graph_literal_torchopt.log 2>&1 || exit 1
-timeout -k 10 200 python tools/debug_graph.py --mode eager-gs > $O/eager_gs.log 2>&1 || exit 1
-timeout -k 10 200 python tools/debug_graph.py --mode eager > $O/eager.log 2>&1 || exit 1
-timeout -k 10 600 python -m pytest tests -m gpu -q > $O/gpu_tests.log 2>&1
-echo "tests rc=$?" >> $O/gpu_tests.log
+timeout -k 10 200 python -m pytest tests/test_embedding_gpu.py tests/test_relattn_gpu.py -x -q > $O/new_tests.log 2>&1
+rc=$?; echo "rc=$rc" >> $O/new_tests.log; [ $rc -gt 1 ] && exit $rc
+timeout -k 10 240 python tools/debug_graph.py --mode graph --batch 32 --steps 16 > $O/graph_b32.log 2>&1 || exit 1
