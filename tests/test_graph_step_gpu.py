@@ -56,7 +56,7 @@ def test_graph_replay_matches_eager(gpu):
     for a, b in zip(l_g, l_e):
         assert abs(a - b) <= 1e-5 * abs(b), (l_g, l_e)
     for a, b in zip(p_g, p_e):
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     # MIOpen may pick other (deterministic) conv solvers under capture: rounding-level
     # gradient differences, which Adam turns into <= lr-sized parameter differences.
     for (k, a), (_, b) in zip(m_g.named_parameters(), m_e.named_parameters()):
