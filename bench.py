@@ -61,7 +61,15 @@ def parse():
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--roofline-only", action="store_true", help="skip the step timing")
     ap.add_argument("--progress", action="store_true", help="progress lines on stderr")
-    return ap.parse_args()
+    ap.add_argument("--mode", default="train",
+                    choices=["train", "quant-off", "infer", "infer-fp32act"],
+                    help="train: configs[1]/[2] (default); quant-off: configs[3] (BitLinear -> "
+                         "bf16 nn.Linear); infer / infer-fp32act: configs[4] (B=256, 2-bit, "
+                         "int8 / fp32 activations, greedy CTC decode)")
+    args = ap.parse_args()
+    if args.mode.startswith("infer") and args.batch == 32:
+        args.batch = 256  # configs[4]
+    return args
 
 
 # ------------------------------------------------------------------------- roofline
@@ -254,6 +262,139 @@ def cpu_baseline(seconds: float):
                       f"{threads} threads on {cpu}"}
 
 
+# ------------------------------------------------------------------------- inference
+PEAK_I8_MFMA_TOPS = 5000.0  # 2x the dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
+
+
+def roofline_i8(batch, frames, dev, act_quant, reps=20):
+    """The inference step's BitLinear kernels at their B=256 shapes (one pass, 2-bit):
+    int8 path = absmax + i8-MFMA GEMM, fp32 path = bf16x3 GEMM; HIP events around a
+    graph of `reps` launches on the launch stream."""
+    from onebit_asr import _lib
+    from onebit_asr.conformer import subsampled_length
+    from onebit_asr.quant import pack_codes
+
+    lib = _lib.load()
+    t = subsampled_length(frames)
+    m = batch * t
+    shapes = [("lin1", m, 144, 576, 32), ("lin2", m, 576, 144, 32), ("qkvo", m, 144, 144, 64),
+              ("pos", t, 144, 144, 16)]
+    side = torch.cuda.Stream(dev)
+    tot_t = tot_b = tot_f = 0.0
+    n_launch = 0
+    detail = []
+    for name, M, K, N, count in shapes:
+        g = torch.Generator(device=dev).manual_seed(M + K + N)
+        X = torch.randn(M, K, device=dev, generator=g)
+        W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
+        alpha = W.abs().mean()
+        b = torch.zeros(N, device=dev)
+        c2, _ = pack_codes(W, alpha, 2)
+        Y = torch.empty(M, N, device=dev)
+        amax = torch.empty(1, device=dev)
+
+        def gemm(s):
+            if act_quant:
+                return lib.ob_bitlinear_fwd_i8(X.data_ptr(), 1, M, K, c2.data_ptr(), None, None,
+                                               alpha.data_ptr(), 1, amax.data_ptr(), b.data_ptr(),
+                                               N, Y.data_ptr(), s)
+            return lib.ob_bitlinear_fwd(X.data_ptr(), M, K, c2.data_ptr(), alpha.data_ptr(), 1,
+                                        b.data_ptr(), N, Y.data_ptr(), s)
+
+        wsb = lib.ob_act_absmax_workspace(1)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+
+        def absmax(s):
+            return lib.ob_act_absmax(X.data_ptr(), 1, M * K, amax.data_ptr(), ws.data_ptr(), wsb, s)
+
+        def timed(fn):
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    _lib.check(fn(side.cuda_stream), "roofline warm-up")
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=side):
+                    for _ in range(reps):
+                        fn(torch.cuda.current_stream(dev).cuda_stream)
+                graph.replay()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+                graph.replay()
+                e1.record(side)
+            e1.synchronize()
+            return e0.elapsed_time(e1) * 1e3 / reps
+
+        if act_quant:
+            _lib.check(absmax(side.cuda_stream), "absmax")
+            torch.cuda.synchronize()
+        tg = timed(gemm)
+        ta = timed(absmax) if act_quant else 0.0
+        by = 4 * (M * K + M * N + N) + 4 * N * ((K + 15) // 16)
+        fl = 2.0 * M * K * N
+        tot_t += count * tg
+        tot_b += count * by
+        tot_f += count * fl
+        n_launch += count
+        detail.append({"layer": name, "M": M, "K": K, "N": N, "launches_per_step": count,
+                       "gemm_us": round(tg, 2), "absmax_us": round(ta, 2),
+                       "gemm_GBs": round(by / (tg * 1e-6) / 1e9, 1),
+                       "gemm_TOPs": round(fl / (tg * 1e-6) / 1e12, 2)})
+    avg = tot_t / n_launch
+    gbs = (tot_b / n_launch) / (avg * 1e-6) / 1e9
+    tops = (tot_f / n_launch) / (avg * 1e-6) / 1e12
+    peak_c = PEAK_I8_MFMA_TOPS if act_quant else 2500.0
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "kernel": "tgemm_i8 (i8 MFMA)" if act_quant else "tgemm_bf16x3",
+            "avg_launch_us": round(avg, 3), "bytes_per_launch": int(tot_b / n_launch),
+            "flops_per_launch": int(tot_f / n_launch), "achieved_TOPs": round(tops, 2),
+            "mfma_peak_TOPs": peak_c, "mfma_frac": round(tops / peak_c, 4),
+            "ql_kernel_ms_per_step": round(tot_t / 1e3, 3), "shapes": detail, "traffic": None}
+
+
+def run_infer(args):
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CONFORMER_S, synthetic_batch
+    from onebit_asr.infer import GraphedInference
+
+    dev = torch.device("cuda", 0)
+    act = "absmax_int8" if args.mode == "infer" else None
+    torch.manual_seed(1234)
+    model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S).to(dev)
+    batch = synthetic_batch([args.frames] * args.batch, [args.tokens] * args.batch, seed=1234,
+                            device=dev)
+    gi = GraphedInference(model, precision=2, act_quant=act, use_graph=not args.eager)
+    log(args, "inference: capture")
+    out = gi.run(batch)
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        out = gi.run(batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = gi.run(batch)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    frames = args.batch * args.frames * args.steps
+    res = {
+        "metric": "mel-frames/sec (Conformer-S 1.58-bit inference + greedy CTC decode)",
+        "value": round(frames / elapsed, 1), "unit": "mel-frames/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "int8 x ternary (i8 MFMA), fp32 elsewhere" if act else "fp32",
+        "data": "synthetic (N(0,1) 80-mel x 1000-frame padded batches, random-init weights)",
+        "config": {"workload": "conformer-s-1.58bit-inference-greedy-ctc",
+                   "execution": "eager" if args.eager else "hip-graph", "global_batch": args.batch,
+                   "frames": args.frames, "precision": 2, "act_quant": act,
+                   "d_model": 144, "blocks": 16, "vocab": VOCAB},
+        "mean_tokens_per_utt": round(out[1].float().mean().item(), 2),
+    }
+    if not args.no_roofline:
+        res["roofline"] = roofline_i8(args.batch, args.frames, dev, act)
+    print(json.dumps(res), flush=True)
+
+
 # ------------------------------------------------------------------------- main
 def log(args, msg):
     if args.progress:
@@ -262,6 +403,8 @@ def log(args, msg):
 
 def main():
     args = parse()
+    if args.mode.startswith("infer"):
+        return run_infer(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -2,6 +2,7 @@
 // carving and launch-error reporting around the launchers in quant.hip / gemm.hip.
 #include "../../include/onebit_hip.h"
 #include "ob_launch.h"
+#include <stdint.h>
 
 using namespace ob;
 
@@ -217,6 +218,51 @@ int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t K,
   return launched();
 }
 
+size_t ob_act_absmax_workspace(int64_t P) {
+  return (P < 1 || P > 65535) ? 0 : act_absmax_workspace((int)P);
+}
+
+int ob_act_absmax(const float* X, int64_t P, int64_t n_per_pass, float* amax, void* ws,
+                  size_t ws_bytes, void* stream) {
+  if (P < 1 || P > 65535 || n_per_pass < 0) return OB_ERR_SHAPE;
+  if (!amax || !ws || (n_per_pass > 0 && !X)) return OB_ERR_NULL;
+  if (ws_bytes < act_absmax_workspace((int)P)) return OB_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (n_per_pass % 4) || !aligned4(amax) ||
+      !aligned4(ws))
+    return OB_ERR_ALIGN;
+  launch_act_absmax(X, (int)P, n_per_pass, amax, ws, as_stream(stream));
+  return launched();
+}
+
+int ob_act_dequant_i8(const float* X, int64_t P, int64_t n_per_pass, const float* amax,
+                      float* X_deq, void* stream) {
+  if (P < 1 || P > 65535 || n_per_pass < 0) return OB_ERR_SHAPE;
+  if (!amax || (n_per_pass > 0 && (!X || !X_deq))) return OB_ERR_NULL;
+  if (!aligned4(X) || !aligned4(X_deq) || !aligned4(amax)) return OB_ERR_ALIGN;
+  launch_act_dequant(X, (int)P, n_per_pass, amax, X_deq, as_stream(stream));
+  return launched();
+}
+
+int ob_bitlinear_fwd_i8(const float* X, int64_t P, int64_t M, int64_t K, const uint32_t* codes,
+                        const uint32_t* codes1, const int32_t* pass_bits, const float* alpha,
+                        int alpha_raw, const float* amax, const float* bias, int64_t N, float* Y,
+                        void* stream) {
+  if (M < 0 || K < 0 || N < 0 || P < 1 || P > 65535) return OB_ERR_SHAPE;
+  if (P > 1 && !pass_bits) return OB_ERR_NULL;
+  if (!alpha || !amax || (M * N > 0 && !Y) || (M * K > 0 && !X) || (N * K > 0 && !codes) ||
+      (pass_bits && N * K > 0 && !codes1))
+    return OB_ERR_NULL;
+  if (M * N > 0 && !ternary_gemm_i8_supported(K, N)) return OB_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || !aligned4(Y) || !aligned4(bias) ||
+      !aligned4(amax) || !aligned4(pass_bits))
+    return OB_ERR_ALIGN;
+  if (!launch_ternary_gemm_i8(X, (int)P, M, K, codes, pass_bits ? codes1 : codes,
+                              reinterpret_cast<const int*>(pass_bits), N, alpha, alpha_raw, amax,
+                              bias, Y, as_stream(stream)))
+    return OB_ERR_SHAPE;
+  return launched();
+}
+
 int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
                                const uint32_t* codes2_t, const uint32_t* codes1_t,
                                const int32_t* pass_bits, const float* alpha, int alpha_raw,
@@ -304,6 +350,46 @@ int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets, const int64_
   if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
   launch_ctc_bwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, grad_out,
                  grad, static_cast<float*>(ws), as_stream(stream));
+  return launched();
+}
+
+int ob_ctc_greedy_decode(const float* logits, const int64_t* lens, int64_t B, int64_t T,
+                         int64_t V, int blank, int32_t* ids, int32_t* out, int32_t* out_len,
+                         void* stream) {
+  if (B < 0 || T < 0 || V < 1 || V > INT32_MAX || blank < 0 || blank >= V) return OB_ERR_SHAPE;
+  if (B > 0 && (!lens || !out_len || (T > 0 && (!logits || !ids || !out)))) return OB_ERR_NULL;
+  if (!aligned4(logits) || !aligned4(ids) || !aligned4(out) || !aligned4(out_len))
+    return OB_ERR_ALIGN;
+  launch_ctc_greedy(logits, lens, B, T, V, blank, reinterpret_cast<int*>(ids),
+                    reinterpret_cast<int*>(out), reinterpret_cast<int*>(out_len),
+                    as_stream(stream));
+  return launched();
+}
+
+int ob_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
+                     int64_t d, float eps, float* y, float* mean, float* rstd, void* stream) {
+  if (rows < 0 || !layernorm_supported(d) || !(eps >= 0.0f)) return OB_ERR_SHAPE;
+  if (rows > 0 && (!x || !y)) return OB_ERR_NULL;
+  if (!aligned4(x) || !aligned4(y) || !aligned4(gamma) || !aligned4(beta)) return OB_ERR_ALIGN;
+  launch_layernorm_fwd(x, gamma, beta, rows, d, eps, y, mean, rstd, as_stream(stream));
+  return launched();
+}
+
+size_t ob_layernorm_bwd_workspace(int64_t rows, int64_t d) {
+  if (rows < 0 || !layernorm_supported(d)) return 0;
+  return layernorm_bwd_workspace(rows, d);
+}
+
+int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
+                     const float* rstd, int64_t rows, int64_t d, float* dx, float* dgamma,
+                     float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  if (rows < 0 || !layernorm_supported(d)) return OB_ERR_SHAPE;
+  if (rows > 0 && (!dy || !x || !mean || !rstd || !dx)) return OB_ERR_NULL;
+  if ((dgamma || dbeta) && !ws) return OB_ERR_NULL;
+  if ((dgamma || dbeta) && ws_bytes < layernorm_bwd_workspace(rows, d)) return OB_ERR_WORKSPACE;
+  if (!aligned4(dy) || !aligned4(x) || !aligned4(dx)) return OB_ERR_ALIGN;
+  launch_layernorm_bwd(dy, x, gamma, mean, rstd, rows, d, dx, dgamma, dbeta, ws,
+                       as_stream(stream));
   return launched();
 }
 

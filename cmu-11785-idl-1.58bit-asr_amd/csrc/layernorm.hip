@@ -1,0 +1,229 @@
+// layernorm.hip — LayerNorm over the last dim for the Conformer's LN wrappers
+// (reference onebit_asr/conformer.py:19-24 ``LayerNorm`` = nn.LayerNorm(d), eps 1e-5, used
+// before every BitLinear call site: ff1/ff2 (:36), mhsa (:109), conv (:145), block out (:228)).
+//
+// At Conformer-S the three stacked passes normalise 23,904 rows of d = 144 per call, ~90
+// calls per step. torch's kernels reach ~1 TB/s on these short rows (one block per row
+// forward; three kernels backward). Here:
+//   forward : 16 lanes per row (lane j holds columns j, j+16, ...: 64-byte coalesced
+//             segments), the row's values stay in registers for a two-pass mean/variance;
+//             writes y and the per-row (mean, rstd) the backward needs;
+//   backward: the same row mapping; dx in one pass over (dy, x); dgamma/dbeta are
+//             accumulated per lane over the block's rows and written as per-block
+//             partials, summed over blocks in fixed order by a second launch
+//             (deterministic, no atomics).
+// Numerics: var = mean((x - mean)^2) (biased, as torch), rstd = 1/sqrt(var + eps).
+#include "ob_launch.h"
+
+namespace ob {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kLanesPerRow = 16;
+constexpr int kRowsPerBlock = kThreads / kLanesPerRow;  // 16
+
+__device__ __forceinline__ float row_sum16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int NPL>  // columns per lane: d <= 16 * NPL
+__global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out) {
+  const int j = threadIdx.x & (kLanesPerRow - 1);
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
+  if (row >= rows) return;
+  const float* xr = x + row * d;
+  float v[NPL];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = j + kLanesPerRow * i;
+    v[i] = c < d ? xr[c] : 0.0f;
+    s += v[i];
+  }
+  const float inv_d = 1.0f / (float)d;
+  const float mean = row_sum16(s) * inv_d;
+  float q = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = j + kLanesPerRow * i;
+    const float t = c < d ? v[i] - mean : 0.0f;
+    q = fmaf(t, t, q);
+  }
+  const float var = row_sum16(q) * inv_d;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  float* yr = y + row * d;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = j + kLanesPerRow * i;
+    if (c < d) {
+      const float g = gamma ? gamma[c] : 1.0f;
+      const float b = beta ? beta[c] : 0.0f;
+      yr[c] = fmaf((v[i] - mean) * rstd, g, b);
+    }
+  }
+  if (j == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
+template <int NPL>
+__global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows, int d,
+    int rows_per_block, float* __restrict__ dx, float* __restrict__ part_g,
+    float* __restrict__ part_b) {
+  __shared__ float red_g[kRowsPerBlock][kLanesPerRow * NPL];
+  __shared__ float red_b[kRowsPerBlock][kLanesPerRow * NPL];
+  const int j = threadIdx.x & (kLanesPerRow - 1);
+  const int sub = threadIdx.x / kLanesPerRow;
+  const float inv_d = 1.0f / (float)d;
+  float gam[NPL], acc_g[NPL], acc_b[NPL];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c = j + kLanesPerRow * i;
+    gam[i] = (gamma && c < d) ? gamma[c] : (c < d ? 1.0f : 0.0f);
+    acc_g[i] = 0.0f;
+    acc_b[i] = 0.0f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  for (int64_t row = r0 + sub; row < r1; row += kRowsPerBlock) {
+    const float mu = mean_in[row], rs = rstd_in[row];
+    const float* xr = x + row * d;
+    const float* gr = dy + row * d;
+    float xh[NPL], g[NPL];
+    float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = j + kLanesPerRow * i;
+      const float xv = c < d ? xr[c] : 0.0f;
+      const float dv = c < d ? gr[c] : 0.0f;
+      xh[i] = (xv - mu) * rs;
+      acc_g[i] = fmaf(dv, xh[i], acc_g[i]);
+      acc_b[i] += dv;
+      g[i] = dv * gam[i];
+      s1 += g[i];
+      s2 = fmaf(g[i], xh[i], s2);
+    }
+    const float m1 = row_sum16(s1) * inv_d;
+    const float m2 = row_sum16(s2) * inv_d;
+    float* dr = dx + row * d;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = j + kLanesPerRow * i;
+      if (c < d) dr[c] = rs * (g[i] - m1 - xh[i] * m2);
+    }
+  }
+  if (!part_g) return;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    red_g[sub][j + kLanesPerRow * i] = acc_g[i];
+    red_b[sub][j + kLanesPerRow * i] = acc_b[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += kThreads) {
+    float sg = 0.0f, sb = 0.0f;
+#pragma unroll
+    for (int r = 0; r < kRowsPerBlock; ++r) {
+      sg += red_g[r][c];
+      sb += red_b[r][c];
+    }
+    part_g[(int64_t)blockIdx.x * d + c] = sg;
+    part_b[(int64_t)blockIdx.x * d + c] = sb;
+  }
+}
+
+// dgamma[c] = sum over blocks of part_g[blk][c] (fixed order), same for dbeta.
+__global__ __launch_bounds__(kThreads) void ln_param_reduce_kernel(
+    const float* __restrict__ part_g, const float* __restrict__ part_b, int nblk, int d,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  // 64 columns per block, 4 block-slices per column summed in fixed order through LDS
+  __shared__ float sg[4][64], sb[4][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float ag = 0.0f, ab = 0.0f;
+  if (c < d) {
+    for (int b = sl; b < nblk; b += 4) {
+      ag += part_g[(int64_t)b * d + c];
+      ab += part_b[(int64_t)b * d + c];
+    }
+  }
+  sg[sl][cl] = ag;
+  sb[sl][cl] = ab;
+  __syncthreads();
+  if (sl == 0 && c < d) {
+    if (dgamma) dgamma[c] = ((sg[0][cl] + sg[1][cl]) + sg[2][cl]) + sg[3][cl];
+    if (dbeta) dbeta[c] = ((sb[0][cl] + sb[1][cl]) + sb[2][cl]) + sb[3][cl];
+  }
+}
+
+constexpr int kMaxBwdBlocks = 1024;
+
+int bwd_blocks(int64_t rows, int* rows_per_block) {
+  int64_t nb = ceil_div(rows, kRowsPerBlock);
+  if (nb > kMaxBwdBlocks) nb = kMaxBwdBlocks;
+  if (nb < 1) nb = 1;
+  int64_t rpb = ceil_div(rows, nb);
+  rpb = ceil_div(rpb, kRowsPerBlock) * kRowsPerBlock;
+  *rows_per_block = (int)rpb;
+  return (int)ceil_div(rows, rpb);
+}
+
+}  // namespace
+
+bool layernorm_supported(int64_t d) { return d >= 1 && d <= 16 * 32; }
+
+size_t layernorm_bwd_workspace(int64_t rows, int64_t d) {
+  int rpb;
+  const int nb = rows > 0 ? bwd_blocks(rows, &rpb) : 1;
+  return sizeof(float) * (size_t)(2 * nb * d) + 256;
+}
+
+#define OB_LN_NPL(MACRO) \
+  if (npl <= 4) MACRO(4) else if (npl <= 9) MACRO(9) else if (npl <= 16) MACRO(16) \
+  else MACRO(32)
+
+void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
+                          int64_t d, float eps, float* y, float* mean, float* rstd,
+                          hipStream_t s) {
+  if (rows == 0) return;
+  const int npl = (int)ceil_div(d, kLanesPerRow);
+  const dim3 grid((unsigned)ceil_div(rows, kRowsPerBlock));
+#define OB_LNF(N)                                                                             \
+  hipLaunchKernelGGL((ln_fwd_kernel<N>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
+                     (int)d, eps, y, mean, rstd);
+  OB_LN_NPL(OB_LNF)
+#undef OB_LNF
+}
+
+void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
+                          const float* rstd, int64_t rows, int64_t d, float* dx, float* dgamma,
+                          float* dbeta, void* ws, hipStream_t s) {
+  const int npl = (int)ceil_div(d, kLanesPerRow);
+  float* part_g = static_cast<float*>(ws);
+  int rpb = kRowsPerBlock;
+  const int nb = rows > 0 ? bwd_blocks(rows, &rpb) : 0;
+  float* part_b = part_g + (size_t)nb * d;
+  const bool params = dgamma || dbeta;
+  if (rows > 0) {
+#define OB_LNB(N)                                                                           \
+  hipLaunchKernelGGL((ln_bwd_kernel<N>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
+                     gamma, mean, rstd, rows, (int)d, rpb, dx, params ? part_g : nullptr,   \
+                     part_b);
+    OB_LN_NPL(OB_LNB)
+#undef OB_LNB
+  }
+  if (params)
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, 64)), dim3(kThreads), 0,
+                       s, part_g, part_b, nb, (int)d, dgamma, dbeta);
+}
+
+}  // namespace ob

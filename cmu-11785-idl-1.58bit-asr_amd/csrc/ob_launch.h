@@ -64,6 +64,31 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
                        hipStream_t s);
 
+// tgemm_i8.hip (opt-in absmax-int8 activations x ternary codes on the i8 matrix cores)
+bool ternary_gemm_i8_supported(int64_t K, int64_t N);
+size_t act_absmax_workspace(int P);
+void launch_act_absmax(const float* X, int P, int64_t n_per_pass, float* amax, void* ws,
+                       hipStream_t s);
+void launch_act_dequant(const float* X, int P, int64_t n_per_pass, const float* amax, float* Xd,
+                        hipStream_t s);
+bool launch_ternary_gemm_i8(const float* A, int P, int64_t M, int64_t K, const uint32_t* codes,
+                            const uint32_t* codes1, const int* pass_bits, int64_t N,
+                            const float* alpha, int alpha_raw, const float* amax,
+                            const float* bias, float* C, hipStream_t s);
+
+// decode.hip (batched greedy CTC decode: argmax per frame, collapse per utterance)
+void launch_ctc_greedy(const float* logits, const int64_t* lens, int64_t B, int64_t T, int64_t V,
+                       int blank, int* ids, int* out, int* out_len, hipStream_t s);
+
+// layernorm.hip (LayerNorm over the last dim, d <= 512; deterministic dgamma/dbeta)
+bool layernorm_supported(int64_t d);
+size_t layernorm_bwd_workspace(int64_t rows, int64_t d);
+void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
+                          int64_t d, float eps, float* y, float* mean, float* rstd, hipStream_t s);
+void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
+                          const float* rstd, int64_t rows, int64_t d, float* dx, float* dgamma,
+                          float* dbeta, void* ws, hipStream_t s);
+
 // dwconv.hip (depthwise Conv1d of the conv module, odd kernel width, 'same' padding)
 bool dwconv_supported(int KT);
 void launch_dwconv_fwd(const float* x, const float* w, const float* bias, int64_t B, int64_t C,

@@ -1,0 +1,344 @@
+// tgemm_i8.hip — the north-star int8 path of BitLinear: per-tensor absmax int8 activations
+// times ternary weights on the int8 matrix cores (v_mfma_i32_16x16x64_i8).
+//
+// The reference keeps activations fp32 (quant.py:126 F.linear(x, W_hat, b); SURVEY.md §0
+// F3), so this is an OPT-IN mode (QuantizedLinear.act_quant = "absmax_int8"), used by the
+// inference path and available to training. Its semantics (BitNet b1.58 activation
+// quantizer, restated bit-exactly by oracle/quant_oracle.py::np_bitlinear_fwd_i8):
+//
+//   g   = max(max|X_p|, 1e-5)           per pass p (the tensor one reference call sees)
+//   sx  = 127 / g                        fp32, correctly rounded
+//   xq  = clamp(rint(x * sx), -127, 127) int8 (rint: round half to even, like torch.round)
+//   acc = sum_k xq[m][k] * Q[n][k]       int32, exact (|acc| <= 127*K < 2^24)
+//   y   = float(acc) * (a * (g / 127)) + b      two roundings (mul, then add), no fma
+//
+// so the GPU result is bit-identical to a numpy float32 restatement. Q is the same 2-bit
+// code set as the fp32 path (bits 1 / 2, a = |alpha| + 1e-8).
+//
+// Kernel layout (block = 4 waves, 64 rows x 16*NT columns, persistent over row tiles like
+// tgemm.hip): the block decodes its code rows into an int8 image of Q in LDS
+// ([16*NT][64*NCH + 16] bytes, sign-extended codes); per 64-wide k chunk a lane loads 16
+// consecutive fp32 of its row (4 x dwordx4), quantizes them in registers into one
+// 16-byte fragment and issues one i8 MFMA per 16-column tile. A and B fragments take
+// element j of lane (r, g) from k = 64c + 16g + j; any k permutation the hardware applies
+// is the same for both operands, so the sum over k is unaffected.
+#include "ob_launch.h"
+#include "ob_quant.h"
+
+namespace ob {
+
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kRows = 64;
+constexpr int kTargetBlocks = 512;
+constexpr size_t kMaxLds = 64 * 1024;
+
+__device__ __forceinline__ int xcd_logical(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// 16 codes of one word -> 16 sign-extended int8 bytes (0 -> 0, 1 -> +1, 3 -> -1).
+__device__ __forceinline__ u32x4 decode_i8(uint32_t word) {
+  u32x4 out;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * q + e;
+      const int c = (int)(word << (30 - 2 * j)) >> 30;  // two's-complement 2-bit field
+      v |= ((uint32_t)c & 0xFFu) << (8 * e);
+    }
+    out[q] = v;
+  }
+  return out;
+}
+
+__device__ __forceinline__ uint32_t q4(const f32x4& x, float sx) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float q = rintf(x[e] * sx);
+    q = fminf(fmaxf(q, -127.0f), 127.0f);
+    v |= ((uint32_t)(int)q & 0xFFu) << (8 * e);
+  }
+  return v;
+}
+
+// y = float(acc) * osc + b with two roundings: hipcc contracts a*b+c into an fma by
+// default (-ffp-contract=fast), which would round once and differ from the restatement.
+__device__ __forceinline__ float epilogue(int acc, float osc, float b) {
+#pragma clang fp contract(off)
+  const float p = (float)acc * osc;
+  return p + b;
+}
+
+__device__ __forceinline__ float act_gamma(const float* amax, int p) {
+  return fmaxf(amax[p], 1e-5f);
+}
+
+// Per-pass max|x|, two launches without atomics: kAbsParts blocks per pass each write the
+// max of their slice (|x| >= 0, so comparing the fp32 bit patterns as unsigned is the
+// float order), then one wave per pass reduces the partials. Max is order-independent,
+// hence deterministic. (A single-address atomicMax from every wave serialised at the L2:
+// 53 us for a 37 MB tensor, measured.)
+constexpr int kAbsParts = 256;
+
+__global__ __launch_bounds__(kThreads) void act_absmax_part_kernel(const float* __restrict__ X,
+                                                                   int64_t n_per_pass,
+                                                                   uint32_t* __restrict__ part) {
+  __shared__ uint32_t red[kThreads / 64];
+  const int p = blockIdx.y;
+  const float* x = X + (int64_t)p * n_per_pass;
+  const int64_t n4 = n_per_pass >> 2;
+  uint32_t m0 = 0, m1 = 0;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {  // two loads in flight per thread
+    const f32x4 a = reinterpret_cast<const f32x4*>(x)[i];
+    const f32x4 b = reinterpret_cast<const f32x4*>(x)[i + stride];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m0 = max(m0, __float_as_uint(a[e]) & 0x7FFFFFFFu);
+      m1 = max(m1, __float_as_uint(b[e]) & 0x7FFFFFFFu);
+    }
+  }
+  for (; i < n4; i += stride) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(x)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m0 = max(m0, __float_as_uint(a[e]) & 0x7FFFFFFFu);
+  }
+  for (int64_t t = 4 * n4 + (int64_t)blockIdx.x * kThreads + threadIdx.x; t < n_per_pass;
+       t += stride)
+    m0 = max(m0, __float_as_uint(x[t]) & 0x7FFFFFFFu);
+  uint32_t m = max(m0, m1);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[(int64_t)p * gridDim.x + blockIdx.x] = max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
+__global__ __launch_bounds__(64) void act_absmax_final_kernel(const uint32_t* __restrict__ part,
+                                                              int nparts,
+                                                              uint32_t* __restrict__ amax) {
+  const int p = blockIdx.x;
+  uint32_t m = 0;
+  for (int i = threadIdx.x; i < nparts; i += 64) m = max(m, part[(int64_t)p * nparts + i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if (threadIdx.x == 0) amax[p] = m;
+}
+
+// X_deq = xq * (g / 127): the activation the int8 forward actually multiplied (the
+// backward's dW = dY^T X_deq under the straight-through estimator).
+__global__ __launch_bounds__(kThreads) void act_dequant_kernel(const float* __restrict__ X,
+                                                               int64_t n_per_pass,
+                                                               const float* __restrict__ amax,
+                                                               float* __restrict__ Xd) {
+  const int p = blockIdx.y;
+  const float g = act_gamma(amax, p);
+  const float sx = 127.0f / g;
+  const float ds = g / 127.0f;
+  const float* x = X + (int64_t)p * n_per_pass;
+  float* y = Xd + (int64_t)p * n_per_pass;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n_per_pass; i += stride) {
+    float q = rintf(x[i] * sx);
+    q = fminf(fmaxf(q, -127.0f), 127.0f);
+    y[i] = q * ds;
+  }
+}
+
+template <int NT, int NCH>
+__global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
+    const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
+    int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
+    const float* __restrict__ amax, const float* __restrict__ bias, float* __restrict__ C,
+    const uint32_t* __restrict__ codes1, const int* __restrict__ pass_bits) {
+  int p = 0;
+  if (pass_bits) {
+    p = blockIdx.y;
+    if (pass_bits[p] == 1) codes = codes1;
+    A += (int64_t)p * M * K;
+    C += (int64_t)p * M * N;
+  }
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kpad = 64 * NCH;
+  constexpr int stride = kpad + 16;  // bytes per image row
+  constexpr int kwp = kpad / 16;     // code words per padded row
+
+  const int L = xcd_logical(blockIdx.x, gridDim.x);
+  const int ct = L % n_ct;
+  const int rg = L / n_ct;
+  const int n0 = ct * (16 * NT);
+
+  constexpr int nwords = 16 * NT * kwp;
+  for (int idx = threadIdx.x; idx < nwords; idx += kThreads) {
+    const int nl = idx / kwp, w = idx - nl * kwp;
+    const int n = n0 + nl;
+    const uint32_t word = (n < N && w < KW) ? codes[(int64_t)n * KW + w] : 0u;
+    *reinterpret_cast<u32x4*>(smem + nl * stride + 16 * w) = decode_i8(word);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const char* brow = smem + r * stride + 16 * g;
+  const float gam = act_gamma(amax, p);
+  const float sx = 127.0f / gam;
+  const float osc = __fmul_rn(effective_alpha(alpha, alpha_raw), gam / 127.0f);
+  float bcol[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 16 * t + r;
+    bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
+  }
+
+  for (int rt = rg; rt < n_rt; rt += rgroups) {
+    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
+    const int64_t row = m0 + r < M ? m0 + r : M - 1;
+    const float* arow = A + row * (int64_t)K;
+    i32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = i32x4{0, 0, 0, 0};
+
+    // the chunk's 16 floats: clamped start (k >= K meets zero codes, K % 16 == 0)
+    auto load16 = [&](int c, f32x4* v) {
+      int k = 64 * c + 16 * g;
+      k = k < K ? k : K - 16;
+      const f32x4* src = reinterpret_cast<const f32x4*>(arow + k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = src[e];
+    };
+    constexpr int kWin = NCH < 3 ? NCH : 3;
+    f32x4 buf[NCH][4];
+#pragma unroll
+    for (int c = 0; c < kWin; ++c) load16(c, buf[c]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + kWin < NCH) load16(c + kWin, buf[c + kWin]);
+      __builtin_amdgcn_sched_barrier(0);
+      i32x4 bq[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        bq[t] = *reinterpret_cast<const i32x4*>(brow + t * 16 * stride + 64 * c);
+      i32x4 a;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = (int)q4(buf[c][e], sx);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[t], acc[t], 0, 0, 0);
+    }
+
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 16 * t + r;
+      if (col >= N) continue;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t orow = m0 + 4 * g + reg;
+        if (orow < M) C[orow * N + col] = epilogue(acc[t][reg], osc, bcol[t]);
+      }
+    }
+  }
+}
+
+size_t i8_image_bytes(int nt, int64_t K) {
+  return (size_t)(16 * nt) * (size_t)(64 * ceil_div(K, 64) + 16);
+}
+
+int pick_nt_i8(int64_t N, int64_t K) {
+  static const int cands[] = {12, 9, 6, 4, 3, 2, 1};
+  for (int nt : cands)
+    if (N % (16 * nt) == 0 && i8_image_bytes(nt, K) <= kMaxLds) return nt;
+  for (int nt : cands)
+    if (16 * nt <= ((N + 15) & ~int64_t(15)) && i8_image_bytes(nt, K) <= kMaxLds) return nt;
+  return 0;
+}
+
+template <int NT>
+bool launch_i8_nt(const float* A, int P, int64_t M, int64_t K, const uint32_t* codes,
+                  const uint32_t* codes1, const int* pass_bits, int64_t N, const float* alpha,
+                  int alpha_raw, const float* amax, const float* bias, float* C, hipStream_t s) {
+  const int n_ct = (int)ceil_div(N, 16 * NT);
+  const int n_rt = (int)ceil_div(M, kRows);
+  int rgroups = kTargetBlocks / (n_ct * P);
+  if (rgroups < 1) rgroups = 1;
+  if (rgroups > n_rt) rgroups = n_rt;
+  const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
+  const size_t lds = i8_image_bytes(NT, K);
+  const int KW = (int)ceil_div(K, 16);
+#define OB_I8(NCH)                                                                          \
+  hipLaunchKernelGGL((tgemm_i8_kernel<NT, NCH>), grid, dim3(kThreads), lds, s, A, M, (int)K, \
+                     codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, amax, bias, C, \
+                     codes1, pass_bits);                                                     \
+  return true;
+  switch (ceil_div(K, 64)) {
+    case 1: OB_I8(1)
+    case 2: OB_I8(2)
+    case 3: OB_I8(3)
+    case 4: OB_I8(4)
+    case 5: OB_I8(5)
+    case 6: OB_I8(6)
+    case 7: OB_I8(7)
+    case 8: OB_I8(8)
+    case 9: OB_I8(9)
+    default: return false;
+  }
+#undef OB_I8
+}
+
+}  // namespace
+
+bool ternary_gemm_i8_supported(int64_t K, int64_t N) {
+  return K >= 16 && K % 16 == 0 && K <= 576 && N >= 1 && pick_nt_i8(N, K) > 0;
+}
+
+size_t act_absmax_workspace(int P) { return sizeof(uint32_t) * (size_t)P * kAbsParts; }
+
+void launch_act_absmax(const float* X, int P, int64_t n_per_pass, float* amax, void* ws,
+                       hipStream_t s) {
+  uint32_t* part = static_cast<uint32_t*>(ws);
+  hipLaunchKernelGGL(act_absmax_part_kernel, dim3(kAbsParts, (unsigned)P), dim3(kThreads), 0, s,
+                     X, n_per_pass, part);
+  hipLaunchKernelGGL(act_absmax_final_kernel, dim3((unsigned)P), dim3(64), 0, s,
+                     (const uint32_t*)part, kAbsParts, reinterpret_cast<uint32_t*>(amax));
+}
+
+void launch_act_dequant(const float* X, int P, int64_t n_per_pass, const float* amax, float* Xd,
+                        hipStream_t s) {
+  if (n_per_pass == 0) return;
+  int64_t blocks = ceil_div(n_per_pass, kThreads * 4);
+  if (blocks > 2048 / P) blocks = 2048 / P > 0 ? 2048 / P : 1;
+  hipLaunchKernelGGL(act_dequant_kernel, dim3((unsigned)blocks, (unsigned)P), dim3(kThreads), 0,
+                     s, X, n_per_pass, amax, Xd);
+}
+
+bool launch_ternary_gemm_i8(const float* A, int P, int64_t M, int64_t K, const uint32_t* codes,
+                            const uint32_t* codes1, const int* pass_bits, int64_t N,
+                            const float* alpha, int alpha_raw, const float* amax,
+                            const float* bias, float* C, hipStream_t s) {
+  if (M == 0 || N == 0 || P == 0) return true;
+  switch (pick_nt_i8(N, K)) {
+    case 12: return launch_i8_nt<12>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    case 9: return launch_i8_nt<9>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    case 6: return launch_i8_nt<6>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    case 4: return launch_i8_nt<4>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    case 3: return launch_i8_nt<3>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    case 2: return launch_i8_nt<2>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    case 1: return launch_i8_nt<1>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
+    default: return false;
+  }
+}
+
+}  // namespace ob

@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from .attention import fused_attention_supported, rel_pos_attention
 from .conv import depthwise_conv1d
 from .embedding import embedding
+from .layernorm import layer_norm
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
 __all__ = [
@@ -46,14 +47,15 @@ def swish(x: torch.Tensor) -> torch.Tensor:
 
 
 class LayerNorm(nn.Module):
-    """Wrapper kept for the ``<...>.ln.ln.weight`` checkpoint keys (conformer.py:19-24)."""
+    """Wrapper kept for the ``<...>.ln.ln.weight`` checkpoint keys (conformer.py:19-24).
+    On a ROCm device the normalisation runs on the HIP LayerNorm kernels (layernorm.py)."""
 
     def __init__(self, d_model: int):
         super().__init__()
         self.ln = nn.LayerNorm(d_model)
 
     def forward(self, x):
-        return self.ln(x)
+        return layer_norm(x, self.ln.weight, self.ln.bias, self.ln.eps)
 
 
 def _pad_rows(y: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
@@ -316,8 +318,17 @@ class ConformerEncoder(nn.Module):
     def forward(self, feats: torch.Tensor, feat_lens: torch.Tensor,
                 precision: int, sp_mask: Optional[List[int]] = None):
         """conformer.py:243-272. Frame validity uses feat_lens // 4 against the T' actually
-        produced by the convolutions (so it can disagree by one frame, as in the reference)."""
+        produced by the convolutions (so it can disagree by one frame, as in the reference).
+
+        With a ``StackedBits`` table (the three passes of a training step stacked on the
+        batch dim) ``feats`` holds ONE copy of the batch: the subsampling convolutions have
+        no dropout and full-precision weights, so all passes compute the same [B, T', d]
+        output; it is computed once and repeated per pass (autograd sums the passes'
+        gradients into the one backward)."""
         x = self.subsample(feats)
+        if isinstance(sp_mask, StackedBits):
+            x = x.repeat(sp_mask.passes, 1, 1)
+            feat_lens = feat_lens.repeat(sp_mask.passes)
         tsub = x.size(1)
         x, pos_emb = self.pos_enc(x)
         frames = torch.arange(tsub, device=feats.device).unsqueeze(0)

@@ -34,7 +34,8 @@ import torch.nn.functional as F
 from . import _lib
 
 __all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "DeviceBits",
-           "DynamicBitwidth", "PassBits", "StackedBits"]
+           "DynamicBitwidth", "PassBits", "StackedBits", "set_act_quant", "ACT_QUANT_MODES",
+           "act_absmax"]
 
 _VALID = (1, 2, 32)
 
@@ -129,6 +130,24 @@ def _check_bitwidth(bitwidth) -> int:
     if bitwidth not in _VALID:
         raise ValueError("bitwidth must be one of {1,2,32}")
     return int(bitwidth)
+
+
+ACT_QUANT_MODES = (None, "absmax_int8")
+
+
+def _check_act_quant(mode):
+    if mode not in ACT_QUANT_MODES:
+        raise ValueError(f"act_quant must be one of {ACT_QUANT_MODES}, got {mode!r}")
+    return mode
+
+
+def set_act_quant(module: nn.Module, mode: Optional[str]) -> nn.Module:
+    """Switch every QuantizedLinear under ``module`` to activation mode ``mode``."""
+    _check_act_quant(mode)
+    for m in module.modules():
+        if isinstance(m, QuantizedLinear):
+            m.act_quant = mode
+    return module
 
 
 def _require_device(*tensors: torch.Tensor) -> None:
@@ -279,6 +298,96 @@ class _BitLinearPassesFn(torch.autograd.Function):
         return gx, gw, galpha, gb, None, None, None, None, None, None
 
 
+def act_absmax(x: torch.Tensor, passes: int = 1) -> torch.Tensor:
+    """Per-pass max|x| (device fp32 [passes]) of a contiguous fp32 tensor whose leading
+    rows split into ``passes`` equal passes (the int8 mode's per-tensor scale)."""
+    lib = _lib.load()
+    n = x.numel() // passes
+    amax = torch.empty((passes,), dtype=torch.float32, device=x.device)
+    wsb = lib.ob_act_absmax_workspace(passes)
+    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x.device)
+    _lib.check(lib.ob_act_absmax(x.data_ptr(), passes, n, amax.data_ptr(), ws.data_ptr(), wsb,
+                                 _lib.stream_of(x)), "ob_act_absmax")
+    return amax
+
+
+class _BitLinearI8Fn(torch.autograd.Function):
+    """Opt-in north-star mode (act_quant="absmax_int8"; not the reference's arithmetic,
+    which keeps activations fp32 -- quant.py:126): per-pass absmax int8
+    activations x ternary codes on the int8 matrix cores (csrc/tgemm_i8.hip). Backward is
+    the straight-through estimator on both quantizers: dX = dY . W_hat (the fp32-path dX
+    kernel), dW / dalpha / db from dY and the dequantized activations the forward used."""
+
+    @staticmethod
+    def forward(ctx, x2d, weight, alpha, bias, bits, P, codes, codes_t, codes1, codes1_t):
+        rows, k = x2d.shape
+        m = rows // P
+        n = weight.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(x2d)
+        amax = act_absmax(x2d, P)
+        y = torch.empty((rows, n), dtype=torch.float32, device=x2d.device)
+        pb = bits.tensor if isinstance(bits, PassBits) else None
+        _lib.check(
+            lib.ob_bitlinear_fwd_i8(x2d.data_ptr(), P, m, k, codes.data_ptr(), _lib.ptr(codes1),
+                                    _lib.ptr(pb), alpha.data_ptr(), 1, amax.data_ptr(),
+                                    _lib.ptr(bias), n, y.data_ptr(), stream),
+            "ob_bitlinear_fwd_i8",
+        )
+        ctx.bits = bits
+        ctx.P = P
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x2d, weight, alpha, amax, codes_t, codes1_t)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2d, weight, alpha, amax, codes_t, codes1_t = ctx.saved_tensors
+        gy = gy.contiguous()
+        rows, k = x2d.shape
+        P = ctx.P
+        m = rows // P
+        n = weight.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(gy)
+        stacked = isinstance(ctx.bits, PassBits)
+        gx = gw = galpha = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty((rows, k), dtype=torch.float32, device=gy.device)
+            if stacked:
+                st = lib.ob_bitlinear_bwd_dx_passes(gy.data_ptr(), P, m, n, codes_t.data_ptr(),
+                                                    codes1_t.data_ptr(), ctx.bits.tensor.data_ptr(),
+                                                    alpha.data_ptr(), 1, k, gx.data_ptr(), stream)
+            else:
+                st = lib.ob_bitlinear_bwd_dx(gy.data_ptr(), m, n, codes_t.data_ptr(),
+                                             alpha.data_ptr(), 1, k, gx.data_ptr(), stream)
+            _lib.check(st, "ob_bitlinear_bwd_dx")
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            xd = torch.empty_like(x2d)
+            _lib.check(lib.ob_act_dequant_i8(x2d.data_ptr(), P, m * k, amax.data_ptr(),
+                                             xd.data_ptr(), stream), "ob_act_dequant_i8")
+            gw = torch.empty_like(weight)
+            galpha = torch.empty((), dtype=torch.float32, device=gy.device)
+            gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            if stacked:
+                ws_bytes = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
+                ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
+                st = lib.ob_bitlinear_bwd_dw_passes(gy.data_ptr(), xd.data_ptr(), P, m, n, k,
+                                                    weight.data_ptr(), alpha.data_ptr(), 1,
+                                                    ctx.bits.tensor.data_ptr(), gw.data_ptr(),
+                                                    galpha.data_ptr(), _lib.ptr(gb), ws.data_ptr(),
+                                                    ws_bytes, stream)
+            else:
+                ws_bytes = lib.ob_bitlinear_bwd_dw_workspace(m, n, k)
+                ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
+                st = lib.ob_bitlinear_bwd_dw(gy.data_ptr(), xd.data_ptr(), m, n, k,
+                                             weight.data_ptr(), alpha.data_ptr(), 1, ctx.bits,
+                                             gw.data_ptr(), galpha.data_ptr(), _lib.ptr(gb),
+                                             ws.data_ptr(), ws_bytes, stream)
+            _lib.check(st, "ob_bitlinear_bwd_dw")
+        return gx, gw, galpha, gb, None, None, None, None, None, None
+
+
 class _QuantizeSTE(torch.autograd.Function):
     """quantize_weight's autograd function (quant.py:38-92): W_hat = a * Q(W/a) with the
     STE / LSQ-style alpha gradient. ``alpha`` is used as given (no abs/eps), as in the
@@ -330,10 +439,14 @@ def quantize_weight(W: torch.Tensor, alpha: torch.Tensor, bitwidth: int) -> torc
 class QuantizedLinear(nn.Module):
     """quant.py:99-127, same constructor, parameters, init and forward signature."""
 
-    def __init__(self, in_features: int, out_features: int, bias: bool = True):
+    def __init__(self, in_features: int, out_features: int, bias: bool = True,
+                 act_quant: Optional[str] = None):
         super().__init__()
         self.in_features = in_features
         self.out_features = out_features
+        # None: the reference's fp32 activations. "absmax_int8": the opt-in north-star mode
+        # (per-tensor absmax int8 activations on the int8 matrix cores; own tolerance).
+        self.act_quant = _check_act_quant(act_quant)
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
         # quant.py:104-108: kaiming_uniform(a=sqrt(5)) then x2, i.e. U(-2/sqrt(in), 2/sqrt(in)).
         nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
@@ -348,7 +461,9 @@ class QuantizedLinear(nn.Module):
         self._codes_cache: dict = {}
 
     def extra_repr(self) -> str:
-        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
+        extra = f", act_quant={self.act_quant!r}" if self.act_quant else ""
+        return (f"in_features={self.in_features}, out_features={self.out_features}, "
+                f"bias={self.bias is not None}{extra}")
 
     def _codes(self, bits: int):
         """Codes for the current (weight, alpha) values: repacked only when either
@@ -374,10 +489,16 @@ class QuantizedLinear(nn.Module):
         if not x2d.is_contiguous():
             x2d = x2d.contiguous()
         if bits == 0:  # DynamicBitwidth: codes depend on a device value, never cached
+            if self.act_quant is not None:
+                raise NotImplementedError("act_quant with a DynamicBitwidth: use StackedBits")
             codes, codes_t = pack_codes(self.weight, self.alpha, bitwidth, alpha_raw=True)
             bits = bitwidth
         else:
             codes, codes_t = self._codes(bits)
+        if self.act_quant == "absmax_int8":
+            y = _BitLinearI8Fn.apply(x2d, self.weight, self.alpha, self.bias, bits, 1, codes,
+                                     codes_t, None, None)
+            return y.view(*lead, self.out_features)
         y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bits, codes, codes_t)
         return y.view(*lead, self.out_features)
 
@@ -393,6 +514,10 @@ class QuantizedLinear(nn.Module):
             x2d = x2d.contiguous()
         codes2, codes2_t = self._codes(2)
         codes1, codes1_t = self._codes(1)
+        if self.act_quant == "absmax_int8":
+            y = _BitLinearI8Fn.apply(x2d, self.weight, self.alpha, self.bias, pb, P, codes2,
+                                     codes2_t, codes1, codes1_t)
+            return y.view(*lead, self.out_features)
         y = _BitLinearPassesFn.apply(x2d, self.weight, self.alpha, self.bias, pb.tensor, P,
                                      codes2, codes2_t, codes1, codes1_t)
         return y.view(*lead, self.out_features)

@@ -155,11 +155,8 @@ class OneBitStep(nn.Module):
         P = bits.passes  # 0: teacher (2-bit), 1: student (1-bit), 2: SP
         bsz = batch["feats"].size(0)
         t_inp, t_out, t_pad = make_att_targets(batch["tokens"], sp["bos_id"], sp["eos_id"], sp["pad_id"])
-        stacked = {
-            "feats": batch["feats"].repeat(P, 1, 1),
-            "feat_lens": batch["feat_lens"].repeat(P),
-        }
-        enc, mask, ctc = self.model(stacked, precision=2, sp_mask=bits)
+        # the encoder repeats the (pass-independent) subsampling output P times itself
+        enc, mask, ctc = self.model(batch, precision=2, sp_mask=bits)
         logits = self.model.decode_logits(enc, mask, t_inp.repeat(P, 1), t_pad.repeat(P, 1))
         vocab = logits.size(-1)
         u1 = logits.size(1)

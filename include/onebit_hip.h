@@ -181,6 +181,33 @@ OB_API int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t
                                    const uint32_t* codes2, const uint32_t* codes1,
                                    const int32_t* pass_bits, const float* alpha, int alpha_raw,
                                    const float* bias, int64_t N, float* Y, void* stream);
+/*
+ * Opt-in int8 activation mode (north_star "per-tensor absmax int8 activations"; NOT the
+ * reference's arithmetic, which keeps activations fp32 at quant.py:126 -- SURVEY.md §0
+ * F3). Replaces, for QuantizedLinear.act_quant == "absmax_int8", the F.linear call of
+ * quant.py:126 by BitNet-b1.58 activation quantization x int8 matrix cores:
+ *   g_p = max(max|X_p|, 1e-5); sx = 127/g_p; xq = clamp(rint(x*sx), -127, 127);
+ *   Y = float(sum_k xq*Q) * (a * (g_p/127)) + b   (mul then add, each rounded: no fma).
+ * ob_act_absmax: amax[p] = max|X_p| over the n_per_pass elements of pass p (per-block
+ *   partials in ws, then a final reduce; order-independent, so deterministic). X 16-byte
+ *   aligned, n_per_pass % 4 == 0; ws of ob_act_absmax_workspace(P) bytes.
+ * ob_act_dequant_i8: X_deq = xq * (g_p/127) (the activations the int8 forward multiplied;
+ *   dW = dY^T X_deq under the straight-through estimator).
+ * ob_bitlinear_fwd_i8: P passes stacked on rows like ob_bitlinear_fwd_passes; P == 1 may
+ *   pass pass_bits = NULL (then codes is used and codes1 is ignored). Needs K % 16 == 0,
+ *   K <= 576 (OB_ERR_SHAPE otherwise) and X 16-byte aligned.
+ */
+OB_API size_t ob_act_absmax_workspace(int64_t P);
+OB_API int ob_act_absmax(const float* X, int64_t P, int64_t n_per_pass, float* amax, void* ws,
+                         size_t ws_bytes, void* stream);
+OB_API int ob_act_dequant_i8(const float* X, int64_t P, int64_t n_per_pass, const float* amax,
+                             float* X_deq, void* stream);
+OB_API int ob_bitlinear_fwd_i8(const float* X, int64_t P, int64_t M, int64_t K,
+                               const uint32_t* codes, const uint32_t* codes1,
+                               const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                               const float* amax, const float* bias, int64_t N, float* Y,
+                               void* stream);
+
 OB_API int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
                                       const uint32_t* codes2_t, const uint32_t* codes1_t,
                                       const int32_t* pass_bits, const float* alpha,
@@ -265,6 +292,36 @@ OB_API int ob_adamw_clip_step(const ob_adamw_tensor* table, int64_t n_tensors,
                               double eps, double weight_decay, double max_norm,
                               float* total_norm, void* ws,
                               size_t ws_bytes, void* stream);
+
+/*
+ * LayerNorm over the last dim (the Conformer's LayerNorm wrappers, conformer.py:19-24:
+ * nn.LayerNorm(d) before every BitLinear call site). x, y [rows][d], d <= 512;
+ * gamma/beta [d] or NULL (1 / 0); mean, rstd [rows] (either may be NULL when no backward
+ * follows). var is biased (torch), rstd = 1/sqrt(var + eps).
+ * Backward: dx [rows][d]; dgamma/dbeta [d] (NULL to skip) summed over rows in a fixed
+ * order (deterministic) through the workspace.
+ */
+OB_API int ob_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
+                            int64_t d, float eps, float* y, float* mean, float* rstd,
+                            void* stream);
+OB_API size_t ob_layernorm_bwd_workspace(int64_t rows, int64_t d);
+OB_API int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma,
+                            const float* mean, const float* rstd, int64_t rows, int64_t d,
+                            float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+                            void* stream);
+
+/*
+ * Batched greedy CTC decode (inference path). Replaces onebit_asr/metrics.py:51-60
+ * ctc_greedy_decode(logits[T, V], blank_id) called per utterance: for utterance b over its
+ * first lens[b] frames, pred = argmax_v logits[b][t][v] (lowest index on ties, as
+ * torch.argmax), emit pred[t] when pred[t] != blank and pred[t] != pred[t-1].
+ *   logits [B][T][V] fp32; lens int64 [B] (device); ids int32 [B][T] workspace (the
+ *   per-frame argmax, left for the caller); out int32 [B][T] (tokens first, -1 after);
+ *   out_len int32 [B].
+ */
+OB_API int ob_ctc_greedy_decode(const float* logits, const int64_t* lens, int64_t B, int64_t T,
+                                int64_t V, int blank, int32_t* ids, int32_t* out,
+                                int32_t* out_len, void* stream);
 
 #ifdef __cplusplus
 }

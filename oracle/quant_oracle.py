@@ -107,6 +107,38 @@ def np_bitlinear_fwd(X: np.ndarray, W: np.ndarray, alpha: float, bias, bits: int
 _clib = None
 
 
+# ------------------------------------------------------ opt-in int8 activation mode
+# NOT reference arithmetic (the reference keeps activations fp32, quant.py:126; SURVEY.md
+# §0 F3). This restates the north-star mode the HIP path implements
+# (cmu-11785-idl-1.58bit-asr_amd/csrc/tgemm_i8.hip) so it can be checked bit-exactly:
+# BitNet-b1.58 per-tensor absmax activations, then the reference's F.linear with W_hat.
+def np_act_quant_i8(X: np.ndarray):
+    """(xq int32, gamma f32): gamma = max(max|X|, 1e-5), xq = clamp(rint(X * (127/gamma)))."""
+    X = np.asarray(X, np.float32)
+    gam = np.float32(max(np.float32(np.abs(X).max()) if X.size else np.float32(0), np.float32(1e-5)))
+    sx = np.float32(np.float32(127.0) / gam)
+    xq = np.clip(np.rint((X * sx).astype(np.float32)), -127, 127).astype(np.int32)
+    return xq, gam
+
+
+def np_act_dequant_i8(X: np.ndarray) -> np.ndarray:
+    xq, gam = np_act_quant_i8(X)
+    return (xq.astype(np.float32) * np.float32(gam / np.float32(127.0))).astype(np.float32)
+
+
+def np_bitlinear_fwd_i8(X: np.ndarray, W: np.ndarray, alpha: float, bias, bits: int,
+                        alpha_raw: bool = True) -> np.ndarray:
+    """Y = float(xq . Q^T) * (a * (gamma/127)) + b, each op rounded once in fp32."""
+    xq, gam = np_act_quant_i8(X)
+    q = np_quant_q(W, alpha, bits, alpha_raw).astype(np.int64)
+    acc = (xq.astype(np.int64) @ q.T).astype(np.float32)  # exact integers (< 2^24)
+    osc = np.float32(np_effective_alpha(alpha, alpha_raw) * np.float32(gam / np.float32(127.0)))
+    y = (acc * osc).astype(np.float32)
+    if bias is not None:
+        y = (y + np.asarray(bias, np.float32)).astype(np.float32)
+    return y
+
+
 def c_lib() -> ctypes.CDLL:
     global _clib
     if _clib is None:

@@ -83,3 +83,21 @@ def test_bitlinear_python_surface_on_cpu():
     with pytest.raises(RuntimeError, match="ROCm device"):
         m(x, 2)
     assert QuantizedLinear(4, 4, bias=False).bias is None
+
+
+def test_i8_entry_validation_without_gpu():
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    fake = 0x1000
+    # K % 16 != 0 -> shape; P > 1 without pass_bits -> null; misaligned X -> align
+    assert lib.ob_bitlinear_fwd_i8(fake, 1, 4, 20, fake, None, None, fake, 1, fake, None, 8,
+                                   fake, None) == -2
+    assert lib.ob_bitlinear_fwd_i8(fake, 3, 4, 16, fake, fake, None, fake, 1, fake, None, 8,
+                                   fake, None) == -1
+    assert lib.ob_bitlinear_fwd_i8(0x1004, 1, 4, 16, fake, None, None, fake, 1, fake, None, 8,
+                                   fake, None) == -5
+    assert lib.ob_act_absmax(fake, 0, 16, fake, fake, 1 << 20, None) == -2
+    assert lib.ob_act_absmax(fake, 1, 18, fake, fake, 1 << 20, None) == -5
+    assert lib.ob_act_absmax(fake, 1, 16, fake, fake, 4, None) == -4
+    assert lib.ob_act_dequant_i8(fake, 1, 16, None, fake, None) == -1

@@ -136,3 +136,23 @@ def test_bad_bitwidth():
         qo.c_quant_q(W, 1.0, 4)
     with pytest.raises(ValueError, match=r"bitwidth must be one of \{1,2,32\}"):
         qo.ref_quantize_weight(torch.zeros(2, 2), torch.tensor(1.0), 8)
+
+
+def test_i8_mode_kat():
+    """Hand-derived known answer for the opt-in int8 activation restatement: gamma = 127 so
+    sx = 1 and rint's half-to-even ties are visible (-63.5 -> -64, 2.5 -> 2, 0.5 -> 0)."""
+    X = np.array([[127.0, -63.5, 31.75, 2.5, 0.5]], np.float32)
+    xq, gam = qo.np_act_quant_i8(X)
+    assert gam == np.float32(127.0)
+    assert xq.tolist() == [[127, -64, 32, 2, 0]]
+    W = np.array([[1.0, -1.0, 0.1, 1.0, 1.0], [0.0, 0.6, -0.7, 0.2, -1.0]], np.float32)
+    b = np.array([0.5, -0.25], np.float32)
+    y = qo.np_bitlinear_fwd_i8(X, W, 1.0, b, 2)  # a = fp32(1 + 1e-8) = 1; Q2 = [1,-1,0,1,1], [0,1,-1,0,-1]
+    acc = np.array([127 + 64 + 2 + 0, -64 - 32 - 0], np.float32)
+    expect = (acc * np.float32(np.float32(1.0) * np.float32(np.float32(127.0) / np.float32(127.0)))).astype(np.float32) + b
+    np.testing.assert_array_equal(y[0], expect)
+    # all-zero input: gamma clamps to 1e-5, every code is 0, y = bias
+    np.testing.assert_array_equal(qo.np_bitlinear_fwd_i8(np.zeros((2, 5), np.float32), W, 1.0, b, 1),
+                                  np.broadcast_to(b, (2, 2)))
+    deq = qo.np_act_dequant_i8(X)
+    np.testing.assert_array_equal(deq, np.array([[127, -64, 32, 2, 0]], np.float32))
