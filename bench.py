@@ -66,7 +66,11 @@ def parse():
                     help="train: configs[1]/[2] (default); quant-off: configs[3] (BitLinear -> "
                          "bf16 nn.Linear); infer / infer-fp32act: configs[4] (B=256, 2-bit, "
                          "int8 / fp32 activations, greedy CTC decode)")
+    ap.add_argument("--conv-find", action="store_true",
+                    help="torch.backends.cudnn.benchmark (MIOpen Find) for the subsampling convs")
     args = ap.parse_args()
+    if args.conv_find:
+        torch.backends.cudnn.benchmark = True
     if args.mode.startswith("infer") and args.batch == 32:
         args.batch = 256  # configs[4]
     return args

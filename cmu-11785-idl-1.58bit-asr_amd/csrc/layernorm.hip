@@ -141,31 +141,51 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
   }
 }
 
-// dgamma[c] = sum over blocks of part_g[blk][c] (fixed order), same for dbeta.
+// dgamma[c] = sum over blocks of part_g[blk][c], same for dbeta. Block = 16 columns x 16
+// block-slices; slice s sums blocks s, s+16, ... (4 independent accumulators in flight),
+// then the 16 slices are added in slice order through LDS (fixed order: deterministic).
+constexpr int kRedCols = 16, kRedSlices = kThreads / kRedCols;
+
 __global__ __launch_bounds__(kThreads) void ln_param_reduce_kernel(
     const float* __restrict__ part_g, const float* __restrict__ part_b, int nblk, int d,
     float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  // 64 columns per block, 4 block-slices per column summed in fixed order through LDS
-  __shared__ float sg[4][64], sb[4][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float sg[kRedSlices][kRedCols], sb[kRedSlices][kRedCols];
+  const int cl = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int c = blockIdx.x * kRedCols + cl;
   float ag = 0.0f, ab = 0.0f;
   if (c < d) {
-    for (int b = sl; b < nblk; b += 4) {
-      ag += part_g[(int64_t)b * d + c];
-      ab += part_b[(int64_t)b * d + c];
+    float g4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = sl;
+    for (; b + 3 * kRedSlices < nblk; b += 4 * kRedSlices) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g4[u] += part_g[(int64_t)(b + u * kRedSlices) * d + c];
+        b4[u] += part_b[(int64_t)(b + u * kRedSlices) * d + c];
+      }
     }
+    for (int u = 0; b < nblk; b += kRedSlices, ++u) {
+      g4[u & 3] += part_g[(int64_t)b * d + c];
+      b4[u & 3] += part_b[(int64_t)b * d + c];
+    }
+    ag = (g4[0] + g4[1]) + (g4[2] + g4[3]);
+    ab = (b4[0] + b4[1]) + (b4[2] + b4[3]);
   }
   sg[sl][cl] = ag;
   sb[sl][cl] = ab;
   __syncthreads();
   if (sl == 0 && c < d) {
-    if (dgamma) dgamma[c] = ((sg[0][cl] + sg[1][cl]) + sg[2][cl]) + sg[3][cl];
-    if (dbeta) dbeta[c] = ((sb[0][cl] + sb[1][cl]) + sb[2][cl]) + sb[3][cl];
+    float tg = 0.0f, tb = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kRedSlices; ++q) {
+      tg += sg[q][cl];
+      tb += sb[q][cl];
+    }
+    if (dgamma) dgamma[c] = tg;
+    if (dbeta) dbeta[c] = tb;
   }
 }
 
-constexpr int kMaxBwdBlocks = 1024;
+constexpr int kMaxBwdBlocks = 512;
 
 int bwd_blocks(int64_t rows, int* rows_per_block) {
   int64_t nb = ceil_div(rows, kRowsPerBlock);
@@ -222,7 +242,7 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
 #undef OB_LNB
   }
   if (params)
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, 64)), dim3(kThreads), 0,
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, kRedCols)), dim3(kThreads), 0,
                        s, part_g, part_b, nb, (int)d, dgamma, dbeta);
 }
 

@@ -19,7 +19,7 @@
 // Layout: q, k, v, ctx, dq, dk, dv [Bt][T][H*d]; pos, dpos [P][T][H*d] (batch row b uses
 // pass b / (Bt/P)); u, vb, du, dvb [H][d]; probs [Bt][H][T][T]; lens int32 [Bt].
 // Products on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, like torch's fp32 matmul).
-// Dropout keeps (i, j) when hash(seed, counter, index) >= p * 2^32 (a counter-based hash:
+// Dropout keeps (i, j) when hash(key(seed, counter), index) >= p * 2^32 (a counter hash:
 // the backward regenerates the same mask; torch's own RNG stream is not reproduced).
 #include <math.h>
 
@@ -38,14 +38,26 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t ctr, uint64_t idx) {
-  uint64_t x = idx * 0x9E3779B97F4A7C15ull ^ (seed + ctr * 0xD1B54A32D192ED03ull);
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return (uint32_t)(x >> 32);
+// Dropout keep-hash: a 32-bit counter hash (murmur3 fmix32 of the element index mixed with
+// a per-call key). The key folds (seed, counter) once per kernel; each element then costs
+// ~8 VALU ops -- the earlier 64-bit splitmix form (three 64-bit multiplies per element,
+// evaluated twice in the backward) cost more than the kernels' matrix work.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint64_t ctr) {
+  return fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ 0x9E3779B9u) ^
+                fmix32((uint32_t)ctr * 0x27D4EB2Fu + (uint32_t)(ctr >> 32)));
+}
+
+__device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t idx) {
+  return fmix32(((uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x165667B1u)) * 0x9E3779B1u + key);
 }
 
 struct DropCfg {
@@ -156,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   }
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
-  const uint64_t seed = dc.on ? rng[0] : 0, ctr = dc.on ? rng[1] : 0;
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
   const size_t prow_off = (((size_t)b * H + h) * T + qic) * T;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
@@ -168,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       if (probs && qi < T && jj < T) probs[prow_off + jj] = pr;
       float pd = pr;
       if (dc.on) {
-        const bool keep = drop_hash(seed, ctr, prow_off + jj) >= dc.thresh;
+        const bool keep = drop_hash(dkey, prow_off + jj) >= dc.thresh;
         pd = keep ? pr * dc.scale : 0.0f;
       }
       sreg[t][j] = pd;
@@ -238,11 +250,11 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* ub = u + h * D;
   const float* vbb = vbias + h * D;
   const float* prb = probs + ((size_t)b * H + h) * T * T;
-  const uint64_t seed = dc.on ? rng[0] : 0, ctr = dc.on ? rng[1] : 0;
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
   const size_t pbase = ((size_t)b * H + h) * T * T;
   auto keep_scale = [&](int i, int j) -> float {
     if (!dc.on) return 1.0f;
-    return drop_hash(seed, ctr, pbase + (size_t)i * T + j) >= dc.thresh ? dc.scale : 0.0f;
+    return drop_hash(dkey, pbase + (size_t)i * T + j) >= dc.thresh ? dc.scale : 0.0f;
   };
 
   const int qi = i0 + 16 * w + r;
@@ -442,8 +454,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   }
 }
 
-// dk, dv [Bt][T][H*D]: sum over query tiles; dpos [P][T][H*D]: over the pass's rows and
-// tiles; du, dvb [H][D]: over rows and tiles. Thread per output element, fixed order.
+// dk, dv [Bt][T][H*D]: sum over query tiles. Thread per output element, fixed order.
+// (dpos: relattn_dpos_reduce_kernel; du, dvb: relattn_bias_reduce_kernel.)
 __global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
     const float* __restrict__ dk_part, const float* __restrict__ dv_part,
     const float* __restrict__ dp_part, const float* __restrict__ du_part,
@@ -452,9 +464,7 @@ __global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
     float* __restrict__ du, float* __restrict__ dvb) {
   const int C = H * D;
   const int64_t n_kv = (int64_t)Bt * T * C;
-  const int64_t n_p = (int64_t)P * T * C;
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int Bp = Bt / P;
   if (e < n_kv) {
     const int b = (int)(e / ((int64_t)T * C));
     const int rem = (int)(e - (int64_t)b * T * C);
@@ -467,25 +477,68 @@ __global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
     }
     dk[e] = sk;
     dv[e] = sv;
-  } else if (e < n_kv + n_p) {
-    const int64_t f = e - n_kv;
+  }
+}
+
+// du, dvb [H][D]: sum over (batch row, query tile) of the per-tile partials. Block = one
+// (which, head) x 64 columns x 16 slices (slice s: pairs s, s+16, ...), slices added in
+// order through LDS (fixed order). A thread per output with a serial loop over the
+// Bt*nqt partials measured 170 us at Conformer-S (one dependent load chain per thread).
+constexpr int kBiasSlices = 16;
+
+__global__ __launch_bounds__(64 * kBiasSlices) void relattn_bias_reduce_kernel(
+    const float* __restrict__ du_part, const float* __restrict__ dvb_part, int Bt, int H, int D,
+    int nqt, float* __restrict__ du, float* __restrict__ dvb) {
+  __shared__ float red[kBiasSlices][64];
+  const int which = blockIdx.x / H, h = blockIdx.x - which * H;
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const float* src = which == 0 ? du_part : dvb_part;
+  const int pairs = Bt * nqt;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < D) {
+    int u = 0;
+    for (int q = sl; q < pairs; q += kBiasSlices, ++u) {
+      const int b = q / nqt, qt = q - b * nqt;
+      a[u & 3] += src[(((size_t)b * H + h) * nqt + qt) * D + c];
+    }
+  }
+  red[sl][c] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (sl == 0 && c < D) {
+    float t = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kBiasSlices; ++q) t += red[q][c];
+    (which == 0 ? du : dvb)[h * D + c] = t;
+  }
+}
+
+// dpos [P][T][H*D]: sum over the pass's Bp batch rows and the query tiles. Block = 64
+// consecutive output elements x 4 batch slices (slice s: rows s, s+4, ... of the pass);
+// the slices are added in slice order through LDS (fixed order: deterministic).
+__global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
+    const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D, int nqt,
+    float* __restrict__ dpos) {
+  __shared__ float red[4][64];
+  const int C = H * D;
+  const int64_t n_p = (int64_t)P * T * C;
+  const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t f = (int64_t)blockIdx.x * 64 + el;
+  const int Bp = Bt / P;
+  float s = 0.0f;
+  if (f < n_p) {
     const int p = (int)(f / ((int64_t)T * C));
     const int rem = (int)(f - (int64_t)p * T * C);
     const int t = rem / C, hc = rem - t * C, h = hc / D, c = hc - h * D;
-    float s = 0.0f;
-    for (int b = p * Bp; b < (p + 1) * Bp; ++b)
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int u = 0;
+    for (int b = p * Bp + sl; b < (p + 1) * Bp; b += 4, ++u)
       for (int qt = 0; qt < nqt; ++qt)
-        s += dp_part[(((((size_t)qt * Bt + b) * H + h) * T) + t) * D + c];
-    dpos[f] = s;
-  } else if (e < n_kv + n_p + 2 * C) {
-    const int f = (int)(e - n_kv - n_p);
-    const int which = f / C, hc = f - which * C, h = hc / D, c = hc - h * D;
-    const float* src = which == 0 ? du_part : dvb_part;
-    float s = 0.0f;
-    for (int b = 0; b < Bt; ++b)
-      for (int qt = 0; qt < nqt; ++qt) s += src[(((size_t)b * H + h) * nqt + qt) * D + c];
-    (which == 0 ? du : dvb)[hc] = s;
+        a[u & 3] += dp_part[(((((size_t)qt * Bt + b) * H + h) * T) + t) * D + c];
+    s = (a[0] + a[1]) + (a[2] + a[3]);
   }
+  red[sl][el] = s;
+  __syncthreads();
+  if (sl == 0 && f < n_p) dpos[f] = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
 }
 
 __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropCfg dc,
@@ -493,7 +546,7 @@ __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropC
                                                                 uint8_t* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e >= n) return;
-  out[e] = (!dc.on || drop_hash(rng[0], rng[1], (uint64_t)e) >= dc.thresh) ? 1 : 0;
+  out[e] = (!dc.on || drop_hash(drop_key(rng[0], rng[1]), (uint64_t)e) >= dc.thresh) ? 1 : 0;
 }
 
 DropCfg make_drop(float p_drop) {
@@ -570,10 +623,16 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
   const int64_t C = H * d;
-  const int64_t total = Bt * T * C + P * T * C + 2 * C;
+  const int64_t total = Bt * T * C;
   hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)),
                      dim3(kThreads), 0, s, dk_part, dv_part, dp_part, du_part, dvb_part, (int)Bt,
                      (int)P, (int)T, (int)H, (int)d, nqt, dk, dv, dpos, du, dvb);
+  hipLaunchKernelGGL(relattn_bias_reduce_kernel, dim3((unsigned)(2 * H)), dim3(64 * kBiasSlices),
+                     0, s, (const float*)du_part, (const float*)dvb_part, (int)Bt, (int)H, (int)d,
+                     nqt, du, dvb);
+  hipLaunchKernelGGL(relattn_dpos_reduce_kernel, dim3((unsigned)ceil_div(P * T * C, 64)),
+                     dim3(kThreads), 0, s, dp_part, (int)Bt, (int)P, (int)T, (int)H, (int)d, nqt,
+                     dpos);
 }
 
 void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,

@@ -62,9 +62,14 @@ def test_graph_replay_matches_eager(gpu):
     # gradient differences, which Adam turns into up to lr-sized steps where a gradient
     # element is ~0 (its sign is noise). Bound: every element within 2 * lr_max per step
     # (5 steps, lr <= 5e-4); all but 0.5% of each tensor within 1e-5 * max|p| + 1e-4.
+    # Parameters whose true gradient is zero (a bias before BatchNorm, key biases under the
+    # softmax's shift invariance) move by lr-sized noise steps everywhere: max bound only.
+    zero_grad = ("conv.dw.bias", "k_proj.bias", "in_proj_bias")
     for (k, a), (_, b) in zip(m_g.named_parameters(), m_e.named_parameters()):
         diff = (a - b).abs()
         assert diff.max().item() <= 5 * 2 * 5e-4, (k, diff.max().item())
+        if any(z in k for z in zero_grad):
+            continue
         loose = (diff > 1e-5 * b.abs().max().item() + 1e-4).float().mean().item()
         assert loose <= 5e-3, (k, loose)
 
