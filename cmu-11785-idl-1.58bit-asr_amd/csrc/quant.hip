@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kThreads) void quant_dequant_kernel(const float* __
 // elements' chunks in chunk order with all loads independent. Few, wide blocks keep the
 // number of ticket atomics on the one completion counter small (each costs ~12 ns
 // serialised; 1300 blocks cost 16 us at Conformer-S). Deterministic.
-constexpr int kReduceEPT = 4;
+constexpr int kReduceEPT = 2;  // 2: ~160 blocks for an 83k-element layer (4 left 2/3 of the CUs idle)
 constexpr int kReduceElems = kThreads * kReduceEPT;
 
 __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
@@ -119,6 +119,13 @@ __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
       const float* sp = src + (int64_t)p * cpp * stride;
       float gp = 0.0f;
       int c = 0;
+      for (; c + 8 <= cpp; c += 8) {  // 8 loads in flight, summed in chunk order
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = sp[(int64_t)(c + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gp += v[u];
+      }
       for (; c + 4 <= cpp; c += 4) {
         const float v0 = sp[(int64_t)c * stride];
         const float v1 = sp[(int64_t)(c + 1) * stride];

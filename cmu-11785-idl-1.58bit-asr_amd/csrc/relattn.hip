@@ -60,6 +60,29 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t idx) {
   return fmix32(((uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x165667B1u)) * 0x9E3779B1u + key);
 }
 
+// Bijective XCD-aware remap (hardware block b runs on XCD b % 8): consecutive logical ids
+// share an XCD, so the query tiles and heads of one batch row -- which read the same
+// q/k/v/pos cache lines (heads are column slices of one row) -- share one L2.
+__device__ __forceinline__ int xcd_logical(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+struct BlockId {
+  int qt, h, b;
+};
+
+// 1-D grid of nqt * H * Bt blocks -> (query tile, head, batch row), tile fastest.
+__device__ __forceinline__ BlockId block_id(int nqt, int H) {
+  const int L = xcd_logical((int)blockIdx.x, (int)gridDim.x);
+  BlockId id;
+  id.qt = L % nqt;
+  const int rest = L / nqt;
+  id.h = rest % H;
+  id.b = rest / H;
+  return id;
+}
+
 struct DropCfg {
   uint32_t thresh;  // keep iff hash >= thresh
   float scale;      // 1 / (1 - p)
@@ -81,7 +104,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   extern __shared__ float xs[];
   const int nt = (T + 15) >> 4;
   const int ldx = 16 * nt + 1;
-  const int b = blockIdx.z, h = blockIdx.y, i0 = blockIdx.x * kTile;
+  const BlockId bid = block_id((T + kTile - 1) / kTile, H);
+  const int b = bid.b, h = bid.h, i0 = bid.qt * kTile;
   const int pass = b / Bp;
   const int C = H * D;
   const int L = min(lens[b], T);
@@ -105,16 +129,29 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   }
 
   // X = (q + v) p^T for the wave's 16 rows: D[m][query] with A = p rows, B = (q+v)
+  // four key tiles at a time, s-major: consecutive MFMAs feed different accumulators
+  // (per-accumulator order unchanged)
 #pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* prow = pb + (size_t)min(16 * t + r, T - 1) * C + g * DQ;
+  for (int t0 = 0; t0 < NTT; t0 += 4) {
+    if (t0 >= nt) continue;
+    f32x4 acc[4];
+    const float* prow[4];
 #pragma unroll
-    for (int s = 0; s < DQ; ++s) acc = mfma4(prow[s], qv[s], acc);
-    float* dst = xs + (16 * w + r) * ldx + 16 * t + 4 * g;
+    for (int u = 0; u < 4; ++u) {
+      acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      prow[u] = pb + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ;
+    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = acc[j];
+    for (int s = 0; s < DQ; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = mfma4(prow[u][s], qv[s], acc[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (t0 + u >= nt) continue;
+      float* dst = xs + (16 * w + r) * ldx + 16 * (t0 + u) + 4 * g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = acc[u][j];
+    }
   }
   // row 64: the next tile's first query (fp32 fma chain on the VALU)
   if (i0 + kTile < T) {
@@ -133,12 +170,24 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   float mx = -INFINITY;
   const float* xrow = xs + (16 * w + r) * ldx;
 #pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* krow = kb + (size_t)min(16 * t + r, T - 1) * C + g * DQ;
+  for (int t0 = 0; t0 < NTT; t0 += 4) {
+    if (t0 >= nt) continue;
+    f32x4 acc4[4];
+    const float* krow[4];
 #pragma unroll
-    for (int s = 0; s < DQ; ++s) acc = mfma4(krow[s], qu[s], acc);
+    for (int u = 0; u < 4; ++u) {
+      acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      krow[u] = kb + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ;
+    }
+#pragma unroll
+    for (int s = 0; s < DQ; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc4[u] = mfma4(krow[u][s], qu[s], acc4[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    const int t = t0 + u;
+    if (t >= nt) continue;
+    const f32x4 acc = acc4[u];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
@@ -150,6 +199,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       const bool valid = qi < L && jj < L;
       sreg[t][j] = valid ? sc : -INFINITY;
       mx = fmaxf(mx, sreg[t][j]);
+    }
     }
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16));
@@ -235,9 +285,10 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   __shared__ float rsum[kThreads / 64];
   const int nt = (T + 15) >> 4;
   const int ldx = 16 * nt + 1;
-  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x, i0 = qt * kTile;
-  const int nqt = gridDim.x;
-  const int Bt = gridDim.z;
+  const int nqt = (T + kTile - 1) / kTile;
+  const int Bt = (int)gridDim.x / (nqt * H);
+  const BlockId bid = block_id(nqt, H);
+  const int b = bid.b, h = bid.h, qt = bid.qt, i0 = qt * kTile;
   const int pass = b / Bp;
   const int C = H * D;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
@@ -267,12 +318,24 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   float dsr[NTT][4];
   float rowdot = 0.0f;
 #pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* vrow = vbp + (size_t)min(16 * t + r, T - 1) * C + g * DQ;
+  for (int t0 = 0; t0 < NTT; t0 += 4) {
+    if (t0 >= nt) continue;
+    f32x4 acc4[4];
+    const float* vrow[4];
 #pragma unroll
-    for (int s = 0; s < DQ; ++s) acc = mfma4(vrow[s], dor[s], acc);
+    for (int u = 0; u < 4; ++u) {
+      acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      vrow[u] = vbp + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ;
+    }
+#pragma unroll
+    for (int s = 0; s < DQ; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc4[u] = mfma4(vrow[u][s], dor[s], acc4[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+    const int t = t0 + u;
+    if (t >= nt) continue;
+    f32x4 acc = acc4[u];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
@@ -286,6 +349,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     float* dst = ds + (1 + 16 * w + r) * ldx + 16 * t + 4 * g;
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j] = acc[j];
+    }
   }
   rowdot += __shfl_xor(rowdot, 16);
   rowdot += __shfl_xor(rowdot, 32);
@@ -590,7 +654,7 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
                         const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
                         int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
                         float* probs, float* ctx, hipStream_t s) {
-  const dim3 grid((unsigned)((T + kTile - 1) / kTile), (unsigned)H, (unsigned)Bt);
+  const dim3 grid((unsigned)(((T + kTile - 1) / kTile) * H * Bt));
   const DropCfg dc = make_drop(p_drop);
   const float sqrt_d = (float)sqrt((double)d);
   const size_t lds = lds_bytes((int)T);
@@ -607,7 +671,7 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
                         const uint64_t* rng, const float* probs, float* dq, float* dk, float* dv,
                         float* dpos, float* du, float* dvb, void* ws, hipStream_t s) {
   const int nqt = (int)((T + kTile - 1) / kTile);
-  const dim3 grid((unsigned)nqt, (unsigned)H, (unsigned)Bt);
+  const dim3 grid((unsigned)(nqt * H * Bt));
   const DropCfg dc = make_drop(p_drop);
   const float sqrt_d = (float)sqrt((double)d);
   const size_t lds = lds_bytes((int)T);

@@ -98,7 +98,7 @@ __device__ __forceinline__ void select_pass(const float* __restrict__& A, float*
 }
 
 template <int NT, int NCH>
-__global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
+__global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
@@ -189,12 +189,14 @@ __global__ __launch_bounds__(kThreads) void tgemm_bf16x3_kernel(
       __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (hipcc would pair them up)
       bf16x8 hi, mid, lo;
       split3(x0, x1, hi, mid, lo);
+      // part-major: consecutive MFMAs update different accumulators (no back-to-back
+      // dependence on the MFMA just issued)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        acc[t] = mfma_bf16(lo, bq[t], acc[t]);
-        acc[t] = mfma_bf16(mid, bq[t], acc[t]);
-        acc[t] = mfma_bf16(hi, bq[t], acc[t]);
-      }
+      for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(lo, bq[t], acc[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(mid, bq[t], acc[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(hi, bq[t], acc[t]);
     };
 
     if constexpr (NCH > 0) {
