@@ -9,8 +9,10 @@
 // torch materialises ac, bd (padded, shifted copies), S, A and the dropout mask as
 // [B,H,T,T] fp32 tensors, ~10 full passes per block per pass. Here the forward is one
 // kernel that keeps a query tile's scores in registers and writes only ctx and the
-// softmax probabilities (kept for the backward); the backward is one kernel plus a small
-// fixed-order reduction, writing dq, dk, dv, dpos, du, dv_bias.
+// softmax probabilities (kept for the backward). The backward is a query-side kernel (dq,
+// dS' to global) and a key-side kernel (dk, dv, per-row dpos over all queries: no
+// per-query-tile partials), plus two small fixed-order reductions (du/dvb over tiles,
+// dpos over the pass's batch rows).
 //
 // rel_shift as a gather: with X = (q + v) p^T,
 //   bd[i][j] = X[i][T-1-i+j]   (j <= i);   0   (j == i+1);   X[i+1][j-i-2]   (j >= i+2)
@@ -265,10 +267,10 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------
-// Backward: block = (query tile, head, batch row). dq is final; dk, dv, dpos, du, dvb
-// are written as per-tile partials and summed by relattn_reduce_kernel in fixed order.
-// LDS holds dS' = dS / sqrt(d) for query rows i0-1 .. i0+63 (row 0 = i0-1, recomputed
-// here on the VALU) -- the rows the rel_shift adjoint of the tile needs.
+// Backward, query side: block = (query tile, head, batch row). Writes dq (final), the
+// tile's du / dvb partials (summed by relattn_bias_reduce_kernel) and dS' = dS / sqrt(d)
+// to global for the key-side kernel. LDS holds dS' for query rows i0-1 .. i0+63 (row 0 =
+// i0-1, recomputed here on the VALU) -- the rows the rel_shift adjoint of the tile needs.
 // ------------------------------------------------------------------------------------
 template <int DQ, int NTT>
 __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
@@ -276,8 +278,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     const float* __restrict__ v, const float* __restrict__ pos, const float* __restrict__ u,
     const float* __restrict__ vbias, const int* __restrict__ lens, int Bp, int T, int H,
     float sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, const float* __restrict__ probs,
-    float* __restrict__ dq, float* __restrict__ dk_part, float* __restrict__ dv_part,
-    float* __restrict__ dp_part, float* __restrict__ du_part, float* __restrict__ dvb_part) {
+    float* __restrict__ dq, float* __restrict__ dsg, float* __restrict__ du_part,
+    float* __restrict__ dvb_part) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   extern __shared__ float ds[];
@@ -286,20 +288,16 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const int nt = (T + 15) >> 4;
   const int ldx = 16 * nt + 1;
   const int nqt = (T + kTile - 1) / kTile;
-  const int Bt = (int)gridDim.x / (nqt * H);
   const BlockId bid = block_id(nqt, H);
   const int b = bid.b, h = bid.h, qt = bid.qt, i0 = qt * kTile;
   const int pass = b / Bp;
   const int C = H * D;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
   const size_t bo = (size_t)b * T * C + h * D;
-  const float* qb = q + bo;
   const float* kb = k + bo;
   const float* vbp = v + bo;
   const float* dob = dctx + bo;
   const float* pb = pos + (size_t)pass * T * C + h * D;
-  const float* ub = u + h * D;
-  const float* vbb = vbias + h * D;
   const float* prb = probs + ((size_t)b * H + h) * T * T;
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
   const size_t pbase = ((size_t)b * H + h) * T * T;
@@ -469,78 +467,113 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     dvb_part[tile_id * D + c] = ((red[0][1][c] + red[1][1][c]) + red[2][1][c]) + red[3][1][c];
   }
 
-  // key-side partials over this tile's 64 queries; wave w takes key tiles t = w, w+4, ...
-  // dK = dS'^T (q+u), dV = Pd^T dO, dpos = dX^T (q+v)
-  const size_t part_base = ((size_t)qt * Bt + b) * H + h;  // [qt][b][h] then [T][D]
-  for (int t = w; t < nt; t += 4) {
-    f32x4 ak[CT], av[CT], ap[CT];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      ak[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-      av[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const int key = 16 * t + r;  // A row = key (or position m) r of the tile
-    for (int qk = 0; qk < kTile / 4; ++qk) {
-      const int qrow = i0 + 4 * qk + g;  // k index = query
-      const bool qok = qrow < T;
-      const int qrc = min(qrow, T - 1);
-      const float* lrow = ds + (1 + 4 * qk + g) * ldx;  // dS' row qrow
-      const float a_k = (qok && key < T) ? lrow[key] : 0.0f;
-      const float pv = (qok && key < T) ? prb[(size_t)qrow * T + key] : 0.0f;
-      const float a_v = pv * keep_scale(qrc, min(key, T - 1));
-      const float a_p = (qok && key < T) ? dX(qrow, lrow, lrow - ldx, key) : 0.0f;
-      const float* qrowp = qb + (size_t)qrc * C;
-      const float* drowp = dob + (size_t)qrc * C;
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int c = min(16 * ct + r, D - 1);
-        const float qx = qrowp[c];
-        ak[ct] = mfma4(a_k, qx + ub[c], ak[ct]);
-        av[ct] = mfma4(a_v, drowp[c], av[ct]);
-        ap[ct] = mfma4(a_p, qx + vbb[c], ap[ct]);
-      }
-    }
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int col = 16 * ct + r;
-      if (col >= D) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kk = 16 * t + 4 * g + j;
-        if (kk >= T) continue;
-        const size_t o = (part_base * T + kk) * D + col;
-        dk_part[o] = ak[ct][j];
-        dv_part[o] = av[ct][j];
-        dp_part[o] = ap[ct][j];
-      }
-    }
+  // dS' rows of this tile to global for the key-side kernel (row-contiguous copy of the
+  // LDS image: wave w copies rows 16w .. 16w+15, 64 consecutive columns per instruction)
+  float* dsb = dsg + ((size_t)b * H + h) * T * T;
+  for (int rr = 0; rr < 16; ++rr) {
+    const int qrow = i0 + 16 * w + rr;
+    if (qrow >= T) break;
+    const float* src = ds + (1 + 16 * w + rr) * ldx;
+    for (int jj = lane; jj < T; jj += 64) dsb[(size_t)qrow * T + jj] = src[jj];
   }
 }
 
-// dk, dv [Bt][T][H*D]: sum over query tiles. Thread per output element, fixed order.
-// (dpos: relattn_dpos_reduce_kernel; du, dvb: relattn_bias_reduce_kernel.)
-__global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
-    const float* __restrict__ dk_part, const float* __restrict__ dv_part,
-    const float* __restrict__ dp_part, const float* __restrict__ du_part,
-    const float* __restrict__ dvb_part, int Bt, int P, int T, int H, int D, int nqt,
-    float* __restrict__ dk, float* __restrict__ dv, float* __restrict__ dpos,
-    float* __restrict__ du, float* __restrict__ dvb) {
+// ------------------------------------------------------------------------------------
+// Backward, key side: block = (key tile of 64, head, batch row), wave w = keys 16w..16w+15
+// of the tile; every query row is visited (no per-query-tile partials):
+//   dK[key]  = sum_i dS'[i][key] (q+u)[i]       dV[key] = sum_i Pd[i][key] dO[i]
+//   dpos[m]  = sum_i dX[i][m] (q+v)[i]          (per batch row; summed over the pass later)
+// MFMA 16x16x4: A[key r][query g] from dS' / probs (global, coalesced over keys), B[query
+// g][column] from q / dO rows; four query steps are issued per iteration.
+// ------------------------------------------------------------------------------------
+template <int DQ>
+__global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
+    const float* __restrict__ dsg, const float* __restrict__ probs, const float* __restrict__ q,
+    const float* __restrict__ dctx, const float* __restrict__ u, const float* __restrict__ vbias,
+    int T, int H, DropCfg dc, const uint64_t* __restrict__ rng, float* __restrict__ dk,
+    float* __restrict__ dv, float* __restrict__ dp_part) {
+  constexpr int D = 4 * DQ;
+  constexpr int CT = (D + 15) / 16;
+  const int nkt = (T + kTile - 1) / kTile;
+  const BlockId bid = block_id(nkt, H);
+  const int b = bid.b, h = bid.h, k0 = bid.qt * kTile;
   const int C = H * D;
-  const int64_t n_kv = (int64_t)Bt * T * C;
-  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (e < n_kv) {
-    const int b = (int)(e / ((int64_t)T * C));
-    const int rem = (int)(e - (int64_t)b * T * C);
-    const int t = rem / C, hc = rem - t * C, h = hc / D, c = hc - h * D;
-    float sk = 0.0f, sv = 0.0f;
-    for (int qt = 0; qt < nqt; ++qt) {
-      const size_t o = (((((size_t)qt * Bt + b) * H + h) * T) + t) * D + c;
-      sk += dk_part[o];
-      sv += dv_part[o];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const size_t bo = (size_t)b * T * C + h * D;
+  const float* qb = q + bo;
+  const float* dob = dctx + bo;
+  const float* ub = u + h * D;
+  const float* vbb = vbias + h * D;
+  const float* dsb = dsg + ((size_t)b * H + h) * T * T;
+  const float* prb = probs + ((size_t)b * H + h) * T * T;
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
+  const size_t pbase = ((size_t)b * H + h) * T * T;
+  const int key = k0 + 16 * w + r;  // A row: key / position m
+  const bool kok = key < T;
+  const int kc = min(key, T - 1);
+  float bu[CT], bv[CT];
+  int cc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    cc[ct] = min(16 * ct + r, D - 1);
+    bu[ct] = ub[cc[ct]];
+    bv[ct] = vbb[cc[ct]];
+  }
+  f32x4 ak[CT], av[CT], ap[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    ak[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    av[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // dX[i][m] = dS'[i][m-T+1+i] (m >= T-1-i), else dS'[i-1][m+i+1] (i >= 1)
+  auto dx_at = [&](int i) -> float {
+    if (kc >= T - 1 - i) return dsb[(size_t)i * T + (kc - T + 1 + i)];
+    return i >= 1 ? dsb[(size_t)(i - 1) * T + (kc + i + 1)] : 0.0f;
+  };
+  constexpr int kU = 4;  // query steps (of 4 rows) in flight
+  for (int i0 = 0; i0 < T; i0 += 4 * kU) {
+    float a_k[kU], a_v[kU], a_p[kU], qx[kU][CT], dx[kU][CT];
+#pragma unroll
+    for (int uu = 0; uu < kU; ++uu) {
+      const int i = i0 + 4 * uu + g;
+      const bool ok = kok && i < T;
+      const int ic = min(i, T - 1);
+      a_k[uu] = ok ? dsb[(size_t)ic * T + kc] : 0.0f;
+      const float pv = ok ? prb[(size_t)ic * T + kc] : 0.0f;
+      a_v[uu] = dc.on ? (drop_hash(dkey, pbase + (size_t)ic * T + kc) >= dc.thresh ? pv * dc.scale : 0.0f) : pv;
+      a_p[uu] = ok ? dx_at(ic) : 0.0f;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        qx[uu][ct] = qb[(size_t)ic * C + cc[ct]];
+        dx[uu][ct] = dob[(size_t)ic * C + cc[ct]];
+      }
     }
-    dk[e] = sk;
-    dv[e] = sv;
+#pragma unroll
+    for (int uu = 0; uu < kU; ++uu) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        ak[ct] = mfma4(a_k[uu], qx[uu][ct] + bu[ct], ak[ct]);
+        av[ct] = mfma4(a_v[uu], dx[uu][ct], av[ct]);
+        ap[ct] = mfma4(a_p[uu], qx[uu][ct] + bv[ct], ap[ct]);
+      }
+    }
+  }
+  float* dkb = dk + bo;
+  float* dvb = dv + bo;
+  float* dpb = dp_part + ((size_t)b * H + h) * T * D;  // [b][h][T][D]
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = 16 * ct + r;
+    if (col >= D) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kk = k0 + 16 * w + 4 * g + j;
+      if (kk >= T) continue;
+      dkb[(size_t)kk * C + col] = ak[ct][j];
+      dvb[(size_t)kk * C + col] = av[ct][j];
+      dpb[(size_t)kk * D + col] = ap[ct][j];
+    }
   }
 }
 
@@ -631,9 +664,10 @@ bool relattn_supported(int64_t T, int64_t d) {
   return T >= 1 && T <= 512 && (d == 16 || d == 32 || d == 36 || d == 64);
 }
 
+// ws: dS' [Bt][H][T][T] | dpos per batch row [Bt][H][T][d] | du, dvb tile partials.
 size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
   const int64_t nqt = (T + kTile - 1) / kTile;
-  return sizeof(float) * (size_t)(3 * nqt * Bt * H * T * d + 2 * Bt * H * nqt * d + 64);
+  return sizeof(float) * (size_t)(Bt * H * T * T + Bt * H * T * d + 2 * Bt * H * nqt * d + 64);
 }
 
 #define OB_RA_DISPATCH(KERNEL)                 \
@@ -675,28 +709,28 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
   const DropCfg dc = make_drop(p_drop);
   const float sqrt_d = (float)sqrt((double)d);
   const size_t lds = lds_bytes((int)T);
-  float* dk_part = (float*)ws;
-  float* dv_part = dk_part + (size_t)nqt * Bt * H * T * d;
-  float* dp_part = dv_part + (size_t)nqt * Bt * H * T * d;
-  float* du_part = dp_part + (size_t)nqt * Bt * H * T * d;
+  float* dsg = (float*)ws;
+  float* dp_part = dsg + (size_t)Bt * H * T * T;
+  float* du_part = dp_part + (size_t)Bt * H * T * d;
   float* dvb_part = du_part + (size_t)Bt * H * nqt * d;
 #define OB_RA_BWD(DQ, NTT)                                                                     \
   hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, q, k, v,  \
                      pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, sqrt_d, dc, rng, probs, dq, \
-                     dk_part, dv_part, dp_part, du_part, dvb_part)
+                     dsg, du_part, dvb_part)
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
+#define OB_RA_KV(DQ, NTT)                                                                       \
+  hipLaunchKernelGGL((relattn_bwd_kv_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg, \
+                     probs, q, dctx, u, vb, (int)T, (int)H, dc, rng, dk, dv, dp_part)
+  OB_RA_DISPATCH(OB_RA_KV);
+#undef OB_RA_KV
   const int64_t C = H * d;
-  const int64_t total = Bt * T * C;
-  hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, s, dk_part, dv_part, dp_part, du_part, dvb_part, (int)Bt,
-                     (int)P, (int)T, (int)H, (int)d, nqt, dk, dv, dpos, du, dvb);
   hipLaunchKernelGGL(relattn_bias_reduce_kernel, dim3((unsigned)(2 * H)), dim3(64 * kBiasSlices),
                      0, s, (const float*)du_part, (const float*)dvb_part, (int)Bt, (int)H, (int)d,
                      nqt, du, dvb);
   hipLaunchKernelGGL(relattn_dpos_reduce_kernel, dim3((unsigned)ceil_div(P * T * C, 64)),
-                     dim3(kThreads), 0, s, dp_part, (int)Bt, (int)P, (int)T, (int)H, (int)d, nqt,
-                     dpos);
+                     dim3(kThreads), 0, s, (const float*)dp_part, (int)Bt, (int)P, (int)T, (int)H,
+                     (int)d, 1, dpos);
 }
 
 void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,

@@ -317,8 +317,18 @@ size_t bimg_bytes(int nt, int64_t K) {
 }
 
 // Widest column tile whose bf16 image fits the LDS budget, preferring tiles that divide N.
+// OB_TGEMM_NTMAX (tuning experiments) caps the width.
 int pick_nt(int64_t N, int64_t K) {
-  static const int cands[] = {12, 9, 6, 4, 3, 2, 1};
+  static const int cap = [] {
+    const char* e = getenv("OB_TGEMM_NTMAX");
+    return e ? atoi(e) : 12;
+  }();
+  static const int cands_all[] = {12, 9, 6, 4, 3, 2, 1};
+  int cands[7];
+  int nc = 0;
+  for (int c : cands_all)
+    if (c <= cap) cands[nc++] = c;
+  for (int i = nc; i < 7; ++i) cands[i] = 1;
   for (int nt : cands)
     if (N % (16 * nt) == 0 && bimg_bytes(nt, K) <= kMaxLds) return nt;
   for (int nt : cands)
