@@ -76,6 +76,20 @@ int ob_quant_pack_dyn(const float* W, const float* alpha, int alpha_raw, const i
   return launched();
 }
 
+int64_t ob_quant_pack_item_blocks(int64_t N, int64_t K) {
+  if (N < 0 || K < 0) return OB_ERR_SHAPE;
+  return quant_pack_item_blocks(N, K);
+}
+
+int ob_quant_pack_group(const ob_pack_item* items, int n_items, int64_t total_blocks,
+                        void* stream) {
+  if (n_items < 0 || total_blocks < 0 || total_blocks > 0x7fffffff) return OB_ERR_SHAPE;
+  if (n_items > 0 && !items) return OB_ERR_NULL;
+  if (((uintptr_t)items & 7u) != 0) return OB_ERR_ALIGN;
+  launch_quant_pack_group(items, n_items, total_blocks, as_stream(stream));
+  return launched();
+}
+
 int ob_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
                      float* W_hat, void* stream) {
   if (int st = check_bits(bits)) return st;
@@ -215,6 +229,108 @@ int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t K,
   if (!aligned4(X) || !aligned4(Y) || !aligned4(bias) || !aligned4(pass_bits)) return OB_ERR_ALIGN;
   launch_ternary_gemm_passes(X, (int)P, M, K, codes2, codes1, reinterpret_cast<const int*>(pass_bits),
                              N, alpha, alpha_raw, bias, Y, as_stream(stream));
+  return launched();
+}
+
+namespace {
+
+// Shared argument checks of the fused-epilogue GEMM entries.
+int fused_gemm_check(const float* A, int64_t P, int64_t M, int64_t K, const uint32_t* codes2,
+                     const uint32_t* codes1, const int32_t* pass_bits, const float* alpha,
+                     int64_t N, const float* out, float p_drop, const uint64_t* rng) {
+  if (M < 0 || K < 0 || N < 0 || P < 1 || P > 65535) return OB_ERR_SHAPE;
+  if (!(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+  if (P > 1 && !pass_bits) return OB_ERR_NULL;
+  if (!alpha || (M * N > 0 && !out) || (M * K > 0 && !A) ||
+      (N * K > 0 && (!codes2 || (pass_bits && !codes1))) || (p_drop > 0.0f && !rng))
+    return OB_ERR_NULL;
+  if (!aligned4(A) || !aligned4(out) || !aligned4(pass_bits)) return OB_ERR_ALIGN;
+  return OB_OK;
+}
+
+}  // namespace
+
+int ob_bitlinear_fwd_swish_drop(const float* X, int64_t P, int64_t M, int64_t K,
+                                const uint32_t* codes2, const uint32_t* codes1,
+                                const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                const float* bias, int64_t N, float p_drop, const uint64_t* rng,
+                                int64_t rng_offset, float* Y_pre, float* Y_act, void* stream) {
+  if (int st = fused_gemm_check(X, P, M, K, codes2, codes1, pass_bits, alpha, N, Y_act, p_drop, rng))
+    return st;
+  if (M * N > 0 && !Y_pre) return OB_ERR_NULL;
+  if (!aligned4(Y_pre) || !aligned4(bias)) return OB_ERR_ALIGN;
+  TgemmEpi ep{};
+  ep.mode = kEpiSwishDrop;
+  ep.C2 = Y_pre;
+  ep.p_drop = p_drop;
+  ep.rng = rng;
+  ep.rng_off = (uint64_t)rng_offset;
+  launch_ternary_gemm_passes(X, (int)P, M, K, codes2, pass_bits ? codes1 : codes2,
+                             reinterpret_cast<const int*>(pass_bits), N, alpha, alpha_raw, bias,
+                             Y_act, as_stream(stream), &ep);
+  return launched();
+}
+
+int ob_bitlinear_fwd_residual(const float* X, int64_t P, int64_t M, int64_t K,
+                              const uint32_t* codes2, const uint32_t* codes1,
+                              const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                              const float* bias, int64_t N, const float* R, float rscale,
+                              float p_drop, const uint64_t* rng, int64_t rng_offset,
+                              const int32_t* lens, int64_t T, float* Y, void* stream) {
+  if (int st = fused_gemm_check(X, P, M, K, codes2, codes1, pass_bits, alpha, N, Y, p_drop, rng))
+    return st;
+  if (M * N > 0 && !R) return OB_ERR_NULL;
+  if (lens && (T < 1 || (P * M) % T)) return OB_ERR_SHAPE;
+  if (T > 0x7fffffff) return OB_ERR_SHAPE;
+  if (!aligned4(R) || !aligned4(bias) || !aligned4(lens)) return OB_ERR_ALIGN;
+  TgemmEpi ep{};
+  ep.mode = kEpiResidual;
+  ep.R = R;
+  ep.rscale = rscale;
+  ep.lens = reinterpret_cast<const int*>(lens);
+  ep.T = (int)T;
+  ep.p_drop = p_drop;
+  ep.rng = rng;
+  ep.rng_off = (uint64_t)rng_offset;
+  launch_ternary_gemm_passes(X, (int)P, M, K, codes2, pass_bits ? codes1 : codes2,
+                             reinterpret_cast<const int*>(pass_bits), N, alpha, alpha_raw, bias, Y,
+                             as_stream(stream), &ep);
+  return launched();
+}
+
+int ob_bitlinear_bwd_dx_swish_drop(const float* dY, int64_t P, int64_t M, int64_t N,
+                                   const uint32_t* codes2_t, const uint32_t* codes1_t,
+                                   const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                   int64_t K, const float* pre, float p_drop, const uint64_t* rng,
+                                   int64_t rng_offset, float* dPre, void* stream) {
+  if (int st = fused_gemm_check(dY, P, M, N, codes2_t, codes1_t, pass_bits, alpha, K, dPre, p_drop,
+                                rng))
+    return st;
+  if (M * K > 0 && !pre) return OB_ERR_NULL;
+  if (!aligned4(pre)) return OB_ERR_ALIGN;
+  TgemmEpi ep{};
+  ep.mode = kEpiSwishDropBwd;
+  ep.R = pre;
+  ep.p_drop = p_drop;
+  ep.rng = rng;
+  ep.rng_off = (uint64_t)rng_offset;
+  launch_ternary_gemm_passes(dY, (int)P, M, N, codes2_t, pass_bits ? codes1_t : codes2_t,
+                             reinterpret_cast<const int*>(pass_bits), K, alpha, alpha_raw, nullptr,
+                             dPre, as_stream(stream), &ep);
+  return launched();
+}
+
+int ob_drop_scale_bwd(const float* dOut, int64_t rows, int64_t N, float rscale, float p_drop,
+                      const uint64_t* rng, int64_t rng_offset, const int32_t* lens, int64_t T,
+                      float* dY, void* stream) {
+  if (rows < 0 || N < 0 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+  if (lens && (T < 1 || T > 0x7fffffff || rows % T)) return OB_ERR_SHAPE;
+  if ((rows * N > 0 && (!dOut || !dY)) || (p_drop > 0.0f && !rng)) return OB_ERR_NULL;
+  if ((reinterpret_cast<uintptr_t>(dOut) & 15) || (reinterpret_cast<uintptr_t>(dY) & 15) ||
+      !aligned4(lens))
+    return OB_ERR_ALIGN;
+  launch_drop_scale_bwd(dOut, rows, N, rscale, p_drop, rng, (uint64_t)rng_offset,
+                        reinterpret_cast<const int*>(lens), (int)T, dY, as_stream(stream));
   return launched();
 }
 

@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/onebit_hip.h"
+
 namespace ob {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -15,6 +17,10 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bits,
                        const int* bits_dev, int64_t N, int64_t K, uint32_t* codes,
                        uint32_t* codes_t, hipStream_t s);
+// Grouped pack (ob_pack_item from include/onebit_hip.h; table on device).
+int64_t quant_pack_item_blocks(int64_t N, int64_t K);
+void launch_quant_pack_group(const ob_pack_item* items_dev, int n_items, int64_t total_blocks,
+                             hipStream_t s);
 void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,
                           float* W_hat, hipStream_t s);
 
@@ -44,10 +50,45 @@ void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* c
 
 // P stacked passes of one layer (rows p*M .. p*M+M of A and C): pass p multiplies by the
 // codes1 operand when pass_bits[p] (DEVICE int32 [P]) == 1, else by `codes`.
+// `ep` (optional) fuses the elementwise ops that follow the GEMM at its call sites into
+// the store; see TgemmEpi.
+struct TgemmEpi;
 void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
                                 const uint32_t* codes, const uint32_t* codes1,
                                 const int* pass_bits, int64_t N, const float* alpha,
-                                int alpha_raw, const float* bias, float* C, hipStream_t s);
+                                int alpha_raw, const float* bias, float* C, hipStream_t s,
+                                const TgemmEpi* ep = nullptr);
+
+// Fused epilogues of the ternary GEMM, y = a * acc + bias; element (row, col) of the
+// P*M x N output has dropout index row * N + col (ob_drop.h):
+//   kEpiSwishDrop    C2 = y;  C = drop(silu(y))                 (FFN lin1 -> swish -> dropout,
+//                                                                 conformer.py:36-38)
+//   kEpiResidual     C = R + rscale * rowvalid * drop(y)          (lin2 -> dropout -> x + 0.5*h,
+//                                                                 conformer.py:39-45; out_proj ->
+//                                                                 dropout -> pad zero -> x + out,
+//                                                                 :131-138)
+//   kEpiSwishDropBwd C = y * keep * scale * silu'(R), R = the forward's pre-activation
+//                                                                (dX of lin2 chained through the
+//                                                                 dropout and swish backward)
+// rowvalid = (lens == NULL) || (row % T < lens[row / T]).
+enum { kEpiNone = 0, kEpiSwishDrop = 1, kEpiResidual = 2, kEpiSwishDropBwd = 3 };
+struct TgemmEpi {
+  int mode;
+  const float* R;
+  float* C2;
+  float rscale;
+  const int* lens;
+  int T;
+  float p_drop;
+  const uint64_t* rng;  // device {seed, counter}; required when p_drop > 0
+  uint64_t rng_off;     // added to the counter (per call site)
+};
+
+// dY = rscale * rowvalid * drop(dOut) over [rows][N] (the backward of kEpiResidual's
+// dropout / pad / scale, same keep mask).
+void launch_drop_scale_bwd(const float* dout, int64_t rows, int64_t N, float rscale,
+                           float p_drop, const uint64_t* rng, uint64_t rng_off, const int* lens,
+                           int T, float* dy, hipStream_t s);
 
 // Split-M partial of G = dY^T . X: part[c][N*K] for chunk c, part_db[c][N] (optional).
 // With P stacked passes the chunks never straddle a pass: chunk c belongs to pass

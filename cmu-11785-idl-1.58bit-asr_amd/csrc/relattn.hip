@@ -25,6 +25,7 @@
 // the backward regenerates the same mask; torch's own RNG stream is not reproduced).
 #include <math.h>
 
+#include "ob_drop.h"
 #include "ob_launch.h"
 
 namespace ob {
@@ -38,28 +39,6 @@ constexpr int kTile = 64;  // query rows per block (16 per wave)
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// Dropout keep-hash: a 32-bit counter hash (murmur3 fmix32 of the element index mixed with
-// a per-call key). The key folds (seed, counter) once per kernel; each element then costs
-// ~8 VALU ops -- the earlier 64-bit splitmix form (three 64-bit multiplies per element,
-// evaluated twice in the backward) cost more than the kernels' matrix work.
-__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x85EBCA6Bu;
-  x ^= x >> 13;
-  x *= 0xC2B2AE35u;
-  x ^= x >> 16;
-  return x;
-}
-
-__device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint64_t ctr) {
-  return fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ 0x9E3779B9u) ^
-                fmix32((uint32_t)ctr * 0x27D4EB2Fu + (uint32_t)(ctr >> 32)));
-}
-
-__device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t idx) {
-  return fmix32(((uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x165667B1u)) * 0x9E3779B1u + key);
 }
 
 // Bijective XCD-aware remap (hardware block b runs on XCD b % 8): consecutive logical ids
@@ -85,11 +64,6 @@ __device__ __forceinline__ BlockId block_id(int nqt, int H) {
   return id;
 }
 
-struct DropCfg {
-  uint32_t thresh;  // keep iff hash >= thresh
-  float scale;      // 1 / (1 - p)
-  int on;
-};
 
 // ------------------------------------------------------------------------------------
 // Forward: block = (query tile of 64, head, batch row). X rows i0 .. i0+64 live in LDS
@@ -646,15 +620,6 @@ __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropC
   out[e] = (!dc.on || drop_hash(drop_key(rng[0], rng[1]), (uint64_t)e) >= dc.thresh) ? 1 : 0;
 }
 
-DropCfg make_drop(float p_drop) {
-  DropCfg dc;
-  dc.on = p_drop > 0.0f ? 1 : 0;
-  double t = (double)p_drop * 4294967296.0;
-  if (t > 4294967295.0) t = 4294967295.0;
-  dc.thresh = (uint32_t)t;
-  dc.scale = p_drop > 0.0f ? (float)(1.0 / (1.0 - (double)p_drop)) : 1.0f;
-  return dc;
-}
 
 size_t lds_bytes(int T) { return sizeof(float) * (size_t)(kTile + 1) * (16 * ((T + 15) / 16) + 1); }
 

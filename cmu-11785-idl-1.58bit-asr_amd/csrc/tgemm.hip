@@ -25,6 +25,7 @@
 // does not take (K % 4 != 0, misaligned A, B image over 64 KB).
 #include <cstdlib>
 
+#include "ob_drop.h"
 #include "ob_launch.h"
 #include "ob_quant.h"
 
@@ -65,6 +66,55 @@ __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Kernel-side form of TgemmEpi (ob_launch.h): the dropout config resolved on the host.
+struct EpiArgs {
+  int mode;
+  const float* R;
+  float* C2;
+  float rscale;
+  const int* lens;
+  int T;
+  DropCfg dc;
+  const uint64_t* rng;
+  uint64_t rng_off;
+};
+
+// torch's silu and silu backward formulas: x / (1 + exp(-x)) and
+// (dy * s) * (1 + x * (1 - s)), s = 1 / (1 + exp(-x)), evaluated in that order.
+__device__ __forceinline__ float silu_f(float z) { return z / (1.0f + expf(-z)); }
+__device__ __forceinline__ float silu_bwd_f(float dy, float z) {
+  const float s = 1.0f / (1.0f + expf(-z));
+  return __fmul_rn(__fmul_rn(dy, s), 1.0f + z * (1.0f - s));
+}
+
+// Store y = a*acc + b through the fused epilogue. `c` is this element's output address,
+// grow its pass-inclusive row. Explicit _rn ops keep hipcc from contracting the unfused
+// reference sequence (y, then *scale, then +R) into an fma.
+template <int MODE>
+__device__ __forceinline__ void epi_store(const EpiArgs& ep, uint32_t dkey, float* c,
+                                          int64_t grow, int col, int N, float y, float rv) {
+  const int64_t i = grow * N + col;
+  const float keep =
+      ep.dc.on ? (drop_hash(dkey, (uint64_t)i) >= ep.dc.thresh ? ep.dc.scale : 0.0f) : 1.0f;
+  if constexpr (MODE == kEpiSwishDrop) {
+    ep.C2[i] = y;
+    const float sv = silu_f(y);
+    *c = ep.dc.on ? __fmul_rn(sv, keep) : sv;
+  } else if constexpr (MODE == kEpiResidual) {
+    bool valid = true;
+    if (ep.lens) {
+      const int64_t b = grow / ep.T;
+      valid = (grow - b * ep.T) < ep.lens[b];
+    }
+    float v = ep.dc.on ? __fmul_rn(y, keep) : y;
+    v = valid ? v : __fmul_rn(v, 0.0f);
+    *c = __fadd_rn(rv, ep.rscale == 1.0f ? v : __fmul_rn(ep.rscale, v));
+  } else {  // kEpiSwishDropBwd
+    const float d = ep.dc.on ? __fmul_rn(y, keep) : y;
+    *c = silu_bwd_f(d, rv);
+  }
+}
+
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): consecutive logical ids land on one XCD under round-robin dispatch.
 __device__ __forceinline__ int xcd_logical(int b, int nb) {
@@ -97,13 +147,14 @@ __device__ __forceinline__ void select_pass(const float* __restrict__& A, float*
   C += (int64_t)p * M * N;
 }
 
-template <int NT, int NCH>
+template <int NT, int NCH, int EPI>
 __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
-    const int* __restrict__ pass_bits) {
+    const int* __restrict__ pass_bits, EpiArgs ep) {
   select_pass(A, C, codes, codes1, pass_bits, M, K, N);
+  const int64_t rowbase = pass_bits ? (int64_t)blockIdx.y * M : 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
   const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
@@ -163,6 +214,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   const int kg = 8 * g;
   const __bf16* brow = bimg + r * stride + kg;
   const float a_eff = effective_alpha(alpha, alpha_raw);
+  const uint32_t dkey = (EPI != kEpiNone && ep.dc.on) ? drop_key(ep.rng[0], ep.rng[1] + ep.rng_off) : 0u;
   float bcol[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -202,7 +254,8 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     if constexpr (NCH > 0) {
       // Fully unrolled; a window of kWin chunks in flight. sched_barrier keeps hipcc from
       // sinking each load next to its use (one load in flight, vmcnt(0) per chunk).
-      constexpr int kWin = NCH < (NT > 6 ? 3 : 5) ? NCH : (NT > 6 ? 3 : 5);
+      constexpr int kWmax = NT > 6 ? 3 : 5;
+      constexpr int kWin = NCH < kWmax ? NCH : kWmax;
       f32x4 buf[NCH][2];
 #pragma unroll
       for (int c = 0; c < kWin; ++c) load8(arow, 32 * c + kg, K, buf[c][0], buf[c][1]);
@@ -229,6 +282,22 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       }
     }
 
+    // keep the epilogue's loads (residual / pre-activation) from being hoisted into the
+    // main loop, where they would hold NT*4 VGPRs across it
+    __builtin_amdgcn_sched_barrier(0);
+    // epilogue operand: all NT*4 loads issued before any is used (one latency, not 4*NT)
+    float rv[NT][4];
+    if constexpr (EPI == kEpiResidual || EPI == kEpiSwishDropBwd) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = min(n0 + 16 * t + r, N - 1);
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int64_t orow = min(m0 + 4 * g + reg, M - 1);
+          rv[t][reg] = ep.R[(rowbase + orow) * N + col];
+        }
+      }
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = n0 + 16 * t + r;
@@ -236,8 +305,14 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const int64_t orow = m0 + 4 * g + reg;
-        if (orow < M) C[orow * N + col] = fmaf(a_eff, acc[t][reg], bcol[t]);
+        if (orow >= M) continue;
+        const float y = fmaf(a_eff, acc[t][reg], bcol[t]);
+        if constexpr (EPI == kEpiNone) C[orow * N + col] = y;
+        else epi_store<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, rv[t][reg]);
       }
+      // one tile's elementwise work at a time: hipcc would otherwise interleave all NT*4
+      // exp/div sequences and spill
+      if constexpr (EPI != kEpiNone) __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
@@ -253,7 +328,8 @@ __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
     const float* __restrict__ A, int64_t M, int64_t K, const uint32_t* __restrict__ codes,
     int64_t KW, int64_t N, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
-    const int* __restrict__ pass_bits) {
+    const int* __restrict__ pass_bits, EpiArgs ep) {
+  const int64_t rowbase = pass_bits ? (int64_t)blockIdx.z * M : 0;
   if (pass_bits) {  // stacked passes: blockIdx.z = pass
     const int p = blockIdx.z;
     if (pass_bits[p] == 1) codes = codes1;
@@ -290,6 +366,7 @@ __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
     }
   }
   const float a = effective_alpha(alpha, alpha_raw);
+  const uint32_t dkey = ep.dc.on ? drop_key(ep.rng[0], ep.rng[1] + ep.rng_off) : 0u;
 #pragma unroll
   for (int t = 0; t < kF32NT; ++t) {
     const int64_t col = n0 + 16 * t + r;
@@ -298,7 +375,17 @@ __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int64_t orow = m0 + 4 * g + reg;
-      if (orow < M) C[orow * N + col] = fmaf(a, acc[t][reg], b);
+      if (orow >= M) continue;
+      const float y = fmaf(a, acc[t][reg], b);
+      float* c = C + orow * N + col;
+      const float rv = ep.R ? ep.R[(rowbase + orow) * N + col] : 0.0f;
+      if (ep.mode == kEpiNone) *c = y;
+      else if (ep.mode == kEpiSwishDrop)
+        epi_store<kEpiSwishDrop>(ep, dkey, c, rowbase + orow, (int)col, (int)N, y, rv);
+      else if (ep.mode == kEpiResidual)
+        epi_store<kEpiResidual>(ep, dkey, c, rowbase + orow, (int)col, (int)N, y, rv);
+      else
+        epi_store<kEpiSwishDropBwd>(ep, dkey, c, rowbase + orow, (int)col, (int)N, y, rv);
     }
   }
 }
@@ -318,11 +405,16 @@ size_t bimg_bytes(int nt, int64_t K) {
 
 // Widest column tile whose bf16 image fits the LDS budget, preferring tiles that divide N.
 // OB_TGEMM_NTMAX (tuning experiments) caps the width.
-int pick_nt(int64_t N, int64_t K) {
-  static const int cap = [] {
+// The swish epilogues (exp + divide per element) cap the width at 4: wider tiles spill
+// (hipcc interleaves the NT*4 element sequences; measured with -Rpass-analysis).
+int pick_nt(int64_t N, int64_t K, int epi_mode) {
+  static const int env_cap = [] {
     const char* e = getenv("OB_TGEMM_NTMAX");
     return e ? atoi(e) : 12;
   }();
+  const int cap =
+      (epi_mode == kEpiSwishDrop || epi_mode == kEpiSwishDropBwd) ? (env_cap < 4 ? env_cap : 4)
+                                                                    : env_cap;
   static const int cands_all[] = {12, 9, 6, 4, 3, 2, 1};
   int cands[7];
   int nc = 0;
@@ -339,7 +431,8 @@ int pick_nt(int64_t N, int64_t K) {
 template <int NT>
 void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
                    const float* alpha, int alpha_raw, const float* bias, float* C,
-                   const uint32_t* codes1, const int* pass_bits, int P, hipStream_t s) {
+                   const uint32_t* codes1, const int* pass_bits, int P, const EpiArgs& ep,
+                   hipStream_t s) {
   const int n_ct = (int)ceil_div(N, 16 * NT);
   const int n_rt = (int)ceil_div(M, kRows);
   int rgroups = kTargetBlocks / (n_ct * P);
@@ -348,10 +441,21 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
   const size_t lds = bimg_bytes(NT, K);
   const int KW = (int)ceil_div(K, 16);
-#define OB_TGEMM(NCH)                                                                        \
-  hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH>), grid, dim3(kThreads), lds, s, A, M, (int)K, \
-                     codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C, codes1, \
-                     pass_bits)
+#define OB_TGEMM_E(NCH, E)                                                                     \
+  hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E>), grid, dim3(kThreads), lds, s, A, M,       \
+                     (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C,   \
+                     codes1, pass_bits, ep)
+#define OB_TGEMM(NCH)                                                   \
+  switch (ep.mode) {                                                    \
+    case kEpiSwishDrop: /* pick_nt caps these at NT = 4 */            \
+      if constexpr (NT <= 4) OB_TGEMM_E(NCH, kEpiSwishDrop);            \
+      break;                                                            \
+    case kEpiResidual: OB_TGEMM_E(NCH, kEpiResidual); break;            \
+    case kEpiSwishDropBwd:                                              \
+      if constexpr (NT <= 4) OB_TGEMM_E(NCH, kEpiSwishDropBwd);         \
+      break;                                                            \
+    default: OB_TGEMM_E(NCH, kEpiNone); break;                          \
+  }
   switch ((K + 31) / 32) {  // Conformer widths: 64, 144, 256, 576
     case 2: OB_TGEMM(2); break;
     case 5: OB_TGEMM(5); break;
@@ -360,6 +464,7 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
     default: OB_TGEMM(0); break;
   }
 #undef OB_TGEMM
+#undef OB_TGEMM_E
 }
 
 }  // namespace
@@ -367,13 +472,27 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
 void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
                                 const uint32_t* codes, const uint32_t* codes1,
                                 const int* pass_bits, int64_t N, const float* alpha,
-                                int alpha_raw, const float* bias, float* C, hipStream_t s) {
+                                int alpha_raw, const float* bias, float* C, hipStream_t s,
+                                const TgemmEpi* epi) {
   if (M == 0 || N == 0 || P == 0) return;
+  EpiArgs ep{};
+  ep.mode = kEpiNone;
+  if (epi && epi->mode != kEpiNone) {
+    ep.mode = epi->mode;
+    ep.R = epi->R;
+    ep.C2 = epi->C2;
+    ep.rscale = epi->rscale;
+    ep.lens = epi->lens;
+    ep.T = epi->T > 0 ? epi->T : 1;
+    ep.dc = make_drop(epi->p_drop);
+    ep.rng = epi->rng;
+    ep.rng_off = epi->rng_off;
+  }
   const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-  const int nt = vec && !use_f32_gemm() ? pick_nt(N, K) : 0;
+  const int nt = vec && !use_f32_gemm() ? pick_nt(N, K, ep.mode) : 0;
 #define OB_NT(V)                                                                            \
   case V:                                                                                   \
-    launch_bf16x3<V>(A, M, K, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, s); \
+    launch_bf16x3<V>(A, M, K, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); \
     return;
   switch (nt) {
     OB_NT(12)
@@ -389,7 +508,7 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
   // fp32 path (K == 0 included: its k-loop is empty and never reads A).
   const dim3 grid((unsigned)ceil_div(M, kRows), (unsigned)ceil_div(N, 16 * kF32NT), (unsigned)P);
   hipLaunchKernelGGL(tgemm_f32_kernel, grid, dim3(kThreads), 0, s, A, M, K, codes,
-                     ceil_div(K, 16), N, alpha, alpha_raw, bias, C, codes1, pass_bits);
+                     ceil_div(K, 16), N, alpha, alpha_raw, bias, C, codes1, pass_bits, ep);
 }
 
 void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,

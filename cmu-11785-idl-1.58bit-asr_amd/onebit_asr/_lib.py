@@ -35,6 +35,18 @@ SIGNATURES = {
     "ob_abi_version": (_int, []),
     "ob_status_string": (ctypes.c_char_p, [_int]),
     "ob_quant_pack": (_int, [_c_f, _c_f, _int, _int, _i64, _i64, _c_f, _c_f, _c_f]),
+    "ob_quant_pack_item_blocks": (_i64, [_i64, _i64]),
+    "ob_quant_pack_group": (_int, [_c_f, _int, _i64, _c_f]),
+    "ob_bitlinear_fwd_swish_drop": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _f32, _c_f, _i64,
+               _c_f, _c_f, _c_f]),
+    "ob_bitlinear_fwd_residual": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _c_f, _f32, _f32,
+               _c_f, _i64, _c_f, _i64, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dx_swish_drop": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _i64, _c_f, _f32, _c_f, _i64,
+               _c_f, _c_f]),
+    "ob_drop_scale_bwd": (_int, [_c_f, _i64, _i64, _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f, _c_f]),
     "ob_quant_dequant": (_int, [_c_f, _c_f, _int, _int, _i64, _c_f, _c_f]),
     "ob_quant_ste_bwd_workspace": (_sz, [_i64]),
     "ob_quant_ste_bwd": (_int, [_c_f, _c_f, _c_f, _int, _int, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),

@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from .attention import fused_attention_supported, rel_pos_attention
 from .conv import depthwise_conv1d
 from .embedding import embedding
+from .fused import ffn_residual, fused_supported, linear_residual
 from .layernorm import layer_norm
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
@@ -76,6 +77,10 @@ class FeedForwardModule(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x, bitwidth: int, mask=None):
+        if mask is None and fused_supported(x, self.lin1, self.lin2, bitwidth=bitwidth):
+            # same computation, elementwise ops in the GEMM epilogues (onebit_asr/fused.py)
+            p = self.dropout.p if self.training else 0.0
+            return ffn_residual(self.ln(x), x, self.lin1, self.lin2, bitwidth, p)
         h = self.lin1(self.ln(x), bitwidth)
         h = self.dropout(swish(h))
         h = self.dropout(self.lin2(h, bitwidth))
@@ -165,9 +170,14 @@ class MHSA(nn.Module):
         else:
             lens = getattr(mask, "_ob_lens", None)
             if lens is None:  # prefix masks (valid_i & valid_j): row 0 column = valid frames
-                lens = mask[:, :, 0].sum(dim=1)
+                lens = mask[:, :, 0].sum(dim=1, dtype=torch.int32)
+        p = self.dropout.p if self.training else 0.0
         ctx = rel_pos_attention(qp, kp, vp, pp, self.pos_bias_u, self.pos_bias_v, lens,
-                                self.n_heads, self.dropout.p if self.training else 0.0)
+                                self.n_heads, p)
+        if fused_supported(ctx, self.out_proj, bitwidth=bitwidth):
+            # out_proj -> dropout -> zero padded rows -> + x in the GEMM epilogue
+            return linear_residual(ctx, x, self.out_proj, bitwidth, p, 1.0,
+                                   None if mask is None else lens, tlen)
         out = self.dropout(self.out_proj(ctx, bitwidth))
         return x + _pad_rows(out, mask)
 

@@ -1,0 +1,242 @@
+"""Fused BitLinear call sites: the elementwise ops around a QuantizedLinear at its call
+sites in the reference, folded into the ternary GEMM's epilogue (csrc/tgemm.hip) and one
+elementwise backward kernel (csrc/fused.hip).
+
+* ``ffn_residual`` -- FeedForwardModule.forward after its LayerNorm (conformer.py:34-45):
+  ``x + 0.5 * dropout(lin2(dropout(swish(lin1(h)))))`` as two GEMM launches forward
+  (lin1 -> swish -> dropout; lin2 -> dropout -> *0.5 -> +x) and, backward, one dropout/scale
+  kernel, lin2's dX GEMM with the dropout and swish backward in its epilogue, and the two
+  layers' dX / dW kernels. torch's unfused sequence is 5 extra elementwise kernels forward
+  and 4 backward, each a full pass over a [rows, 576] or [rows, 144] fp32 tensor.
+* ``linear_residual`` -- MHSA's tail (conformer.py:131-138):
+  ``x + pad_zero(dropout(out_proj(ctx)))`` as one GEMM launch (+ one kernel backward).
+
+Results equal the unfused module code: with dropout off (p = 0 or eval) bit for bit -- the
+epilogue performs the same fp32 operations in the same order -- and with dropout on, the
+same function of a different (hash-based) keep mask.
+
+Dropout masks: one device {seed, counter} per device; ``advance_step`` (called once per
+training step, also inside a captured step) moves the counter by 2^32 and each call site
+draws with counter + its own host-side offset, so no per-call device copy is needed and a
+replayed graph draws fresh masks every step. The backward regenerates the forward's mask
+from the same (seed, counter + offset).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+from .quant import PassBits, QuantizedLinear
+
+__all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step"]
+
+_STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
+
+
+def _rng(device: torch.device):
+    st = _STATE.get(device)
+    if st is None:
+        seed = (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + 0x5851F42D) & ((1 << 62) - 1)
+        st = [torch.tensor([seed, 0], dtype=torch.int64, device=device), 0]
+        _STATE[device] = st
+    off = st[1]
+    st[1] = (st[1] + 1) & ((1 << 32) - 1)
+    return st[0], off
+
+
+def advance_step(device: torch.device) -> None:
+    """New dropout masks for every fused call site of the next step (one tiny kernel)."""
+    st = _STATE.get(device)
+    if st is not None:
+        st[0][1:].add_(1 << 32)
+
+
+def fused_supported(x: torch.Tensor, *layers: QuantizedLinear, bitwidth=None) -> bool:
+    if os.environ.get("OB_FUSED", "1") == "0":
+        return False
+    if not (isinstance(bitwidth, PassBits) or bitwidth in (1, 2)):
+        return False  # 32 (F.linear), DynamicBitwidth and invalid values take the module path
+    return x.is_cuda and x.dtype == torch.float32 and all(m.act_quant is None for m in layers)
+
+
+def _bits_args(bitwidth):
+    """(P, pass_bits tensor or None, bits for single-pass entries)."""
+    if isinstance(bitwidth, PassBits):
+        return bitwidth.passes, bitwidth.tensor, None
+    return 1, None, int(bitwidth)
+
+
+def _codes(layer: QuantizedLinear, P: int, bits: Optional[int]):
+    """(codes2, codes1, codes2_t, codes1_t); single-pass: both slots hold the layer's bits."""
+    if P == 1 and bits is not None and bits != 2:
+        c, ct = layer._codes(bits)
+        return c, c, ct, ct
+    c2, c2t = layer._codes(2)
+    if P == 1:
+        return c2, c2, c2t, c2t
+    c1, c1t = layer._codes(1)
+    return c2, c1, c2t, c1t
+
+
+def _dx(lib, dy, P, m, n, codes, pb, alpha, k, stream):
+    dx = torch.empty((P * m, k), dtype=torch.float32, device=dy.device)
+    _lib.check(lib.ob_bitlinear_bwd_dx_passes(dy.data_ptr(), P, m, n, codes[2].data_ptr(),
+                                              codes[3].data_ptr(), pb.data_ptr(), alpha.data_ptr(),
+                                              1, k, dx.data_ptr(), stream)
+               if pb is not None else
+               lib.ob_bitlinear_bwd_dx(dy.data_ptr(), m, n, codes[2].data_ptr(), alpha.data_ptr(),
+                                       1, k, dx.data_ptr(), stream), "ob_bitlinear_bwd_dx")
+    return dx
+
+
+def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream):
+    gw = torch.empty_like(weight)
+    ga = torch.empty((), dtype=torch.float32, device=dy.device)
+    gb = torch.empty((n,), dtype=torch.float32, device=dy.device) if has_bias else None
+    if pb is not None:
+        wsb = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
+        ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dy.device)
+        st = lib.ob_bitlinear_bwd_dw_passes(dy.data_ptr(), x.data_ptr(), P, m, n, k,
+                                            weight.data_ptr(), alpha.data_ptr(), 1, pb.data_ptr(),
+                                            gw.data_ptr(), ga.data_ptr(), _lib.ptr(gb),
+                                            ws.data_ptr(), wsb, stream)
+    else:
+        wsb = lib.ob_bitlinear_bwd_dw_workspace(m, n, k)
+        ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dy.device)
+        st = lib.ob_bitlinear_bwd_dw(dy.data_ptr(), x.data_ptr(), m, n, k, weight.data_ptr(),
+                                     alpha.data_ptr(), 1, bits, gw.data_ptr(), ga.data_ptr(),
+                                     _lib.ptr(gb), ws.data_ptr(), wsb, stream)
+    _lib.check(st, "ob_bitlinear_bwd_dw")
+    return gw, ga, gb
+
+
+class _FFNFn(torch.autograd.Function):
+    """conformer.py:36-45 from the LN output h: x + 0.5 * drop(lin2(drop(swish(lin1(h)))))."""
+
+    @staticmethod
+    def forward(ctx, h, x, w1, a1, b1, w2, a2, b2, meta):
+        P, pb, bits, codes1, codes2, p, rng, off1, off2 = meta
+        rows, k = h.shape
+        m = rows // P
+        n1, n2 = w1.shape[0], w2.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(h)
+        pre = torch.empty((rows, n1), dtype=torch.float32, device=h.device)
+        act = torch.empty((rows, n1), dtype=torch.float32, device=h.device)
+        _lib.check(lib.ob_bitlinear_fwd_swish_drop(
+            h.data_ptr(), P, m, k, codes1[0].data_ptr(), codes1[1].data_ptr(), _lib.ptr(pb),
+            a1.data_ptr(), 1, _lib.ptr(b1), n1, p, _lib.ptr(rng), off1, pre.data_ptr(),
+            act.data_ptr(), stream), "ob_bitlinear_fwd_swish_drop")
+        out = torch.empty((rows, n2), dtype=torch.float32, device=h.device)
+        _lib.check(lib.ob_bitlinear_fwd_residual(
+            act.data_ptr(), P, m, n1, codes2[0].data_ptr(), codes2[1].data_ptr(), _lib.ptr(pb),
+            a2.data_ptr(), 1, _lib.ptr(b2), n2, x.data_ptr(), 0.5, p, _lib.ptr(rng), off2, None, 0,
+            out.data_ptr(), stream), "ob_bitlinear_fwd_residual")
+        ctx.meta = meta
+        ctx.has_bias = (b1 is not None, b2 is not None)
+        ctx.save_for_backward(h, pre, act, w1, a1, w2, a2)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        h, pre, act, w1, a1, w2, a2 = ctx.saved_tensors
+        P, pb, bits, codes1, codes2, p, rng, off1, off2 = ctx.meta
+        gout = gout.contiguous()
+        rows, k = h.shape
+        m = rows // P
+        n1, n2 = w1.shape[0], w2.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(gout)
+        dy2 = torch.empty_like(gout)
+        _lib.check(lib.ob_drop_scale_bwd(gout.data_ptr(), rows, n2, 0.5, p, _lib.ptr(rng), off2,
+                                         None, 0, dy2.data_ptr(), stream), "ob_drop_scale_bwd")
+        dpre = torch.empty((rows, n1), dtype=torch.float32, device=gout.device)
+        _lib.check(lib.ob_bitlinear_bwd_dx_swish_drop(
+            dy2.data_ptr(), P, m, n2, codes2[2].data_ptr(), codes2[3].data_ptr(), _lib.ptr(pb),
+            a2.data_ptr(), 1, n1, pre.data_ptr(), p, _lib.ptr(rng), off1, dpre.data_ptr(), stream),
+            "ob_bitlinear_bwd_dx_swish_drop")
+        gw2, ga2, gb2 = _dw(lib, dy2, act, P, m, n2, n1, w2, a2, ctx.has_bias[1], pb, bits, stream)
+        gh = _dx(lib, dpre, P, m, n1, codes1, pb, a1, k, stream) if ctx.needs_input_grad[0] else None
+        gw1, ga1, gb1 = _dw(lib, dpre, h, P, m, n1, k, w1, a1, ctx.has_bias[0], pb, bits, stream)
+        return gh, gout, gw1, ga1, gb1, gw2, ga2, gb2, None
+
+
+class _LinearResidualFn(torch.autograd.Function):
+    """conformer.py:131-138: R + rscale * rowvalid * drop(lin(x))."""
+
+    @staticmethod
+    def forward(ctx, x, resid, w, a, b, meta):
+        P, pb, bits, codes, rscale, p, rng, off, lens, T = meta
+        rows, k = x.shape
+        m = rows // P
+        n = w.shape[0]
+        lib = _lib.load()
+        out = torch.empty((rows, n), dtype=torch.float32, device=x.device)
+        _lib.check(lib.ob_bitlinear_fwd_residual(
+            x.data_ptr(), P, m, k, codes[0].data_ptr(), codes[1].data_ptr(), _lib.ptr(pb),
+            a.data_ptr(), 1, _lib.ptr(b), n, resid.data_ptr(), rscale, p, _lib.ptr(rng), off,
+            _lib.ptr(lens), T, out.data_ptr(), _lib.stream_of(x)), "ob_bitlinear_fwd_residual")
+        ctx.meta = meta
+        ctx.has_bias = b is not None
+        ctx.save_for_backward(x, w, a)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, w, a = ctx.saved_tensors
+        P, pb, bits, codes, rscale, p, rng, off, lens, T = ctx.meta
+        gout = gout.contiguous()
+        rows, k = x.shape
+        m = rows // P
+        n = w.shape[0]
+        lib = _lib.load()
+        stream = _lib.stream_of(gout)
+        dy = torch.empty_like(gout)
+        _lib.check(lib.ob_drop_scale_bwd(gout.data_ptr(), rows, n, rscale, p, _lib.ptr(rng), off,
+                                         _lib.ptr(lens), T, dy.data_ptr(), stream),
+                   "ob_drop_scale_bwd")
+        gx = _dx(lib, dy, P, m, n, codes, pb, a, k, stream) if ctx.needs_input_grad[0] else None
+        gw, ga, gb = _dw(lib, dy, x, P, m, n, k, w, a, ctx.has_bias, pb, bits, stream)
+        return gx, gout, gw, ga, gb, None
+
+
+def _flat(t: torch.Tensor, width: int) -> torch.Tensor:
+    t2 = t.reshape(-1, width)
+    return t2 if t2.is_contiguous() else t2.contiguous()
+
+
+def ffn_residual(h: torch.Tensor, x: torch.Tensor, lin1: QuantizedLinear, lin2: QuantizedLinear,
+                 bitwidth, p_drop: float) -> torch.Tensor:
+    """x + 0.5 * dropout(lin2(dropout(swish(lin1(h))))) (conformer.py:36-45); h = LN(x)."""
+    P, pb, bits = _bits_args(bitwidth)
+    h2, x2 = _flat(h, lin1.in_features), _flat(x, lin2.out_features)
+    if h2.shape[0] % P:
+        raise ValueError(f"{h2.shape[0]} rows do not split into {P} passes")
+    rng, off1 = _rng(h.device) if p_drop > 0 else (None, 0)
+    off2 = _rng(h.device)[1] if p_drop > 0 else 0
+    meta = (P, pb, bits, _codes(lin1, P, bits), _codes(lin2, P, bits), float(p_drop), rng,
+            off1, off2)
+    out = _FFNFn.apply(h2, x2, lin1.weight, lin1.alpha, lin1.bias, lin2.weight, lin2.alpha,
+                       lin2.bias, meta)
+    return out.view(x.shape)
+
+
+def linear_residual(inp: torch.Tensor, x: torch.Tensor, lin: QuantizedLinear, bitwidth,
+                    p_drop: float, rscale: float = 1.0, lens: Optional[torch.Tensor] = None,
+                    frames: int = 0) -> torch.Tensor:
+    """x + rscale * pad_zero(dropout(lin(inp))) (conformer.py:131-138); ``lens`` int32 [B]
+    valid frames per utterance of ``frames`` rows each (None: no padding)."""
+    P, pb, bits = _bits_args(bitwidth)
+    i2, x2 = _flat(inp, lin.in_features), _flat(x, lin.out_features)
+    if i2.shape[0] % P:
+        raise ValueError(f"{i2.shape[0]} rows do not split into {P} passes")
+    rng, off = _rng(inp.device) if p_drop > 0 else (None, 0)
+    if lens is not None:
+        lens = lens.to(torch.int32).contiguous()
+    meta = (P, pb, bits, _codes(lin, P, bits), float(rscale), float(p_drop), rng, off, lens,
+            int(frames))
+    out = _LinearResidualFn.apply(i2, x2, lin.weight, lin.alpha, lin.bias, meta)
+    return out.view(x.shape)

@@ -27,6 +27,7 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -35,7 +36,7 @@ from . import _lib
 
 __all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "DeviceBits",
            "DynamicBitwidth", "PassBits", "StackedBits", "set_act_quant", "ACT_QUANT_MODES",
-           "act_absmax"]
+           "act_absmax", "PackGroup"]
 
 _VALID = (1, 2, 32)
 
@@ -525,6 +526,67 @@ class QuantizedLinear(nn.Module):
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate cached codes
         self._codes_cache = {}
         return super()._apply(fn, *args, **kwargs)
+
+
+class PackGroup:
+    """Packs every QuantizedLinear under ``module`` for bitwidths ``bits`` in ONE launch
+    (``ob_quant_pack_group``) and hands the codes to the layers' caches, so their
+    forwards find fresh codes without a pack launch each. The reference quantizes per
+    layer inside each forward (quant.py:123-126); a Conformer-S training step packs 144
+    layers x 2 bitwidths, each a launch-bound ~5 us kernel.
+
+    The descriptor table (parameter and code buffer addresses) is built once; ``run()``
+    rebuilds it if a layer's weight moved (``.to()``, re-allocation)."""
+
+    ITEM = np.dtype([("W", "<u8"), ("alpha", "<u8"), ("codes", "<u8"), ("codes_t", "<u8"),
+                     ("N", "<i8"), ("K", "<i8"), ("block0", "<i8"), ("bits", "<i4"),
+                     ("alpha_raw", "<i4")])  # == ob_pack_item (include/onebit_hip.h)
+
+    def __init__(self, module: nn.Module, bits=(2, 1)):
+        self.layers = [m for m in module.modules() if isinstance(m, QuantizedLinear)]
+        self.bits = tuple(bits)
+        self._ptrs = None
+        self.table = None
+        self.codes = []
+
+    def _build(self):
+        lib = _lib.load()
+        items = np.zeros(len(self.layers) * len(self.bits), dtype=self.ITEM)
+        self.codes = []
+        block0 = 0
+        i = 0
+        for m in self.layers:
+            _require_device(m.weight, m.alpha)
+            n, k = m.weight.shape
+            per = {}
+            for b in self.bits:
+                c = torch.empty((n, (k + 15) // 16), dtype=torch.int32, device=m.weight.device)
+                ct = torch.empty((k, (n + 15) // 16), dtype=torch.int32, device=m.weight.device)
+                items[i] = (m.weight.data_ptr(), m.alpha.data_ptr(), c.data_ptr(), ct.data_ptr(),
+                            n, k, block0, b, 1)
+                block0 += int(lib.ob_quant_pack_item_blocks(n, k))
+                per[b] = (c, ct)
+                i += 1
+            self.codes.append(per)
+        self.total_blocks = block0
+        dev = self.layers[0].weight.device
+        self.table = torch.from_numpy(items.view(np.uint8).copy()).to(dev)
+        self._ptrs = [m.weight.data_ptr() for m in self.layers]
+
+    def run(self) -> None:
+        if not self.layers:
+            return
+        if self._ptrs != [m.weight.data_ptr() for m in self.layers]:
+            self._build()
+        lib = _lib.load()
+        w0 = self.layers[0].weight
+        _lib.check(lib.ob_quant_pack_group(self.table.data_ptr(), len(self.codes) * len(self.bits),
+                                           self.total_blocks, _lib.stream_of(w0)),
+                   "ob_quant_pack_group")
+        for m, per in zip(self.layers, self.codes):
+            key = (m.weight.data_ptr(), m.weight._version, m.alpha.data_ptr(), m.alpha._version)
+            for b, (c, ct) in per.items():
+                m._codes_cache[b] = (key, c, ct)
 
 
 # north_star's name for the same layer.

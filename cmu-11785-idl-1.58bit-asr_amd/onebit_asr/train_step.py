@@ -99,6 +99,7 @@ class OneBitStep(nn.Module):
         self.label_smoothing = label_smoothing
         self.stacked = stacked
         self._bits = None
+        self._packer = None
 
     def _use_stacked(self) -> bool:
         if self.stacked is not None:
@@ -151,6 +152,13 @@ class OneBitStep(nn.Module):
     def _forward_stacked(self, batch, bits):
         from .ctc import ctc_loss_mean
 
+        from .fused import advance_step
+        from .quant import PackGroup
+
+        if self._packer is None:
+            self._packer = PackGroup(self.model, bits=(2, 1))
+        self._packer.run()  # codes of every BitLinear, both bitwidths, in one launch
+        advance_step(batch["feats"].device)  # fresh dropout masks for the fused call sites
         sp = self.special
         P = bits.passes  # 0: teacher (2-bit), 1: student (1-bit), 2: SP
         bsz = batch["feats"].size(0)

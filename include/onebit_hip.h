@@ -68,6 +68,30 @@ OB_API int ob_quant_pack(const float* W, const float* alpha, int alpha_raw, int 
                          void* stream);
 
 /*
+ * Grouped pack: ob_quant_pack over a whole model's (layer, bitwidth) items in ONE launch
+ * (the reference quantizes each QuantizedLinear inside its own forward, quant.py:123-126;
+ * at Conformer-S a step needs 144 layers x 2 bitwidths). `items` is a DEVICE array of
+ * n_items descriptors in block order: items[0].block0 = 0 and
+ * items[i+1].block0 = items[i].block0 + ob_quant_pack_item_blocks(N_i, K_i);
+ * total_blocks = the sum over all items. The table is built once (it holds the
+ * persistent parameter and code buffer addresses) and the call is capture-safe.
+ */
+typedef struct ob_pack_item {
+  const float* W;      /* [N][K] */
+  const float* alpha;  /* 1 fp32, device */
+  uint32_t* codes;     /* [N][ceil(K/16)] */
+  uint32_t* codes_t;   /* [K][ceil(N/16)] */
+  int64_t N, K;
+  int64_t block0;      /* first block of this item */
+  int32_t bits;        /* 1 or 2 */
+  int32_t alpha_raw;
+} ob_pack_item;
+
+OB_API int64_t ob_quant_pack_item_blocks(int64_t N, int64_t K);
+OB_API int ob_quant_pack_group(const ob_pack_item* items, int n_items, int64_t total_blocks,
+                               void* stream);
+
+/*
  * quantize_weight forward, elementwise (quant.py:49-70): W_hat[i] = a * Q(W[i]/a).
  */
 OB_API int ob_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits,
@@ -322,6 +346,51 @@ OB_API int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma,
 OB_API int ob_ctc_greedy_decode(const float* logits, const int64_t* lens, int64_t B, int64_t T,
                                 int64_t V, int blank, int32_t* ids, int32_t* out,
                                 int32_t* out_len, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Fused epilogues: the elementwise ops that follow a BitLinear GEMM at its call sites in
+ * the reference, applied in the GEMM's store instead of separate torch kernels.
+ * X / Y rows are P stacked passes as in ob_bitlinear_fwd_passes; pass_bits may be NULL
+ * when P == 1 (codes2 is used). Element (row, col) of a [P*M][N] output has dropout index
+ * row * N + col; keep = hash(seed, counter, index) >= p * 2^32, kept values scale by
+ * 1 / (1 - p); rng is a DEVICE {seed, counter} int64[2] (required when p_drop > 0) and the
+ * mask is drawn for counter + rng_offset (a per-call-site offset: no per-call device copy).
+ * Outputs must not alias inputs.
+ *
+ * swish_drop   Y_pre = a X.Q^T + b;  Y_act = dropout(silu(Y_pre))
+ *              (FeedForwardModule lin1 -> swish -> dropout, conformer.py:36-38)
+ * residual     Y = R + rscale * rowvalid * dropout(a X.Q^T + b),
+ *              rowvalid = (lens == NULL) || (row % T < lens[row / T])
+ *              (lin2 -> dropout -> x + 0.5 h, conformer.py:39-45, rscale 0.5, lens NULL;
+ *               out_proj -> dropout -> pad zero -> x + out, conformer.py:131-138, rscale 1)
+ * bwd_dx_swish_drop
+ *              dPre = (a dY.Q) * keep * scale * silu'(pre): the dX GEMM of lin2 chained
+ *              through the dropout and swish backward of swish_drop (same rng, same p)
+ * drop_scale_bwd
+ *              dY = rscale * rowvalid * dropout(dOut) with the residual entry's mask:
+ *              the gradient of `residual`'s output w.r.t. its GEMM output.
+ * ------------------------------------------------------------------------------------ */
+OB_API int ob_bitlinear_fwd_swish_drop(const float* X, int64_t P, int64_t M, int64_t K,
+                                       const uint32_t* codes2, const uint32_t* codes1,
+                                       const int32_t* pass_bits, const float* alpha,
+                                       int alpha_raw, const float* bias, int64_t N, float p_drop,
+                                       const uint64_t* rng, int64_t rng_offset, float* Y_pre,
+                                       float* Y_act, void* stream);
+OB_API int ob_bitlinear_fwd_residual(const float* X, int64_t P, int64_t M, int64_t K,
+                                     const uint32_t* codes2, const uint32_t* codes1,
+                                     const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                     const float* bias, int64_t N, const float* R, float rscale,
+                                     float p_drop, const uint64_t* rng, int64_t rng_offset,
+                                     const int32_t* lens, int64_t T, float* Y, void* stream);
+OB_API int ob_bitlinear_bwd_dx_swish_drop(const float* dY, int64_t P, int64_t M, int64_t N,
+                                          const uint32_t* codes2_t, const uint32_t* codes1_t,
+                                          const int32_t* pass_bits, const float* alpha,
+                                          int alpha_raw, int64_t K, const float* pre,
+                                          float p_drop, const uint64_t* rng, int64_t rng_offset,
+                                          float* dPre, void* stream);
+OB_API int ob_drop_scale_bwd(const float* dOut, int64_t rows, int64_t N, float rscale,
+                             float p_drop, const uint64_t* rng, int64_t rng_offset,
+                             const int32_t* lens, int64_t T, float* dY, void* stream);
 
 #ifdef __cplusplus
 }

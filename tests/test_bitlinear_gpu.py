@@ -217,3 +217,35 @@ def test_alpha_zero_chain(gpu):
     m(x, 2).sum().backward()
     assert torch.count_nonzero(m.weight.grad) == 0
     assert m.alpha.grad.item() == 0.0
+
+
+def test_pack_group_matches_oracle(gpu):
+    """ob_quant_pack_group (one launch for every layer and bitwidth) == the oracle's codes,
+    for layers of ragged shapes (K, N not multiples of 16, a 1x1 layer), and the layers'
+    forwards then use those codes without packing again."""
+    import torch.nn as nn
+    from onebit_asr.quant import PackGroup, QuantizedLinear
+
+    torch.manual_seed(5)
+    shapes = [(144, 576), (576, 144), (7, 37), (1, 1), (33, 130), (144, 144)]
+    mod = nn.ModuleList([QuantizedLinear(k, n) for k, n in shapes]).to(gpu)
+    with torch.no_grad():
+        mod[1].alpha.fill_(-0.03)  # negative raw alpha: |alpha| + 1e-8 is what quantizes
+    grp = PackGroup(mod, bits=(2, 1))
+    grp.run()
+    for m, per in zip(mod, grp.codes):
+        W = m.weight.detach().cpu().numpy()
+        a = np.float32(m.alpha.item())
+        for bits, (c, ct) in per.items():
+            c_ref, ct_ref = qo.np_codes(W, a, bits)
+            assert np.array_equal(c.cpu().numpy().view(np.uint32), c_ref)
+            assert np.array_equal(ct.cpu().numpy().view(np.uint32), ct_ref)
+            got = m._codes(bits)
+            assert got[0].data_ptr() == c.data_ptr()  # cache hit: no per-layer pack
+    # after an in-place update the cache is stale until the next run()
+    with torch.no_grad():
+        mod[0].weight.mul_(-1.0)
+    assert mod[0]._codes(2)[0].data_ptr() != grp.codes[0][2][0].data_ptr()
+    grp.run()
+    c_ref, _ = qo.np_codes(mod[0].weight.detach().cpu().numpy(), np.float32(mod[0].alpha.item()), 2)
+    assert np.array_equal(grp.codes[0][2][0].cpu().numpy().view(np.uint32), c_ref)

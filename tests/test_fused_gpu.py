@@ -1,0 +1,180 @@
+"""GPU parity of the fused BitLinear call sites (onebit_asr/fused.py, csrc/tgemm.hip
+epilogues, csrc/fused.hip) against the unfused module code they replace
+(conformer.py:34-45 FFN, :131-138 MHSA tail).
+
+Bars (written here): dropout off -- forward max|err| <= 1e-6 * max|ref| and every gradient
+rel-L2 <= 1e-6 (the same fp32 operations; only torch's own elementwise kernels may contract
+differently); dropout on -- against a torch fp32 restatement driven by the kernels' own keep
+masks (ob_relattn_dropout_mask on the same {seed, counter + offset}): forward and gradients
+within the same bars, plus the kept fraction within 5 sigma of 1 - p.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double()
+    b = b.detach().double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _maxrel(a, b):
+    return float((a.detach() - b.detach()).abs().max() / b.detach().abs().max().clamp_min(1e-30))
+
+
+def _ffn_pair(gpu, d=144, dff=576, p=0.0):
+    from onebit_asr.conformer import FeedForwardModule
+
+    torch.manual_seed(3)
+    m = FeedForwardModule(d, dff, p).to(gpu)
+    with torch.no_grad():
+        for lin in (m.lin1, m.lin2):
+            lin.bias.uniform_(-0.1, 0.1)
+    return m
+
+
+def _run(m, x, bits, fused, monkeypatch):
+    monkeypatch.setenv("OB_FUSED", "1" if fused else "0")
+    for prm in m.parameters():
+        prm.grad = None
+    xx = x.clone().requires_grad_(True)
+    y = m(xx, bits)
+    g = torch.randn_like(y, generator=torch.Generator(device=y.device).manual_seed(11))
+    (y * g).sum().backward()
+    grads = {n: prm.grad.clone() for n, prm in m.named_parameters()}
+    return y.detach(), xx.grad.clone(), grads
+
+
+@pytest.mark.parametrize("bits", [1, 2])
+def test_ffn_fused_equals_unfused(gpu, bits, monkeypatch):
+    m = _ffn_pair(gpu).eval()
+    x = torch.randn(4, 50, 144, device=gpu)
+    y0, gx0, g0 = _run(m, x, bits, False, monkeypatch)
+    y1, gx1, g1 = _run(m, x, bits, True, monkeypatch)
+    assert _maxrel(y1, y0) <= 1e-6
+    assert _rel(gx1, gx0) <= 1e-6
+    for n in g0:
+        # alpha: one cancellation-prone sum over N*K terms (its own bar, as elsewhere)
+        assert _rel(g1[n], g0[n]) <= (1e-5 if n.endswith("alpha") else 1e-6), n
+
+
+def test_ffn_fused_stacked_passes(gpu, monkeypatch):
+    """P = 3 stacked passes (2-bit, 1-bit, 2-bit) == three single-pass calls."""
+    from onebit_asr.quant import PassBits
+
+    m = _ffn_pair(gpu).eval()
+    x = torch.randn(3 * 2, 40, 144, device=gpu)
+    pb = PassBits(torch.tensor([2, 1, 2], dtype=torch.int32, device=gpu))
+    y, gx, g = _run(m, x, pb, True, monkeypatch)
+    ys, gxs = [], []
+    gsum = None
+    gg = torch.randn_like(y, generator=torch.Generator(device=gpu).manual_seed(11))
+    for p, bits in enumerate([2, 1, 2]):
+        for prm in m.parameters():
+            prm.grad = None
+        xp = x[2 * p:2 * p + 2].clone().requires_grad_(True)
+        yp = m(xp, bits)
+        (yp * gg[2 * p:2 * p + 2]).sum().backward()
+        ys.append(yp.detach())
+        gxs.append(xp.grad)
+        cur = {n: prm.grad.clone() for n, prm in m.named_parameters()}
+        gsum = cur if gsum is None else {n: gsum[n] + cur[n] for n in cur}
+    assert _maxrel(y, torch.cat(ys)) <= 1e-6
+    assert _rel(gx, torch.cat(gxs)) <= 1e-6
+    for n in g:
+        assert _rel(g[n], gsum[n]) <= 1e-5, n  # per-pass sums in another order
+
+
+def _mask(rng_state, off, n, p, gpu):
+    from onebit_asr.attention import dropout_mask
+
+    r = rng_state.clone()
+    r[1] += off
+    return dropout_mask((n,), p, r).bool()
+
+
+def test_ffn_dropout_matches_torch_restatement(gpu, monkeypatch):
+    from onebit_asr import fused
+
+    p = 0.1
+    m = _ffn_pair(gpu, p=p).train()
+    x = torch.randn(2, 64, 144, device=gpu)
+    monkeypatch.setenv("OB_FUSED", "1")
+    fused._rng(torch.device(gpu))  # make sure the device state exists
+    st = fused._STATE[torch.device(gpu)]
+    rng0, off0 = st[0].clone(), st[1]
+    xx = x.clone().requires_grad_(True)
+    y = m(xx, 2)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    got = {n: prm.grad.clone() for n, prm in m.named_parameters()}
+    rows = x.numel() // 144
+    k1 = _mask(rng0, off0, rows * 576, p, gpu).view(rows, 576)
+    k2 = _mask(rng0, off0 + 1, rows * 144, p, gpu).view(rows, 144)
+    frac = k1.float().mean().item()
+    assert abs(frac - (1 - p)) < 5 * np.sqrt(p * (1 - p) / k1.numel())
+    # torch fp32 restatement with the same masks (layers through the unfused module code)
+    monkeypatch.setenv("OB_FUSED", "0")
+    for prm in m.parameters():
+        prm.grad = None
+    xr = x.clone().requires_grad_(True)
+    h = m.lin1(m.ln(xr), 2)
+    a = F.silu(h) * k1.view(2, 64, 576) / (1 - p)
+    o = m.lin2(a, 2) * k2.view(2, 64, 144) / (1 - p)
+    yr = xr + 0.5 * o
+    (yr * g).sum().backward()
+    assert _maxrel(y, yr) <= 1e-6
+    assert _rel(xx.grad, xr.grad) <= 1e-6
+    for n, prm in m.named_parameters():
+        assert _rel(got[n], prm.grad) <= 1e-6, n
+
+
+def test_linear_residual_padding_and_dropout(gpu):
+    """x + pad_zero(dropout(out_proj(ctx))) with ragged lengths and P = 3 passes."""
+    from onebit_asr import fused
+    from onebit_asr.quant import PassBits, QuantizedLinear
+
+    torch.manual_seed(4)
+    lin = QuantizedLinear(144, 144).to(gpu)
+    with torch.no_grad():
+        lin.bias.uniform_(-0.1, 0.1)
+    P, B, T, p = 3, 2, 37, 0.1
+    pb = PassBits(torch.tensor([2, 1, 1], dtype=torch.int32, device=gpu))
+    lens = torch.tensor([37, 20] * P, dtype=torch.int32, device=gpu)
+    ctx = torch.randn(P * B, T, 144, device=gpu, requires_grad=True)
+    x = torch.randn(P * B, T, 144, device=gpu, requires_grad=True)
+    fused._rng(torch.device(gpu))
+    st = fused._STATE[torch.device(gpu)]
+    rng0, off0 = st[0].clone(), st[1]
+    y = fused.linear_residual(ctx, x, lin, pb, p, 1.0, lens, T)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    got = (ctx.grad.clone(), x.grad.clone(), lin.weight.grad.clone(), lin.alpha.grad.clone(),
+           lin.bias.grad.clone())
+    keep = _mask(rng0, off0, P * B * T * 144, p, gpu).view(P * B, T, 144)
+    valid = (torch.arange(T, device=gpu)[None, :] < lens[:, None]).float()[..., None]
+    for prm in (ctx, x, lin.weight, lin.alpha, lin.bias):
+        prm.grad = None
+    outs = [lin(ctx[q * B:(q + 1) * B], b) for q, b in enumerate([2, 1, 1])]
+    yr = x + torch.cat(outs) * keep / (1 - p) * valid
+    (yr * g).sum().backward()
+    assert _maxrel(y, yr) <= 1e-6
+    assert torch.all(y[1, 20:] == x[1, 20:])  # padded rows carry the residual only
+    ref = (ctx.grad, x.grad, lin.weight.grad, lin.alpha.grad, lin.bias.grad)
+    for a, b, name in zip(got, ref, ["dctx", "dx", "dW", "dalpha", "db"]):
+        assert _rel(a, b) <= 1e-5, name
+
+
+def test_fused_entry_errors(gpu):
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    # p_drop out of range and missing rng are rejected, nothing launched
+    assert lib.ob_drop_scale_bwd(None, 0, 0, 1.0, 1.5, None, 0, None, 0, None, None) == -2
+    assert lib.ob_drop_scale_bwd(16, 1, 4, 1.0, 0.1, None, 0, None, 0, 16, None) == -1

@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--shape", default=None, help="only this layer (lin1|lin2|qkvo|pos)")
     ap.add_argument("--op", default=None, help="only this op (pack|fwd|dx|dw)")
+    ap.add_argument("--fused", action="store_true", help="also time the fused-epilogue entries")
     ap.add_argument("--passes", type=int, default=3,
                     help="stacked passes per launch (the training step runs 3; 0 = single-pass entries)")
     args = ap.parse_args()
@@ -106,12 +107,37 @@ def main():
                     pbits.data_ptr(), dW.data_ptr(), da.data_ptr(), db.data_ptr(), ws.data_ptr(),
                     wsb, cs),
             })
+        if args.passes > 0 and args.fused:
+            Yp = torch.empty(P * M, N, device=dev)
+            R = torch.randn(P * M, N, device=dev)
+            pre = torch.randn(P * M, K, device=dev)
+            rng = torch.tensor([1234, 5], dtype=torch.int64, device=dev)
+            pd = 0.1
+            fns.update({
+                "fswish": lambda cs=s: lib.ob_bitlinear_fwd_swish_drop(
+                    X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, b.data_ptr(), N, pd, rng.data_ptr(), 0, Yp.data_ptr(),
+                    Y.data_ptr(), cs),
+                "fres": lambda cs=s: lib.ob_bitlinear_fwd_residual(
+                    X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, b.data_ptr(), N, R.data_ptr(), 0.5, pd, rng.data_ptr(), 0,
+                    None, 0, Y.data_ptr(), cs),
+                "dxswish": lambda cs=s: lib.ob_bitlinear_bwd_dx_swish_drop(
+                    dY.data_ptr(), P, M, N, codes_t.data_ptr(), c1t.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, K, pre.data_ptr(), pd, rng.data_ptr(), 0, dX.data_ptr(),
+                    cs),
+                "dropbwd": lambda cs=s: lib.ob_drop_scale_bwd(
+                    dY.data_ptr(), P * M, N, 0.5, pd, rng.data_ptr(), 0, None, 0, R.data_ptr(), cs),
+            })
         res = {}
         for k, fn in fns.items():
             res[k] = timed(fn, args.reps, args.graph) if (not args.op or k == args.op) else float("nan")
         gb_f = 4 * P * (M * K + M * N) / res["fwd"] / 1e3
         gb_w = 4 * P * (M * K + M * N) / res["dw"] / 1e3
         print(f"{name:6s} {M:5d} {K:4d} {N:4d} | {res['pack']:7.2f} {res['fwd']:7.2f} {res['dx']:7.2f} {res['dw']:7.2f} us | {gb_f:8.0f} {gb_w:8.0f}")
+        if "fswish" in res:
+            print(f"{'':6s} fused: fwd+swish {res['fswish']:7.2f}  fwd+residual {res['fres']:7.2f}  "
+                  f"dx+swish-bwd {res['dxswish']:7.2f}  drop-scale-bwd {res['dropbwd']:7.2f} us")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""HBM bytes per launch of the BitLinear kernel families from tools/traffic.sh output.
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. gfx950 correction (MI355X_MICROARCH.md,
+HBM/rocprofv3 section): FETCH_SIZE reports half the bytes of a wide coalesced streaming
+read, so it is doubled; WRITE_SIZE is taken as is. Per (shape, op) the median over the
+timed dispatches of each kernel is used; one "launch" of the dW family is one dw_bf16x6
+dispatch plus its ste_reduce dispatch. Families are weighted by launches per training
+step exactly as bench.py's roofline() weights its time and algorithmic bytes.
+
+usage: python tools/traffic_json.py gpurun_out/TAG > profiles/pmc_traffic.json"""
+import csv
+import glob
+import json
+import statistics
+import sys
+
+# launches per step (bench.py ql_shapes at Conformer-S: 16 blocks, 2 FFNs, 4 q/k/v/out)
+COUNT = {"lin1": 32, "lin2": 32, "qkvo": 64, "pos": 16}
+KERNELS = {"fwd": ("tgemm",), "dx": ("tgemm",), "dw": ("dw_bf16x6", "ste_reduce")}
+
+
+def per_dispatch(path, sub):
+    vals = {}
+    for f in glob.glob(f"{path}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if sub in r["Kernel_Name"]:
+                vals.setdefault(r.get("Dispatch_Id", len(vals)), 0.0)
+                vals[r.get("Dispatch_Id", len(vals))] += float(r["Counter_Value"])
+    return statistics.median(vals.values()) if vals else None
+
+
+def main():
+    d = sys.argv[1]
+    out, fam = {"source": d, "note": __doc__.split("\n\n")[1].replace("\n", " ")}, {}
+    for shape, cnt in COUNT.items():
+        for op, subs in KERNELS.items():
+            if shape == "pos" and op == "dx":
+                continue  # pos_emb needs no input gradient (bench.py n_dx)
+            tot = 0.0
+            for sub in subs:
+                f = per_dispatch(f"{d}/{shape}_{op}_FETCH_SIZE", sub)
+                w = per_dispatch(f"{d}/{shape}_{op}_WRITE_SIZE", sub)
+                if f is None or w is None:
+                    raise SystemExit(f"missing counters for {shape} {op} {sub}")
+                tot += (2.0 * f + w) * 1024.0
+            out[f"{shape}_{op}_hbm_bytes"] = int(tot)
+            key = "dw_partial+ste_reduce" if op == "dw" else "ternary_gemm"
+            b, n = fam.get(key, (0.0, 0))
+            fam[key] = (b + cnt * tot, n + cnt)
+    for key, (b, n) in fam.items():
+        out[key] = {"hbm_bytes_per_launch": int(b / n), "launches_per_step": n}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
