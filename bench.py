@@ -417,6 +417,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if os.environ.get("OB_BLAS_ALL"):  # A/B experiments: one BLAS library for every GEMM
+        torch.backends.cuda.preferred_blas_library(os.environ["OB_BLAS_ALL"])
 
     from onebit_asr.conformer import ConformerASR
     from onebit_asr.data import CONFORMER_S, synthetic_batch

@@ -334,6 +334,65 @@ int ob_drop_scale_bwd(const float* dOut, int64_t rows, int64_t N, float rscale, 
   return launched();
 }
 
+int ob_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int64_t N, float rscale,
+                         float p_drop, const uint64_t* rng, int64_t rng_offset,
+                         const int32_t* lens, int64_t T, float* out, void* stream) {
+  if (rows < 0 || N < 0 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+  if (lens && (T < 1 || T > 0x7fffffff || rows % T)) return OB_ERR_SHAPE;
+  if ((rows * N > 0 && (!R || !Y || !out)) || (p_drop > 0.0f && !rng)) return OB_ERR_NULL;
+  if (!aligned4(R) || !aligned4(Y) || !aligned4(out) || !aligned4(lens)) return OB_ERR_ALIGN;
+  launch_residual_drop_fwd(R, Y, rows, N, rscale, p_drop, rng, (uint64_t)rng_offset,
+                           reinterpret_cast<const int*>(lens), (int)T, out, as_stream(stream));
+  return launched();
+}
+
+namespace {
+int convmod_check(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K) {
+  if (P < 1 || Bt < 0 || T < 0 || C < 1 || K < 1 || Bt % P || Bt > 65535) return OB_ERR_SHAPE;
+  if (!convmod_supported(C, K) || Bt * T * 2 * C > ((int64_t)1 << 40)) return OB_ERR_SHAPE;
+  return OB_OK;
+}
+}  // namespace
+
+size_t ob_convmod_workspace(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K) {
+  if (convmod_check(P, Bt, T, C, K)) return 0;
+  return convmod_workspace(P, Bt, T, C, K);
+}
+
+int ob_convmod_fwd(const float* u, const float* w_dw, const float* b_dw, const float* gamma,
+                   const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
+                   float eps, float* z, float* g, float* stats, float* v, void* ws,
+                   size_t ws_bytes, void* stream) {
+  if (int st = convmod_check(P, Bt, T, C, K)) return st;
+  if (Bt * T == 0) return OB_OK;
+  if (!u || !w_dw || !gamma || !beta || !z || !g || !stats || !v || !ws) return OB_ERR_NULL;
+  if (ws_bytes < convmod_workspace(P, Bt, T, C, K)) return OB_ERR_WORKSPACE;
+  if (((uintptr_t)ws & 7u) || !aligned4(u) || !aligned4(z) || !aligned4(v) || !aligned4(stats) ||
+      !aligned4(w_dw) || !aligned4(b_dw))
+    return OB_ERR_ALIGN;
+  if (!aligned4(g)) return OB_ERR_ALIGN;
+  launch_convmod_fwd(u, w_dw, b_dw, gamma, beta, P, Bt, T, C, K, eps, z, g, stats, v, ws,
+                     as_stream(stream));
+  return launched();
+}
+
+int ob_convmod_bwd(const float* dv, const float* u, const float* z, const float* g,
+                   const float* stats, const float* w_dw, const float* gamma, const float* beta,
+                   int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K, float* du,
+                   float* dw_dw, float* db_dw, float* dgamma, float* dbeta, void* ws,
+                   size_t ws_bytes, void* stream) {
+  if (int st = convmod_check(P, Bt, T, C, K)) return st;
+  if (!dw_dw || !dgamma || !dbeta || !w_dw || !gamma || !beta) return OB_ERR_NULL;
+  if (Bt * T > 0 && (!dv || !u || !z || !g || !stats || !du || !ws)) return OB_ERR_NULL;
+  if (ws_bytes < convmod_workspace(P, Bt, T, C, K)) return OB_ERR_WORKSPACE;
+  if (((uintptr_t)ws & 7u) || !aligned4(dv) || !aligned4(u) || !aligned4(z) || !aligned4(g) ||
+      !aligned4(du))
+    return OB_ERR_ALIGN;
+  launch_convmod_bwd(dv, u, z, g, stats, w_dw, gamma, beta, P, Bt, T, C, K, du, dw_dw, db_dw,
+                     dgamma, dbeta, ws, as_stream(stream));
+  return launched();
+}
+
 size_t ob_act_absmax_workspace(int64_t P) {
   return (P < 1 || P > 65535) ? 0 : act_absmax_workspace((int)P);
 }

@@ -1,0 +1,481 @@
+// convmod.hip — the Conformer conv module's elementwise/depthwise core, channels-last.
+//
+// Reference: onebit_asr/conformer.py:139-167 (full precision):
+//   y = LN(x) -> [B,C,T] -> pw1 (1x1, C -> 2C) -> GLU(dim=C) -> depthwise k (pad k/2)
+//     -> BatchNorm1d (batch statistics over B and T, padded frames included,
+//        track_running_stats=False) -> swish -> pw2 (1x1) -> dropout -> [B,T,C];  x + y
+// The reference transposes to [B,C,T] for nn.Conv1d. Here everything stays [rows, C]
+// (rows = Bt*T, channel fastest): pw1 / pw2 are plain GEMMs on that layout (hipBLASLt,
+// bias in its epilogue) and this file covers what lies between them:
+//   forward   u [rows][2C] -> g = u[:, :C] * sigmoid(u[:, C:]) -> z = dw(g) + b_dw
+//             -> per-(pass, channel) mean / rstd of z -> v = swish(BN(z))        (4 launches)
+//   backward  dv -> dz (BN + swish backward, per-pass batch statistics) -> dg = dw^T(dz)
+//             -> du (GLU backward); dw_dw, db_dw, dgamma, dbeta                   (6 launches)
+// The forward keeps g (GLU output) and z for the backward.
+// Stacked passes (P > 1, Bt = P*B): pass p's utterances are rows [p*B*T, (p+1)*B*T) and
+// BatchNorm uses that pass's own statistics (each reference pass normalises its own batch);
+// gamma / beta / the depthwise weights are shared, so their gradients sum over passes.
+// Reductions are fixed-order (deterministic); statistics accumulate in fp64.
+#include <math.h>
+
+#include "ob_launch.h"
+
+namespace ob {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr size_t kMaxLds = 160 * 1024;
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// out[r] = sum_j wt[j] * tile[(tl0 + r + j) * C + c], r < R: one channel, R consecutive
+// frames, the R + KT - 1 tile values held in registers (KT compile-time) -- 1 + (KT-1)/R LDS
+// reads per output instead of 2 KT.
+template <int KT, int R>
+__device__ __forceinline__ void conv_window(const float* __restrict__ tile, int C, int c, int tl0,
+                                            const float (&wt)[KT], float (&out)[R]) {
+  float win[R + KT - 1];
+#pragma unroll
+  for (int i = 0; i < R + KT - 1; ++i) win[i] = tile[(tl0 + i) * C + c];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KT; ++j) acc = fmaf(wt[j], win[r + j], acc);
+    out[r] = acc;
+  }
+}
+
+constexpr int kR = 8;  // frames per register window
+
+// ------------------------------------------------------------------ forward
+// Block = (time tile of TT frames, utterance). LDS holds g over [t0-P, t0+TT+P) x C and
+// the depthwise weights; outputs z for the tile (consecutive threads = consecutive
+// channels: coalesced global access, conflict-free LDS).
+// KT > 0: the kernel width as a compile-time constant (register windows); KT == 0: generic.
+template <int KT>
+__global__ __launch_bounds__(kThreads) void cm_glu_dw_fwd_kernel(
+    const float* __restrict__ u, const float* __restrict__ wdw, const float* __restrict__ bdw,
+    int T, int C, int K, int TT, float* __restrict__ z, float* __restrict__ gout) {
+  extern __shared__ float sm[];
+  const int P = K / 2;
+  const int W = TT + K - 1;
+  float* gs = sm;                 // [W][C]
+  float* ws = sm + (size_t)W * C;  // [C][K]
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * TT;
+  const size_t rb = (size_t)b * T;
+  for (int i = threadIdx.x; i < C * K; i += kThreads) ws[i] = wdw[i];
+#pragma unroll 4
+  for (int i = threadIdx.x; i < W * C; i += kThreads) {
+    const int tl = i / C, c = i - tl * C;
+    const int t = t0 - P + tl;
+    float g = 0.0f;
+    if (t >= 0 && t < T) {
+      const float* ur = u + (rb + t) * (size_t)(2 * C);
+      g = ur[c] * sigm(ur[C + c]);
+    }
+    gs[i] = g;
+  }
+  __syncthreads();
+  if constexpr (KT > 0) {
+    const int nrb = (TT + kR - 1) / kR;
+    for (int it = threadIdx.x; it < C * nrb; it += kThreads) {
+      const int c = it % C, tl0 = kR * (it / C);
+      if (t0 + tl0 >= T) break;
+      float wt[KT], out[kR];
+#pragma unroll
+      for (int j = 0; j < KT; ++j) wt[j] = ws[c * KT + j];
+      conv_window<KT, kR>(gs, C, c, tl0, wt, out);
+      const float bc = bdw ? bdw[c] : 0.0f;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int t = t0 + tl0 + r;
+        if (tl0 + r < TT && t < T) {
+          z[(rb + t) * C + c] = out[r] + bc;
+          gout[(rb + t) * C + c] = gs[(tl0 + r + P) * C + c];  // kept for the weight gradient
+        }
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < TT * C; i += kThreads) {
+      const int tl = i / C, c = i - tl * C;
+      const int t = t0 + tl;
+      if (t >= T) break;  // i increases monotonically: later i are later frames
+      float acc = 0.0f;
+      const float* wc = ws + c * K;
+      for (int j = 0; j < K; ++j) acc = fmaf(wc[j], gs[(tl + j) * C + c], acc);
+      z[(rb + t) * C + c] = acc + (bdw ? bdw[c] : 0.0f);
+      gout[(rb + t) * C + c] = gs[(tl + P) * C + c];  // kept for the weight gradient
+    }
+  }
+}
+
+// Per-(pass, chunk) partial sums of x and x^2 (fp64) per channel: block = (chunk, pass),
+// thread c < C walks the chunk's rows.
+__global__ __launch_bounds__(kThreads) void cm_stats_part_kernel(const float* __restrict__ x,
+                                                                 int64_t rows_pp, int C, int S,
+                                                                 double* __restrict__ part) {
+  const int s = blockIdx.x, p = blockIdx.y;
+  const int64_t r0 = rows_pp * s / S, r1 = rows_pp * (s + 1) / S;
+  const float* xp = x + (size_t)p * rows_pp * C;
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
+    for (int64_t r = r0; r < r1; ++r) {
+      const double v = xp[r * C + c];
+      s1 += v;
+      s2 += v * v;
+    }
+    double* o = part + (((size_t)p * S + s) * C + c) * 2;
+    o[0] = s1;
+    o[1] = s2;
+  }
+}
+
+// Fixed-order wave sum of a per-lane fp64 value (deterministic).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// stats[p][c] = {mean, rstd} (biased variance, as BatchNorm's normalisation uses).
+// One wave per (p, c): lanes take chunks s = lane, lane + 64, ...
+__global__ __launch_bounds__(64) void cm_stats_final_kernel(const double* __restrict__ part,
+                                                            int P, int C, int S, int64_t n,
+                                                            float eps, float* __restrict__ stats) {
+  const int i = blockIdx.x;  // p * C + c
+  const int p = i / C, c = i - p * C;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = threadIdx.x; s < S; s += 64) {
+    const double* o = part + (((size_t)p * S + s) * C + c) * 2;
+    s1 += o[0];
+    s2 += o[1];
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (threadIdx.x == 0) {
+    const double mean = s1 / (double)n;
+    double var = s2 / (double)n - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    stats[2 * i] = (float)mean;
+    stats[2 * i + 1] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+}
+
+// v = swish(gamma * (z - mean) * rstd + beta), pass-wise statistics.
+__global__ __launch_bounds__(kThreads) void cm_bn_swish_fwd_kernel(
+    const float* __restrict__ z, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int64_t rows_pp, int C, int64_t total,
+    float* __restrict__ v) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride) {
+    const int64_t row = i / C;
+    const int c = (int)(i - row * C);
+    const int p = (int)(row / rows_pp);
+    const float* st = stats + 2 * ((size_t)p * C + c);
+    const float y = (z[i] - st[0]) * st[1] * gamma[c] + beta[c];
+    v[i] = y / (1.0f + expf(-y));
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// dy_bn = dv * swish'(y) at element (row, c), y recomputed from z and the statistics.
+__device__ __forceinline__ float bn_dy(float dv, float zz, const float* st, float gm, float bt,
+                                       float& xhat) {
+  xhat = (zz - st[0]) * st[1];
+  const float y = xhat * gm + bt;
+  const float s = sigm(y);
+  return dv * s * (1.0f + y * (1.0f - s));
+}
+
+// Per-(pass, chunk) partials of sum(dy_bn) and sum(dy_bn * xhat) (fp64).
+__global__ __launch_bounds__(kThreads) void cm_bn_bwd_part_kernel(
+    const float* __restrict__ dv, const float* __restrict__ z, const float* __restrict__ stats,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int64_t rows_pp, int C,
+    int S, double* __restrict__ part) {
+  const int s = blockIdx.x, p = blockIdx.y;
+  const int64_t r0 = rows_pp * s / S, r1 = rows_pp * (s + 1) / S;
+  const size_t base = (size_t)p * rows_pp * C;
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float* st = stats + 2 * ((size_t)p * C + c);
+    const float gm = gamma[c], bt = beta[c];
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
+    for (int64_t r = r0; r < r1; ++r) {
+      float xh;
+      const float d = bn_dy(dv[base + r * C + c], z[base + r * C + c], st, gm, bt, xh);
+      s1 += d;
+      s2 += (double)d * xh;
+    }
+    double* o = part + (((size_t)p * S + s) * C + c) * 2;
+    o[0] = s1;
+    o[1] = s2;
+  }
+}
+
+// coef[p][c] = {mean(dy_bn), mean(dy_bn * xhat)}; dgamma / dbeta summed over passes.
+// One wave per channel.
+__global__ __launch_bounds__(64) void cm_bn_bwd_final_kernel(
+    const double* __restrict__ part, int P, int C, int S, int64_t n, float* __restrict__ coef,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x;
+  double tg = 0.0, tb = 0.0;
+  for (int p = 0; p < P; ++p) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int s = threadIdx.x; s < S; s += 64) {
+      const double* o = part + (((size_t)p * S + s) * C + c) * 2;
+      s1 += o[0];
+      s2 += o[1];
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (threadIdx.x == 0) {
+      coef[2 * ((size_t)p * C + c)] = (float)(s1 / (double)n);
+      coef[2 * ((size_t)p * C + c) + 1] = (float)(s2 / (double)n);
+    }
+    tb += s1;
+    tg += s2;
+  }
+  if (threadIdx.x == 0) {
+    dgamma[c] = (float)tg;
+    dbeta[c] = (float)tb;
+  }
+}
+
+// dz = dL/dz (BatchNorm + swish backward with per-pass batch statistics), elementwise.
+__global__ __launch_bounds__(kThreads) void cm_dz_kernel(
+    const float* __restrict__ dv, const float* __restrict__ z, const float* __restrict__ stats,
+    const float* __restrict__ coef, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int64_t rows_pp, int C, int64_t total,
+    float* __restrict__ dz) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride) {
+    const int64_t row = i / C;
+    const int c = (int)(i - row * C);
+    const size_t pc = 2 * ((size_t)(row / rows_pp) * C + c);
+    float xh;
+    const float dy = bn_dy(dv[i], z[i], stats + pc, gamma[c], beta[c], xh);
+    dz[i] = gamma[c] * stats[pc + 1] * (dy - coef[pc] - xh * coef[pc + 1]);
+  }
+}
+
+// Block = (time tile, utterance). LDS: dz over [t0-P, t0+TT+P) and g over the same window
+// (plain copies of the global tensors), plus the weights. Writes dg = sum_j w[j]
+// dz[t-j+P] for the tile's frames, and this block's depthwise weight/bias gradient partial:
+// part[blk][c][j] = sum_t dz[t] g[t+j-P] over the tile's frames, part[blk][c][K] = sum dz.
+template <int KT>
+__global__ __launch_bounds__(kThreads) void cm_dw_bwd_kernel(
+    const float* __restrict__ dz, const float* __restrict__ g, const float* __restrict__ wdw,
+    int T, int C, int K, int TT, float* __restrict__ dg, float* __restrict__ wpart) {
+  extern __shared__ float sm[];
+  const int P = K / 2;
+  const int W = TT + K - 1;
+  float* dzs = sm;                 // [W][C], frame t0-P+i
+  float* gs = sm + (size_t)W * C;  // [W][C]
+  float* ws = gs + (size_t)W * C;  // [C][K]
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * TT;
+  const size_t rb = (size_t)b * T;
+  for (int i = threadIdx.x; i < C * K; i += kThreads) ws[i] = wdw[i];
+#pragma unroll 4
+  for (int i = threadIdx.x; i < W * C; i += kThreads) {
+    const int tl = i / C, c = i - tl * C;
+    const int t = t0 - P + tl;
+    const bool in = t >= 0 && t < T;
+    const size_t e = (rb + (in ? t : 0)) * C + c;
+    dzs[i] = in ? dz[e] : 0.0f;
+    gs[i] = in ? g[e] : 0.0f;
+  }
+  __syncthreads();
+  // dg[t] = sum_j w[j] dz[t - j + P] = sum_j' w[K-1-j'] dz-tile[tl + j'] (flipped weights)
+  if constexpr (KT > 0) {
+    const int nrb = (TT + kR - 1) / kR;
+    for (int it = threadIdx.x; it < C * nrb; it += kThreads) {
+      const int c = it % C, tl0 = kR * (it / C);
+      if (t0 + tl0 >= T) break;
+      float wt[KT], out[kR];
+#pragma unroll
+      for (int j = 0; j < KT; ++j) wt[j] = ws[c * KT + (KT - 1 - j)];
+      conv_window<KT, kR>(dzs, C, c, tl0, wt, out);
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int t = t0 + tl0 + r;
+        if (tl0 + r < TT && t < T) dg[(rb + t) * C + c] = out[r];
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < TT * C; i += kThreads) {
+      const int tl = i / C, c = i - tl * C;
+      const int t = t0 + tl;
+      if (t >= T) break;
+      const float* wc = ws + c * K;
+      float acc = 0.0f;  // dz index for tap j: frame t - j + P  ->  LDS row tl + 2P - j
+      for (int j = 0; j < K; ++j) acc = fmaf(wc[j], dzs[(tl + 2 * P - j) * C + c], acc);
+      dg[(rb + t) * C + c] = acc;
+    }
+  }
+  // weight-gradient partial over this tile's frames (frame t = t0 + tl, tl < n_t):
+  // item = (channel c, 8 consecutive taps j0..j0+7; tap K is the bias, g == 1)
+  const int n_t = min(TT, T - t0);
+  float* wp = wpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * C * (K + 1);
+  const int ngrp = (K + 1 + 7) / 8;
+  for (int it = threadIdx.x; it < C * ngrp; it += kThreads) {
+    const int c = it % C, j0 = 8 * (it / C);  // consecutive threads = consecutive channels
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
+    // sliding window of raw tile values gr[q] = g-tile[tl + j0 + q] (row clamped: rows past
+    // the window only meet taps j >= K), one new LDS read per frame; tap K (the bias) uses 1.
+    const int W = TT + K - 1;
+    float gr[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gr[q] = gs[min(j0 + q, W - 1) * C + c];
+    for (int tl = 0; tl < n_t; ++tl) {
+      const float d = dzs[(tl + P) * C + c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int j = j0 + q;
+        acc[q] = fmaf(d, j < K ? gr[q] : (j == K ? 1.0f : 0.0f), acc[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 7; ++q) gr[q] = gr[q + 1];
+      gr[7] = gs[min(tl + 1 + j0 + 7, W - 1) * C + c];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (j0 + q <= K) wp[(size_t)c * (K + 1) + j0 + q] = acc[q];
+  }
+}
+
+// GLU backward (conformer.py:156, g = a * sigmoid(b)): du = [dg * s, dg * a * s * (1 - s)].
+__global__ __launch_bounds__(kThreads) void cm_glu_bwd_kernel(const float* __restrict__ dg,
+                                                              const float* __restrict__ u, int C,
+                                                              int64_t total,
+                                                              float* __restrict__ du) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride) {
+    const int64_t row = i / C;
+    const int c = (int)(i - row * C);
+    const size_t ua = row * (size_t)(2 * C) + c;
+    const float a = u[ua];
+    const float sb = sigm(u[ua + C]);
+    const float d = dg[i];
+    du[ua] = d * sb;
+    du[ua + C] = d * a * sb * (1.0f - sb);
+  }
+}
+
+// dw_dw[c][j] = sum over blocks (fixed order) of the partials; db_dw[c] likewise.
+// One wave per output: lanes take blocks k = lane, lane + 64, ... (fp64 lane sums).
+__global__ __launch_bounds__(64) void cm_wgrad_final_kernel(const float* __restrict__ wpart,
+                                                            int nblk, int C, int K,
+                                                            float* __restrict__ dw,
+                                                            float* __restrict__ db) {
+  const int i = blockIdx.x;  // c * (K + 1) + j
+  const int c = i / (K + 1), j = i - c * (K + 1);
+  double acc = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 64) acc += wpart[(size_t)k * C * (K + 1) + i];
+  acc = wave_sum(acc);
+  if (threadIdx.x == 0) {
+    if (j < K) dw[(size_t)c * K + j] = (float)acc;
+    else if (db) db[c] = (float)acc;
+  }
+}
+
+int stats_chunks(int64_t rows_pp) { return (int)(rows_pp < 128 ? (rows_pp > 0 ? rows_pp : 1) : 128); }
+
+size_t lds_fwd(int C, int K, int TT) { return sizeof(float) * ((size_t)(TT + K - 1) * C + (size_t)C * K); }
+size_t lds_bwd(int C, int K, int TT) {
+  return sizeof(float) * (2 * (size_t)(TT + K - 1) * C + (size_t)C * K);
+}
+
+// Frames per depthwise block: the widest tile whose backward LDS image fits (0: none).
+int pick_tt(int64_t C, int64_t K) {
+  for (int tt : {64, 32, 16})
+    if (lds_bwd((int)C, (int)K, tt) <= kMaxLds) return tt;
+  return 0;
+}
+
+}  // namespace
+
+bool convmod_supported(int64_t C, int64_t K) {
+  return C >= 1 && K >= 1 && K % 2 == 1 && K <= 127 && pick_tt(C, K) > 0;
+}
+
+size_t convmod_workspace(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K) {
+  const int64_t rows_pp = Bt / P * T;
+  const int S = stats_chunks(rows_pp);
+  const int64_t ntt = ceil_div(T, pick_tt(C, K));
+  size_t b = sizeof(double) * (size_t)(P * S * C * 2);         // stats / bn partials
+  b += sizeof(float) * (size_t)(P * C * 2);                     // bn backward coefficients
+  b += sizeof(float) * (size_t)(Bt * ntt * C * (K + 1));        // weight-gradient partials
+  b += 2 * sizeof(float) * (size_t)(Bt * T * C);                 // dz, dg
+  return b + 256;
+}
+
+void launch_convmod_fwd(const float* u, const float* wdw, const float* bdw, const float* gamma,
+                        const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
+                        float eps, float* z, float* g, float* stats, float* v, void* ws,
+                        hipStream_t s) {
+  const int64_t rows_pp = Bt / P * T;
+  const int S = stats_chunks(rows_pp);
+  double* part = reinterpret_cast<double*>(ws);
+  const int TT = pick_tt(C, K);
+  const dim3 gdw((unsigned)ceil_div(T, TT), (unsigned)Bt);
+  if (K == 31)  // the Conformer width (reference default, every config here)
+    hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<31>, gdw, dim3(kThreads), lds_fwd((int)C, (int)K, TT),
+                       s, u, wdw, bdw, (int)T, (int)C, (int)K, TT, z, g);
+  else
+    hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<0>, gdw, dim3(kThreads), lds_fwd((int)C, (int)K, TT),
+                       s, u, wdw, bdw, (int)T, (int)C, (int)K, TT, z, g);
+  hipLaunchKernelGGL(cm_stats_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
+                     (const float*)z, rows_pp, (int)C, S, part);
+  hipLaunchKernelGGL(cm_stats_final_kernel, dim3((unsigned)(P * C)), dim3(64), 0, s,
+                     (const double*)part, (int)P, (int)C, S, rows_pp, eps, stats);
+  const int64_t total = Bt * T * C;
+  int64_t blocks = ceil_div(total, kThreads);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cm_bn_swish_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                     (const float*)z, (const float*)stats, gamma, beta, rows_pp, (int)C, total, v);
+}
+
+void launch_convmod_bwd(const float* dv, const float* u, const float* z, const float* g,
+                        const float* stats, const float* wdw, const float* gamma,
+                        const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
+                        float* du, float* dwdw, float* dbdw, float* dgamma, float* dbeta, void* ws,
+                        hipStream_t s) {
+  const int64_t rows_pp = Bt / P * T;
+  const int S = stats_chunks(rows_pp);
+  const int TT = pick_tt(C, K);
+  const int64_t ntt = ceil_div(T, TT);
+  double* part = reinterpret_cast<double*>(ws);
+  float* coef = reinterpret_cast<float*>(part + (size_t)(P * S * C * 2));
+  float* wpart = coef + (size_t)(P * C * 2);
+  float* dz = wpart + (size_t)(Bt * ntt * C * (K + 1));
+  float* dg = dz + (size_t)(Bt * T * C);
+  const int64_t total = Bt * T * C;
+  int64_t eblocks = ceil_div(total, kThreads);
+  if (eblocks > 8192) eblocks = 8192;
+  hipLaunchKernelGGL(cm_bn_bwd_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
+                     dv, z, stats, gamma, beta, rows_pp, (int)C, S, part);
+  hipLaunchKernelGGL(cm_bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, s,
+                     (const double*)part, (int)P, (int)C, S, rows_pp, coef, dgamma, dbeta);
+  hipLaunchKernelGGL(cm_dz_kernel, dim3((unsigned)eblocks), dim3(kThreads), 0, s, dv, z, stats,
+                     (const float*)coef, gamma, beta, rows_pp, (int)C, total, dz);
+  const dim3 gdw((unsigned)ntt, (unsigned)Bt);
+  if (K == 31)
+    hipLaunchKernelGGL(cm_dw_bwd_kernel<31>, gdw, dim3(kThreads), lds_bwd((int)C, (int)K, TT), s,
+                       (const float*)dz, g, wdw, (int)T, (int)C, (int)K, TT, dg, wpart);
+  else
+    hipLaunchKernelGGL(cm_dw_bwd_kernel<0>, gdw, dim3(kThreads), lds_bwd((int)C, (int)K, TT), s,
+                       (const float*)dz, g, wdw, (int)T, (int)C, (int)K, TT, dg, wpart);
+  hipLaunchKernelGGL(cm_glu_bwd_kernel, dim3((unsigned)eblocks), dim3(kThreads), 0, s,
+                     (const float*)dg, u, (int)C, total, du);
+  hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)(C * (K + 1))), dim3(64), 0, s,
+                     (const float*)wpart, (int)(Bt * ntt), (int)C, (int)K, dwdw, dbdw);
+}
+
+}  // namespace ob

@@ -46,6 +46,24 @@ __global__ __launch_bounds__(kThreads) void drop_scale_bwd_kernel(
     dy[i] = one(i, dout[i]);
 }
 
+__global__ __launch_bounds__(kThreads) void residual_drop_fwd_kernel(
+    const float* __restrict__ R, const float* __restrict__ Y, int64_t rows, int64_t N,
+    float rscale, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off,
+    const int* __restrict__ lens, int T, float* __restrict__ out) {
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
+  const int64_t total = rows * N;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride) {
+    float v = Y[i];
+    if (dc.on) v = __fmul_rn(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
+    if (lens) {
+      const int64_t row = i / N, b = row / T;
+      if (row - b * T >= lens[b]) v = __fmul_rn(v, 0.0f);
+    }
+    out[i] = __fadd_rn(R[i], rscale == 1.0f ? v : __fmul_rn(rscale, v));
+  }
+}
+
 }  // namespace
 
 void launch_drop_scale_bwd(const float* dout, int64_t rows, int64_t N, float rscale,
@@ -57,6 +75,17 @@ void launch_drop_scale_bwd(const float* dout, int64_t rows, int64_t N, float rsc
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(drop_scale_bwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, dout,
                      rows, N, rscale, make_drop(p_drop), rng, rng_off, lens, T > 0 ? T : 1, dy);
+}
+
+void launch_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int64_t N,
+                              float rscale, float p_drop, const uint64_t* rng, uint64_t rng_off,
+                              const int* lens, int T, float* out, hipStream_t s) {
+  const int64_t total = rows * N;
+  if (total == 0) return;
+  int64_t blocks = ceil_div(total, kThreads);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(residual_drop_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, R, Y,
+                     rows, N, rscale, make_drop(p_drop), rng, rng_off, lens, T > 0 ? T : 1, out);
 }
 
 }  // namespace ob

@@ -84,6 +84,24 @@ struct TgemmEpi {
   uint64_t rng_off;     // added to the counter (per call site)
 };
 
+// out = R + rscale * rowvalid * drop(Y) over [rows][N] (forward twin of drop_scale_bwd).
+void launch_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int64_t N,
+                              float rscale, float p_drop, const uint64_t* rng, uint64_t rng_off,
+                              const int* lens, int T, float* out, hipStream_t s);
+
+// convmod.hip (conv module core, channels-last; see the file header)
+bool convmod_supported(int64_t C, int64_t K);
+size_t convmod_workspace(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K);
+void launch_convmod_fwd(const float* u, const float* wdw, const float* bdw, const float* gamma,
+                        const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
+                        float eps, float* z, float* g, float* stats, float* v, void* ws,
+                        hipStream_t s);
+void launch_convmod_bwd(const float* dv, const float* u, const float* z, const float* g,
+                        const float* stats, const float* wdw, const float* gamma,
+                        const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
+                        float* du, float* dwdw, float* dbdw, float* dgamma, float* dbeta, void* ws,
+                        hipStream_t s);
+
 // dY = rscale * rowvalid * drop(dOut) over [rows][N] (the backward of kEpiResidual's
 // dropout / pad / scale, same keep mask).
 void launch_drop_scale_bwd(const float* dout, int64_t rows, int64_t N, float rscale,

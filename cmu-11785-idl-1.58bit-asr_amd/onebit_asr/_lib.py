@@ -47,6 +47,15 @@ SIGNATURES = {
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _i64, _c_f, _f32, _c_f, _i64,
                _c_f, _c_f]),
     "ob_drop_scale_bwd": (_int, [_c_f, _i64, _i64, _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f, _c_f]),
+    "ob_residual_drop_fwd": (
+        _int, [_c_f, _c_f, _i64, _i64, _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f, _c_f]),
+    "ob_convmod_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "ob_convmod_fwd": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32, _c_f, _c_f, _c_f,
+               _c_f, _c_f, _sz, _c_f]),
+    "ob_convmod_bwd": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _c_f,
+               _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_quant_dequant": (_int, [_c_f, _c_f, _int, _int, _i64, _c_f, _c_f]),
     "ob_quant_ste_bwd_workspace": (_sz, [_i64]),
     "ob_quant_ste_bwd": (_int, [_c_f, _c_f, _c_f, _int, _int, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),

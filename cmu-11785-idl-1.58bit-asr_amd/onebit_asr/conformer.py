@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .attention import fused_attention_supported, rel_pos_attention
-from .conv import depthwise_conv1d
+from .conv import conv_module_fused, conv_module_supported, depthwise_conv1d
 from .embedding import embedding
 from .fused import ffn_residual, fused_supported, linear_residual
 from .layernorm import layer_norm
@@ -243,6 +243,10 @@ class ConvModule(nn.Module):
         return y.view(b, passes, c, t).transpose(0, 1).reshape(pb, c, t)
 
     def forward(self, x, mask=None, passes: int = 1):
+        if mask is None and conv_module_supported(x, self):
+            # channels-last on the HIP kernels (conv.py / csrc/convmod.hip), same computation
+            p = self.dropout.p if self.training else 0.0
+            return conv_module_fused(x, self.ln(x), self, passes, p)
         h = self.glu(self.pw1(self.ln(x).transpose(1, 2)))
         h = self.pw2(swish(self._bn(depthwise_conv1d(h, self.dw), passes)))
         h = self.dropout(h).transpose(1, 2)

@@ -1,4 +1,10 @@
-"""Depthwise Conv1d of the conv module on the HIP kernel.
+"""The Conformer conv module on the HIP library.
+
+* ``conv_module_fused`` -- ConvModule.forward (conformer.py:139-167) channels-last: pw1 /
+  pw2 as GEMMs on [rows, C] (no [B,C,T] transposes), GLU + depthwise conv + per-pass
+  BatchNorm (batch statistics) + swish in csrc/convmod.hip (4 launches forward, 5
+  backward), dropout + residual in one kernel.
+* ``depthwise_conv1d`` -- the depthwise conv alone on [B, C, T] (the unfused path).
 
 Reference: onebit_asr/conformer.py:147 ``nn.Conv1d(C, C, k, padding=k//2, groups=C)``,
 full precision. The module keeps its ``nn.Conv1d`` (checkpoint keys ``...conv.dw.weight``
@@ -8,12 +14,15 @@ the reference behaviour of this full-precision op (it is not the BitLinear hot p
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["depthwise_conv1d"]
+__all__ = ["depthwise_conv1d", "conv_module_supported", "conv_module_fused"]
 
 
 class _DwConv1dFn(torch.autograd.Function):
@@ -59,3 +68,174 @@ def depthwise_conv1d(x: torch.Tensor, conv: nn.Conv1d) -> torch.Tensor:
     if not eligible:
         return conv(x)
     return _DwConv1dFn.apply(x, conv.weight, conv.bias)
+
+
+class _ConvCoreFn(torch.autograd.Function):
+    """GLU -> depthwise conv -> BatchNorm (batch statistics, per pass) -> swish on the
+    channels-last pw1 output (csrc/convmod.hip; conformer.py:156-159)."""
+
+    @staticmethod
+    def forward(ctx, u, wdw, bdw, gamma, beta, P, T, eps):
+        rows, c2 = u.shape
+        C = c2 // 2
+        K = wdw.shape[-1]
+        Bt = rows // T
+        lib = _lib.load()
+        z = torch.empty((rows, C), dtype=torch.float32, device=u.device)
+        g = torch.empty_like(z)
+        v = torch.empty_like(z)
+        stats = torch.empty((P, C, 2), dtype=torch.float32, device=u.device)
+        wsb = lib.ob_convmod_workspace(P, Bt, T, C, K)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=u.device)
+        w2 = wdw.detach().reshape(C, K).contiguous()
+        _lib.check(lib.ob_convmod_fwd(u.data_ptr(), w2.data_ptr(), _lib.ptr(bdw), gamma.data_ptr(),
+                                      beta.data_ptr(), P, Bt, T, C, K, eps, z.data_ptr(),
+                                      g.data_ptr(), stats.data_ptr(), v.data_ptr(), ws.data_ptr(), wsb,
+                                      _lib.stream_of(u)), "ob_convmod_fwd")
+        ctx.meta = (P, T, K, bdw is not None, wdw.shape)
+        ctx.save_for_backward(u, z, g, stats, w2, gamma, beta)
+        return v
+
+    @staticmethod
+    def backward(ctx, dv):
+        u, z, g, stats, w2, gamma, beta = ctx.saved_tensors
+        P, T, K, has_b, wshape = ctx.meta
+        dv = dv.contiguous()
+        rows, c2 = u.shape
+        C = c2 // 2
+        Bt = rows // T
+        lib = _lib.load()
+        du = torch.empty_like(u)
+        dw = torch.empty((C, K), dtype=torch.float32, device=u.device)
+        db = torch.empty((C,), dtype=torch.float32, device=u.device) if has_b else None
+        dg = torch.empty_like(gamma)
+        dbt = torch.empty_like(beta)
+        wsb = lib.ob_convmod_workspace(P, Bt, T, C, K)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=u.device)
+        _lib.check(lib.ob_convmod_bwd(dv.data_ptr(), u.data_ptr(), z.data_ptr(), g.data_ptr(),
+                                      stats.data_ptr(),
+                                      w2.data_ptr(), gamma.data_ptr(), beta.data_ptr(), P, Bt, T, C,
+                                      K, du.data_ptr(), dw.data_ptr(), _lib.ptr(db), dg.data_ptr(),
+                                      dbt.data_ptr(), ws.data_ptr(), wsb, _lib.stream_of(dv)),
+                   "ob_convmod_bwd")
+        return du, dw.reshape(wshape), db, dg, dbt, None, None, None
+
+
+class _ResidualDropFn(torch.autograd.Function):
+    """x + dropout(y) (conformer.py:160-167) with the fused kernels' hash mask."""
+
+    @staticmethod
+    def forward(ctx, x, y, p, rng, off):
+        x, y = x.contiguous(), y.contiguous()
+        out = torch.empty_like(y)
+        n = y.shape[-1]
+        rows = y.numel() // n
+        _lib.check(_lib.load().ob_residual_drop_fwd(x.data_ptr(), y.data_ptr(), rows, n, 1.0, p,
+                                                    _lib.ptr(rng), off, None, 0, out.data_ptr(),
+                                                    _lib.stream_of(y)), "ob_residual_drop_fwd")
+        ctx.meta = (p, rng, off)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p, rng, off = ctx.meta
+        g = g.contiguous()
+        n = g.shape[-1]
+        rows = g.numel() // n
+        gy = torch.empty_like(g)
+        _lib.check(_lib.load().ob_drop_scale_bwd(g.data_ptr(), rows, n, 1.0, p, _lib.ptr(rng), off,
+                                                 None, 0, gy.data_ptr(), _lib.stream_of(g)),
+                   "ob_drop_scale_bwd")
+        return g, gy, None, None, None
+
+
+class _BlasPref:
+    """Route the GEMMs issued inside the block to one BLAS library. For the conv module's
+    fp32 pointwise GEMMs ([B*T, C] x [C, 2C] and [B*T, C] x [C, C]) hipBLASLt's heuristic
+    picks 16x16x1 fp32 tiles; rocBLAS's 16x16x4 / 32x32x2 fp32 kernels are faster here
+    (tools/blas_pick.py: 118 vs 145 us backward at [23904, 144] x [144, 288])."""
+
+    def __init__(self, lib: str):
+        self.lib = lib
+
+    def __enter__(self):
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            self.prev = torch.backends.cuda.preferred_blas_library()
+            torch.backends.cuda.preferred_blas_library(self.lib)
+
+    def __exit__(self, *exc):
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            torch.backends.cuda.preferred_blas_library(self.prev)
+        return False
+
+
+_PW_BLAS = os.environ.get("OB_PW_BLAS", "cublas")  # "cublas" selects rocBLAS on ROCm
+
+
+class _PointwiseFn(torch.autograd.Function):
+    """A 1x1 Conv1d on channels-last rows: y = x W^T + b (conformer.py:143,147)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b):
+        with _BlasPref(_PW_BLAS):
+            y = torch.addmm(b, x2d, w.t()) if b is not None else x2d @ w.t()
+        ctx.save_for_backward(x2d, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, w = ctx.saved_tensors
+        gx = gw = gb = None
+        with _BlasPref(_PW_BLAS):
+            if ctx.needs_input_grad[0]:
+                gx = g @ w
+            if ctx.needs_input_grad[1]:
+                gw = g.t() @ x2d
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = g.sum(0)
+        return gx, gw, gb
+
+
+def _pointwise(x: torch.Tensor, conv: nn.Conv1d) -> torch.Tensor:
+    c_in = x.shape[-1]
+    y = _PointwiseFn.apply(x.reshape(-1, c_in), conv.weight.view(conv.out_channels, c_in),
+                           conv.bias)
+    return y.view(*x.shape[:-1], conv.out_channels)
+
+
+def conv_module_supported(x: torch.Tensor, module) -> bool:
+    """The channels-last fused conv module applies (HIP kernels, eligible shapes)."""
+    if os.environ.get("OB_FUSED", "1") == "0":
+        return False
+    dw, bn = module.dw, module.bn
+    kt = dw.kernel_size[0]
+    ok = (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3
+          and dw.groups == dw.in_channels == dw.out_channels == x.size(-1)
+          and kt % 2 == 1 and dw.padding[0] == kt // 2 and dw.stride[0] == 1
+          and dw.dilation[0] == 1 and bn.affine and not bn.track_running_stats
+          and module.pw1.kernel_size[0] == 1 and module.pw2.kernel_size[0] == 1)
+    if not ok:
+        return False
+    return _lib.load().ob_convmod_workspace(1, x.size(0), x.size(1), x.size(-1), kt) > 0
+
+
+def conv_module_fused(x: torch.Tensor, h: torch.Tensor, module, passes: int, p_drop: float):
+    """ConvModule.forward (conformer.py:149-167) on [Bt, T, C] without leaving channels-last:
+    pw1 / pw2 as GEMMs (bias in the GEMM epilogue), the GLU / depthwise / BatchNorm / swish
+    core in csrc/convmod.hip, dropout + residual in one kernel. ``h`` = LN(x)."""
+    from .fused import _rng
+
+    bt, t, c = x.shape
+    u = _pointwise(h, module.pw1)
+    v = _ConvCoreFn.apply(u.reshape(bt * t, 2 * c), module.dw.weight, module.dw.bias,
+                          module.bn.weight, module.bn.bias, passes, t, float(module.bn.eps))
+    o = _pointwise(v, module.pw2)
+    rng, off = _rng(x.device) if p_drop > 0 else (None, 0)
+    return _ResidualDropFn.apply(x, o.view(bt, t, c), float(p_drop), rng, off)

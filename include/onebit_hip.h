@@ -392,6 +392,41 @@ OB_API int ob_drop_scale_bwd(const float* dOut, int64_t rows, int64_t N, float r
                              float p_drop, const uint64_t* rng, int64_t rng_offset,
                              const int32_t* lens, int64_t T, float* dY, void* stream);
 
+/* out = R + rscale * rowvalid * dropout(Y) over [rows][N]: the residual/dropout tail of a
+ * call site whose producer is not a BitLinear GEMM (the conv module's pw2, conformer.py:
+ * 160-167), with the mask convention of the fused entries above. */
+OB_API int ob_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int64_t N,
+                                float rscale, float p_drop, const uint64_t* rng,
+                                int64_t rng_offset, const int32_t* lens, int64_t T, float* out,
+                                void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Conv module core (ConvModule, conformer.py:139-167; full precision), channels-last.
+ * Rows = Bt*T frames (utterance b = rows [b*T, (b+1)*T)), channel fastest; P stacked
+ * passes (Bt = P*B) keep per-pass BatchNorm statistics. pw1 / pw2 are plain GEMMs left to
+ * the caller; between them:
+ *   fwd: u [rows][2C] -> g = u[:, :C] * sigmoid(u[:, C:])      (GLU over channels, :156)
+ *        z = depthwise_K(g) + b_dw   (zero padding K/2 at utterance edges, :157)
+ *        stats[p][c] = {mean, rstd} of z over pass p's B*T frames (batch statistics,
+ *        padded frames included, biased variance, eps; :158)
+ *        v = swish(gamma * (z - mean) * rstd + beta)               (:159)
+ *        g [rows][C] (the GLU output) is kept for the backward.
+ *   bwd: from dv = dL/dv: du [rows][2C], dw_dw [C][K], db_dw [C], dgamma [C], dbeta [C]
+ *        (weight gradients summed over passes). u, z, g, stats are the forward's.
+ * K odd; ob_convmod_workspace() == 0 means the shape is not supported (C too wide for the
+ * LDS tile). Deterministic (fixed-order reductions, fp64 statistics).
+ * ------------------------------------------------------------------------------------ */
+OB_API size_t ob_convmod_workspace(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K);
+OB_API int ob_convmod_fwd(const float* u, const float* w_dw, const float* b_dw,
+                          const float* gamma, const float* beta, int64_t P, int64_t Bt,
+                          int64_t T, int64_t C, int64_t K, float eps, float* z, float* g,
+                          float* stats, float* v, void* ws, size_t ws_bytes, void* stream);
+OB_API int ob_convmod_bwd(const float* dv, const float* u, const float* z, const float* g,
+                          const float* stats, const float* w_dw, const float* gamma,
+                          const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C,
+                          int64_t K, float* du, float* dw_dw, float* db_dw, float* dgamma,
+                          float* dbeta, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
