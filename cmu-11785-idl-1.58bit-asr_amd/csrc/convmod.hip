@@ -55,10 +55,11 @@ constexpr int kR = 8;  // frames per register window
 // channels: coalesced global access, conflict-free LDS).
 // KT > 0: the kernel width as a compile-time constant (register windows); KT == 0: generic.
 template <int KT>
-__global__ __launch_bounds__(kThreads) void cm_glu_dw_fwd_kernel(
+__global__ __launch_bounds__(1024) void cm_glu_dw_fwd_kernel(
     const float* __restrict__ u, const float* __restrict__ wdw, const float* __restrict__ bdw,
     int T, int C, int K, int TT, float* __restrict__ z, float* __restrict__ gout) {
   extern __shared__ float sm[];
+  const int nth = blockDim.x;
   const int P = K / 2;
   const int W = TT + K - 1;
   float* gs = sm;                 // [W][C]
@@ -66,9 +67,9 @@ __global__ __launch_bounds__(kThreads) void cm_glu_dw_fwd_kernel(
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * TT;
   const size_t rb = (size_t)b * T;
-  for (int i = threadIdx.x; i < C * K; i += kThreads) ws[i] = wdw[i];
+  for (int i = threadIdx.x; i < C * K; i += nth) ws[i] = wdw[i];
 #pragma unroll 4
-  for (int i = threadIdx.x; i < W * C; i += kThreads) {
+  for (int i = threadIdx.x; i < W * C; i += nth) {
     const int tl = i / C, c = i - tl * C;
     const int t = t0 - P + tl;
     float g = 0.0f;
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(kThreads) void cm_glu_dw_fwd_kernel(
   __syncthreads();
   if constexpr (KT > 0) {
     const int nrb = (TT + kR - 1) / kR;
-    for (int it = threadIdx.x; it < C * nrb; it += kThreads) {
+    for (int it = threadIdx.x; it < C * nrb; it += nth) {
       const int c = it % C, tl0 = kR * (it / C);
       if (t0 + tl0 >= T) break;
       float wt[KT], out[kR];
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(kThreads) void cm_glu_dw_fwd_kernel(
       }
     }
   } else {
-    for (int i = threadIdx.x; i < TT * C; i += kThreads) {
+    for (int i = threadIdx.x; i < TT * C; i += nth) {
       const int tl = i / C, c = i - tl * C;
       const int t = t0 + tl;
       if (t >= T) break;  // i increases monotonically: later i are later frames
@@ -267,10 +268,11 @@ __global__ __launch_bounds__(kThreads) void cm_dz_kernel(
 // dz[t-j+P] for the tile's frames, and this block's depthwise weight/bias gradient partial:
 // part[blk][c][j] = sum_t dz[t] g[t+j-P] over the tile's frames, part[blk][c][K] = sum dz.
 template <int KT>
-__global__ __launch_bounds__(kThreads) void cm_dw_bwd_kernel(
+__global__ __launch_bounds__(1024) void cm_dw_bwd_kernel(
     const float* __restrict__ dz, const float* __restrict__ g, const float* __restrict__ wdw,
     int T, int C, int K, int TT, float* __restrict__ dg, float* __restrict__ wpart) {
   extern __shared__ float sm[];
+  const int nth = blockDim.x;
   const int P = K / 2;
   const int W = TT + K - 1;
   float* dzs = sm;                 // [W][C], frame t0-P+i
@@ -279,9 +281,9 @@ __global__ __launch_bounds__(kThreads) void cm_dw_bwd_kernel(
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * TT;
   const size_t rb = (size_t)b * T;
-  for (int i = threadIdx.x; i < C * K; i += kThreads) ws[i] = wdw[i];
+  for (int i = threadIdx.x; i < C * K; i += nth) ws[i] = wdw[i];
 #pragma unroll 4
-  for (int i = threadIdx.x; i < W * C; i += kThreads) {
+  for (int i = threadIdx.x; i < W * C; i += nth) {
     const int tl = i / C, c = i - tl * C;
     const int t = t0 - P + tl;
     const bool in = t >= 0 && t < T;
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void cm_dw_bwd_kernel(
   // dg[t] = sum_j w[j] dz[t - j + P] = sum_j' w[K-1-j'] dz-tile[tl + j'] (flipped weights)
   if constexpr (KT > 0) {
     const int nrb = (TT + kR - 1) / kR;
-    for (int it = threadIdx.x; it < C * nrb; it += kThreads) {
+    for (int it = threadIdx.x; it < C * nrb; it += nth) {
       const int c = it % C, tl0 = kR * (it / C);
       if (t0 + tl0 >= T) break;
       float wt[KT], out[kR];
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void cm_dw_bwd_kernel(
       }
     }
   } else {
-    for (int i = threadIdx.x; i < TT * C; i += kThreads) {
+    for (int i = threadIdx.x; i < TT * C; i += nth) {
       const int tl = i / C, c = i - tl * C;
       const int t = t0 + tl;
       if (t >= T) break;
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(kThreads) void cm_dw_bwd_kernel(
   const int n_t = min(TT, T - t0);
   float* wp = wpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * C * (K + 1);
   const int ngrp = (K + 1 + 7) / 8;
-  for (int it = threadIdx.x; it < C * ngrp; it += kThreads) {
+  for (int it = threadIdx.x; it < C * ngrp; it += nth) {
     const int c = it % C, j0 = 8 * (it / C);  // consecutive threads = consecutive channels
     float acc[8];
 #pragma unroll
@@ -401,6 +403,14 @@ int pick_tt(int64_t C, int64_t K) {
 
 }  // namespace
 
+// Threads of the depthwise blocks: one per (channel, 8-tap group) of the weight gradient
+// (576 = 9 waves at C = 144, K = 31), within [256, 1024].
+int dw_threads(int64_t C, int64_t K) {
+  int64_t n = C * ((K + 1 + 7) / 8);
+  n = (n + 63) / 64 * 64;
+  return (int)(n < 256 ? 256 : (n > 1024 ? 1024 : n));
+}
+
 bool convmod_supported(int64_t C, int64_t K) {
   return C >= 1 && K >= 1 && K % 2 == 1 && K <= 127 && pick_tt(C, K) > 0;
 }
@@ -426,10 +436,10 @@ void launch_convmod_fwd(const float* u, const float* wdw, const float* bdw, cons
   const int TT = pick_tt(C, K);
   const dim3 gdw((unsigned)ceil_div(T, TT), (unsigned)Bt);
   if (K == 31)  // the Conformer width (reference default, every config here)
-    hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<31>, gdw, dim3(kThreads), lds_fwd((int)C, (int)K, TT),
+    hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<31>, gdw, dim3(dw_threads(C, K)), lds_fwd((int)C, (int)K, TT),
                        s, u, wdw, bdw, (int)T, (int)C, (int)K, TT, z, g);
   else
-    hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<0>, gdw, dim3(kThreads), lds_fwd((int)C, (int)K, TT),
+    hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<0>, gdw, dim3(dw_threads(C, K)), lds_fwd((int)C, (int)K, TT),
                        s, u, wdw, bdw, (int)T, (int)C, (int)K, TT, z, g);
   hipLaunchKernelGGL(cm_stats_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
                      (const float*)z, rows_pp, (int)C, S, part);
@@ -467,10 +477,10 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
                      (const float*)coef, gamma, beta, rows_pp, (int)C, total, dz);
   const dim3 gdw((unsigned)ntt, (unsigned)Bt);
   if (K == 31)
-    hipLaunchKernelGGL(cm_dw_bwd_kernel<31>, gdw, dim3(kThreads), lds_bwd((int)C, (int)K, TT), s,
+    hipLaunchKernelGGL(cm_dw_bwd_kernel<31>, gdw, dim3(dw_threads(C, K)), lds_bwd((int)C, (int)K, TT), s,
                        (const float*)dz, g, wdw, (int)T, (int)C, (int)K, TT, dg, wpart);
   else
-    hipLaunchKernelGGL(cm_dw_bwd_kernel<0>, gdw, dim3(kThreads), lds_bwd((int)C, (int)K, TT), s,
+    hipLaunchKernelGGL(cm_dw_bwd_kernel<0>, gdw, dim3(dw_threads(C, K)), lds_bwd((int)C, (int)K, TT), s,
                        (const float*)dz, g, wdw, (int)T, (int)C, (int)K, TT, dg, wpart);
   hipLaunchKernelGGL(cm_glu_bwd_kernel, dim3((unsigned)eblocks), dim3(kThreads), 0, s,
                      (const float*)dg, u, (int)C, total, du);
