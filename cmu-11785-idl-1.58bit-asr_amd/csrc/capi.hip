@@ -563,7 +563,20 @@ int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma, const 
   if ((dgamma || dbeta) && !ws) return OB_ERR_NULL;
   if ((dgamma || dbeta) && ws_bytes < layernorm_bwd_workspace(rows, d)) return OB_ERR_WORKSPACE;
   if (!aligned4(dy) || !aligned4(x) || !aligned4(dx)) return OB_ERR_ALIGN;
-  launch_layernorm_bwd(dy, x, gamma, mean, rstd, rows, d, dx, dgamma, dbeta, ws,
+  launch_layernorm_bwd(dy, x, gamma, mean, rstd, rows, d, nullptr, dx, dgamma, dbeta, ws,
+                       as_stream(stream));
+  return launched();
+}
+
+int ob_layernorm_bwd_res(const float* dy, const float* x, const float* gamma, const float* mean,
+                         const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx,
+                         float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  if (rows < 0 || !layernorm_supported(d)) return OB_ERR_SHAPE;
+  if (rows > 0 && (!dy || !x || !mean || !rstd || !dx || !dres)) return OB_ERR_NULL;
+  if ((dgamma || dbeta) && !ws) return OB_ERR_NULL;
+  if ((dgamma || dbeta) && ws_bytes < layernorm_bwd_workspace(rows, d)) return OB_ERR_WORKSPACE;
+  if (!aligned4(dy) || !aligned4(x) || !aligned4(dx) || !aligned4(dres)) return OB_ERR_ALIGN;
+  launch_layernorm_bwd(dy, x, gamma, mean, rstd, rows, d, dres, dx, dgamma, dbeta, ws,
                        as_stream(stream));
   return launched();
 }

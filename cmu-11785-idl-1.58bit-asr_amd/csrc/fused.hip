@@ -7,6 +7,7 @@
 // the same (seed, counter). HBM-bound: one read, one write per element, dwordx4 when N % 4
 // == 0.
 #include "ob_drop.h"
+#include "ob_fp.h"
 #include "ob_launch.h"
 
 namespace ob {
@@ -26,12 +27,12 @@ __global__ __launch_bounds__(kThreads) void drop_scale_bwd_kernel(
   auto one = [&](int64_t i, float g) -> float {
     const int64_t row = i / N;
     float v = g;
-    if (dc.on) v = __fmul_rn(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
+    if (dc.on) v = nc_mul(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
     if (lens) {
       const int64_t b = row / T;
-      if (row - b * T >= lens[b]) v = __fmul_rn(v, 0.0f);
+      if (row - b * T >= lens[b]) v = nc_mul(v, 0.0f);
     }
-    return rscale == 1.0f ? v : __fmul_rn(rscale, v);
+    return rscale == 1.0f ? v : nc_mul(rscale, v);
   };
   for (int64_t q = blockIdx.x * (int64_t)kThreads + threadIdx.x; q < nvec; q += stride) {
     float4 g = reinterpret_cast<const float4*>(dout)[q];
@@ -55,12 +56,12 @@ __global__ __launch_bounds__(kThreads) void residual_drop_fwd_kernel(
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride) {
     float v = Y[i];
-    if (dc.on) v = __fmul_rn(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
+    if (dc.on) v = nc_mul(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
     if (lens) {
       const int64_t row = i / N, b = row / T;
-      if (row - b * T >= lens[b]) v = __fmul_rn(v, 0.0f);
+      if (row - b * T >= lens[b]) v = nc_mul(v, 0.0f);
     }
-    out[i] = __fadd_rn(R[i], rscale == 1.0f ? v : __fmul_rn(rscale, v));
+    out[i] = nc_add(R[i], rscale == 1.0f ? v : nc_mul(rscale, v));
   }
 }
 

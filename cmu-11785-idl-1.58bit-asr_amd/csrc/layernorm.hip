@@ -13,6 +13,7 @@
 //             partials, summed over blocks in fixed order by a second launch
 //             (deterministic, no atomics).
 // Numerics: var = mean((x - mean)^2) (biased, as torch), rstd = 1/sqrt(var + eps).
+#include "ob_fp.h"
 #include "ob_launch.h"
 
 namespace ob {
@@ -78,8 +79,8 @@ template <int NPL>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows, int d,
-    int rows_per_block, float* __restrict__ dx, float* __restrict__ part_g,
-    float* __restrict__ part_b) {
+    int rows_per_block, const float* __restrict__ dres, float* __restrict__ dx,
+    float* __restrict__ part_g, float* __restrict__ part_b) {
   __shared__ float red_g[kRowsPerBlock][kLanesPerRow * NPL];
   __shared__ float red_b[kRowsPerBlock][kLanesPerRow * NPL];
   const int j = threadIdx.x & (kLanesPerRow - 1);
@@ -99,8 +100,16 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const float mu = mean_in[row], rs = rstd_in[row];
     const float* xr = x + row * d;
     const float* gr = dy + row * d;
-    float xh[NPL], g[NPL];
+    float xh[NPL], g[NPL], res[NPL];
     float s1 = 0.0f, s2 = 0.0f;
+    const float* rr = dres ? dres + row * d : nullptr;
+    if (rr) {  // issued with x / dy, not after the row reductions (one latency, not two)
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        const int c = j + kLanesPerRow * i;
+        res[i] = c < d ? rr[c] : 0.0f;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
       const int c = j + kLanesPerRow * i;
@@ -119,7 +128,13 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
       const int c = j + kLanesPerRow * i;
-      if (c < d) dr[c] = rs * (g[i] - m1 - xh[i] * m2);
+      if (c < d) {
+        // explicit roundings: identical with and without dres (hipcc may contract the two
+        // loop versions differently otherwise)
+        const float v = nc_mul(rs, nc_sub(nc_sub(g[i], m1), nc_mul(xh[i], m2)));
+        // + the residual branch's gradient (the add autograd would do), not contracted
+        dr[c] = rr ? nc_add(v, res[i]) : v;
+      }
     }
   }
   if (!part_g) return;
@@ -225,8 +240,8 @@ void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta,
 }
 
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
-                          const float* rstd, int64_t rows, int64_t d, float* dx, float* dgamma,
-                          float* dbeta, void* ws, hipStream_t s) {
+                          const float* rstd, int64_t rows, int64_t d, const float* dres,
+                          float* dx, float* dgamma, float* dbeta, void* ws, hipStream_t s) {
   const int npl = (int)ceil_div(d, kLanesPerRow);
   float* part_g = static_cast<float*>(ws);
   int rpb = kRowsPerBlock;
@@ -236,7 +251,8 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
   if (rows > 0) {
 #define OB_LNB(N)                                                                           \
   hipLaunchKernelGGL((ln_bwd_kernel<N>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
-                     gamma, mean, rstd, rows, (int)d, rpb, dx, params ? part_g : nullptr,   \
+                     gamma, mean, rstd, rows, (int)d, rpb, dres, dx,                        \
+                     params ? part_g : nullptr,                                             \
                      part_b);
     OB_LN_NPL(OB_LNB)
 #undef OB_LNB

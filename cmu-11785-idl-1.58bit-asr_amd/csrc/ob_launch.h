@@ -145,7 +145,7 @@ size_t layernorm_bwd_workspace(int64_t rows, int64_t d);
 void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                           int64_t d, float eps, float* y, float* mean, float* rstd, hipStream_t s);
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
-                          const float* rstd, int64_t rows, int64_t d, float* dx, float* dgamma,
+                          const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx, float* dgamma,
                           float* dbeta, void* ws, hipStream_t s);
 
 // dwconv.hip (depthwise Conv1d of the conv module, odd kernel width, 'same' padding)

@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "ob_drop.h"
+#include "ob_fp.h"
 #include "ob_launch.h"
 #include "ob_quant.h"
 
@@ -84,11 +85,11 @@ struct EpiArgs {
 __device__ __forceinline__ float silu_f(float z) { return z / (1.0f + expf(-z)); }
 __device__ __forceinline__ float silu_bwd_f(float dy, float z) {
   const float s = 1.0f / (1.0f + expf(-z));
-  return __fmul_rn(__fmul_rn(dy, s), 1.0f + z * (1.0f - s));
+  return nc_mul(nc_mul(dy, s), 1.0f + z * (1.0f - s));
 }
 
 // Store y = a*acc + b through the fused epilogue. `c` is this element's output address,
-// grow its pass-inclusive row. Explicit _rn ops keep hipcc from contracting the unfused
+// grow its pass-inclusive row. Non-contracting ops (ob_fp.h) keep hipcc from contracting the unfused
 // reference sequence (y, then *scale, then +R) into an fma.
 template <int MODE>
 __device__ __forceinline__ void epi_store(const EpiArgs& ep, uint32_t dkey, float* c,
@@ -99,18 +100,18 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ep, uint32_t dkey, floa
   if constexpr (MODE == kEpiSwishDrop) {
     ep.C2[i] = y;
     const float sv = silu_f(y);
-    *c = ep.dc.on ? __fmul_rn(sv, keep) : sv;
+    *c = ep.dc.on ? nc_mul(sv, keep) : sv;
   } else if constexpr (MODE == kEpiResidual) {
     bool valid = true;
     if (ep.lens) {
       const int64_t b = grow / ep.T;
       valid = (grow - b * ep.T) < ep.lens[b];
     }
-    float v = ep.dc.on ? __fmul_rn(y, keep) : y;
-    v = valid ? v : __fmul_rn(v, 0.0f);
-    *c = __fadd_rn(rv, ep.rscale == 1.0f ? v : __fmul_rn(ep.rscale, v));
+    float v = ep.dc.on ? nc_mul(y, keep) : y;
+    v = valid ? v : nc_mul(v, 0.0f);
+    *c = nc_add(rv, ep.rscale == 1.0f ? v : nc_mul(ep.rscale, v));
   } else {  // kEpiSwishDropBwd
-    const float d = ep.dc.on ? __fmul_rn(y, keep) : y;
+    const float d = ep.dc.on ? nc_mul(y, keep) : y;
     *c = silu_bwd_f(d, rv);
   }
 }

@@ -87,6 +87,8 @@ SIGNATURES = {
     "ob_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
     "ob_layernorm_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_layernorm_bwd_res": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_act_absmax_workspace": (_sz, [_i64]),
     "ob_act_absmax": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _sz, _c_f]),
     "ob_act_dequant_i8": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _c_f]),

@@ -32,7 +32,7 @@ from .attention import fused_attention_supported, rel_pos_attention
 from .conv import conv_module_fused, conv_module_supported, depthwise_conv1d
 from .embedding import embedding
 from .fused import ffn_residual, fused_supported, linear_residual
-from .layernorm import layer_norm
+from .layernorm import layer_norm, layer_norm_fork
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
 __all__ = [
@@ -58,6 +58,10 @@ class LayerNorm(nn.Module):
     def forward(self, x):
         return layer_norm(x, self.ln.weight, self.ln.bias, self.ln.eps)
 
+    def fork(self, x):
+        """(LN(x), x) with the residual branch's gradient added in the LN backward."""
+        return layer_norm_fork(x, self.ln.weight, self.ln.bias, self.ln.eps)
+
 
 def _pad_rows(y: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
     # Zero padded frames: mask is the [B,T,T] attention mask, mask[:, :, 0] the frame mask.
@@ -80,7 +84,8 @@ class FeedForwardModule(nn.Module):
         if mask is None and fused_supported(x, self.lin1, self.lin2, bitwidth=bitwidth):
             # same computation, elementwise ops in the GEMM epilogues (onebit_asr/fused.py)
             p = self.dropout.p if self.training else 0.0
-            return ffn_residual(self.ln(x), x, self.lin1, self.lin2, bitwidth, p)
+            h, xr = self.ln.fork(x)
+            return ffn_residual(h, xr, self.lin1, self.lin2, bitwidth, p)
         h = self.lin1(self.ln(x), bitwidth)
         h = self.dropout(swish(h))
         h = self.dropout(self.lin2(h, bitwidth))
@@ -184,6 +189,10 @@ class MHSA(nn.Module):
     def forward(self, x, mask, bitwidth: int, pos_emb: torch.Tensor):
         bsz, tlen, width = x.shape
         assert width == self.d_model, f"Expected {self.d_model}, got {width}"
+        if fused_attention_supported(x, self.d_head) and fused_supported(x, self.out_proj,
+                                                                         bitwidth=bitwidth):
+            h, xr = self.ln.fork(x)
+            return self._fused(xr, h, mask, bitwidth, pos_emb)
         h = self.ln(x)
         if fused_attention_supported(h, self.d_head):
             return self._fused(x, h, mask, bitwidth, pos_emb)
@@ -246,7 +255,8 @@ class ConvModule(nn.Module):
         if mask is None and conv_module_supported(x, self):
             # channels-last on the HIP kernels (conv.py / csrc/convmod.hip), same computation
             p = self.dropout.p if self.training else 0.0
-            return conv_module_fused(x, self.ln(x), self, passes, p)
+            h, xr = self.ln.fork(x)
+            return conv_module_fused(xr, h, self, passes, p)
         h = self.glu(self.pw1(self.ln(x).transpose(1, 2)))
         h = self.pw2(swish(self._bn(depthwise_conv1d(h, self.dw), passes)))
         h = self.dropout(h).transpose(1, 2)

@@ -14,7 +14,7 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["layer_norm", "fused_layernorm_supported"]
+__all__ = ["layer_norm", "layer_norm_fork", "fused_layernorm_supported"]
 
 
 def fused_layernorm_supported(x: torch.Tensor, d: int) -> bool:
@@ -66,3 +66,47 @@ def layer_norm(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.Tensor
     if not fused_layernorm_supported(x, d):
         return F.layer_norm(x, (d,), weight, bias, eps)
     return _LayerNormFn.apply(x, weight, bias, eps)
+
+
+class _LayerNormForkFn(torch.autograd.Function):
+    """(LN(x), x) for a residual junction x -> (LN -> module) + x: the backward receives both
+    branches' gradients and forms dx = LN_backward(dy) + dres in the LN backward kernel,
+    instead of autograd's separate add over the [rows, d] tensor."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        y = _LayerNormFn.forward(ctx, x, weight, bias, eps)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gres):
+        if gres is None:
+            return _LayerNormFn.backward(ctx, gy)
+        x2, weight, mean, rstd = ctx.saved_tensors
+        rows, d = x2.shape
+        if gy is None:
+            return gres, None, None, None
+        g2 = gy.contiguous().view(rows, d)
+        r2 = gres.contiguous().view(rows, d)
+        dx = torch.empty_like(x2)
+        has_w, has_b = ctx.has
+        dw = torch.empty((d,), dtype=torch.float32, device=x2.device) if has_w and ctx.needs_input_grad[1] else None
+        db = torch.empty((d,), dtype=torch.float32, device=x2.device) if has_b and ctx.needs_input_grad[2] else None
+        lib = _lib.load()
+        wsb = lib.ob_layernorm_bwd_workspace(rows, d)
+        ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
+        _lib.check(lib.ob_layernorm_bwd_res(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
+                                            mean.data_ptr(), rstd.data_ptr(), rows, d,
+                                            r2.data_ptr(), dx.data_ptr(), _lib.ptr(dw),
+                                            _lib.ptr(db), ws.data_ptr(), wsb,
+                                            _lib.stream_of(g2)), "ob_layernorm_bwd_res")
+        return dx.view(gy.shape), dw, db, None
+
+
+def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):
+    """(LN(x), x_residual): use x_residual for the junction's skip connection so the
+    backward adds the two gradient branches inside the LN backward kernel."""
+    d = x.shape[-1]
+    if not fused_layernorm_supported(x, d) or not torch.is_grad_enabled() or not x.requires_grad:
+        return layer_norm(x, weight, bias, eps), x
+    return _LayerNormForkFn.apply(x, weight, bias, eps)

@@ -333,6 +333,13 @@ OB_API int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma,
                             const float* mean, const float* rstd, int64_t rows, int64_t d,
                             float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                             void* stream);
+/* ob_layernorm_bwd plus an additive gradient: dx = LN_backward(dy) + dres. At a residual
+ * junction x -> (LN -> module) + x (conformer.py:34-45, :105-138, :149-167) this is the
+ * sum autograd would form with a separate add kernel. */
+OB_API int ob_layernorm_bwd_res(const float* dy, const float* x, const float* gamma,
+                                const float* mean, const float* rstd, int64_t rows, int64_t d,
+                                const float* dres, float* dx, float* dgamma, float* dbeta,
+                                void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Batched greedy CTC decode (inference path). Replaces onebit_asr/metrics.py:51-60

@@ -178,3 +178,26 @@ def test_fused_entry_errors(gpu):
     # p_drop out of range and missing rng are rejected, nothing launched
     assert lib.ob_drop_scale_bwd(None, 0, 0, 1.0, 1.5, None, 0, None, 0, None, None) == -2
     assert lib.ob_drop_scale_bwd(16, 1, 4, 1.0, 0.1, None, 0, None, 0, 16, None) == -1
+
+
+def test_layer_norm_fork_gradient(gpu):
+    """(LN(x), x) fork: dx = LN_backward(dy) + d(residual), bit-identical to autograd's
+    separate add (the kernel adds the two rounded terms, as the add kernel does)."""
+    from onebit_asr.layernorm import layer_norm, layer_norm_fork
+
+    torch.manual_seed(9)
+    w = torch.randn(144, device=gpu, requires_grad=True)
+    b = torch.randn(144, device=gpu, requires_grad=True)
+    x = torch.randn(3, 77, 144, device=gpu, requires_grad=True)
+    gy = torch.randn(3, 77, 144, device=gpu)
+    gr = torch.randn(3, 77, 144, device=gpu)
+    y, xr = layer_norm_fork(x, w, b)
+    (y * gy + xr * gr).sum().backward()
+    got = (x.grad.clone(), w.grad.clone(), b.grad.clone())
+    for t in (x, w, b):
+        t.grad = None
+    y0 = layer_norm(x, w, b)
+    (y0 * gy + x * gr).sum().backward()
+    assert torch.equal(y, y0)
+    assert torch.equal(got[0], x.grad)
+    assert torch.equal(got[1], w.grad) and torch.equal(got[2], b.grad)
