@@ -346,6 +346,43 @@ int ob_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int64_t N
   return launched();
 }
 
+int ob_bias_relu_fwd(float* y, const float* bias, int64_t B, int64_t C, int64_t hw,
+                     void* stream) {
+  if (B < 0 || C < 0 || hw < 0) return OB_ERR_SHAPE;
+  if (B * C * hw > 0 && (!y || !bias)) return OB_ERR_NULL;
+  if (!aligned4(y) || !aligned4(bias)) return OB_ERR_ALIGN;
+  if (hw % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15)) return OB_ERR_ALIGN;
+  launch_bias_relu_fwd(y, bias, B, C, hw, as_stream(stream));
+  return launched();
+}
+
+size_t ob_relu_bias_bwd_workspace(int64_t B, int64_t C) {
+  return (B < 0 || C < 0) ? 0 : relu_bias_bwd_workspace(B, C);
+}
+
+int ob_relu_bias_bwd(const float* g, const float* y, int64_t B, int64_t C, int64_t hw,
+                     float* gout, float* dbias, void* ws, size_t ws_bytes, void* stream) {
+  if (B < 0 || C < 0 || hw < 0 || B * C > 0x7fffffff) return OB_ERR_SHAPE;
+  if (B * C * hw > 0 && (!g || !y || !gout)) return OB_ERR_NULL;
+  if (B * C > 0 && !ws) return OB_ERR_NULL;
+  if (ws_bytes < relu_bias_bwd_workspace(B, C)) return OB_ERR_WORKSPACE;
+  if (!aligned4(g) || !aligned4(y) || !aligned4(gout) || !aligned4(dbias)) return OB_ERR_ALIGN;
+  launch_relu_bias_bwd(g, y, B, C, hw, gout, dbias, ws, as_stream(stream));
+  return launched();
+}
+
+size_t ob_colsum_workspace(int64_t N) { return N < 0 ? 0 : colsum_workspace(N); }
+
+int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, size_t ws_bytes,
+              void* stream) {
+  if (rows < 0 || N < 0 || N > 0x7fffffff) return OB_ERR_SHAPE;
+  if (N > 0 && (!out || !ws || (rows > 0 && !x))) return OB_ERR_NULL;
+  if (ws_bytes < colsum_workspace(N)) return OB_ERR_WORKSPACE;
+  if (!aligned4(x) || !aligned4(out)) return OB_ERR_ALIGN;
+  launch_colsum(x, rows, N, out, ws, as_stream(stream));
+  return launched();
+}
+
 namespace {
 int convmod_check(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K) {
   if (P < 1 || Bt < 0 || T < 0 || C < 1 || K < 1 || Bt % P || Bt > 65535) return OB_ERR_SHAPE;

@@ -65,6 +65,93 @@ __global__ __launch_bounds__(kThreads) void residual_drop_fwd_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Conv2dSubsampling's `conv -> +bias -> ReLU` tails (conformer.py:183-186) on NCHW planes:
+// forward y = max(x + b[c], 0) in place; backward g' = g * (y > 0) and db[c] = sum over
+// the batch's planes of g' (per-plane partials, then a fixed-order sum over b). One pass
+// each instead of torch's add + clamp / threshold_backward + sum.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void bias_relu_fwd_kernel(float* __restrict__ y,
+                                                                 const float* __restrict__ bias,
+                                                                 int64_t planes, int C,
+                                                                 int64_t hw) {
+  const int64_t total = planes * hw;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  if (hw % 4 == 0) {
+    float4* y4 = reinterpret_cast<float4*>(y);
+    const int64_t hw4 = hw / 4;
+    for (int64_t q = blockIdx.x * (int64_t)kThreads + threadIdx.x; q < total / 4; q += stride) {
+      const float b = bias[(q / hw4) % C];
+      float4 v = y4[q];
+      v.x = fmaxf(v.x + b, 0.0f);
+      v.y = fmaxf(v.y + b, 0.0f);
+      v.z = fmaxf(v.z + b, 0.0f);
+      v.w = fmaxf(v.w + b, 0.0f);
+      y4[q] = v;
+    }
+    return;
+  }
+  for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride)
+    y[i] = fmaxf(y[i] + bias[(i / hw) % C], 0.0f);
+}
+
+// block = one (b, c) plane: g' = g * (y > 0) written to gout, plane sum -> part[plane].
+__global__ __launch_bounds__(kThreads) void relu_bias_bwd_kernel(
+    const float* __restrict__ g, const float* __restrict__ y, int64_t hw,
+    float* __restrict__ gout, float* __restrict__ part) {
+  __shared__ float red[kThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * hw;
+  float acc = 0.0f;
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) {
+    const float v = y[base + i] > 0.0f ? g[base + i] : 0.0f;
+    gout[base + i] = v;
+    acc += v;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// out[i] = sum over slices of part[slice * n + i] (fixed order): one wave per output, lanes
+// take slices lane, lane + 64, ..., then a fixed shuffle tree (a thread per output summing
+// 128 slices serially was latency-bound: 30 us).
+__global__ __launch_bounds__(64) void slice_sum_kernel(const float* __restrict__ part,
+                                                       int slices, int n,
+                                                       float* __restrict__ out) {
+  const int i = blockIdx.x;
+  float acc = 0.0f;
+  for (int sl = threadIdx.x; sl < slices; sl += 64) acc += part[(int64_t)sl * n + i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (threadIdx.x == 0) out[i] = acc;
+}
+
+// Column sums of a [rows][N] matrix (the bias gradient of a GEMM on rows): block = (row
+// slice, 64-column group); lane = column, waves split the slice's rows; fixed order.
+constexpr int kColSlices = 128;
+
+__global__ __launch_bounds__(kThreads) void colsum_part_kernel(const float* __restrict__ x,
+                                                               int64_t rows, int n,
+                                                               float* __restrict__ part) {
+  __shared__ float red[kThreads / 64][64];
+  const int col = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  const int64_t r0 = rows * blockIdx.x / kColSlices, r1 = rows * (blockIdx.x + 1) / kColSlices;
+  float acc = 0.0f;
+  if (col < n) {
+#pragma unroll 4
+    for (int64_t r = r0 + w; r < r1; r += kThreads / 64) acc += x[r * n + col];
+  }
+  red[w][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (w == 0 && col < n)
+    part[(int64_t)blockIdx.x * n + col] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
 }  // namespace
 
 void launch_drop_scale_bwd(const float* dout, int64_t rows, int64_t N, float rscale,
@@ -87,6 +174,40 @@ void launch_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int6
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(residual_drop_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, R, Y,
                      rows, N, rscale, make_drop(p_drop), rng, rng_off, lens, T > 0 ? T : 1, out);
+}
+
+void launch_bias_relu_fwd(float* y, const float* bias, int64_t B, int64_t C, int64_t hw,
+                          hipStream_t s) {
+  const int64_t total = B * C * hw;
+  if (total == 0) return;
+  int64_t blocks = ceil_div(hw % 4 == 0 ? total / 4 : total, kThreads);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(bias_relu_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, y, bias,
+                     B * C, (int)C, hw);
+}
+
+size_t relu_bias_bwd_workspace(int64_t B, int64_t C) { return sizeof(float) * (size_t)(B * C) + 256; }
+
+void launch_relu_bias_bwd(const float* g, const float* y, int64_t B, int64_t C, int64_t hw,
+                          float* gout, float* dbias, void* ws, hipStream_t s) {
+  if (B * C == 0) return;
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(relu_bias_bwd_kernel, dim3((unsigned)(B * C)), dim3(kThreads), 0, s, g, y,
+                     hw, gout, part);
+  if (dbias)
+    hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)C), dim3(64), 0, s, (const float*)part,
+                       (int)B, (int)C, dbias);
+}
+
+size_t colsum_workspace(int64_t N) { return sizeof(float) * (size_t)(kColSlices * N) + 256; }
+
+void launch_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, hipStream_t s) {
+  if (N == 0) return;
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(kColSlices, (unsigned)ceil_div(N, 64)),
+                     dim3(kThreads), 0, s, x, rows, (int)N, part);
+  hipLaunchKernelGGL(slice_sum_kernel, dim3((unsigned)N), dim3(64), 0, s, (const float*)part,
+                     kColSlices, (int)N, out);
 }
 
 }  // namespace ob

@@ -89,6 +89,17 @@ void launch_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int6
                               float rscale, float p_drop, const uint64_t* rng, uint64_t rng_off,
                               const int* lens, int T, float* out, hipStream_t s);
 
+// Subsampling conv tails (NCHW planes of hw elements): y = relu(y + b[c]) in place; and
+// g' = g * (y > 0), db[c] = sum over planes of channel c (ws: relu_bias_bwd_workspace).
+void launch_bias_relu_fwd(float* y, const float* bias, int64_t B, int64_t C, int64_t hw,
+                          hipStream_t s);
+size_t relu_bias_bwd_workspace(int64_t B, int64_t C);
+void launch_relu_bias_bwd(const float* g, const float* y, int64_t B, int64_t C, int64_t hw,
+                          float* gout, float* dbias, void* ws, hipStream_t s);
+// out[n] = sum over rows of x[rows][N] (fixed order; ws: colsum_workspace(N)).
+size_t colsum_workspace(int64_t N);
+void launch_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, hipStream_t s);
+
 // convmod.hip (conv module core, channels-last; see the file header)
 bool convmod_supported(int64_t C, int64_t K);
 size_t convmod_workspace(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K);

@@ -59,8 +59,11 @@ __global__ __launch_bounds__(kThreads) void quant_pack_kernel(
 
 // Grouped pack: every (layer, bitwidth) item of a model in ONE launch. Item i owns blocks
 // [block0_i, block0_{i+1}); a block finds its item by binary search over the (device)
-// table, then does exactly what quant_pack_kernel does for that item. At Conformer-S this
-// replaces 288 launch-bound 5 us packs per step with one launch.
+// table, then does what quant_pack_kernel does for kPackIters x 256 of the item's threads
+// (few blocks: the search's dependent loads are paid once per 4096 code slots). At
+// Conformer-S this replaces 288 launch-bound 5 us packs per step with one launch.
+constexpr int kPackIters = 16;  // 16-lane word groups per thread slot: blocks do 16x the work
+
 __global__ __launch_bounds__(kThreads) void quant_pack_group_kernel(
     const ob_pack_item* __restrict__ items, int n_items) {
   int lo = 0, hi = n_items - 1;
@@ -72,25 +75,28 @@ __global__ __launch_bounds__(kThreads) void quant_pack_group_kernel(
   const ob_pack_item it = items[lo];
   const float a = effective_alpha(it.alpha, it.alpha_raw);
   const int64_t N = it.N, K = it.K, KW = (K + 15) >> 4, NW = (N + 15) >> 4;
-  const int64_t t = (blk - it.block0) * kThreads + threadIdx.x;
   const int j = threadIdx.x & 15;
   const int64_t n_words = N * KW, n_words_t = K * NW;
-  const int64_t wi = t >> 4;
-  if (wi < n_words) {
-    const int64_t n = wi / KW, w = wi - n * KW;
-    const int64_t k = 16 * w + j;
-    const uint32_t c = (k < K) ? quant_code(it.W[n * K + k], a, it.bits) : 0u;
-    const uint32_t word = or16(c << (2 * j));
-    if (j == 0) it.codes[wi] = word;
-    return;
-  }
-  const int64_t wt = wi - n_words;
-  if (wt < n_words_t) {
-    const int64_t w = wt / K, k = wt - w * K;
-    const int64_t n = 16 * w + j;
-    const uint32_t c = (n < N) ? quant_code(it.W[n * K + k], a, it.bits) : 0u;
-    const uint32_t word = or16(c << (2 * j));
-    if (j == 0) it.codes_t[k * NW + w] = word;
+#pragma unroll 4
+  for (int i = 0; i < kPackIters; ++i) {
+    const int64_t t = ((blk - it.block0) * kPackIters + i) * kThreads + threadIdx.x;
+    const int64_t wi = t >> 4;
+    if (wi < n_words) {
+      const int64_t n = wi / KW, w = wi - n * KW;
+      const int64_t k = 16 * w + j;
+      const uint32_t c = (k < K) ? quant_code(it.W[n * K + k], a, it.bits) : 0u;
+      const uint32_t word = or16(c << (2 * j));
+      if (j == 0) it.codes[wi] = word;
+      continue;
+    }
+    const int64_t wt = wi - n_words;
+    if (wt < n_words_t) {
+      const int64_t w = wt / K, k = wt - w * K;
+      const int64_t n = 16 * w + j;
+      const uint32_t c = (n < N) ? quant_code(it.W[n * K + k], a, it.bits) : 0u;
+      const uint32_t word = or16(c << (2 * j));
+      if (j == 0) it.codes_t[k * NW + w] = word;
+    }
   }
 }
 
@@ -239,7 +245,7 @@ void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bi
 }
 
 int64_t quant_pack_item_blocks(int64_t N, int64_t K) {
-  return ceil_div(16 * (N * ceil_div(K, 16) + K * ceil_div(N, 16)), kThreads);
+  return ceil_div(16 * (N * ceil_div(K, 16) + K * ceil_div(N, 16)), (int64_t)kThreads * kPackIters);
 }
 
 void launch_quant_pack_group(const ob_pack_item* items_dev, int n_items, int64_t total_blocks,

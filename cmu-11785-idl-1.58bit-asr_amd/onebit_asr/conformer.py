@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .attention import fused_attention_supported, rel_pos_attention
-from .conv import conv_module_fused, conv_module_supported, depthwise_conv1d
+from .conv import conv2d_bias_relu, conv_module_fused, conv_module_supported, depthwise_conv1d
 from .embedding import embedding
 from .fused import ffn_residual, fused_supported, linear_residual
 from .layernorm import layer_norm, layer_norm_fork
@@ -287,7 +287,10 @@ class Conv2dSubsampling(nn.Module):
         self.out = nn.Linear(d_model * f_out, d_model)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = self.conv(x.unsqueeze(1))                      # [B, C, T', F']
+        if x.is_cuda and x.dtype == torch.float32:  # bias + ReLU fused (conv.py)
+            y = conv2d_bias_relu(conv2d_bias_relu(x.unsqueeze(1), self.conv[0]), self.conv[2])
+        else:
+            y = self.conv(x.unsqueeze(1))                  # [B, C, T', F']
         bsz, ch, tsub, fsub = y.shape
         y = y.transpose(1, 2).reshape(bsz, tsub, ch * fsub)  # channel-major per frame
         return self.out(y)

@@ -22,7 +22,8 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["depthwise_conv1d", "conv_module_supported", "conv_module_fused"]
+__all__ = ["depthwise_conv1d", "conv_module_supported", "conv_module_fused", "colsum",
+           "conv2d_bias_relu"]
 
 
 class _DwConv1dFn(torch.autograd.Function):
@@ -199,8 +200,58 @@ class _PointwiseFn(torch.autograd.Function):
             if ctx.needs_input_grad[1]:
                 gw = g.t() @ x2d
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = g.sum(0)
+            gb = colsum(g)
         return gx, gw, gb
+
+
+def colsum(x2d: torch.Tensor) -> torch.Tensor:
+    """Column sums of a [rows, N] fp32 matrix (fixed order; csrc/fused.hip)."""
+    x2d = x2d.contiguous()
+    rows, n = x2d.shape
+    out = torch.empty((n,), dtype=torch.float32, device=x2d.device)
+    lib = _lib.load()
+    wsb = lib.ob_colsum_workspace(n)
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=x2d.device)
+    _lib.check(lib.ob_colsum(x2d.data_ptr(), rows, n, out.data_ptr(), ws.data_ptr(), wsb,
+                             _lib.stream_of(x2d)), "ob_colsum")
+    return out
+
+
+class _BiasReluFn(torch.autograd.Function):
+    """relu(y + b[c]) on an NCHW conv output, in place (conformer.py:183-186: Conv2d's bias
+    and the ReLU after it); backward gives dy and db in one pass over the planes."""
+
+    @staticmethod
+    def forward(ctx, y, bias):
+        b, c, h, w = y.shape
+        _lib.check(_lib.load().ob_bias_relu_fwd(y.data_ptr(), bias.data_ptr(), b, c, h * w,
+                                                _lib.stream_of(y)), "ob_bias_relu_fwd")
+        ctx.mark_dirty(y)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        g = g.contiguous()
+        b, c, h, w = y.shape
+        gy = torch.empty_like(y)
+        db = torch.empty((c,), dtype=torch.float32, device=y.device)
+        lib = _lib.load()
+        wsb = lib.ob_relu_bias_bwd_workspace(b, c)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=y.device)
+        _lib.check(lib.ob_relu_bias_bwd(g.data_ptr(), y.data_ptr(), b, c, h * w, gy.data_ptr(),
+                                        db.data_ptr(), ws.data_ptr(), wsb, _lib.stream_of(g)),
+                   "ob_relu_bias_bwd")
+        return gy, db
+
+
+def conv2d_bias_relu(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """relu(conv(x)) with the bias add and the ReLU in one HIP pass each way."""
+    y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    if conv.bias is None:
+        return F.relu(y)
+    return _BiasReluFn.apply(y.contiguous(), conv.bias)
 
 
 def _pointwise(x: torch.Tensor, conv: nn.Conv1d) -> torch.Tensor:

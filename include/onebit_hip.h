@@ -407,6 +407,20 @@ OB_API int ob_residual_drop_fwd(const float* R, const float* Y, int64_t rows, in
                                 int64_t rng_offset, const int32_t* lens, int64_t T, float* out,
                                 void* stream);
 
+/* Conv2dSubsampling's conv -> +bias -> ReLU tails (conformer.py:183-186), NCHW planes of
+ * hw = H*W elements: fwd y = max(y + b[c], 0) in place; bwd g' = g * (y > 0) (torch's
+ * threshold_backward on the ReLU output) and db[c] = sum over (b, h, w) of g'. */
+OB_API int ob_bias_relu_fwd(float* y, const float* bias, int64_t B, int64_t C, int64_t hw,
+                            void* stream);
+OB_API size_t ob_relu_bias_bwd_workspace(int64_t B, int64_t C);
+OB_API int ob_relu_bias_bwd(const float* g, const float* y, int64_t B, int64_t C, int64_t hw,
+                            float* gout, float* dbias, void* ws, size_t ws_bytes, void* stream);
+/* out[n] = sum over rows of x[rows][N], fixed order: the bias gradient of a GEMM on rows
+ * (the conv module's pointwise convolutions, conformer.py:143,147). */
+OB_API size_t ob_colsum_workspace(int64_t N);
+OB_API int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws,
+                     size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Conv module core (ConvModule, conformer.py:139-167; full precision), channels-last.
  * Rows = Bt*T frames (utterance b = rows [b*T, (b+1)*T)), channel fastest; P stacked

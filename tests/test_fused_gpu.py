@@ -201,3 +201,30 @@ def test_layer_norm_fork_gradient(gpu):
     assert torch.equal(y, y0)
     assert torch.equal(got[0], x.grad)
     assert torch.equal(got[1], w.grad) and torch.equal(got[2], b.grad)
+
+
+def test_subsampling_bias_relu_and_colsum(gpu):
+    """conv2d_bias_relu == relu(conv2d(x, w, b)) bit for bit, gradients included; colsum ==
+    torch's column sum within fp32 summation order."""
+    import torch.nn as nn
+    from onebit_asr.conv import colsum, conv2d_bias_relu
+
+    torch.manual_seed(12)
+    conv = nn.Conv2d(3, 8, kernel_size=3, stride=2).to(gpu)
+    x = torch.randn(2, 3, 37, 21, device=gpu, requires_grad=True)
+    y = conv2d_bias_relu(x, conv)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    got = (x.grad.clone(), conv.weight.grad.clone(), conv.bias.grad.clone())
+    x.grad = None
+    conv.weight.grad = None
+    conv.bias.grad = None
+    y0 = torch.relu(conv(x))
+    (y0 * g).sum().backward()
+    assert torch.equal(y, y0)
+    assert torch.equal(got[0], x.grad)
+    # the weight gradient is MIOpen's (it may pick another algorithm for a bias-free conv)
+    assert _rel(got[1], conv.weight.grad) <= 1e-5
+    assert _rel(got[2], conv.bias.grad) <= 1e-6
+    m = torch.randn(1000, 77, device=gpu)
+    assert _rel(colsum(m), m.double().sum(0)) <= 1e-6
