@@ -439,7 +439,11 @@ DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
     const int64_t tiles = p.tiles_n * p.tiles_k;
     // Chunk = 4 waves x S steps x 32 rows, S in {2, 4, 8}: the longest chunk that still
     // gives >= 256 blocks (one per CU), so the partial slabs stay few.
-    int64_t steps = 8;
+    static const int64_t max_steps = [] {  // OB_DW_MAXSTEPS: tuning experiments
+      const char* e = getenv("OB_DW_MAXSTEPS");
+      return (int64_t)(e ? atoi(e) : 8);
+    }();
+    int64_t steps = max_steps;
     while (steps > 2 && tiles * ceil_div(M, 128 * steps) < 256) steps /= 2;
     p.rows_per_chunk = 128 * steps;
   }
@@ -468,7 +472,8 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
                      (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db, ticket)
   if (p.variant != 0) {
     const int64_t steps = p.rows_per_chunk / 128;
-    if (steps == 8) OB_DW6(8);
+    if (steps == 16) OB_DW6(16);
+    else if (steps == 8) OB_DW6(8);
     else if (steps == 4) OB_DW6(4);
     else OB_DW6(2);
     return;

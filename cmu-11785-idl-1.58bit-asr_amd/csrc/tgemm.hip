@@ -287,20 +287,29 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     // main loop, where they would hold NT*4 VGPRs across it
     __builtin_amdgcn_sched_barrier(0);
     // epilogue operand: all NT*4 loads issued before any is used (one latency, not 4*NT)
+    // epilogue operand (residual / pre-activation): rolling prefetch kPre tiles ahead, so at
+    // most (kPre + 1) * 4 values are live (all NT * 4 at once spilled at NT = 12)
+    constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
+    constexpr int kPre = 2;
     float rv[NT][4];
-    if constexpr (EPI == kEpiResidual || EPI == kEpiSwishDropBwd) {
+    auto load_r = [&](int t) {
+      const int col = min(n0 + 16 * t + r, N - 1);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int col = min(n0 + 16 * t + r, N - 1);
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int64_t orow = min(m0 + 4 * g + reg, M - 1);
-          rv[t][reg] = ep.R[(rowbase + orow) * N + col];
-        }
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t orow = min(m0 + 4 * g + reg, M - 1);
+        rv[t][reg] = ep.R[(rowbase + orow) * N + col];
       }
+    };
+    if constexpr (kHasR) {
+#pragma unroll
+      for (int t = 0; t < kPre && t < NT; ++t) load_r(t);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      if constexpr (kHasR) {
+        if (t + kPre < NT) load_r(t + kPre);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       const int col = n0 + 16 * t + r;
       if (col >= N) continue;
 #pragma unroll
@@ -493,20 +502,29 @@ __global__ __launch_bounds__(kThreads, 1) void tgemm_lds_kernel(
     }
 
     __builtin_amdgcn_sched_barrier(0);
+    // epilogue operand (residual / pre-activation): rolling prefetch kPre tiles ahead, so at
+    // most (kPre + 1) * 4 values are live (all NT * 4 at once spilled at NT = 12)
+    constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
+    constexpr int kPre = 2;
     float rv[NT][4];
-    if constexpr (EPI == kEpiResidual || EPI == kEpiSwishDropBwd) {
+    auto load_r = [&](int t) {
+      const int col = min(n0 + 16 * t + r, N - 1);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int col = min(n0 + 16 * t + r, N - 1);
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int64_t orow = min(m0 + 4 * g + reg, M - 1);
-          rv[t][reg] = ep.R[(rowbase + orow) * N + col];
-        }
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t orow = min(m0 + 4 * g + reg, M - 1);
+        rv[t][reg] = ep.R[(rowbase + orow) * N + col];
       }
+    };
+    if constexpr (kHasR) {
+#pragma unroll
+      for (int t = 0; t < kPre && t < NT; ++t) load_r(t);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      if constexpr (kHasR) {
+        if (t + kPre < NT) load_r(t + kPre);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       const int col = n0 + 16 * t + r;
       if (col >= N) continue;
 #pragma unroll
@@ -610,16 +628,24 @@ size_t bimg_bytes(int nt, int64_t K) {
 
 // Widest column tile whose bf16 image fits the LDS budget, preferring tiles that divide N.
 // OB_TGEMM_NTMAX (tuning experiments) caps the width.
-// The swish epilogues (exp + divide per element) cap the width at 4: wider tiles spill
-// (hipcc interleaves the NT*4 element sequences; measured with -Rpass-analysis).
+// Fused epilogues: widths whose instantiation spills are excluded (hipcc's allocation of
+// the exp/div epilogues is erratic in NT; checked with -Rpass-analysis=kernel-resource-usage):
+// swish fwd <= 4 (NT 12 compiles spill-free but measured 49 vs 44 us at lin1), swish bwd
+// {6, <=4}, residual any at K <= 160; all <= 4 beyond.
+bool epi_nt_ok(int nt, int64_t K, int epi_mode) {
+  if (epi_mode == kEpiNone) return true;
+  if (K > 160) return nt <= 4;
+  if (epi_mode == kEpiSwishDrop) return nt <= 4;
+  if (epi_mode == kEpiSwishDropBwd) return nt == 6 || nt <= 4;
+  return true;
+}
+
 int pick_nt(int64_t N, int64_t K, int epi_mode) {
   static const int env_cap = [] {
     const char* e = getenv("OB_TGEMM_NTMAX");
     return e ? atoi(e) : 12;
   }();
-  const int cap =
-      (epi_mode == kEpiSwishDrop || epi_mode == kEpiSwishDropBwd) ? (env_cap < 4 ? env_cap : 4)
-                                                                    : env_cap;
+  const int cap = env_cap;
   static const int cands_all[] = {12, 9, 6, 4, 3, 2, 1};
   int cands[7];
   int nc = 0;
@@ -627,9 +653,12 @@ int pick_nt(int64_t N, int64_t K, int epi_mode) {
     if (c <= cap) cands[nc++] = c;
   for (int i = nc; i < 7; ++i) cands[i] = 1;
   for (int nt : cands)
-    if (N % (16 * nt) == 0 && bimg_bytes(nt, K) <= kMaxLds) return nt;
+    if (epi_nt_ok(nt, K, epi_mode) && N % (16 * nt) == 0 && bimg_bytes(nt, K) <= kMaxLds)
+      return nt;
   for (int nt : cands)
-    if (16 * nt <= ((N + 15) & ~int64_t(15)) && bimg_bytes(nt, K) <= kMaxLds) return nt;
+    if (epi_nt_ok(nt, K, epi_mode) && 16 * nt <= ((N + 15) & ~int64_t(15)) &&
+        bimg_bytes(nt, K) <= kMaxLds)
+      return nt;
   return 0;
 }
 
@@ -656,13 +685,9 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
                      codes1, pass_bits, ep)
 #define OB_TGEMM(NCH)                                                   \
   switch (ep.mode) {                                                    \
-    case kEpiSwishDrop: /* pick_nt caps these at NT = 4 */            \
-      if constexpr (NT <= 4) OB_TGEMM_E(NCH, kEpiSwishDrop);            \
-      break;                                                            \
+    case kEpiSwishDrop: OB_TGEMM_E(NCH, kEpiSwishDrop); break;          \
     case kEpiResidual: OB_TGEMM_E(NCH, kEpiResidual); break;            \
-    case kEpiSwishDropBwd:                                              \
-      if constexpr (NT <= 4) OB_TGEMM_E(NCH, kEpiSwishDropBwd);         \
-      break;                                                            \
+    case kEpiSwishDropBwd: OB_TGEMM_E(NCH, kEpiSwishDropBwd); break;    \
     default: OB_TGEMM_E(NCH, kEpiNone); break;                          \
   }
   switch ((K + 31) / 32) {  // Conformer widths: 64, 144, 256, 576
