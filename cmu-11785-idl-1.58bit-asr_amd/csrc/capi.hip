@@ -546,7 +546,22 @@ int ob_ctc_loss_fwd(const float* log_probs, const int64_t* targets, const int64_
   if (!log_probs || !input_lengths || !target_lengths || !loss || !ws || (S > 0 && !targets))
     return OB_ERR_NULL;
   if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
-  launch_ctc_fwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, loss,
+  launch_ctc_fwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, 1, loss,
+                 static_cast<float*>(ws), as_stream(stream));
+  return launched();
+}
+
+int ob_ctc_loss_fwd_groups(const float* log_probs, const int64_t* targets,
+                           const int64_t* input_lengths, const int64_t* target_lengths, int64_t G,
+                           int64_t B, int64_t T, int64_t V, int64_t S, int blank, float* loss,
+                           void* ws, size_t ws_bytes, void* stream) {
+  if (G < 1 || G > 64 || B < 1 || B % G || T < 0 || V < 1 || S < 0 || blank < 0 || blank >= V ||
+      !ctc_supported(S))
+    return OB_ERR_SHAPE;
+  if (!log_probs || !input_lengths || !target_lengths || !loss || !ws || (S > 0 && !targets))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
+  launch_ctc_fwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, G, loss,
                  static_cast<float*>(ws), as_stream(stream));
   return launched();
 }
@@ -560,8 +575,24 @@ int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets, const int64_
   if (!log_probs || !input_lengths || !target_lengths || !grad || !ws || (S > 0 && !targets))
     return OB_ERR_NULL;
   if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
-  launch_ctc_bwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, grad_out,
-                 grad, static_cast<float*>(ws), as_stream(stream));
+  launch_ctc_bwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, 1,
+                 grad_out, grad, static_cast<float*>(ws), as_stream(stream));
+  return launched();
+}
+
+int ob_ctc_loss_bwd_groups(const float* log_probs, const int64_t* targets,
+                           const int64_t* input_lengths, const int64_t* target_lengths, int64_t G,
+                           int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                           const float* grad_out, float* grad, void* ws, size_t ws_bytes,
+                           void* stream) {
+  if (G < 1 || G > 64 || B < 1 || B % G || T < 0 || V < 1 || S < 0 || blank < 0 || blank >= V ||
+      !ctc_supported(S))
+    return OB_ERR_SHAPE;
+  if (!log_probs || !input_lengths || !target_lengths || !grad || !ws || (S > 0 && !targets))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_ctc_loss_workspace(B, T, S)) return OB_ERR_WORKSPACE;
+  launch_ctc_bwd(log_probs, targets, input_lengths, target_lengths, B, T, V, S, blank, G,
+                 grad_out, grad, static_cast<float*>(ws), as_stream(stream));
   return launched();
 }
 

@@ -126,19 +126,24 @@ __global__ __launch_bounds__(kThreads) void ctc_beta_kernel(
 }
 
 // Per-sample loss and gradient scale: 'mean' = mean_b(nll_b / max(L_b, 1)); zero_infinity.
+// G groups of B/G consecutive samples (the stacked passes of a training step, each the
+// reference's own ctc_loss_from_logits call): loss[g], scale from grad_out[g]. Thread g
+// sums its group in sample order (deterministic).
 __global__ void ctc_reduce_kernel(const float* __restrict__ nll, const int64_t* __restrict__ tg_len,
-                                  int B, const float* __restrict__ grad_out, float* __restrict__ loss,
-                                  float* __restrict__ scale) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+                                  int B, int G, const float* __restrict__ grad_out,
+                                  float* __restrict__ loss, float* __restrict__ scale) {
+  const int g = threadIdx.x;
+  if (blockIdx.x != 0 || g >= G) return;
+  const int Bg = B / G;
   float s = 0.0f;
-  for (int b = 0; b < B; ++b) {
+  for (int b = g * Bg; b < (g + 1) * Bg; ++b) {
     const float n = nll[b];
     const float L = (float)(tg_len[b] > 1 ? tg_len[b] : 1);
     const bool inf = isinf(n);
     s += inf ? 0.0f : n / L;
-    if (scale) scale[b] = inf ? 0.0f : (grad_out ? grad_out[0] : 1.0f) / (L * (float)B);
+    if (scale) scale[b] = inf ? 0.0f : (grad_out ? grad_out[g] : 1.0f) / (L * (float)Bg);
   }
-  if (loss) loss[0] = s / (float)B;
+  if (loss) loss[g] = s / (float)Bg;
 }
 
 // grad[b][t][v] = exp(lp) * scale_b for t < T_b, else 0 (labels are fixed up afterwards).
@@ -198,18 +203,18 @@ bool ctc_supported(int64_t S) { return 2 * S + 1 <= kMaxStates; }
 
 void launch_ctc_fwd(const float* lp, const int64_t* targets, const int64_t* in_len,
                     const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
-                    float* loss, float* ws, hipStream_t s) {
+                    int64_t G, float* loss, float* ws, hipStream_t s) {
   float* alpha = ws;
   float* nll = ws + 2 * B * T * (2 * S + 1);
   hipLaunchKernelGGL(ctc_alpha_kernel, dim3((unsigned)B), dim3(kThreads), 0, s, lp, targets,
                      in_len, tg_len, (int)T, (int)V, (int)S, blank, alpha, nll);
-  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(64), 0, s, nll, tg_len, (int)B,
+  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(64), 0, s, nll, tg_len, (int)B, (int)G,
                      (const float*)nullptr, loss, (float*)nullptr);
 }
 
 void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_len,
                     const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
-                    const float* grad_out, float* grad, float* ws, hipStream_t s) {
+                    int64_t G, const float* grad_out, float* grad, float* ws, hipStream_t s) {
   const int64_t SS = 2 * S + 1;
   float* alpha = ws;
   float* beta = ws + B * T * SS;
@@ -217,8 +222,8 @@ void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_l
   float* scale = nll + B;
   hipLaunchKernelGGL(ctc_beta_kernel, dim3((unsigned)B), dim3(kThreads), 0, s, lp, targets,
                      in_len, tg_len, (int)T, (int)V, (int)S, blank, beta);
-  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(64), 0, s, nll, tg_len, (int)B, grad_out,
-                     (float*)nullptr, scale);
+  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(64), 0, s, nll, tg_len, (int)B, (int)G,
+                     grad_out, (float*)nullptr, scale);
   hipLaunchKernelGGL(ctc_grad_dense_kernel, dim3((unsigned)(B * T)), dim3(kThreads), 0, s, lp,
                      in_len, scale, (int)T, (int)V, grad);
   hipLaunchKernelGGL(ctc_grad_fixup_kernel, dim3((unsigned)(B * T)), dim3(kThreads), 0, s, lp,

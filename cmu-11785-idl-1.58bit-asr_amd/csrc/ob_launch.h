@@ -172,10 +172,10 @@ void launch_dwconv_bwd(const float* x, const float* dy, const float* w, int64_t 
 size_t ctc_workspace(int64_t B, int64_t T, int64_t S);
 bool ctc_supported(int64_t S);
 void launch_ctc_fwd(const float* lp, const int64_t* targets, const int64_t* in_len,
-                    const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                    const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank, int64_t G,
                     float* loss, float* ws, hipStream_t s);
 void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_len,
-                    const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                    const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank, int64_t G,
                     const float* grad_out, float* grad, float* ws, hipStream_t s);
 
 // adamw.hip (clip_grad_norm_ + AdamW over a tensor table; layout = ob_adamw_tensor)

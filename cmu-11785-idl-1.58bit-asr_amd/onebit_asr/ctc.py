@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["ctc_loss_mean"]
+__all__ = ["ctc_loss_mean", "ctc_loss_mean_groups"]
 
 
 class _CTCFn(torch.autograd.Function):
@@ -52,3 +52,50 @@ class _CTCFn(torch.autograd.Function):
 
 def ctc_loss_mean(log_probs_btv, targets, input_lengths, target_lengths, blank: int):
     return _CTCFn.apply(log_probs_btv, targets, input_lengths, target_lengths, blank)
+
+
+class _CTCGroupsFn(torch.autograd.Function):
+    """G groups of B/G utterances in one launch per direction: losses [G]."""
+
+    @staticmethod
+    def forward(ctx, log_probs, targets, input_lengths, target_lengths, blank, groups):
+        b, t, v = log_probs.shape
+        s = targets.shape[1]
+        lp = log_probs.contiguous()
+        tg = targets.contiguous().to(torch.int64)
+        il = input_lengths.contiguous().to(torch.int64)
+        tl = target_lengths.contiguous().to(torch.int64)
+        lib = _lib.load()
+        wsb = lib.ob_ctc_loss_workspace(b, t, s)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=lp.device)
+        loss = torch.empty((groups,), dtype=torch.float32, device=lp.device)
+        _lib.check(lib.ob_ctc_loss_fwd_groups(lp.data_ptr(), tg.data_ptr(), il.data_ptr(),
+                                              tl.data_ptr(), groups, b, t, v, s, blank,
+                                              loss.data_ptr(), ws.data_ptr(), wsb,
+                                              _lib.stream_of(lp)), "ob_ctc_loss_fwd_groups")
+        ctx.save_for_backward(lp, tg, il, tl, ws)
+        ctx.meta = (blank, groups)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        lp, tg, il, tl, ws = ctx.saved_tensors
+        blank, groups = ctx.meta
+        b, t, v = lp.shape
+        s = tg.shape[1]
+        grad = torch.empty_like(lp)
+        gout = gout.contiguous().to(torch.float32)
+        lib = _lib.load()
+        _lib.check(lib.ob_ctc_loss_bwd_groups(lp.data_ptr(), tg.data_ptr(), il.data_ptr(),
+                                              tl.data_ptr(), groups, b, t, v, s, blank,
+                                              gout.data_ptr(), grad.data_ptr(), ws.data_ptr(),
+                                              ws.numel(), _lib.stream_of(lp)),
+                   "ob_ctc_loss_bwd_groups")
+        return grad, None, None, None, None, None
+
+
+def ctc_loss_mean_groups(log_probs_btv, targets, input_lengths, target_lengths, blank: int,
+                         groups: int):
+    """ctc_loss_mean of each of ``groups`` consecutive equal slices of the batch, one launch:
+    returns the [groups] losses (the stacked passes' CTC terms)."""
+    return _CTCGroupsFn.apply(log_probs_btv, targets, input_lengths, target_lengths, blank, groups)

@@ -150,7 +150,7 @@ class OneBitStep(nn.Module):
 
 
     def _forward_stacked(self, batch, bits):
-        from .ctc import ctc_loss_mean
+        from .ctc import ctc_loss_mean_groups
 
         from .fused import advance_step
         from .quant import PackGroup
@@ -185,10 +185,9 @@ class OneBitStep(nn.Module):
         # CTC per pass (losses.py:41-47)
         ctc_lp = F.log_softmax(ctc, dim=-1)
         in_lens = mask.sum(dim=1).long()
-        l_ctc = torch.stack([
-            ctc_loss_mean(ctc_lp[p * bsz:(p + 1) * bsz], batch["tokens"],
-                          in_lens[p * bsz:(p + 1) * bsz], batch["token_lens"], sp["blank_id"])
-            for p in range(P)])
+        # the P passes' CTC losses in one launch per direction (each pass its own mean)
+        l_ctc = ctc_loss_mean_groups(ctc_lp, batch["tokens"].repeat(P, 1), in_lens,
+                                     batch["token_lens"].repeat(P), sp["blank_id"], P)
         l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
         # KL(teacher || student) for the student and SP passes (losses.py:50-59)
         with torch.no_grad():  # softmax of the detached teacher logits (train.py:101)

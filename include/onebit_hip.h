@@ -183,6 +183,19 @@ OB_API int ob_ctc_loss_bwd(const float* log_probs, const int64_t* targets,
                            const int64_t* input_lengths, const int64_t* target_lengths, int64_t B,
                            int64_t T, int64_t V, int64_t S, int blank, const float* grad_out,
                            float* grad, void* ws, size_t ws_bytes, void* stream);
+/* The same over G groups of B/G consecutive utterances in ONE launch (the three stacked
+ * passes of a training step, each the reference's own ctc_loss_from_logits call,
+ * losses.py:41-47): loss[g] is group g's 'mean' loss, grad_out[g] its incoming gradient. */
+OB_API int ob_ctc_loss_fwd_groups(const float* log_probs, const int64_t* targets,
+                                  const int64_t* input_lengths, const int64_t* target_lengths,
+                                  int64_t G, int64_t B, int64_t T, int64_t V, int64_t S,
+                                  int blank, float* loss, void* ws, size_t ws_bytes,
+                                  void* stream);
+OB_API int ob_ctc_loss_bwd_groups(const float* log_probs, const int64_t* targets,
+                                  const int64_t* input_lengths, const int64_t* target_lengths,
+                                  int64_t G, int64_t B, int64_t T, int64_t V, int64_t S,
+                                  int blank, const float* grad_out, float* grad, void* ws,
+                                  size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Stacked passes. The reference's training step runs every BitLinear three times per

@@ -54,3 +54,27 @@ def test_ctc_matches_torch(gpu, case):
     lg.grad = None
     ctc_loss_mean(F.log_softmax(lg, -1), tg.to(gpu), il.to(gpu), tl.to(gpu), 3).backward()
     assert torch.equal(g1, lg.grad)
+
+
+def test_ctc_groups_equal_per_group_calls(gpu):
+    """ctc_loss_mean_groups over 3 stacked groups == three ctc_loss_mean calls (losses and
+    log-prob gradients), incl. a ragged input length and an infeasible sample (zero_infinity)."""
+    from onebit_asr.ctc import ctc_loss_mean, ctc_loss_mean_groups
+
+    torch.manual_seed(3)
+    G, B, T, V, S = 3, 4, 30, 12, 6
+    lp = torch.randn(G * B, T, V, device=gpu).log_softmax(-1).requires_grad_(True)
+    tg = torch.randint(1, V, (G * B, S), device=gpu)
+    il = torch.tensor([30, 25, 30, 4] * G, device=gpu)  # 4 frames < 6 labels: infeasible
+    tl = torch.tensor([6, 5, 3, 6] * G, device=gpu)
+    w = torch.tensor([0.7, -1.3, 2.0], device=gpu)
+    loss = ctc_loss_mean_groups(lp, tg, il, tl, 0, G)
+    (loss * w).sum().backward()
+    g_grp = lp.grad.clone()
+    lp.grad = None
+    ref = torch.stack([ctc_loss_mean(lp[g * B:(g + 1) * B], tg[g * B:(g + 1) * B],
+                                     il[g * B:(g + 1) * B], tl[g * B:(g + 1) * B], 0)
+                       for g in range(G)])
+    (ref * w).sum().backward()
+    assert torch.allclose(loss, ref, rtol=1e-6, atol=0)
+    assert torch.allclose(g_grp, lp.grad, rtol=1e-6, atol=1e-7)
