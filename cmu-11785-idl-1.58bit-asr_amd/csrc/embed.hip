@@ -16,6 +16,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kRowsPerBlock = 32;
 constexpr int kMaxC = 1024;
+constexpr int kIdxChunk = 4096;
 
 __global__ __launch_bounds__(kThreads) void embed_bwd_kernel(const int64_t* __restrict__ idx,
                                                              int64_t N, const float* __restrict__ g,
@@ -26,15 +27,26 @@ __global__ __launch_bounds__(kThreads) void embed_bwd_kernel(const int64_t* __re
   for (int i = threadIdx.x; i < kRowsPerBlock * C; i += kThreads) acc[i] = 0.0f;
   __syncthreads();
   // Each thread owns columns c = threadIdx.x, +256, ... of every row slot; rows are
-  // visited in index order, so each accumulator sums in ascending n.
-  for (int64_t n = 0; n < N; ++n) {
-    const int64_t v = idx[n];
-    if (v < v0 || v >= v0 + kRowsPerBlock) continue;  // uniform across the block
-    const float* gr = g + n * C;
-    float* ar = acc + (v - v0) * C;
-    for (int c = threadIdx.x; c < C; c += kThreads) ar[c] += gr[c];
+  // visited in index order, so each accumulator sums in ascending n. The indices are
+  // staged through LDS in chunks (a global load per index made the scan latency-bound:
+  // 350 us for 3936 decoder tokens).
+  __shared__ int sidx[kIdxChunk];
+  for (int64_t base = 0; base < N; base += kIdxChunk) {
+    const int cnt = (int)min((int64_t)kIdxChunk, N - base);
+    for (int i = threadIdx.x; i < cnt; i += kThreads) {
+      const int64_t v = idx[base + i];
+      sidx[i] = (v >= v0 && v < v0 + kRowsPerBlock) ? (int)(v - v0) : -1;
+    }
+    __syncthreads();
+    for (int i = 0; i < cnt; ++i) {
+      const int slot = sidx[i];
+      if (slot < 0) continue;  // uniform across the block
+      const float* gr = g + (base + i) * C;
+      float* ar = acc + slot * C;
+      for (int c = threadIdx.x; c < C; c += kThreads) ar[c] += gr[c];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int i = threadIdx.x; i < kRowsPerBlock * C; i += kThreads) {
     const int v = v0 + i / C;
     if (v < V) dW[(int64_t)v * C + (i % C)] = (v == pad) ? 0.0f : acc[i];
