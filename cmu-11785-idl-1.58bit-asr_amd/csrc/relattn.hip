@@ -28,6 +28,51 @@
 #include "ob_drop.h"
 #include "ob_launch.h"
 
+// Profiling switches (tools/variant.sh builds; all 0 in the product): drop one phase of
+// the forward to price it. Results are wrong with any of them set.
+#ifndef RA_EXP_NOX
+#define RA_EXP_NOX 0
+#endif
+#ifndef RA_EXP_NOAC
+#define RA_EXP_NOAC 0
+#endif
+#ifndef RA_EXP_NOCTX
+#define RA_EXP_NOCTX 0
+#endif
+#ifndef RA_EXP_NOPROBS
+#define RA_EXP_NOPROBS 0
+#endif
+#ifndef RA_EXP_NODROP
+#define RA_EXP_NODROP 0
+#endif
+#ifndef RB_EXP_NODP
+#define RB_EXP_NODP 0
+#endif
+#ifndef RB_EXP_NODQU
+#define RB_EXP_NODQU 0
+#endif
+#ifndef RB_EXP_NODQV
+#define RB_EXP_NODQV 0
+#endif
+#ifndef RB_EXP_NODSG
+#define RB_EXP_NODSG 0
+#endif
+#ifndef RB_EXP_NOPROBS
+#define RB_EXP_NOPROBS 0
+#endif
+#ifndef RK_EXP_NOMFMA
+#define RK_EXP_NOMFMA 0
+#endif
+#ifndef RK_EXP_NOFETCH
+#define RK_EXP_NOFETCH 0
+#endif
+#ifndef RK_EXP_NOHASH
+#define RK_EXP_NOHASH 0
+#endif
+#ifndef RK_EXP_NODX
+#define RK_EXP_NODX 0
+#endif
+
 namespace ob {
 
 namespace {
@@ -39,6 +84,33 @@ constexpr int kTile = 64;  // query rows per block (16 per wave)
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// N consecutive floats from a 4-byte-aligned address as dwordx4 runs + a dword tail
+// (gfx950 global loads take unaligned vector addresses).
+typedef f32x4 f32x4u __attribute__((aligned(4)));
+template <int N>
+__device__ __forceinline__ void load_run(const float* __restrict__ p, float (&out)[N]) {
+#pragma unroll
+  for (int i = 0; i + 4 <= N; i += 4) {
+    const f32x4 v = *(const f32x4u*)(p + i);
+    out[i] = v[0];
+    out[i + 1] = v[1];
+    out[i + 2] = v[2];
+    out[i + 3] = v[3];
+  }
+#pragma unroll
+  for (int i = N & ~3; i < N; ++i) out[i] = p[i];
+}
+
+// A operands of key/position tiles t0 .. t0+3 for the 16x16x4 MFMA: lane (r, g) takes
+// columns g*DQ .. g*DQ+DQ-1 of row 16t+r (rows clamped to T-1).
+template <int DQ>
+__device__ __forceinline__ void load_group(const float* __restrict__ base, int C, int t0, int r,
+                                           int g, int T, float (&dst)[4][DQ]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    load_run<DQ>(base + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ, dst[u]);
 }
 
 // Bijective XCD-aware remap (hardware block b runs on XCD b % 8): consecutive logical ids
@@ -73,13 +145,15 @@ template <int DQ, int NTT>
 __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ pos, const float* __restrict__ u, const float* __restrict__ vbias,
-    const int* __restrict__ lens, int Bp, int T, int H, float sqrt_d, DropCfg dc,
+    const int* __restrict__ lens, int Bp, int T, int H, float inv_sqrt_d, DropCfg dc,
     const uint64_t* __restrict__ rng, float* __restrict__ probs, float* __restrict__ ctx) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   extern __shared__ float xs[];
   const int nt = (T + 15) >> 4;
-  const int ldx = 16 * nt + 1;
+  // pitch = 2 mod 32: the rel_shift gather below reads lanes r at stride ldx - 1 (bank
+  // r + 4g, 2-way) -- a pitch of 16nt+1 put all 16 rows of a lane group on one bank
+  const int ldx = 16 * nt + 2;
   const BlockId bid = block_id((T + kTile - 1) / kTile, H);
   const int b = bid.b, h = bid.h, i0 = bid.qt * kTile;
   const int pass = b / Bp;
@@ -96,31 +170,35 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   const int qi = i0 + 16 * w + r;  // this lane's query row (scores phase)
   const int qic = min(qi, T - 1);
   float qu[DQ], qv[DQ];
+  {
+    float x[DQ];
+    load_run<DQ>(qb + (size_t)qic * C + g * DQ, x);
 #pragma unroll
-  for (int s = 0; s < DQ; ++s) {
-    const int c = g * DQ + s;
-    const float x = qb[(size_t)qic * C + c];
-    qu[s] = x + ub[c];
-    qv[s] = x + vbb[c];
+    for (int s = 0; s < DQ; ++s) {
+      const int c = g * DQ + s;
+      qu[s] = x[s] + ub[c];
+      qv[s] = x[s] + vbb[c];
+    }
   }
 
   // X = (q + v) p^T for the wave's 16 rows: D[m][query] with A = p rows, B = (q+v)
   // four key tiles at a time, s-major: consecutive MFMAs feed different accumulators
-  // (per-accumulator order unchanged)
+  // (per-accumulator order unchanged). The next group's p rows are loaded (unaligned
+  // dwordx4 runs) while the current group's MFMAs issue.
+  float opa[4][DQ];
+  load_group<DQ>(pb, C, 0, r, g, T, opa);
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
+    float opn[4][DQ];
+    if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(pb, C, t0 + 4, r, g, T, opn);
     f32x4 acc[4];
-    const float* prow[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      prow[u] = pb + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ;
-    }
+    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = mfma4(prow[u][s], qv[s], acc[u]);
+      for (int u = 0; u < 4; ++u) if (!RA_EXP_NOX) acc[u] = mfma4(opa[u][s], qv[s], acc[u]);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (t0 + u >= nt) continue;
@@ -128,14 +206,24 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) dst[j] = acc[u][j];
     }
+    if (t0 + 4 < NTT) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < DQ; ++s2) opa[u][s2] = opn[u][s2];
+    }
   }
+  // the first key group of the scores phase, in flight over the row-64 work and barrier
+  load_group<DQ>(kb, C, 0, r, g, T, opa);
   // row 64: the next tile's first query (fp32 fma chain on the VALU)
   if (i0 + kTile < T) {
     const float* qe = qb + (size_t)(i0 + kTile) * C;
     for (int m = threadIdx.x; m < T; m += kThreads) {
-      const float* prow = pb + (size_t)m * C;
+      float pr[D];
+      load_run<D>(pb + (size_t)m * C, pr);
       float a = 0.0f;
-      for (int c = 0; c < D; ++c) a = fmaf(qe[c] + vbb[c], prow[c], a);
+#pragma unroll
+      for (int c = 0; c < D; ++c) a = fmaf(qe[c] + vbb[c], pr[c], a);
       xs[kTile * ldx + m] = a;
     }
   }
@@ -148,17 +236,21 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
+    float opn[4][DQ];
+    if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(kb, C, t0 + 4, r, g, T, opn);
     f32x4 acc4[4];
-    const float* krow[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      krow[u] = kb + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ;
-    }
+    for (int u = 0; u < 4; ++u) acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc4[u] = mfma4(krow[u][s], qu[s], acc4[u]);
+      for (int u = 0; u < 4; ++u) if (!RA_EXP_NOAC) acc4[u] = mfma4(opa[u][s], qu[s], acc4[u]);
+    if (t0 + 4 < NTT) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < DQ; ++s2) opa[u][s2] = opn[u][s2];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
     const int t = t0 + u;
@@ -167,11 +259,11 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
-      float bd;
-      if (jj <= qi) bd = xrow[max(T - 1 - qi + jj, 0)];
-      else if (jj == qi + 1) bd = 0.0f;
-      else bd = xrow[ldx + (jj - qi - 2)];
-      const float sc = (acc[j] + bd) / sqrt_d;
+      // bd = X[qi][T-1-qi+jj] (jj <= qi), 0 (jj == qi+1), X[qi+1][jj-qi-2] (jj >= qi+2):
+      // one LDS read at a select-computed offset (always inside the 65-row image)
+      const float xv = xrow[jj - qi + (jj <= qi ? T - 1 : ldx - 2)];
+      const float bd = jj == qi + 1 ? 0.0f : xv;
+      const float sc = (acc[j] + bd) * inv_sqrt_d;
       const bool valid = qi < L && jj < L;
       sreg[t][j] = valid ? sc : -INFINITY;
       mx = fmaxf(mx, sreg[t][j]);
@@ -187,13 +279,14 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     if (t >= nt) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float e = row_live ? expf(sreg[t][j] - mx) : 0.0f;
+      const float e = row_live ? __expf(sreg[t][j] - mx) : 0.0f;
       sreg[t][j] = e;
       sum += e;
     }
   }
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
+  const float rsum = 1.0f / sum;
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
   const size_t prow_off = (((size_t)b * H + h) * T + qic) * T;
 #pragma unroll
@@ -202,10 +295,10 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
-      const float pr = row_live ? sreg[t][j] / sum : 0.0f;
-      if (probs && qi < T && jj < T) probs[prow_off + jj] = pr;
+      const float pr = row_live ? sreg[t][j] * rsum : 0.0f;
+      if (!RA_EXP_NOPROBS && probs && qi < T && jj < T) probs[prow_off + jj] = pr;
       float pd = pr;
-      if (dc.on) {
+      if (dc.on && !RA_EXP_NODROP) {
         const bool keep = drop_hash(dkey, prow_off + jj) >= dc.thresh;
         pd = keep ? pr * dc.scale : 0.0f;
       }
@@ -217,15 +310,32 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   f32x4 o[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // B operands of key tile t (v[16t+4g+j][16ct+r]); tile t+1's are loaded while tile t's
+  // MFMAs issue
+  float vb_cur[4][CT];
+  auto load_v = [&](int t, float (&dst)[4][CT]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* vrow = vbp + (size_t)min(16 * t + 4 * g + j, T - 1) * C;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) dst[j][ct] = vrow[min(16 * ct + r, D - 1)];
+    }
+  };
+  load_v(0, vb_cur);
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     if (t >= nt) continue;
+    float vb_nxt[4][CT];
+    if (t + 1 < NTT && t + 1 < nt) load_v(t + 1, vb_nxt);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int key = min(16 * t + 4 * g + j, T - 1);
-      const float* vrow = vbp + (size_t)key * C;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) o[ct] = mfma4(sreg[t][j], vrow[min(16 * ct + r, D - 1)], o[ct]);
+      for (int ct = 0; ct < CT; ++ct) if (!RA_EXP_NOCTX) o[ct] = mfma4(sreg[t][j], vb_cur[j][ct], o[ct]);
+    if (t + 1 < NTT) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) vb_cur[j][ct] = vb_nxt[j][ct];
     }
   }
 #pragma unroll
@@ -251,7 +361,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     const float* __restrict__ dctx, const float* __restrict__ q, const float* __restrict__ k,
     const float* __restrict__ v, const float* __restrict__ pos, const float* __restrict__ u,
     const float* __restrict__ vbias, const int* __restrict__ lens, int Bp, int T, int H,
-    float sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, const float* __restrict__ probs,
+    float inv_sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, const float* __restrict__ probs,
     float* __restrict__ dq, float* __restrict__ dsg, float* __restrict__ du_part,
     float* __restrict__ dvb_part) {
   constexpr int D = 4 * DQ;
@@ -283,35 +393,52 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const int qi = i0 + 16 * w + r;
   const int qic = min(qi, T - 1);
   float dor[DQ];
-#pragma unroll
-  for (int s = 0; s < DQ; ++s) dor[s] = dob[(size_t)qic * C + g * DQ + s];
+  load_run<DQ>(dob + (size_t)qic * C + g * DQ, dor);
 
   // dPd[query r][key] = dO . v (A = v rows, B = dO row), P from the forward
   float dsr[NTT][4];
   float rowdot = 0.0f;
+  // (v rows of the next four key tiles load while the current tiles' MFMAs issue)
+  float opa[4][DQ];
+  load_group<DQ>(vbp, C, 0, r, g, T, opa);
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
+    float opn[4][DQ];
+    if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(vbp, C, t0 + 4, r, g, T, opn);
     f32x4 acc4[4];
-    const float* vrow[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      vrow[u] = vbp + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ;
-    }
+    for (int u = 0; u < 4; ++u) acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc4[u] = mfma4(vrow[u][s], dor[s], acc4[u]);
+      for (int u = 0; u < 4; ++u) if (!RB_EXP_NODP) acc4[u] = mfma4(opa[u][s], dor[s], acc4[u]);
+    if (t0 + 4 < NTT) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int s2 = 0; s2 < DQ; ++s2) opa[u][s2] = opn[u][s2];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
     const int t = t0 + u;
     if (t >= nt) continue;
     f32x4 acc = acc4[u];
+    // the lane's four probabilities P[qi][16t+4g .. +3]: one unaligned dwordx4 when in range
+    float pp[4];
+    const int jb = 16 * t + 4 * g;
+    if (qi < T && jb + 3 < T) {
+      const f32x4 v4 = *(const f32x4u*)(prb + (size_t)qi * T + jb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pp[j] = v4[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pp[j] = (qi < T && jb + j < T) ? prb[(size_t)qi * T + jb + j] : 0.0f;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
-      const float p = (qi < T && jj < T) ? prb[(size_t)qi * T + jj] : 0.0f;
+      const float p = RB_EXP_NOPROBS ? 0.5f : pp[j];
       const float dp = acc[j] * keep_scale(qic, jj);  // dropout backward
       dsr[t][j] = p;
       acc[j] = dp;
@@ -334,7 +461,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
       const float dp = dprow[jj];
-      dsr[t][j] = (dsr[t][j] * (dp - rowdot)) / sqrt_d;
+      dsr[t][j] = (dsr[t][j] * (dp - rowdot)) * inv_sqrt_d;
     }
   }
   // (each lane rewrites exactly the LDS cells it wrote: no barrier needed in between)
@@ -366,7 +493,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     const float rd = ((rsum[0] + rsum[1]) + rsum[2]) + rsum[3];
     for (int jj = threadIdx.x; jj < T; jj += kThreads) {
       const float p = prb[(size_t)ip * T + jj];
-      ds[jj] = (p * (ds[jj] - rd)) / sqrt_d;
+      ds[jj] = (p * (ds[jj] - rd)) * inv_sqrt_d;
     }
   }
   __syncthreads();
@@ -375,34 +502,76 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   f32x4 oq[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) oq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
+  // (B operands k[16t+4g+j][16ct+r] of tile t+1 load while tile t's MFMAs issue)
+  auto load_b = [&](const float* base, int t, float (&dst)[4][CT]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int key = min(16 * t + 4 * g + j, T - 1);
-      const float* krow = kb + (size_t)key * C;
+      const float* row = base + (size_t)min(16 * t + 4 * g + j, T - 1) * C;
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) oq[ct] = mfma4(dsr[t][j], krow[min(16 * ct + r, D - 1)], oq[ct]);
+      for (int ct = 0; ct < CT; ++ct) dst[j][ct] = row[min(16 * ct + r, D - 1)];
+    }
+  };
+  {
+    float kb_cur[4][CT];
+    load_b(kb, 0, kb_cur);
+#pragma unroll
+    for (int t = 0; t < NTT; ++t) {
+      if (t >= nt) continue;
+      float kb_nxt[4][CT];
+      if (t + 1 < NTT && t + 1 < nt) load_b(kb, t + 1, kb_nxt);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) if (!RB_EXP_NODQU) oq[ct] = mfma4(dsr[t][j], kb_cur[j][ct], oq[ct]);
+      if (t + 1 < NTT) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) kb_cur[j][ct] = kb_nxt[j][ct];
+      }
     }
   }
   // dQv = dX p, dX gathered from LDS by the rel_shift adjoint
   f32x4 ov[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) ov[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* row_i = ds + (1 + 16 * w + r) * ldx;  // dS' row qi
-  const float* row_im1 = row_i - ldx;                 // dS' row qi-1
-  auto dX = [&](int i, const float* ri, const float* rim1, int m) -> float {
-    if (m >= T - 1 - i) return ri[m - T + 1 + i];
-    return i >= 1 ? rim1[m + i + 1] : 0.0f;
-  };
+  // dX[qi][m] = dS'[qi][m-T+1+qi] (m >= T-1-qi), else dS'[qi-1][m+qi+1] (qi >= 1): one LDS
+  // read at a select-computed offset (LDS row 1+16w+r holds dS' row qi, the row above it
+  // qi-1). Positions m = 4mk+g go four MFMA steps at a time, the next four's p operands
+  // loading meanwhile; steps past the end multiply zeros.
+  const float* row_i = ds + (1 + 16 * w + r) * ldx;
   const int nk = (T + 3) >> 2;
-  for (int mk = 0; mk < nk; ++mk) {
-    const int m = 4 * mk + g;
-    const float a = (qi < T && m < T) ? dX(qi, row_i, row_im1, m) : 0.0f;
-    const float* prow = pb + (size_t)min(m, T - 1) * C;
+  constexpr int kMK = 4;
+  auto load_p = [&](int mk0, float (&dst)[kMK][CT]) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) ov[ct] = mfma4(a, prow[min(16 * ct + r, D - 1)], ov[ct]);
+    for (int q = 0; q < kMK; ++q) {
+      const float* prow = pb + (size_t)min(4 * (mk0 + q) + g, T - 1) * C;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) dst[q][ct] = prow[min(16 * ct + r, D - 1)];
+    }
+  };
+  float pv_cur[kMK][CT];
+  load_p(0, pv_cur);
+  for (int mk0 = 0; mk0 < nk; mk0 += kMK) {
+    float pv_nxt[kMK][CT];
+    if (mk0 + kMK < nk) load_p(mk0 + kMK, pv_nxt);
+    float av[kMK];
+#pragma unroll
+    for (int q = 0; q < kMK; ++q) {
+      const int m = 4 * (mk0 + q) + g;
+      const int mm = min(m, T - 1);  // (clamped address; the value is masked below)
+      const bool upper = mm >= T - 1 - qic;
+      const float x = row_i[mm + qic + 1 - (upper ? T : ldx)];
+      av[q] = (qi < T && m < T && (upper || qi >= 1)) ? x : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < kMK; ++q)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) if (!RB_EXP_NODQV) ov[ct] = mfma4(av[q], pv_cur[q][ct], ov[ct]);
+#pragma unroll
+    for (int q = 0; q < kMK; ++q)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) pv_cur[q][ct] = pv_nxt[q][ct];
   }
   // dq = dQu + dQv; per-tile column sums of dQu / dQv for du / dvb
   float su[CT], sv[CT];
@@ -448,7 +617,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     const int qrow = i0 + 16 * w + rr;
     if (qrow >= T) break;
     const float* src = ds + (1 + 16 * w + rr) * ldx;
-    for (int jj = lane; jj < T; jj += 64) dsb[(size_t)qrow * T + jj] = src[jj];
+    for (int jj = lane; jj < T; jj += 64) if (!RB_EXP_NODSG) dsb[(size_t)qrow * T + jj] = src[jj];
   }
 }
 
@@ -457,9 +626,28 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
 // of the tile; every query row is visited (no per-query-tile partials):
 //   dK[key]  = sum_i dS'[i][key] (q+u)[i]       dV[key] = sum_i Pd[i][key] dO[i]
 //   dpos[m]  = sum_i dX[i][m] (q+v)[i]          (per batch row; summed over the pass later)
-// MFMA 16x16x4: A[key r][query g] from dS' / probs (global, coalesced over keys), B[query
-// g][column] from q / dO rows; four query steps are issued per iteration.
+// Queries go in chunks of 32. Per chunk the block stages, once for its 4 waves, the A tiles
+// dS' / Pd (dropout applied) / dX [32 queries][64 keys] (dwordx4 rows, dX gathered by the
+// rel_shift adjoint) and the B tiles q+u / q+v / dO [32 queries][D] in LDS; the next
+// chunk's global loads are in flight in registers while the current chunk's MFMAs
+// (16x16x4: A[key r][query g], B[query g][column r]) issue. Query order per accumulator is
+// ascending, four per MFMA step, as in a plain loop over i.
 // ------------------------------------------------------------------------------------
+template <int D>
+struct KvStage {
+  static constexpr int kQ = 32;                       // queries per chunk
+  static constexpr int kAP = 80;                      // A pitch (= 16 mod 32: conflict-free)
+  static constexpr int kBP = ((D + 16) / 32) * 32 + 16;  // B pitch (= 16 mod 32, >= D)
+  static constexpr int kBVec = kQ * (D / 4);          // float4s per B source (q or dO)
+  static constexpr int kBSlots = (2 * kBVec + kThreads - 1) / kThreads;
+  alignas(16) float ak[kQ][kAP];
+  alignas(16) float av[kQ][kAP];
+  alignas(16) float ap[kQ][kAP];
+  alignas(16) float qu[kQ][kBP];
+  alignas(16) float qv[kQ][kBP];
+  alignas(16) float dob[kQ][kBP];
+};
+
 template <int DQ>
 __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     const float* __restrict__ dsg, const float* __restrict__ probs, const float* __restrict__ q,
@@ -468,6 +656,9 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     float* __restrict__ dv, float* __restrict__ dp_part) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
+  using St = KvStage<D>;
+  constexpr int kQ = St::kQ;
+  __shared__ St st;
   const int nkt = (T + kTile - 1) / kTile;
   const BlockId bid = block_id(nkt, H);
   const int b = bid.b, h = bid.h, k0 = bid.qt * kTile;
@@ -482,17 +673,103 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   const float* prb = probs + ((size_t)b * H + h) * T * T;
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
   const size_t pbase = ((size_t)b * H + h) * T * T;
-  const int key = k0 + 16 * w + r;  // A row: key / position m
-  const bool kok = key < T;
-  const int kc = min(key, T - 1);
-  float bu[CT], bv[CT];
-  int cc[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    cc[ct] = min(16 * ct + r, D - 1);
-    bu[ct] = ub[cc[ct]];
-    bv[ct] = vbb[cc[ct]];
+
+  // pad columns of the B tiles stay zero (their MFMA columns are discarded anyway)
+  for (int e = threadIdx.x; e < kQ * St::kBP; e += kThreads) {
+    (&st.qu[0][0])[e] = 0.0f;
+    (&st.qv[0][0])[e] = 0.0f;
+    (&st.dob[0][0])[e] = 0.0f;
   }
+
+  // staging roles: A -- thread t owns query row t/16, keys k0 + 4(t%16) .. +3;
+  // B -- float4 slot e = t + 256 j: q (e < kBVec) or dO, row e/(D/4), columns 4(e%(D/4))..
+  constexpr int kAH = kQ / 16;  // A rows per thread (ai, ai + 16, ...)
+  const int ai = threadIdx.x >> 4, ax = 4 * (threadIdx.x & 15);
+  f32x4 ra_k[kAH], ra_v[kAH], ra_p[kAH], rb[St::kBSlots];
+  auto fetch = [&](int i0) {
+#pragma unroll
+    for (int hf = 0; hf < kAH; ++hf) {
+    const int i = i0 + ai + 16 * hf;
+    const int key0 = k0 + ax;
+    if (i < T && key0 + 3 < T) {
+      ra_k[hf] = *(const f32x4u*)(dsb + (size_t)i * T + key0);
+      ra_v[hf] = *(const f32x4u*)(prb + (size_t)i * T + key0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = i < T && key0 + j < T;
+        ra_k[hf][j] = ok ? dsb[(size_t)i * T + key0 + j] : 0.0f;
+        ra_v[hf][j] = ok ? prb[(size_t)i * T + key0 + j] : 0.0f;
+      }
+    }
+    // dX[i][m0..m0+3]: one unaligned dwordx4 when the four positions sit in one branch of
+    // the adjoint (upper: dS' row i from column m0-T+1+i; lower: row i-1 from m0+i+1)
+    const int up0 = T - 1 - i;  // first upper position of row i
+    if (i < T && key0 + 3 < T && (key0 >= up0 || (key0 + 3 < up0 && i >= 1))) {
+      const float* src = key0 >= up0 ? dsb + (size_t)i * T + (key0 - up0)
+                                     : dsb + (size_t)(i - 1) * T + (key0 + i + 1);
+      ra_p[hf] = RK_EXP_NODX ? f32x4{0.5f, 0.5f, 0.5f, 0.5f} : *(const f32x4u*)src;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = key0 + j;
+        const bool ok = i < T && m < T;
+        const int ic = min(i, T - 1), mc = min(m, T - 1);
+        const bool upper = mc >= T - 1 - ic;
+        const size_t off = upper ? (size_t)ic * T + (mc - T + 1 + ic)
+                                 : (size_t)max(ic - 1, 0) * T + min(mc + ic + 1, T - 1);
+        const float x = RK_EXP_NODX ? 0.5f : dsb[off];
+        ra_p[hf][j] = (ok && (upper || ic >= 1)) ? x : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = key0 + j;
+      if (!RK_EXP_NOHASH && dc.on && i < T && m < T)
+        ra_v[hf][j] = drop_hash(dkey, pbase + (size_t)i * T + m) >= dc.thresh ? ra_v[hf][j] * dc.scale : 0.0f;
+    }
+    }
+#pragma unroll
+    for (int sl = 0; sl < St::kBSlots; ++sl) {
+      const int e = threadIdx.x + kThreads * sl;
+      const int e2 = e < St::kBVec ? e : e - St::kBVec;
+      const int row = i0 + e2 / DQ, c4 = 4 * (e2 % DQ);
+      if (e < 2 * St::kBVec && row < T) {
+        const float* src = (e < St::kBVec ? qb : dob) + (size_t)row * C + c4;
+        rb[sl] = *(const f32x4u*)src;
+      } else {
+        rb[sl] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int hf = 0; hf < kAH; ++hf) {  // 16-B aligned rows: ds_write_b128
+      *(f32x4*)&st.ak[ai + 16 * hf][ax] = ra_k[hf];
+      *(f32x4*)&st.av[ai + 16 * hf][ax] = ra_v[hf];
+      *(f32x4*)&st.ap[ai + 16 * hf][ax] = ra_p[hf];
+    }
+#pragma unroll
+    for (int sl = 0; sl < St::kBSlots; ++sl) {
+      const int e = threadIdx.x + kThreads * sl;
+      if (e >= 2 * St::kBVec) continue;
+      const int e2 = e < St::kBVec ? e : e - St::kBVec;
+      const int row = e2 / DQ, c4 = 4 * (e2 % DQ);
+      if (e < St::kBVec) {
+        f32x4 xu, xv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xu[j] = rb[sl][j] + ub[c4 + j];
+          xv[j] = rb[sl][j] + vbb[c4 + j];
+        }
+        *(f32x4*)&st.qu[row][c4] = xu;
+        *(f32x4*)&st.qv[row][c4] = xv;
+      } else {
+        *(f32x4*)&st.dob[row][c4] = rb[sl];
+      }
+    }
+  };
+
   f32x4 ak[CT], av[CT], ap[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
@@ -500,36 +777,29 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     av[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  // dX[i][m] = dS'[i][m-T+1+i] (m >= T-1-i), else dS'[i-1][m+i+1] (i >= 1)
-  auto dx_at = [&](int i) -> float {
-    if (kc >= T - 1 - i) return dsb[(size_t)i * T + (kc - T + 1 + i)];
-    return i >= 1 ? dsb[(size_t)(i - 1) * T + (kc + i + 1)] : 0.0f;
-  };
-  constexpr int kU = 4;  // query steps (of 4 rows) in flight
-  for (int i0 = 0; i0 < T; i0 += 4 * kU) {
-    float a_k[kU], a_v[kU], a_p[kU], qx[kU][CT], dx[kU][CT];
+  const int kl = 16 * w + r;  // the lane's key within the tile (A row)
+  fetch(0);
+  for (int i0 = 0; i0 < T; i0 += kQ) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    stage();
+    __syncthreads();
+    if (!RK_EXP_NOFETCH && i0 + kQ < T) fetch(i0 + kQ);
 #pragma unroll
-    for (int uu = 0; uu < kU; ++uu) {
-      const int i = i0 + 4 * uu + g;
-      const bool ok = kok && i < T;
-      const int ic = min(i, T - 1);
-      a_k[uu] = ok ? dsb[(size_t)ic * T + kc] : 0.0f;
-      const float pv = ok ? prb[(size_t)ic * T + kc] : 0.0f;
-      a_v[uu] = dc.on ? (drop_hash(dkey, pbase + (size_t)ic * T + kc) >= dc.thresh ? pv * dc.scale : 0.0f) : pv;
-      a_p[uu] = ok ? dx_at(ic) : 0.0f;
+    for (int s4 = 0; s4 < kQ / 4; ++s4) {
+      const int qq = 4 * s4 + g;
+      const float a_k = st.ak[qq][kl], a_v = st.av[qq][kl], a_p = st.ap[qq][kl];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        qx[uu][ct] = qb[(size_t)ic * C + cc[ct]];
-        dx[uu][ct] = dob[(size_t)ic * C + cc[ct]];
-      }
-    }
-#pragma unroll
-    for (int uu = 0; uu < kU; ++uu) {
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        ak[ct] = mfma4(a_k[uu], qx[uu][ct] + bu[ct], ak[ct]);
-        av[ct] = mfma4(a_v[uu], dx[uu][ct], av[ct]);
-        ap[ct] = mfma4(a_p[uu], qx[uu][ct] + bv[ct], ap[ct]);
+        const int col = 16 * ct + r;
+        if (RK_EXP_NOMFMA) {
+          ak[ct][0] += a_k * st.qu[qq][col];
+          av[ct][0] += a_v * st.dob[qq][col];
+          ap[ct][0] += a_p * st.qv[qq][col];
+          continue;
+        }
+        ak[ct] = mfma4(a_k, st.qu[qq][col], ak[ct]);
+        av[ct] = mfma4(a_v, st.dob[qq][col], av[ct]);
+        ap[ct] = mfma4(a_p, st.qv[qq][col], ap[ct]);
       }
     }
   }
@@ -621,7 +891,8 @@ __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropC
 }
 
 
-size_t lds_bytes(int T) { return sizeof(float) * (size_t)(kTile + 1) * (16 * ((T + 15) / 16) + 1); }
+// (the forward's pitch, 16nt+2; the backward uses 16nt+1)
+size_t lds_bytes(int T) { return sizeof(float) * (size_t)(kTile + 1) * (16 * ((T + 15) / 16) + 2); }
 
 }  // namespace
 
@@ -655,11 +926,11 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
                         float* probs, float* ctx, hipStream_t s) {
   const dim3 grid((unsigned)(((T + kTile - 1) / kTile) * H * Bt));
   const DropCfg dc = make_drop(p_drop);
-  const float sqrt_d = (float)sqrt((double)d);
+  const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
   const size_t lds = lds_bytes((int)T);
 #define OB_RA_FWD(DQ, NTT)                                                                 \
   hipLaunchKernelGGL((relattn_fwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, q, k, v, pos, \
-                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, sqrt_d, dc, rng, probs, ctx)
+                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, probs, ctx)
   OB_RA_DISPATCH(OB_RA_FWD);
 #undef OB_RA_FWD
 }
@@ -672,7 +943,7 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
   const int nqt = (int)((T + kTile - 1) / kTile);
   const dim3 grid((unsigned)(nqt * H * Bt));
   const DropCfg dc = make_drop(p_drop);
-  const float sqrt_d = (float)sqrt((double)d);
+  const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
   const size_t lds = lds_bytes((int)T);
   float* dsg = (float*)ws;
   float* dp_part = dsg + (size_t)Bt * H * T * T;
@@ -680,7 +951,7 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
   float* dvb_part = du_part + (size_t)Bt * H * nqt * d;
 #define OB_RA_BWD(DQ, NTT)                                                                     \
   hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, q, k, v,  \
-                     pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, sqrt_d, dc, rng, probs, dq, \
+                     pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, probs, dq, \
                      dsg, du_part, dvb_part)
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
