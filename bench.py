@@ -426,6 +426,11 @@ def main():
 
     torch.manual_seed(1234)  # identical init on every rank (DDP / the graph path broadcast)
     model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S).to(dev)
+    quant_off = args.mode == "quant-off"
+    if quant_off:  # configs[3]: every BitLinear -> bf16 F.linear (hipBLASLt), same step body
+        from onebit_asr.quant import set_quant_off
+
+        set_quant_off(model, torch.bfloat16)
     n_layers = CONFORMER_S["enc_layers"]
     step_mod = OneBitStep(model, n_layers=n_layers)
     batch = synthetic_batch([args.frames] * args.batch, [args.tokens] * args.batch,
@@ -487,7 +492,8 @@ def main():
     frames_total = world * args.batch * args.frames * args.steps
     value = frames_total / elapsed
     out = {
-        "metric": "mel-frames/sec (Conformer-S 1.58-bit train step)",
+        "metric": ("mel-frames/sec (Conformer-S quant-off train step, BitLinear -> bf16 nn.Linear)"
+                   if quant_off else "mel-frames/sec (Conformer-S 1.58-bit train step)"),
         "value": round(value, 1),
         "unit": "mel-frames/s",
         "n_gpus": world,
@@ -497,20 +503,23 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16 linears (hipBLASLt), fp32 elsewhere" if quant_off else "fp32",
         "data": "synthetic (N(0,1) 80-mel x 1000-frame padded batches, random-init weights)",
-        "config": {"workload": "conformer-s-1.58bit-train-step", "global_batch": args.batch * world,
+        "config": {"workload": ("conformer-s-quant-off-bf16-train-step" if quant_off
+                                else "conformer-s-1.58bit-train-step"), "global_batch": args.batch * world,
                    "execution": "eager" if args.eager else "hip-graph",
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
                    "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
                    "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP"},
         "final_loss": round(loss_val, 4),
     }
-    if rank == 0 and world == 1 and not args.no_roofline:
+    if quant_off:  # no ternary kernel runs: the line is the ceiling the 1.58-bit step is read against
+        out["roofline"] = None
+    elif rank == 0 and world == 1 and not args.no_roofline:
         roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
         roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
         out["roofline"] = roof
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not quant_off:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

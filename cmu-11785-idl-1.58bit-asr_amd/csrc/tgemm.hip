@@ -195,11 +195,37 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     const int wc = w < KW ? w : KW - 1;
     return codes[n * KW + wc];  // clamped, always valid; out-of-range words are zeroed above
   };
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int kg = 8 * g;
+  auto arow_of = [&](int rt) {
+    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
+    const int64_t row = m0 + r < M ? m0 + r : M - 1;
+    return A + row * (int64_t)K;
+  };
+  // K compile-time (NCH > 0): A chunks are software-pipelined ACROSS row tiles. The first
+  // tile's first kWin chunks are issued right after the code words (so the B decode and
+  // the barrier run under their latency), and while a tile computes its last chunks the
+  // next tile's first chunks are already loading (so the epilogue runs under them too).
+  // vmcnt counts in issue order: the code words go first so the decode waits only on them.
+  constexpr int kWmax = NT > 6 ? 3 : 5;
+  // NT 12: the cross-tile live range spills (and a 2-deep window measured slower), so it
+  // keeps the per-tile window (issued at the top of each row tile)
+  constexpr bool kCross = NT <= 9;
+  constexpr int kWin = NCH > 0 ? (NCH < kWmax ? NCH : kWmax) : 1;
+  f32x4 buf[NCH > 0 ? NCH : 1][2];
   if constexpr (NCH > 0) {
     constexpr int kWpt = (16 * NT * 2 * NCH + kThreads - 1) / kThreads;
     uint32_t wv[kWpt];
 #pragma unroll
     for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThreads);
+    if constexpr (kCross) {
+      const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
+#pragma unroll
+      for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThreads, wv[i]);
@@ -208,11 +234,6 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   }
   __syncthreads();
 
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int r = lane & 15;
-  const int g = lane >> 4;
-  const int kg = 8 * g;
   const __bf16* brow = bimg + r * stride + kg;
   const float a_eff = effective_alpha(alpha, alpha_raw);
   const uint32_t dkey = (EPI != kEpiNone && ep.dc.on) ? drop_key(ep.rng[0], ep.rng[1] + ep.rng_off) : 0u;
@@ -253,19 +274,32 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     };
 
     if constexpr (NCH > 0) {
-      // Fully unrolled; a window of kWin chunks in flight. sched_barrier keeps hipcc from
-      // sinking each load next to its use (one load in flight, vmcnt(0) per chunk).
-      constexpr int kWmax = NT > 6 ? 3 : 5;
-      constexpr int kWin = NCH < kWmax ? NCH : kWmax;
-      f32x4 buf[NCH][2];
+      // Fully unrolled; a window of kWin chunks in flight (this tile's chunks 0..kWin-1
+      // were issued by the previous iteration / the prologue). sched_barrier keeps hipcc
+      // from sinking each load next to its use (one load in flight, vmcnt(0) per chunk).
+      // The last tile re-reads its own rows as the "next" tile (L2 hits, never used).
+      if constexpr (!kCross) {  // NT 12: this tile's window is issued here (no cross-tile)
 #pragma unroll
-      for (int c = 0; c < kWin; ++c) load8(arow, 32 * c + kg, K, buf[c][0], buf[c][1]);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int c = 0; c < kWin; ++c) load8(arow, 32 * c + kg, K, buf[c][0], buf[c][1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int rt_next = rt + rgroups < n_rt ? rt + rgroups : rt;
+      const float* anext = arow_of(rt_next);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        if (c + kWin < NCH) load8(arow, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
+        if (c + kWin < NCH)
+          load8(arow, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
         __builtin_amdgcn_sched_barrier(0);
         compute(buf[c][0], buf[c][1], 32 * c);
+        // next tile's chunk into the slot just consumed (slot c + kWin - NCH <= c; it IS
+        // slot c when kWin == NCH, so the load must follow this chunk's compute)
+        if constexpr (kCross) {
+          if (c + kWin >= NCH) {
+            load8(anext, 32 * (c + kWin - NCH) + kg, K, buf[c + kWin - NCH][0],
+                  buf[c + kWin - NCH][1]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
       }
     } else {
       // Generic K: three rotating register sets, unrolled so no register copy of an

@@ -59,7 +59,8 @@ def fused_supported(x: torch.Tensor, *layers: QuantizedLinear, bitwidth=None) ->
         return False
     if not (isinstance(bitwidth, PassBits) or bitwidth in (1, 2)):
         return False  # 32 (F.linear), DynamicBitwidth and invalid values take the module path
-    return x.is_cuda and x.dtype == torch.float32 and all(m.act_quant is None for m in layers)
+    return x.is_cuda and x.dtype == torch.float32 and all(
+        m.act_quant is None and m.quant_off is None for m in layers)
 
 
 def _bits_args(bitwidth):

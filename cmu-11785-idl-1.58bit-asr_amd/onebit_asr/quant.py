@@ -34,7 +34,7 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "DeviceBits",
+__all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "set_quant_off", "DeviceBits",
            "DynamicBitwidth", "PassBits", "StackedBits", "set_act_quant", "ACT_QUANT_MODES",
            "act_absmax", "PackGroup"]
 
@@ -148,6 +148,18 @@ def set_act_quant(module: nn.Module, mode: Optional[str]) -> nn.Module:
     for m in module.modules():
         if isinstance(m, QuantizedLinear):
             m.act_quant = mode
+    return module
+
+
+def set_quant_off(module: nn.Module, dtype: Optional[torch.dtype] = torch.bfloat16) -> nn.Module:
+    """BASELINE configs[3]: every QuantizedLinear under ``module`` becomes a plain
+    ``F.linear`` computed in ``dtype`` (bf16 -> hipBLASLt bf16 MFMA), whatever the bitwidth;
+    ``alpha`` then receives no gradient. ``None`` restores the BitLinear path. The reference
+    has no such mode (its bitwidth 32 is fp32 F.linear, quant.py:121-122); this is the
+    measurement ceiling for the ternary kernels, not a parity path."""
+    for m in module.modules():
+        if isinstance(m, QuantizedLinear):
+            m.quant_off = dtype
     return module
 
 
@@ -448,6 +460,9 @@ class QuantizedLinear(nn.Module):
         # None: the reference's fp32 activations. "absmax_int8": the opt-in north-star mode
         # (per-tensor absmax int8 activations on the int8 matrix cores; own tolerance).
         self.act_quant = _check_act_quant(act_quant)
+        # BASELINE configs[3] ("quant off: BitLinear -> bf16 nn.Linear"): a torch dtype here
+        # makes forward a plain F.linear in that dtype at every bitwidth (set_quant_off).
+        self.quant_off: Optional[torch.dtype] = None
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
         # quant.py:104-108: kaiming_uniform(a=sqrt(5)) then x2, i.e. U(-2/sqrt(in), 2/sqrt(in)).
         nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
@@ -479,6 +494,10 @@ class QuantizedLinear(nn.Module):
         return codes, codes_t
 
     def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
+        if self.quant_off is not None:  # configs[3] ceiling: no quantizer, library GEMM
+            dt = self.quant_off
+            b = self.bias.to(dt) if self.bias is not None else None
+            return F.linear(x.to(dt), self.weight.to(dt), b).to(x.dtype)
         if isinstance(bitwidth, PassBits):
             return self._forward_passes(x, bitwidth)
         bits = _check_bitwidth(bitwidth)
@@ -543,7 +562,8 @@ class PackGroup:
                      ("alpha_raw", "<i4")])  # == ob_pack_item (include/onebit_hip.h)
 
     def __init__(self, module: nn.Module, bits=(2, 1)):
-        self.layers = [m for m in module.modules() if isinstance(m, QuantizedLinear)]
+        self.layers = [m for m in module.modules()
+                       if isinstance(m, QuantizedLinear) and m.quant_off is None]
         self.bits = tuple(bits)
         self._ptrs = None
         self.table = None

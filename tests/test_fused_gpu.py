@@ -51,10 +51,12 @@ def _run(m, x, bits, fused, monkeypatch):
     return y.detach(), xx.grad.clone(), grads
 
 
-@pytest.mark.parametrize("bits", [1, 2])
-def test_ffn_fused_equals_unfused(gpu, bits, monkeypatch):
+@pytest.mark.parametrize("bits,bt,t", [(1, 4, 50), (2, 4, 50), (2, 32, 249), (1, 96, 249)])
+def test_ffn_fused_equals_unfused(gpu, bits, bt, t, monkeypatch):
+    """Small shapes (one row tile per block) and Conformer-S shapes (each block walks several
+    row tiles, so the cross-tile A prefetch of csrc/tgemm.hip is exercised)."""
     m = _ffn_pair(gpu).eval()
-    x = torch.randn(4, 50, 144, device=gpu)
+    x = torch.randn(bt, t, 144, device=gpu)
     y0, gx0, g0 = _run(m, x, bits, False, monkeypatch)
     y1, gx1, g1 = _run(m, x, bits, True, monkeypatch)
     assert _maxrel(y1, y0) <= 1e-6
