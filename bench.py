@@ -66,6 +66,8 @@ def parse():
                     help="train: configs[1]/[2] (default); quant-off: configs[3] (BitLinear -> "
                          "bf16 nn.Linear); infer / infer-fp32act: configs[4] (B=256, 2-bit, "
                          "int8 / fp32 activations, greedy CTC decode)")
+    ap.add_argument("--conv-pw-ternary", action="store_true",
+                    help="opt-in ternary conv-module pw1/pw2 (north_star; not reference math)")
     ap.add_argument("--conv-find", action="store_true",
                     help="torch.backends.cudnn.benchmark (MIOpen Find) for the subsampling convs")
     args = ap.parse_args()
@@ -425,7 +427,8 @@ def main():
     from onebit_asr.train_step import OneBitStep, WarmupCosine, make_optimizer, sample_sp_mask, train_step
 
     torch.manual_seed(1234)  # identical init on every rank (DDP / the graph path broadcast)
-    model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S).to(dev)
+    model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S,
+                         quantize_conv_pointwise=args.conv_pw_ternary).to(dev)
     quant_off = args.mode == "quant-off"
     if quant_off:  # configs[3]: every BitLinear -> bf16 F.linear (hipBLASLt), same step body
         from onebit_asr.quant import set_quant_off
@@ -510,7 +513,8 @@ def main():
                    "execution": "eager" if args.eager else "hip-graph",
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
                    "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
-                   "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP"},
+                   "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP",
+                   "conv_pointwise": "ternary (opt-in)" if args.conv_pw_ternary else "fp32 (reference)"},
         "final_loss": round(loss_val, 4),
     }
     if quant_off:  # no ternary kernel runs: the line is the ceiling the 1.58-bit step is read against

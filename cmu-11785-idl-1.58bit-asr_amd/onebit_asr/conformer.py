@@ -228,15 +228,27 @@ class ConvModule(nn.Module):
     """LN -> pw1 -> GLU -> depthwise k -> BatchNorm(batch stats, track_running_stats=False)
     -> swish -> pw2 (conformer.py:141-167). Full precision."""
 
-    def __init__(self, d_model: int, kernel_size: int = 31, dropout: float = 0.1):
+    def __init__(self, d_model: int, kernel_size: int = 31, dropout: float = 0.1,
+                 quantize_pointwise: bool = False):
         super().__init__()
         self.ln = LayerNorm(d_model)
-        self.pw1 = nn.Conv1d(d_model, 2 * d_model, kernel_size=1)
+        # north_star lists the pointwise 1x1s as BitLinear call sites; the reference keeps
+        # them full precision (conformer.py:225), so ternary pw1/pw2 is opt-in: they become
+        # channels-last QuantizedLinear layers (keys pw1.weight [2C, C], pw1.alpha, pw1.bias)
+        # at the block's bitwidth. Off (default) = the reference's Conv1d(k=1) keys/math.
+        self.quantize_pointwise = quantize_pointwise
+        if quantize_pointwise:
+            self.pw1 = QuantizedLinear(d_model, 2 * d_model)
+        else:
+            self.pw1 = nn.Conv1d(d_model, 2 * d_model, kernel_size=1)
         self.glu = nn.GLU(dim=1)
         self.dw = nn.Conv1d(d_model, d_model, kernel_size=kernel_size,
                             padding=kernel_size // 2, groups=d_model)
         self.bn = nn.BatchNorm1d(d_model, track_running_stats=False)
-        self.pw2 = nn.Conv1d(d_model, d_model, kernel_size=1)
+        if quantize_pointwise:
+            self.pw2 = QuantizedLinear(d_model, d_model)
+        else:
+            self.pw2 = nn.Conv1d(d_model, d_model, kernel_size=1)
         self.dropout = nn.Dropout(dropout)
 
     def _bn(self, h: torch.Tensor, passes: int) -> torch.Tensor:
@@ -251,12 +263,22 @@ class ConvModule(nn.Module):
                          self.bn.bias.repeat(passes), True, self.bn.momentum or 0.0, self.bn.eps)
         return y.view(b, passes, c, t).transpose(0, 1).reshape(pb, c, t)
 
-    def forward(self, x, mask=None, passes: int = 1):
+    def forward(self, x, mask=None, passes: int = 1, bitwidth=None):
+        """``bitwidth``: the block's BitLinear bitwidth, used only by ternary pointwise
+        layers (``quantize_pointwise``); the reference passes none (conformer.py:225)."""
+        if self.quantize_pointwise and bitwidth is None:
+            raise ValueError("quantize_pointwise ConvModule needs the block bitwidth")
         if mask is None and conv_module_supported(x, self):
             # channels-last on the HIP kernels (conv.py / csrc/convmod.hip), same computation
             p = self.dropout.p if self.training else 0.0
             h, xr = self.ln.fork(x)
-            return conv_module_fused(xr, h, self, passes, p)
+            return conv_module_fused(xr, h, self, passes, p, bitwidth)
+        if self.quantize_pointwise:
+            h = self.glu(self.pw1(self.ln(x), bitwidth).transpose(1, 2))
+            h = swish(self._bn(depthwise_conv1d(h, self.dw), passes))
+            h = self.pw2(h.transpose(1, 2), bitwidth)
+            h = self.dropout(h)
+            return x + _pad_rows(h, mask)
         h = self.glu(self.pw1(self.ln(x).transpose(1, 2)))
         h = self.pw2(swish(self._bn(depthwise_conv1d(h, self.dw), passes)))
         h = self.dropout(h).transpose(1, 2)
@@ -300,12 +322,13 @@ class ConformerBlock(nn.Module):
     """ff1 -> mhsa -> conv (FP) -> ff2 -> LN (conformer.py:212-228)."""
 
     def __init__(self, d_model: int, d_ff: int, n_heads: int, conv_kernel: int, dropout: float,
-                 block_index: int):
+                 block_index: int, quantize_conv_pointwise: bool = False):
         super().__init__()
         self.block_index = block_index
         self.ff1 = FeedForwardModule(d_model, d_ff, dropout)
         self.mhsa = MHSA(d_model, n_heads, dropout)
-        self.conv = ConvModule(d_model, kernel_size=conv_kernel, dropout=dropout)
+        self.conv = ConvModule(d_model, kernel_size=conv_kernel, dropout=dropout,
+                               quantize_pointwise=quantize_conv_pointwise)
         self.ff2 = FeedForwardModule(d_model, d_ff, dropout)
         self.ln = LayerNorm(d_model)
 
@@ -313,7 +336,10 @@ class ConformerBlock(nn.Module):
         x = self.ff1(x, bitwidth_linear)
         x = self.mhsa(x, src_mask, bitwidth_linear, pos_emb)
         passes = bitwidth_linear.passes if isinstance(bitwidth_linear, PassBits) else 1
-        x = self.conv(x, passes=passes)  # the reference does not pass the mask here (:225)
+        # the reference does not pass the mask here (:225); the bitwidth reaches only
+        # opt-in ternary pointwise layers
+        x = self.conv(x, passes=passes,
+                      bitwidth=bitwidth_linear if self.conv.quantize_pointwise else None)
         x = self.ff2(x, bitwidth_linear)
         return self.ln(x)
 
@@ -332,12 +358,14 @@ def block_bitwidths(n_layers: int, precision: int, sp_mask: Optional[Sequence[in
 
 class ConformerEncoder(nn.Module):
     def __init__(self, input_dim: int, d_model: int, n_layers: int, n_heads: int,
-                 d_ff: int, conv_kernel: int, dropout: float):
+                 d_ff: int, conv_kernel: int, dropout: float,
+                 quantize_conv_pointwise: bool = False):
         super().__init__()
         self.subsample = Conv2dSubsampling(input_dim, d_model)
         self.pos_enc = RelPositionalEncoding(d_model, dropout)
         self.blocks = nn.ModuleList([
-            ConformerBlock(d_model, d_ff, n_heads, conv_kernel, dropout, i)
+            ConformerBlock(d_model, d_ff, n_heads, conv_kernel, dropout, i,
+                           quantize_conv_pointwise)
             for i in range(n_layers)
         ])
         self.ln_out = LayerNorm(d_model)
@@ -400,10 +428,14 @@ class ConformerASR(nn.Module):
                  enc_d_model=256, enc_layers=12, enc_heads=4, enc_d_ff=1024,
                  enc_conv_kernel=31, enc_dropout=0.1,
                  dec_layers=2, dec_heads=4, dec_d_ff=1024, dec_dropout=0.1,
-                 pad_id=0):
+                 pad_id=0, quantize_conv_pointwise: bool = False):
+        """``quantize_conv_pointwise`` (not in the reference, default off): ternary conv-module
+        pw1/pw2 (north_star's "conv-module pointwise 1x1s"); diverges from the reference's
+        full-precision pointwise convs (conformer.py:225) when on."""
         super().__init__()
         self.encoder = ConformerEncoder(input_dim, enc_d_model, enc_layers, enc_heads,
-                                        enc_d_ff, enc_conv_kernel, enc_dropout)
+                                        enc_d_ff, enc_conv_kernel, enc_dropout,
+                                        quantize_conv_pointwise)
         self.decoder = TransformerDecoder(vocab_size, enc_d_model, dec_layers, dec_heads,
                                           dec_d_ff, dec_dropout, pad_id)
         self.ctc_head = nn.Linear(enc_d_model, vocab_size)

@@ -271,22 +271,25 @@ def conv_module_supported(x: torch.Tensor, module) -> bool:
           and dw.groups == dw.in_channels == dw.out_channels == x.size(-1)
           and kt % 2 == 1 and dw.padding[0] == kt // 2 and dw.stride[0] == 1
           and dw.dilation[0] == 1 and bn.affine and not bn.track_running_stats
-          and module.pw1.kernel_size[0] == 1 and module.pw2.kernel_size[0] == 1)
+          and (getattr(module, "quantize_pointwise", False)
+               or (module.pw1.kernel_size[0] == 1 and module.pw2.kernel_size[0] == 1)))
     if not ok:
         return False
     return _lib.load().ob_convmod_workspace(1, x.size(0), x.size(1), x.size(-1), kt) > 0
 
 
-def conv_module_fused(x: torch.Tensor, h: torch.Tensor, module, passes: int, p_drop: float):
+def conv_module_fused(x: torch.Tensor, h: torch.Tensor, module, passes: int, p_drop: float,
+                      bitwidth=None):
     """ConvModule.forward (conformer.py:149-167) on [Bt, T, C] without leaving channels-last:
     pw1 / pw2 as GEMMs (bias in the GEMM epilogue), the GLU / depthwise / BatchNorm / swish
     core in csrc/convmod.hip, dropout + residual in one kernel. ``h`` = LN(x)."""
     from .fused import _rng
 
     bt, t, c = x.shape
-    u = _pointwise(h, module.pw1)
+    quant = getattr(module, "quantize_pointwise", False)  # ternary pw1/pw2 (opt-in)
+    u = module.pw1(h, bitwidth) if quant else _pointwise(h, module.pw1)
     v = _ConvCoreFn.apply(u.reshape(bt * t, 2 * c), module.dw.weight, module.dw.bias,
                           module.bn.weight, module.bn.bias, passes, t, float(module.bn.eps))
-    o = _pointwise(v, module.pw2)
+    o = module.pw2(v, bitwidth) if quant else _pointwise(v, module.pw2)
     rng, off = _rng(x.device) if p_drop > 0 else (None, 0)
     return _ResidualDropFn.apply(x, o.view(bt, t, c), float(p_drop), rng, off)
