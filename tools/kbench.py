@@ -58,6 +58,10 @@ def main():
     ap.add_argument("--fused", action="store_true", help="also time the fused-epilogue entries")
     ap.add_argument("--passes", type=int, default=3,
                     help="stacked passes per launch (the training step runs 3; 0 = single-pass entries)")
+    ap.add_argument("--i8", action="store_true",
+                    help="also time the opt-in int8-activation forward (absmax + i8 MFMA GEMM)")
+    ap.add_argument("--rows", type=int, default=0,
+                    help="rows per pass for the M=7968 shapes (e.g. 63744 = configs[4] bs=256)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = _lib.load()
@@ -67,6 +71,8 @@ def main():
     for name, M, K, N in SHAPES:
         if args.shape and name != args.shape:
             continue
+        if args.rows and M == 7968:
+            M = args.rows
         P = max(args.passes, 1)
         X = torch.randn(P * M, K, device=dev)
         dY = torch.randn(P * M, N, device=dev)
@@ -129,12 +135,28 @@ def main():
                 "dropbwd": lambda cs=s: lib.ob_drop_scale_bwd(
                     dY.data_ptr(), P * M, N, 0.5, pd, rng.data_ptr(), 0, None, 0, R.data_ptr(), cs),
             })
+        if args.i8:  # north_star's int8 path vs the fp32-exact bf16x3 forward, same shape
+            amax = torch.empty(P, device=dev)
+            wsa = lib.ob_act_absmax_workspace(P)
+            wa = torch.empty(max(wsa, 1), dtype=torch.uint8, device=dev)
+            fns.update({
+                "absmax": lambda cs=s: lib.ob_act_absmax(X.data_ptr(), P, M * K, amax.data_ptr(),
+                                                         wa.data_ptr(), wsa, cs),
+                "fwd_i8": lambda cs=s: lib.ob_bitlinear_fwd_i8(
+                    X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, amax.data_ptr(), b.data_ptr(), N, Y.data_ptr(), cs),
+            })
         res = {}
         for k, fn in fns.items():
             res[k] = timed(fn, args.reps, args.graph) if (not args.op or k == args.op) else float("nan")
         gb_f = 4 * P * (M * K + M * N) / res["fwd"] / 1e3
         gb_w = 4 * P * (M * K + M * N) / res["dw"] / 1e3
         print(f"{name:6s} {M:5d} {K:4d} {N:4d} | {res['pack']:7.2f} {res['fwd']:7.2f} {res['dx']:7.2f} {res['dw']:7.2f} us | {gb_f:8.0f} {gb_w:8.0f}")
+        if "fwd_i8" in res:
+            gb_i8 = 4 * P * (M * K + M * N) / res["fwd_i8"] / 1e3
+            tops = 2 * P * M * K * N / res["fwd_i8"] / 1e6
+            print(f"{'':6s} int8: absmax {res['absmax']:7.2f}  fwd_i8 {res['fwd_i8']:7.2f} us "
+                  f"({gb_i8:.0f} GB/s fp32-in/out, {tops:.1f} TOP/s)  vs bf16x3 fwd {res['fwd']:7.2f} us")
         if "fswish" in res:
             print(f"{'':6s} fused: fwd+swish {res['fswish']:7.2f}  fwd+residual {res['fres']:7.2f}  "
                   f"dx+swish-bwd {res['dxswish']:7.2f}  drop-scale-bwd {res['dropbwd']:7.2f} us")
