@@ -116,8 +116,7 @@ int ob_quant_ste_bwd(const float* grad_W_hat, const float* W, const float* alpha
   // ws: [ticket (16 B)][block partials]
   uint32_t* ticket = static_cast<uint32_t*>(ws);
   float* apart = reinterpret_cast<float*>(static_cast<char*>(ws) + 16);
-  if (hipMemsetAsync(ticket, 0, sizeof(uint32_t), as_stream(stream)) != hipSuccess)
-    return OB_ERR_HIP;
+  launch_zero_words(ticket, 1, as_stream(stream));
   launch_ste_reduce(grad_W_hat, 1, n, nullptr, 0, W, alpha, alpha_raw, bits, nullptr, grad_W,
                     nullptr, apart, ticket, grad_alpha, as_stream(stream));
   return launched();
@@ -178,11 +177,9 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N
   int cpp = (int)p.chunks_per_pass;
   if (M == 0 || N == 0) {
     // No rows: every gradient is zero. Zero the first slab and reduce one chunk.
-    if (N * K > 0 && hipMemsetAsync(part, 0, sizeof(float) * N * K, s) != hipSuccess)
-      return OB_ERR_HIP;
-    if (db && N > 0 && hipMemsetAsync(part_db, 0, sizeof(float) * N, s) != hipSuccess)
-      return OB_ERR_HIP;
-    if (hipMemsetAsync(ticket, 0, sizeof(uint32_t), s) != hipSuccess) return OB_ERR_HIP;
+    launch_zero_words(part, N * K, s);
+    if (db) launch_zero_words(part_db, N, s);
+    launch_zero_words(ticket, 1, s);
     chunks = 1;
     cpp = 1;
     P = 1;

@@ -149,7 +149,7 @@ void launch_dwconv_bwd(const float* x, const float* dy, const float* w, int64_t 
       hipLaunchKernelGGL(dwconv_bwd_kernel, dim3((unsigned)(B * C)), dim3(kThreads), 0, s, x, dy,
                          w, (int)C, (int)T, (int)KT, dx, part);
     } else {
-      (void)hipMemsetAsync(part, 0, dwconv_bwd_workspace(B, C, KT), s);
+      launch_zero_words(part, (int64_t)(dwconv_bwd_workspace(B, C, KT) / sizeof(float)), s);
     }
   }
   const int64_t n = C * (KT + 1);

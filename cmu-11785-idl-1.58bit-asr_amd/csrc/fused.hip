@@ -152,7 +152,23 @@ __global__ __launch_bounds__(kThreads) void colsum_part_kernel(const float* __re
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
+// Zero n 32-bit words. Used instead of hipMemsetAsync, which, captured into a HIP graph
+// on ROCm 7.2, leaves garbage in buffers below ~4 MB on every replay after the first
+// (tools/memset_graph_repro.py).
+__global__ __launch_bounds__(kThreads) void zero_words_kernel(uint32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
+    p[i] = 0u;
+}
+
 }  // namespace
+
+void launch_zero_words(void* p, int64_t n_words, hipStream_t s) {
+  if (n_words <= 0) return;
+  int64_t blocks = ceil_div(n_words, kThreads);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                     static_cast<uint32_t*>(p), n_words);
+}
 
 void launch_drop_scale_bwd(const float* dout, int64_t rows, int64_t N, float rscale,
                            float p_drop, const uint64_t* rng, uint64_t rng_off, const int* lens,

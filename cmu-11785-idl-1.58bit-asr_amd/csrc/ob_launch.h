@@ -96,6 +96,8 @@ void launch_bias_relu_fwd(float* y, const float* bias, int64_t B, int64_t C, int
 size_t relu_bias_bwd_workspace(int64_t B, int64_t C);
 void launch_relu_bias_bwd(const float* g, const float* y, int64_t B, int64_t C, int64_t hw,
                           float* gout, float* dbias, void* ws, hipStream_t s);
+// p[0 .. n_words) = 0 as a kernel (graph-safe; see fused.hip).
+void launch_zero_words(void* p, int64_t n_words, hipStream_t s);
 // out[n] = sum over rows of x[rows][N] (fixed order; ws: colsum_workspace(N)).
 size_t colsum_workspace(int64_t N);
 void launch_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, hipStream_t s);

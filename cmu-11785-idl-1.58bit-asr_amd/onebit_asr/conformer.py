@@ -33,6 +33,7 @@ from .conv import conv2d_bias_relu, conv_module_fused, conv_module_supported, de
 from .embedding import embedding
 from .fused import ffn_residual, fused_supported, linear_residual
 from .layernorm import layer_norm, layer_norm_fork
+from .linear import linear
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
 __all__ = [
@@ -315,7 +316,7 @@ class Conv2dSubsampling(nn.Module):
             y = self.conv(x.unsqueeze(1))                  # [B, C, T', F']
         bsz, ch, tsub, fsub = y.shape
         y = y.transpose(1, 2).reshape(bsz, tsub, ch * fsub)  # channel-major per frame
-        return self.out(y)
+        return linear(y, self.out.weight, self.out.bias)
 
 
 class ConformerBlock(nn.Module):
@@ -397,7 +398,16 @@ class ConformerEncoder(nn.Module):
 
 
 class TransformerDecoder(nn.Module):
-    """Stock 2-layer nn.TransformerDecoder head (conformer.py:275-299), full precision."""
+    """Stock 2-layer nn.TransformerDecoder head (conformer.py:275-299), full precision.
+
+    The modules (and so the initialisation and the checkpoint keys
+    ``decoder.dec.layers.i.{self_attn,multihead_attn}.{in_proj_weight,in_proj_bias,
+    out_proj.*}``, ``linear1/2``, ``norm1/2/3``) are torch's ``nn.TransformerDecoderLayer``
+    (batch_first, post-norm, relu). On a ROCm device the forward is restated functionally
+    (``_layer``) with the same math on graph-safe pieces -- ``linear`` (fixed-order bias
+    gradients), the HIP LayerNorm, explicit scaled-dot-product attention -- because torch's
+    own bias-gradient reductions are not replayable from a HIP graph on this ROCm build
+    (onebit_asr/linear.py). CPU tensors run torch's modules as they are."""
 
     def __init__(self, vocab_size: int, d_model: int, n_layers: int, n_heads: int,
                  d_ff: int, dropout: float, pad_id: int):
@@ -409,18 +419,69 @@ class TransformerDecoder(nn.Module):
         self.ln = LayerNorm(d_model)
         self.out = nn.Linear(d_model, vocab_size)
 
+    @staticmethod
+    def _attention(mha: nn.MultiheadAttention, x, mem, bias, training: bool):
+        """torch.nn.functional.multi_head_attention_forward (need_weights=False) for
+        batch-first inputs: packed in-projection, softmax(q k^T / sqrt(dh) + bias) with
+        attention dropout, out-projection."""
+        e, h = mha.embed_dim, mha.num_heads
+        dh = e // h
+        w, b = mha.in_proj_weight, mha.in_proj_bias
+        bsz, lq, _ = x.shape
+        if mem is None:  # self-attention: one packed projection, chunks q | k | v
+            q, k, v = linear(x, w, b).chunk(3, dim=-1)
+            lk = lq
+        else:
+            q = linear(x, w[:e], b[:e])
+            k, v = linear(mem, w[e:], b[e:]).chunk(2, dim=-1)
+            lk = mem.size(1)
+        q = q.reshape(bsz, lq, h, dh).transpose(1, 2)
+        k = k.reshape(bsz, lk, h, dh).transpose(1, 2)
+        v = v.reshape(bsz, lk, h, dh).transpose(1, 2)
+        att = torch.matmul(q, k.transpose(-2, -1)) * (1.0 / math.sqrt(dh)) + bias
+        att = F.dropout(torch.softmax(att, dim=-1), mha.dropout, training)
+        ctx = torch.matmul(att, v).transpose(1, 2).reshape(bsz, lq, e)
+        return linear(ctx, mha.out_proj.weight, mha.out_proj.bias)
+
+    def _layer(self, lyr: nn.TransformerDecoderLayer, x, mem, self_bias, cross_bias):
+        """nn.TransformerDecoderLayer.forward, norm_first=False:
+        x = norm1(x + sa(x)); x = norm2(x + mha(x, mem)); x = norm3(x + ff(x))."""
+        tr = self.training
+        n1, n2, n3 = lyr.norm1, lyr.norm2, lyr.norm3
+        sa = self._attention(lyr.self_attn, x, None, self_bias, tr)
+        x = layer_norm(x + F.dropout(sa, lyr.dropout1.p, tr), n1.weight, n1.bias, n1.eps)
+        ca = self._attention(lyr.multihead_attn, x, mem, cross_bias, tr)
+        x = layer_norm(x + F.dropout(ca, lyr.dropout2.p, tr), n2.weight, n2.bias, n2.eps)
+        ff = linear(F.dropout(F.relu(linear(x, lyr.linear1.weight, lyr.linear1.bias)),
+                              lyr.dropout.p, tr), lyr.linear2.weight, lyr.linear2.bias)
+        return layer_norm(x + F.dropout(ff, lyr.dropout3.p, tr), n3.weight, n3.bias, n3.eps)
+
     def forward(self, tgt_inp, memory, memory_mask, tgt_key_padding_mask):
         tt = tgt_inp.size(1)
         future = torch.ones(tt, tt, device=tgt_inp.device).triu(diagonal=1).bool()
         causal = torch.zeros(tt, tt, device=tgt_inp.device).masked_fill(future, float("-inf"))
-        # tgt_is_causal=True is what torch's _detect_is_causal_mask concludes for this mask in
-        # the reference call; passing it skips that check's device->host sync (the
-        # attention math is unchanged: the explicit mask is still used).
         tok = embedding(tgt_inp, self.emb.weight, self.emb.padding_idx)
-        y = self.dec(tok, memory, tgt_mask=causal,
-                     memory_key_padding_mask=(memory_mask == 0),
-                     tgt_key_padding_mask=tgt_key_padding_mask, tgt_is_causal=True)
-        return self.out(self.ln(y))
+        if not (memory.is_cuda and memory.dtype == torch.float32):
+            # tgt_is_causal=True is what torch's _detect_is_causal_mask concludes for this mask
+            # in the reference call (the explicit mask is still used).
+            y = self.dec(tok, memory, tgt_mask=causal,
+                         memory_key_padding_mask=(memory_mask == 0),
+                         tgt_key_padding_mask=tgt_key_padding_mask, tgt_is_causal=True)
+            return self.out(self.ln(y))
+        # additive masks as multi_head_attention_forward merges them: causal + key padding
+        # for self-attention, memory padding for cross-attention ([B, 1, Lq, Lk])
+        neg = float("-inf")
+        self_bias = causal.view(1, 1, tt, tt) + torch.zeros(
+            tgt_key_padding_mask.shape, device=tok.device).masked_fill(
+            tgt_key_padding_mask, neg).view(-1, 1, 1, tt)
+        cross_bias = torch.zeros(memory_mask.shape, device=tok.device).masked_fill(
+            memory_mask == 0, neg).view(memory_mask.size(0), 1, 1, -1)
+        y = tok
+        for lyr in self.dec.layers:
+            y = self._layer(lyr, y, memory, self_bias, cross_bias)
+        if self.dec.norm is not None:
+            y = layer_norm(y, self.dec.norm.weight, self.dec.norm.bias, self.dec.norm.eps)
+        return linear(self.ln(y), self.out.weight, self.out.bias)
 
 
 class ConformerASR(nn.Module):
@@ -442,7 +503,7 @@ class ConformerASR(nn.Module):
 
     def forward(self, batch, precision: int, sp_mask=None):
         enc_out, enc_mask = self.encoder(batch["feats"], batch["feat_lens"], precision, sp_mask)
-        return enc_out, enc_mask, self.ctc_head(enc_out)
+        return enc_out, enc_mask, linear(enc_out, self.ctc_head.weight, self.ctc_head.bias)
 
     def decode_logits(self, enc_out, enc_mask, tgt_inp, tgt_pad_mask):
         return self.decoder(tgt_inp, enc_out, enc_mask, tgt_pad_mask)

@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .linear import colsum
 
 __all__ = ["depthwise_conv1d", "conv_module_supported", "conv_module_fused", "colsum",
            "conv2d_bias_relu"]
@@ -202,19 +203,6 @@ class _PointwiseFn(torch.autograd.Function):
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = colsum(g)
         return gx, gw, gb
-
-
-def colsum(x2d: torch.Tensor) -> torch.Tensor:
-    """Column sums of a [rows, N] fp32 matrix (fixed order; csrc/fused.hip)."""
-    x2d = x2d.contiguous()
-    rows, n = x2d.shape
-    out = torch.empty((n,), dtype=torch.float32, device=x2d.device)
-    lib = _lib.load()
-    wsb = lib.ob_colsum_workspace(n)
-    ws = torch.empty((wsb,), dtype=torch.uint8, device=x2d.device)
-    _lib.check(lib.ob_colsum(x2d.data_ptr(), rows, n, out.data_ptr(), ws.data_ptr(), wsb,
-                             _lib.stream_of(x2d)), "ob_colsum")
-    return out
 
 
 class _BiasReluFn(torch.autograd.Function):

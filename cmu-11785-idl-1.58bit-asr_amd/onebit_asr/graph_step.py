@@ -11,6 +11,13 @@ AdamW with a device lr) the whole body is captured once and replayed:
 * graph B (merged into A when N == 1): clip_grad_norm_(5.0) + AdamW as the three-launch
   ``FusedAdamW`` (the 1/world average is folded into its gradient scale).
 
+Both step bodies capture: the stacked one (``OneBitStep(stacked=True)``) and the
+reference's literal three forwards. Nothing inside the captured region may rely on a
+captured ``hipMemsetAsync`` (not replayed correctly on this ROCm build, see
+onebit_asr/linear.py): torch's bias-gradient reductions are replaced by fixed-order HIP
+column sums, and the library zeroes its counters with kernels. ``tests/
+test_graph_step_gpu.py`` checks that every replay reproduces the eager gradients.
+
 What changes per step without re-capture:
 * the stochastic-precision mask: ``StackedBits.set`` / ``DeviceBits.set`` copies the new
   per-block bitwidths into the device slots the captured BitLinear kernels read;
@@ -153,8 +160,27 @@ class GraphedTrainStep:
     def _warm(self):
         for _ in range(self.warmup_iters):
             self.loss, self.parts = self._eager()
-            self.sched.step()
-            self.steps_done += 1
+
+    def _snapshot(self):
+        return [p.detach().clone() for p in self.params]
+
+    @torch.no_grad()
+    def _restore(self, snap):
+        """Undo the warm-up: parameters back to their values, optimizer state and schedule
+        back to a fresh start (AdamW's state starts at zero with step 0), so that the
+        first ``step()`` performs exactly one update (train.py:114-120). In-place writes
+        keep every address the captured graph will use and bump the parameters' versions
+        (which invalidates version-keyed code caches)."""
+        for p, s in zip(self.params, snap):
+            p.copy_(s)
+        if self.fused:
+            self.opt.reset_state()
+        else:
+            for st in self.opt.state.values():
+                for v in st.values():
+                    if isinstance(v, torch.Tensor):
+                        v.zero_()
+        self.sched.reset()
 
     @staticmethod
     def _drop_code_caches(module):
@@ -163,32 +189,25 @@ class GraphedTrainStep:
                 m._codes_cache = {}
 
     def prime(self, batch, sp_mask):
-        """Static inputs, flat grads, optimizer; ``warmup_iters`` real (eager) steps on a side
-        stream; then capture. The warm-up steps are training steps: they update the model
-        and advance the schedule like any other step."""
+        """Static inputs, flat grads, optimizer; ``warmup_iters`` eager steps on a side stream
+        (library heuristics, allocator) whose effects are then undone; then capture. The
+        warm-up leaves no trace: the model, optimizer and schedule are restored."""
         self._set_batch(batch)
         self.bits.set(sp_mask)
         if self.device.type != "cuda":  # host path (gloo tests of the exchange logic)
             self.use_graph = False
             self._discover_params()
-            self._warm()
             return
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             self._discover_params()
+            snap = self._snapshot()
             self._warm()
+            self._restore(snap)
         torch.cuda.current_stream(self.device).wait_stream(side)
         if not self.use_graph:
             return
-        use_stacked = getattr(self.step_module, "_use_stacked", None)
-        if use_stacked is not None and not use_stacked():
-            # Measured: replaying the literal three-forward step corrupts the gradients of
-            # parameters that receive three broadcast-reduced contributions (pos_bias_u/v)
-            # at Conformer-S; the stacked step gives each parameter one contribution.
-            raise ValueError("HIP-graph capture needs OneBitStep(stacked=True); run the "
-                             "literal three-pass step with use_graph=False")
-        warm_loss, warm_parts = self.loss.clone(), self.parts.clone()
         torch.cuda.synchronize(self.device)
         self._drop_code_caches(self.step_module)
         self.graph_a = torch.cuda.CUDAGraph()
@@ -202,19 +221,17 @@ class GraphedTrainStep:
             with torch.cuda.graph(self.graph_b, pool=pool):
                 self._update()
         torch.cuda.synchronize(self.device)
-        self._warm_result = (warm_loss, warm_parts)
 
     # ------------------------------------------------------------------ step
     def step(self, batch, sp_mask):
-        """One training step (train.py:82-120). Returns device (loss, parts); no host sync.
-        The first call primes and captures (and runs ``warmup_iters`` steps)."""
+        """One training step (train.py:82-120): exactly one optimizer update per call.
+        Returns device (loss, parts); no host sync. The first call also primes and
+        captures."""
         if self.opt is None:
             self.prime(batch, sp_mask)
-            if self.graph_a is not None:  # the captured outputs hold nothing yet
-                return self._warm_result
-            return self.loss, self.parts
-        self._set_batch(batch)
-        self.bits.set(sp_mask)
+        else:
+            self._set_batch(batch)
+            self.bits.set(sp_mask)
         if self.graph_a is None:
             self.loss, self.parts = self._eager()
         else:

@@ -1,0 +1,91 @@
+"""Full-precision ``F.linear`` whose backward is safe to replay from a HIP graph.
+
+The reference's full-precision linears (subsampling ``out``, ``ctc_head``, the decoder's
+projections, feed-forward and output layers; onebit_asr/conformer.py:195,275-299,313) run
+stock ``F.linear`` there. Their bias gradient is torch's column reduction, which on this
+ROCm build takes a two-level "global reduce" path whose semaphores are cleared by a
+``hipMemsetAsync``; captured into a HIP graph that memset is not re-executed correctly on
+replays after the first (tools/memset_graph_repro.py, tools/reduce_graph_repro.py), so
+every replayed step after the first produced garbage bias gradients. Here the GEMMs stay
+library GEMMs (hipBLASLt / rocBLAS), and the bias gradient is the fixed-order column sum
+``ob_colsum`` (csrc/fused.hip) -- deterministic and graph-safe. Same arithmetic as
+``F.linear`` up to summation order.
+
+``dtype`` (optional) computes the GEMMs in that type (BASELINE configs[3]: bf16
+``nn.Linear``); inputs, outputs and gradients stay fp32.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+__all__ = ["linear", "colsum"]
+
+
+def colsum(x2d: torch.Tensor) -> torch.Tensor:
+    """Column sums of a [rows, N] fp32 matrix (fixed order; csrc/fused.hip)."""
+    x2d = x2d.contiguous()
+    rows, n = x2d.shape
+    out = torch.empty((n,), dtype=torch.float32, device=x2d.device)
+    lib = _lib.load()
+    wsb = lib.ob_colsum_workspace(n)
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=x2d.device)
+    _lib.check(lib.ob_colsum(x2d.data_ptr(), rows, n, out.data_ptr(), ws.data_ptr(), wsb,
+                             _lib.stream_of(x2d)), "ob_colsum")
+    return out
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, dtype):
+        k = x.shape[-1]
+        x2d = x.reshape(-1, k)
+        if dtype is None:
+            y = torch.addmm(bias, x2d, weight.t()) if bias is not None else x2d @ weight.t()
+        else:
+            wd = weight.to(dtype)
+            yd = (torch.addmm(bias.to(dtype), x2d.to(dtype), wd.t()) if bias is not None
+                  else x2d.to(dtype) @ wd.t())
+            y = yd.to(torch.float32)
+        ctx.save_for_backward(x2d, weight)
+        ctx.meta = (bias is not None, dtype, x.shape)
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x2d, weight = ctx.saved_tensors
+        has_b, dtype, xshape = ctx.meta
+        g2 = g.reshape(-1, weight.shape[0])
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
+        gx = gw = gb = None
+        if dtype is None:
+            if ctx.needs_input_grad[0]:
+                gx = (g2 @ weight).view(xshape)
+            if ctx.needs_input_grad[1]:
+                gw = g2.t() @ x2d
+        else:
+            gd = g2.to(dtype)
+            if ctx.needs_input_grad[0]:
+                gx = (gd @ weight.to(dtype)).to(torch.float32).view(xshape)
+            if ctx.needs_input_grad[1]:
+                gw = (gd.t() @ x2d.to(dtype)).to(torch.float32)
+        if has_b and ctx.needs_input_grad[2]:
+            gb = colsum(g2)
+        return gx, gw, gb, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """``F.linear(x, weight, bias)`` (computed in ``dtype`` if given) with a graph-safe,
+    deterministic bias gradient on a ROCm device; stock ``F.linear`` elsewhere."""
+    if not (x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32):
+        if dtype is not None:
+            b = bias.to(dtype) if bias is not None else None
+            return F.linear(x.to(dtype), weight.to(dtype), b).to(x.dtype)
+        return F.linear(x, weight, bias)
+    return _LinearFn.apply(x, weight, bias, dtype)

@@ -142,6 +142,15 @@ class FusedAdamW:
         for i in self._members:
             torch.autograd.graph.increment_version(self.params[i])
 
+    @torch.no_grad()
+    def reset_state(self):
+        """Back to a fresh optimizer (zero moments, step 0) in place: captured graphs keep
+        their addresses."""
+        for t in self.exp_avg + self.exp_avg_sq:
+            t.zero_()
+        self.step_t.zero_()
+        self.total_norm.zero_()
+
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:
             if set_to_none:

@@ -33,6 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .linear import linear
 
 __all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "set_quant_off", "DeviceBits",
            "DynamicBitwidth", "PassBits", "StackedBits", "set_act_quant", "ACT_QUANT_MODES",
@@ -495,14 +496,12 @@ class QuantizedLinear(nn.Module):
 
     def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
         if self.quant_off is not None:  # configs[3] ceiling: no quantizer, library GEMM
-            dt = self.quant_off
-            b = self.bias.to(dt) if self.bias is not None else None
-            return F.linear(x.to(dt), self.weight.to(dt), b).to(x.dtype)
+            return linear(x, self.weight, self.bias, dtype=self.quant_off)
         if isinstance(bitwidth, PassBits):
             return self._forward_passes(x, bitwidth)
         bits = _check_bitwidth(bitwidth)
-        if bits == 32:  # quant.py:121-122
-            return F.linear(x, self.weight, self.bias)
+        if bits == 32:  # quant.py:121-122 (F.linear; graph-safe bias gradient)
+            return linear(x, self.weight, self.bias)
         _require_device(x, self.weight)
         lead = x.shape[:-1]
         x2d = x.reshape(-1, self.in_features)

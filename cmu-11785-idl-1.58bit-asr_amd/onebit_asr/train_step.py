@@ -58,6 +58,15 @@ class WarmupCosine:
         progress = min(max((step - self.warmup_steps) / span, 0.0), 1.0)
         return self.min_lr_ratio + 0.5 * (1 - self.min_lr_ratio) * (1 + math.cos(math.pi * progress))
 
+    def reset(self):
+        """Back to step 0 at the initial learning rate (before any optimizer step)."""
+        self.step_num = 0
+        for group in self.optimizer.param_groups:
+            if isinstance(group["lr"], torch.Tensor):
+                group["lr"].fill_(group["initial_lr"])
+            else:
+                group["lr"] = group["initial_lr"]
+
     def step(self):
         self.step_num += 1
         s = self.scale(self.step_num)
