@@ -210,22 +210,36 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
 
 
 def traffic_from(path, kernel):
+    """PMC HBM bytes per launch from profiles/pmc_traffic.json, only when it was measured
+    on the kernel sources of this tree (its csrc_sha256 == the current source digest);
+    otherwise None (the counters belong to another kernel revision)."""
+    from onebit_asr._lib import source_digest
+
     try:
         data = json.loads(Path(path).read_text())
-        return data.get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+    if data.get("csrc_sha256") != source_digest():
+        return None
+    return data.get(kernel, {}).get("hbm_bytes_per_launch")
 
 
 # ------------------------------------------------------------------------- cpu baseline
-def cpu_baseline(seconds: float):
-    """The oracle step (CPU restatement) on a bounded sample of the same workload."""
+def cpu_baseline(seconds: float, bsz: int = 4):
+    """The oracle step (CPU restatement) on a bounded sample of the same workload, on the
+    host cores this process may run on (sched_getaffinity; os.cpu_count() is reported
+    too). torch intra-op threads: the faster of all those cores and 16 (the box's CPU
+    share), both timed on one step and stated in the sample."""
     from onebit_asr.conformer import ConformerASR
     from onebit_asr.data import CONFORMER_S, synthetic_batch
+    from onebit_asr.train_step import sample_sp_mask
     from oracle.conformer_oracle import OracleConformer, oracle_step_loss
 
-    threads = min(os.cpu_count() or 1, 16)
-    torch.set_num_threads(threads)
+    n_cpu = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n_aff = n_cpu
     torch.manual_seed(1234)
     prod = ConformerASR(N_MELS, VOCAB, **CONFORMER_S)
     orc = OracleConformer(prod.state_dict(), input_dim=N_MELS, vocab_size=VOCAB, d_model=144,
@@ -233,10 +247,8 @@ def cpu_baseline(seconds: float):
                           dec_heads=4, dec_d_ff=1024, dropout=0.1)
     orc.train()
     opt = torch.optim.AdamW(orc.parameters(), lr=5e-4, betas=(0.9, 0.98), weight_decay=1e-2)
-    bsz = 2
     b = synthetic_batch([1000] * bsz, [40] * bsz, seed=99)
     g = torch.Generator().manual_seed(4321)
-    from onebit_asr.train_step import sample_sp_mask
 
     def one():
         loss, _ = oracle_step_loss(orc, b, sample_sp_mask(16, generator=g))
@@ -245,7 +257,15 @@ def cpu_baseline(seconds: float):
         torch.nn.utils.clip_grad_norm_(orc.parameters(), 5.0)
         opt.step()
 
-    one()  # warm-up
+    trial = {}
+    for th in sorted({n_aff, min(16, n_aff)}):
+        torch.set_num_threads(th)
+        one()  # warm-up at this thread count
+        t0 = time.perf_counter()
+        one()
+        trial[th] = time.perf_counter() - t0
+    threads = min(trial, key=trial.get)
+    torch.set_num_threads(threads)
     times = []
     t_end = time.perf_counter() + seconds
     while time.perf_counter() < t_end and len(times) < 20:
@@ -261,11 +281,13 @@ def cpu_baseline(seconds: float):
                 break
     except Exception:
         pass
+    tried = ", ".join(f"{k} threads {bsz * 1000 / v:.0f}" for k, v in sorted(trial.items()))
     return {"value": round(bsz * 1000 / t, 1), "unit": "mel-frames/s", "cores": threads,
             "kind": "port",
             "sample": f"oracle (CPU fp32 restatement) full 3-pass step + AdamW on Conformer-S, "
-                      f"B={bsz} x 1000 frames, median of {len(times)} steps after 1 warm-up; "
-                      f"{threads} threads on {cpu}"}
+                      f"B={bsz} x 1000 frames, median of {len(times)} steps after warm-up; "
+                      f"{threads} torch threads on {cpu} (affinity {n_aff} cores, "
+                      f"os.cpu_count() {n_cpu}; one-step trial mel-frames/s: {tried})"}
 
 
 # ------------------------------------------------------------------------- inference
@@ -440,8 +462,9 @@ def main():
                             seed=1234 + rank, device=dev)
     sp_gen = torch.Generator().manual_seed(4321)  # same SP masks on every rank
     if distributed:
-        for p in model.parameters():  # replicas start identical (DDP does the same)
-            dist.broadcast(p.data, 0)
+        with torch.no_grad():  # replicas start identical (DDP does the same); in place on
+            for p in model.parameters():  # the parameter itself, so its version is bumped
+                dist.broadcast(p, 0)
 
     if args.eager:
         if distributed:
@@ -514,6 +537,8 @@ def main():
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
                    "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
                    "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP",
+                   "subsampling": "computed once, shared by the 3 stacked passes (exact: no "
+                                  "dropout, full-precision weights; the reference runs it 3x)",
                    "conv_pointwise": "ternary (opt-in)" if args.conv_pw_ternary else "fp32 (reference)"},
         "final_loss": round(loss_val, 4),
     }

@@ -169,5 +169,20 @@ def ptr(t: "torch.Tensor | None") -> int | None:
     return None if t is None else t.data_ptr()
 
 
+def source_digest() -> str:
+    """sha256 over the library's sources (csrc/*.hip, csrc/*.h, include/*.h, file names
+    included): identifies the kernel revision a measurement (e.g. PMC traffic) belongs to."""
+    import hashlib
+
+    pkg = Path(__file__).resolve().parents[1]
+    files = sorted(list((pkg / "csrc").glob("*.hip")) + list((pkg / "csrc").glob("*.h")) +
+                   list((pkg.parent / "include").glob("*.h")))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
 def stream_of(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream

@@ -541,6 +541,16 @@ class QuantizedLinear(nn.Module):
                                      codes2, codes2_t, codes1, codes1_t)
         return y.view(*lead, self.out_features)
 
+    def invalidate_codes(self) -> None:
+        """Drop the cached 2-bit codes. Needed after writing ``weight`` / ``alpha`` through
+        ``.data`` (such writes do not bump the version counter the cache is keyed on);
+        optimizer steps, ``load_state_dict`` and in-place ops on the parameters do not need it."""
+        self._codes_cache = {}
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._codes_cache = {}
+        return super()._load_from_state_dict(*args, **kwargs)
+
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate cached codes
         self._codes_cache = {}
         return super()._apply(fn, *args, **kwargs)

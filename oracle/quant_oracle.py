@@ -13,8 +13,8 @@ Three restatements of y00njaekim/CMU-11785-IDL-1.58bit-ASR ``onebit_asr/quant.py
 Parity anchor: the reference ships no golden vectors or known-answer tests for this path
 (SURVEY.md §4, §8c), and importing/running it here was denied. The
 restatements are pinned by hand-derived known answers in tests/golden/quant_kat.json and by
-agreeing with each other; seeded fixtures in tests/golden/ are generated from them by
-tests/golden/make_golden.py.
+agreeing with each other (tests/test_oracle.py); the model-level restatement
+(conformer_oracle.py) is pinned by tests/golden/model_kat.json (tests/test_model_kat.py).
 """
 from __future__ import annotations
 

@@ -9,7 +9,8 @@ configs[1] -- the measured training step, dropout 0:
     <= 1e-5, parts rtol 1e-5, every parameter gradient rel-L2 <= 1e-4 (parameters whose true
     gradient is zero -- the depthwise bias before BatchNorm, the key biases under softmax
     shift invariance -- within 1e-7 absolute instead; alpha gradients, single
-    cancellation-prone sums over N*K, rel-L2 <= 2e-3 as at cfg1);
+    cancellation-prone sums over N*K, within max(2e-3 relative, 1e-3 x the model's median
+    alpha gradient));
   * the literal step replays too (it used to be refused by GraphedTrainStep).
 configs[3] -- quant off (every BitLinear -> bf16 F.linear): the stacked step is finite,
   replays reproduce eager gradients (rel <= 1e-5), and one layer's output equals
@@ -84,11 +85,19 @@ def test_s_literal_matches_stacked_and_replays(s_model, gpu, stacked_ref):
     assert abs(l_l.item() - l_s.item()) <= 1e-5 * abs(l_s.item()), (l_l, l_s)
     torch.testing.assert_close(p_l, p_s, rtol=1e-5, atol=1e-6)
     errs = rel_errors(g_l, g_s)
+    # an alpha gradient is ONE sum of N*K terms that can cancel to almost nothing (seen:
+    # 2.5e-5 against a median of 0.16); its rounding noise scales with the terms, not
+    # with the sum, so below the model's median it is bounded absolutely
+    med = sorted(abs(g_s[k].item()) for k in errs if k.endswith(".alpha"))
+    med = med[len(med) // 2]
     for k, e in errs.items():
         if any(z in k for z in ZERO_GRAD):
             assert (g_l[k] - g_s[k]).abs().max().item() <= 1e-7, (k, e)
-        else:  # alpha: one cancellation-prone sum over N*K (the cfg1 oracle bar)
-            assert e <= (2e-3 if k.endswith(".alpha") else 1e-4), (k, e)
+        elif k.endswith(".alpha"):
+            d = abs(g_l[k].item() - g_s[k].item())
+            assert d <= max(2e-3 * abs(g_s[k].item()), 1e-3 * med), (k, g_l[k], g_s[k], med)
+        else:
+            assert e <= 1e-4, (k, e)
 
 
 def test_s_quant_off_step(gpu):

@@ -3,8 +3,11 @@
 cfg1 (SURVEY §8d / BASELINE configs[0]): 2-block d_model=64 Conformer, V=5004, B=2 with
 real utterance shapes [734, 349] frames / [27, 12] tokens, dropout 0. Bars:
   CTC logits max|err| <= 1e-3, CTC loss and step loss rel <= 1e-4,
-  every QuantizedLinear parameter gradient rel-L2 <= 1e-3 (alpha, a single
-  cancellation-prone sum: <= 2e-3).
+  EVERY parameter gradient rel-L2 <= 1e-3 (alpha, a single cancellation-prone sum:
+  <= 2e-3) -- QuantizedLinear layers, pos_bias_u/v, LayerNorms, conv module, subsampling,
+  CTC head and decoder; parameters whose true gradient is zero (key biases, the
+  depthwise bias before BatchNorm, the key third of the decoder's in_proj_bias) within
+  1e-6 absolute.
 """
 import numpy as np
 import pytest
@@ -56,6 +59,22 @@ def test_forward_parity(pair, batch, gpu, precision, sp_mask):
     assert abs(lp - lo) <= 1e-4 * abs(lo), (lp, lo)
 
 
+# parameters whose true gradient is zero (softmax shift invariance for key biases, a bias
+# right before BatchNorm): both sides hold rounding noise there
+ZERO_GRAD = ("k_proj.bias", "conv.dw.bias", "in_proj_bias")
+BAR_QL = 1e-3      # QuantizedLinear weight / bias
+BAR_ALPHA = 2e-3   # alpha: one cancellation-prone sum over N*K
+BAR_OTHER = 1e-3   # every other parameter (LN, conv module, subsampling, heads, decoder)
+
+
+def _bar(name):
+    if name.endswith(".alpha"):
+        return BAR_ALPHA
+    if name.startswith("encoder.blocks.") and any(s in name for s in (".lin1.", ".lin2.", "_proj.")):
+        return BAR_QL
+    return BAR_OTHER
+
+
 def test_step_loss_and_grads(pair, batch, gpu):
     from onebit_asr.train_step import OneBitStep
     from oracle.conformer_oracle import oracle_step_loss
@@ -72,20 +91,29 @@ def test_step_loss_and_grads(pair, batch, gpu):
     assert abs(loss_p.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item())
     np.testing.assert_allclose(parts_p.cpu().numpy(), parts_o.numpy(), rtol=1e-4, atol=1e-6)
     ref = dict(orc.named_reference_parameters())
-    checked = 0
+    worst = {}
+    names = [n for n, _ in prod.named_parameters()]
+    assert set(names) == set(ref), set(names) ^ set(ref)
     for name, p in prod.named_parameters():
-        if not name.startswith("encoder.blocks.") or not any(
-                s in name for s in (".lin1.", ".lin2.", "_proj.")):
-            continue
         g_p = p.grad.detach().cpu().double()
         g_o = ref[name].grad.detach().double()
-        denom = g_o.norm().item()
-        rel = (g_p - g_o).norm().item() / max(denom, 1e-12)
-        # alpha gradients are single cancellation-prone sums (sum of G * term over N*K)
-        bar = 2e-3 if name.endswith(".alpha") else 1e-3
-        assert rel <= bar or (g_p - g_o).abs().max().item() <= 1e-7, (name, rel)
-        checked += 1
-    assert checked == 2 * 9 * 3  # weight, alpha, bias of 9 layers x 2 blocks
+        d = g_p - g_o
+        if any(z in name for z in ZERO_GRAD):
+            if name.endswith("in_proj_bias"):  # only the key third is zero in truth
+                e = g_o.numel() // 3
+                for part in (slice(0, e), slice(2 * e, 3 * e)):
+                    rel = d[part].norm().item() / max(g_o[part].norm().item(), 1e-12)
+                    assert rel <= BAR_OTHER, (name, rel)
+                d, g_o = d[e:2 * e], g_o[e:2 * e]
+            # noise of two summation orders around a true zero: absolute, against the
+            # gradient scale of the whole model
+            assert d.abs().max().item() <= 1e-6, (name, d.abs().max().item())
+            continue
+        rel = d.norm().item() / max(g_o.norm().item(), 1e-12)
+        bar = _bar(name)
+        worst[name] = rel
+        assert rel <= bar or d.abs().max().item() <= 1e-7, (name, rel, bar)
+    assert len(worst) > 100
 
 
 def test_train_step_runs_and_updates(gpu):

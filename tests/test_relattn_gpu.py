@@ -27,8 +27,9 @@ CASES = [  # (Bt, P, T, H, d, lens)
 
 
 def _ref(q, k, v, pos, u, vb, lens, H, keep=None, p=0.0):
-    """Reference ops in float64 (conformer.py:115-127 with rel_shift :97-103)."""
-    from onebit_asr.conformer import rel_shift
+    """Reference ops in float64 (conformer.py:115-127 with rel_shift :97-103, the oracle's
+    gather restatement -- not the product's own rel_shift)."""
+    from oracle.conformer_oracle import _rel_shift_gather as rel_shift
 
     bt, t, c = q.shape
     d = c // H

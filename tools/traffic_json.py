@@ -14,6 +14,9 @@ import glob
 import json
 import statistics
 import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
 
 # launches per step (bench.py ql_shapes at Conformer-S: 16 blocks, 2 FFNs, 4 q/k/v/out)
 COUNT = {"lin1": 32, "lin2": 32, "qkvo": 64, "pos": 16}
@@ -32,7 +35,11 @@ def per_dispatch(path, sub):
 
 def main():
     d = sys.argv[1]
-    out, fam = {"source": d, "note": __doc__.split("\n\n")[1].replace("\n", " ")}, {}
+    sys.path[:0] = [str(ROOT / "cmu-11785-idl-1.58bit-asr_amd")]
+    from onebit_asr._lib import source_digest
+
+    out, fam = {"source": d, "note": __doc__.split("\n\n")[1].replace("\n", " "),
+                "csrc_sha256": source_digest()}, {}
     for shape, cnt in COUNT.items():
         for op, subs in KERNELS.items():
             if shape == "pos" and op == "dx":
