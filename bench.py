@@ -193,8 +193,12 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
     avg_t = t_us / n
     gbs = (by / n) / (avg_t * 1e-6) / 1e9
     tfs = (fl / n) / (avg_t * 1e-6) / 1e12
-    # fp32-MFMA-equivalent kernels: the binding roof is whichever takes longer at peak
-    bound_mfma = (fl / PEAK_FP32_MFMA_TFLOPS / 1e12) > (by / PEAK_HBM_GBS / 1e9)
+    # The ternary GEMM streams fp32 activations against 2-bit weights: HBM-bound by
+    # construction (its exact-fp32 bf16x3 MFMA work is far below the bf16 roof). The dW GEMM
+    # is a dense fp32 x fp32 product (exact via bf16x6): priced against the fp32 dense
+    # MFMA peak of its dtype unless its bytes take longer at the HBM peak.
+    bound_mfma = dom != "ternary_gemm" and (
+        (fl / PEAK_FP32_MFMA_TFLOPS / 1e12) > (by / PEAK_HBM_GBS / 1e9))
     if bound_mfma:
         roof = {"bound": "mfma", "achieved": round(tfs, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(tfs / PEAK_FP32_MFMA_TFLOPS, 4)}

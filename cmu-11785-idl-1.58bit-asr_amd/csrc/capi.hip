@@ -1,5 +1,7 @@
 // capi.hip — the C ABI declared in include/onebit_hip.h: argument validation, workspace
 // carving and launch-error reporting around the launchers in quant.hip / gemm.hip.
+#include <algorithm>
+
 #include "../../include/onebit_hip.h"
 #include "ob_launch.h"
 #include <stdint.h>
@@ -32,7 +34,9 @@ DwWorkspace dw_layout(int64_t P, int64_t M, int64_t N, int64_t K) {
   DwWorkspace w;
   w.part = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N * (size_t)K);
   w.part_db = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N);
-  w.apart = align_up(16 + sizeof(float) * (size_t)ste_reduce_blocks(N * K + N));
+  const int64_t napart = std::max<int64_t>(ste_reduce_blocks(N * K + N),
+                                           p.tiles_n * p.tiles_k * p.chunks);
+  w.apart = align_up(16 + sizeof(float) * (size_t)napart);
   w.total = w.part + w.part_db + w.apart;
   return w;
 }
@@ -183,6 +187,13 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N
     chunks = 1;
     cpp = 1;
     P = 1;
+  } else if (p.variant >= 9) {  // LDS path: alpha partials in the GEMM, no ticket
+    const DwAlpha al{W, alpha, alpha_raw, bits, reinterpret_cast<const int*>(bits_dev),
+                     reinterpret_cast<const int*>(pass_bits), apart};
+    launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s, &al);
+    launch_dw_finish(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, apart,
+                     (int)(p.tiles_n * p.tiles_k * p.chunks), dW, db, dalpha, s);
+    return launched();
   } else {
     launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s);
   }

@@ -406,6 +406,354 @@ __global__ __launch_bounds__(kThreads, 2) void dw_bf16x6_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// dW partial, LDS-shared bf16x6 (shapes with N % 48 == 0 and K % 48 == 0, i.e. every
+// Conformer width). Block = WN x WK waves, wave (wn, wk) owns the 48x48 output sub-tile
+// n0 + 48wn.., k0 + 48wk..; block tile BN x BK = 48WN x 48WK; one M chunk per block.
+// Per 32-row step the block loads dY[32][BN] and X[32][BK] once (fp32, coalesced), splits
+// every element ONCE into hi/mid/lo bf16 (round-to-nearest, exact: x = hi + mid + lo) and
+// stores the planes column-major in LDS (column = 32 rows of one n or k, 64 B per plane,
+// slot pitch 224 B = 3 planes + 32 B: conflict-free ds_read_b128 for the
+// MFMA fragments; the three planes of a column sit side by side in its 224-B slot). Every
+// wave then reads its 16x16x32 A / B fragments from LDS, so a split
+// element feeds WK (dY) or WN (X) waves instead of being re-split per output tile (the
+// register-only kernel above split each dY element 3x and each X element 9x at lin1).
+// Double-buffered: step s+1 is split and stored while step s's MFMAs run; one barrier per
+// step. Loader unit = 4 rows x 4 columns of one operand (row quad fastest across lanes:
+// conflict-free ds_write_b64).
+// ---------------------------------------------------------------------------------
+// Profiling switches (tools/variant.sh builds; 0 in the product, results wrong otherwise):
+// drop the MFMAs / the split+store / the global loads of the LDS kernel to price them.
+#ifndef DW_EXP_NOMFMA
+#define DW_EXP_NOMFMA 0
+#endif
+#ifndef DW_EXP_NOSTORE
+#define DW_EXP_NOSTORE 0
+#endif
+#ifndef DW_EXP_NOLOAD
+#define DW_EXP_NOLOAD 0
+#endif
+#ifndef DW_EXP_STEPS1
+#define DW_EXP_STEPS1 0
+#endif
+#ifndef DW_EXP_NOOUT
+#define DW_EXP_NOOUT 0
+#endif
+#ifndef DW_EXP_EXIT
+#define DW_EXP_EXIT 0
+#endif
+constexpr int kLdsPitch = 224;  // bytes per column slot: 3 planes x 32 bf16 rows + 32 B pad
+constexpr int kStepRows = 32;
+
+template <int WN, int WK>
+struct DwLdsCfg {
+  static constexpr int BN = 48 * WN, BK = 48 * WK;
+  static constexpr int kThr = 64 * WN * WK;
+  static constexpr int kCols = BN + BK;                       // dY columns then X columns
+  static constexpr int kBuf = kCols * kLdsPitch;              // one step, three planes
+  static constexpr int kUY = (BN * 4 + kThr - 1) / kThr;      // dY loader units per thread
+  static constexpr int kUX = (BK * 4 + kThr - 1) / kThr;      // X loader units per thread
+};
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// Round two fp32 to bf16 (v_cvt_pk_bf16_f32), packed (a low, b high); also returns the two
+// rounded values as fp32.
+__device__ __forceinline__ uint32_t cvt2(float a, float b, float& ra, float& rb) {
+  const bf16x2 v = __builtin_convertvector(f32x2{a, b}, bf16x2);
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  ra = __uint_as_float(u << 16);
+  rb = __uint_as_float(u & 0xFFFF0000u);
+  return u;
+}
+
+constexpr int kProdA[6] = {1, 2, 0, 1, 0, 0};  // plane of A per product: mm lh hl mh hm hh
+constexpr int kProdB[6] = {1, 0, 2, 0, 1, 0};
+
+template <int WN, int WK>
+__global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
+    const float* __restrict__ dY, const float* __restrict__ X, int64_t M, int N, int K,
+    int tiles_k, int64_t rows_per_chunk, int64_t cpp, float* __restrict__ part,
+    float* __restrict__ part_db, DwAlpha al) {
+  using C = DwLdsCfg<WN, WK>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = wave / WK, wk = wave - wn * WK;
+  const int r = lane & 15, g = lane >> 4;
+  const int tiles = (N / C::BN) * tiles_k;
+  const int L = xcd_logical((int)blockIdx.x, (int)gridDim.x);
+  const int tile = L % tiles;
+  const int tn = tile / tiles_k, tk = tile - tn * tiles_k;
+  const int n0 = tn * C::BN, k0 = tk * C::BK;
+  const int64_t chunk = L / tiles;
+  const int64_t pass = chunk / cpp;
+  const int64_t m_lim = (pass + 1) * M;
+  const int64_t m_begin = pass * M + (chunk - pass * cpp) * rows_per_chunk;
+  const int64_t m_end = m_begin + rows_per_chunk < m_lim ? m_begin + rows_per_chunk : m_lim;
+  const int steps = DW_EXP_STEPS1 ? 1 : (int)((m_end - m_begin + kStepRows - 1) / kStepRows);
+  const bool do_db = (part_db != nullptr) && (tk == 0);
+  if (DW_EXP_EXIT && steps < 1000000) return;
+
+  // Loader units: 2 rows x 4 columns of one operand, row pair fastest across lanes
+  // (conflict-free ds_write_b32: the two columns a 32-lane group writes sit 32 banks
+  // apart). Every thread owns UY dY units and UX X units, so each load instruction reads one
+  // operand through one wave-uniform buffer descriptor (a per-lane choice compiles to a
+  // waterfall loop). Rows at or past the chunk end read 0 (range check).
+  const __amdgpu_buffer_rsrc_t ry = make_rsrc(dY + m_begin * N, (m_end - m_begin) * N * 4);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + m_begin * K, (m_end - m_begin) * K * 4);
+  constexpr int UY = C::kUY, UX = C::kUX;
+  int y_voff[UY], y_c[UY], y_rp[UY], x_voff[UX], x_c[UX], x_rp[UX];
+  bool y_ok[UY], x_ok[UX];
+#pragma unroll
+  for (int j = 0; j < UY; ++j) {
+    const int u = threadIdx.x + j * C::kThr;
+    y_ok[j] = u < C::BN * 4;           // (BN/4 column quads) x 16 row pairs
+    const int uu = y_ok[j] ? u : 0;
+    y_rp[j] = uu & 15;
+    y_c[j] = 4 * (uu >> 4);
+    y_voff[j] = (2 * y_rp[j] * N + n0 + y_c[j]) * 4;
+  }
+#pragma unroll
+  for (int j = 0; j < UX; ++j) {
+    const int u = threadIdx.x + j * C::kThr;
+    x_ok[j] = u < C::BK * 4;
+    const int uu = x_ok[j] ? u : 0;
+    x_rp[j] = uu & 15;
+    x_c[j] = 4 * (uu >> 4);
+    x_voff[j] = (2 * x_rp[j] * K + k0 + x_c[j]) * 4;
+  }
+  struct Raw {
+    f32x4 y[UY][2];
+    f32x4 x[UX][2];
+  };
+  auto load = [&](Raw& raw, int step) {
+    if (DW_EXP_NOLOAD) step = 0;
+    const int soy = step * kStepRows * N * 4, sox = step * kStepRows * K * 4;
+#pragma unroll
+    for (int j = 0; j < UY; ++j)
+      if (y_ok[j])
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          raw.y[j][i] = __builtin_amdgcn_raw_buffer_load_b128(ry, y_voff[j] + i * N * 4, soy, 0);
+#pragma unroll
+    for (int j = 0; j < UX; ++j)
+      if (x_ok[j])
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          raw.x[j][i] = __builtin_amdgcn_raw_buffer_load_b128(rx, x_voff[j] + i * K * 4, sox, 0);
+  };
+  f32x4 dbacc[UY];
+#pragma unroll
+  for (int j = 0; j < UY; ++j) dbacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // split x = hi + mid + lo (each the bf16 rounding of what is left; exact) and store the
+  // three planes of a 2-row x 4-column unit (one packed row pair per plane and column)
+  auto put = [&](unsigned char* base, int col, int rp, const f32x4& r0, const f32x4& r1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float h0, h1, m0, m1, l0, l1;
+      const uint32_t ph = cvt2(r0[e], r1[e], h0, h1);
+      const float s0 = r0[e] - h0, s1 = r1[e] - h1;
+      const uint32_t pm = cvt2(s0, s1, m0, m1);
+      const uint32_t pl = cvt2(s0 - m0, s1 - m1, l0, l1);
+      unsigned char* cb = base + (col + e) * kLdsPitch + rp * 4;
+      *reinterpret_cast<uint32_t*>(cb) = ph;
+      *reinterpret_cast<uint32_t*>(cb + 64) = pm;
+      *reinterpret_cast<uint32_t*>(cb + 128) = pl;
+    }
+  };
+  auto store = [&](const Raw& raw, int buf) {
+    if (DW_EXP_NOSTORE) return;
+    unsigned char* base = lds + buf * C::kBuf;
+#pragma unroll
+    for (int j = 0; j < UY; ++j) {
+      if (!y_ok[j]) continue;
+      if (do_db) dbacc[j] += raw.y[j][0] + raw.y[j][1];
+      put(base, y_c[j], y_rp[j], raw.y[j][0], raw.y[j][1]);
+    }
+#pragma unroll
+    for (int j = 0; j < UX; ++j)
+      if (x_ok[j]) put(base, C::BN + x_c[j], x_rp[j], raw.x[j][0], raw.x[j][1]);
+  };
+
+  f32x4 acc[3][3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int u = 0; u < 3; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto frag = [&](const unsigned char* base, int col, int plane) {
+    return *reinterpret_cast<const bf16x8*>(base + col * kLdsPitch + 64 * plane + 16 * g);
+  };
+  auto compute = [&](int buf) {
+    const unsigned char* base = lds + buf * C::kBuf;
+    // B fragments (this wave's 3 k-tiles x 3 planes) for the whole step, A fragments one
+    // n-tile at a time (register budget: 3 waves per SIMD); 16x16x32 bf16 MFMAs issue
+    // back to back on one accumulator, so per tile row the products go
+    // smallest first (mm, lh, hl, mh, hm, hh) over its 3 accumulators.
+    bf16x8 b[3][3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) b[u][q] = frag(base, C::BN + 48 * wk + 16 * u + r, q);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      bf16x8 a[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] = frag(base, 48 * wn + 16 * t + r, q);
+#pragma unroll
+      for (int p = 0; p < 6; ++p)
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          if (!DW_EXP_NOMFMA) acc[t][u] = mfma_bf16(a[kProdA[p]], b[u][kProdB[p]], acc[t][u]);
+      if (DW_EXP_NOMFMA) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) acc[t][u][0] += (float)a[0][0] * (float)b[u][0][0];
+      }
+    }
+  };
+
+  // Two register stages: step s+1's data is split into LDS while step s's MFMAs run, and
+  // the loads of step s+2 / s+3 are already in flight (two steps of HBM latency covered).
+  Raw ra, rb;
+  load(ra, 0);
+  if (steps > 1) load(rb, 1);
+  store(ra, 0);
+  if (steps > 2) load(ra, 2);
+  __syncthreads();
+  // Waves 0-3 compute before they store, waves 4.. store first (a stagger: the waves
+  // sharing a SIMD -- w and w+4 -- then run their MFMA and their split/store phases at
+  // different times instead of in lockstep between the barriers). Compute-first code issues
+  // its fragment reads before the ds_writes (the compiler cannot tell the two buffers
+  // apart and keeps program order).
+  const bool late = wave >= 4;
+  auto phase = [&](int cb, Raw& nxt, int sb, bool do_store, int ld_step) {
+    if (late) {
+      if (do_store) store(nxt, sb);
+      compute(cb);
+    } else {
+      compute(cb);
+      if (do_store) store(nxt, sb);
+    }
+    if (do_store && ld_step >= 0) load(nxt, ld_step);
+  };
+  for (int s = 0; s < steps; s += 2) {
+    phase(0, rb, 1, s + 1 < steps, s + 3 < steps ? s + 3 : -1);
+    __syncthreads();
+    if (s + 1 >= steps) break;
+    phase(1, ra, 0, s + 2 < steps, s + 4 < steps ? s + 4 : -1);
+    __syncthreads();
+  }
+  // partial tile: D[row = 4g + reg][col = r] of tile (t, u) -> n = n0 + 48wn + 16t + 4g + reg,
+  // k = k0 + 48wk + 16u + r. The same loop forms this block's share of the alpha gradient
+  // (quant.py:84-91 is linear in G: sum_e G[e] term[e] = sum over chunks of the chunk
+  // partial's dot with term), with the term at this chunk's pass bitwidth.
+  const float a = effective_alpha(al.alpha, al.alpha_raw);
+  int bits = al.pass_bits ? al.pass_bits[pass] : (al.bits_dev ? *al.bits_dev : al.bits);
+  bits = bits == 1 ? 1 : 2;
+  float* out = part + chunk * ((int64_t)N * K);
+  float prod = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int n = n0 + 48 * wn + 16 * t + 4 * g + reg;
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int64_t e = (int64_t)n * K + k0 + 48 * wk + 16 * u + r;
+        if (!DW_EXP_NOOUT || acc[t][u][reg] == 12345.0f) out[e] = acc[t][u][reg];
+        prod += acc[t][u][reg] * alpha_term(al.W[e] / a, bits);
+      }
+    }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
+  float* wred = reinterpret_cast<float*>(lds) + 16 * C::BN;  // past the db scratch
+  __syncthreads();  // (the loop's last barrier already ended all LDS reads)
+  if (lane == 0) wred[wave] = prod;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.0f;
+    for (int w = 0; w < WN * WK; ++w) t += wred[w];
+    al.apart[L] = t;  // logical block id: the finish kernel sums these in order
+  }
+  if (do_db) {
+    // column sums: the 16 row pairs of each column quad, added in row-pair order via LDS
+    float* red = reinterpret_cast<float*>(lds);  // [16][BN] (the step buffers are free now)
+#pragma unroll
+    for (int j = 0; j < UY; ++j)
+      if (y_ok[j])
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[y_rp[j] * C::BN + y_c[j] + e] = dbacc[j][e];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C::BN; c += C::kThr) {
+      float v = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v += red[q * C::BN + c];
+      part_db[chunk * N + n0 + c] = v;
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------------
+// Finish of the LDS dW path (quant.py:80-91 given the chunk partials): dW[e] = (sum over
+// chunks in chunk order of part[c][e]) * 1[|W/a| <= 1], db = the same over part_db; the
+// extra last block sums the dW blocks' alpha partials in logical-block order. One
+// element per thread; chunk loads 16 at a time, the next 16 in flight while the current
+// ones are added (memory-level parallelism: the slabs are streamed once). No atomics.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void dw_finish_kernel(
+    const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
+    int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
+    const float* __restrict__ apart, int n_apart, float* __restrict__ dW, float* __restrict__ db,
+    float* __restrict__ dalpha) {
+  if (blockIdx.x == gridDim.x - 1) {  // alpha: fixed order over the dW blocks
+    if (threadIdx.x >= 64) return;
+    float s2 = 0.0f;
+    for (int i = threadIdx.x; i < n_apart; i += 64) s2 += apart[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 64);
+    if (threadIdx.x == 0) dalpha[0] = s2 * alpha_chain(alpha, alpha_raw);
+    return;
+  }
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool is_w = e < nk;
+  if (!is_w && e >= nk + n_db) return;
+  const float* src = is_w ? part + e : part_db + (e - nk);
+  const int64_t stride = is_w ? nk : n_db;
+  constexpr int G = 16;
+  float cur[G], nxt[G];
+  auto fetch = [&](int c0, float (&v)[G]) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) v[u] = c0 + u < chunks ? src[(int64_t)(c0 + u) * stride] : 0.0f;
+  };
+  float g = 0.0f;
+  fetch(0, cur);
+  for (int c0 = 0; c0 < chunks; c0 += G) {
+    if (c0 + G < chunks) fetch(c0 + G, nxt);
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      if (c0 + u < chunks) g += cur[u];
+#pragma unroll
+    for (int u = 0; u < G; ++u) cur[u] = nxt[u];
+  }
+  if (is_w) {
+    const float a = effective_alpha(alpha, alpha_raw);
+    dW[e] = g * ste_indicator(W[e] / a);  // quant.py:81-82
+  } else {
+    db[e - nk] = g;
+  }
+}
+
+bool use_reg_dw() {  // OB_DW=reg: the register-only bf16x6 kernel (A/B experiments)
+  static const int v = [] {
+    const char* e = getenv("OB_DW");
+    return (e && e[0] == 'r') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 bool use_f32_dw() {
   static const int v = [] {
     const char* e = getenv("OB_GEMM");
@@ -429,6 +777,19 @@ DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
     int64_t steps = 32;  // chunk = S steps x 16 rows
     while (steps > 8 && tiles * ceil_div(M, 16 * steps) < 256) steps /= 2;
     p.rows_per_chunk = 16 * steps;
+  } else if (N % 48 == 0 && K % 48 == 0 && !use_reg_dw()) {
+    // LDS-shared bf16x6: 144x144 block tiles (9 waves) where both widths allow it, else
+    // 144x48 / 48x144 (3 waves) or 48x48 (1 wave); chunks of 32-row steps sized for ~256
+    // blocks (one per CU).
+    p.variant = (N % 144 == 0 && K % 144 == 0 && N * K > 144 * 144) ? 9
+                : (N % 144 == 0) ? 31 : (K % 144 == 0) ? 13 : 11;
+    const int64_t bn = p.variant == 9 || p.variant == 31 ? 144 : 48;
+    const int64_t bk = p.variant == 9 || p.variant == 13 ? 144 : 48;
+    p.tiles_n = N / bn;
+    p.tiles_k = K / bk;
+    const int64_t tiles = p.tiles_n * p.tiles_k;
+    const int64_t want = ceil_div(256, tiles * P);  // chunks per pass
+    p.rows_per_chunk = kStepRows * ceil_div(ceil_div(Mp > 0 ? Mp : 1, want), kStepRows);
   } else {
     // 64-wide tiles (one dwordx4 per lane per row). 48-wide tiles (which divide 144 / 576
     // without waste) measured slower: three strided dword loads per row.
@@ -456,7 +817,7 @@ DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
 
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
-                       hipStream_t s) {
+                       hipStream_t s, const DwAlpha* al) {
   if (p.rows_per_pass == 0 || N == 0) return;
   M = p.rows_per_pass;  // kernels index rows per pass (M given = passes * rows_per_pass)
   dim3 grid((unsigned)(p.tiles_n * p.tiles_k), (unsigned)p.chunks);
@@ -470,6 +831,19 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
   hipLaunchKernelGGL((dw_bf16x6_kernel<S>), dim3((unsigned)(p.tiles_n * p.tiles_k * p.chunks)), \
                      dim3(kThreads), 0, s, dY, X, M, (int)N, (int)K, (int)p.tiles_n,            \
                      (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db, ticket)
+  if (p.variant >= 9) {  // requires al (the finish is launch_dw_finish, not ste_reduce)
+    const unsigned nb = (unsigned)(p.tiles_n * p.tiles_k * p.chunks);
+#define OB_DWL(WN, WK)                                                                        \
+  hipLaunchKernelGGL((dw_lds_kernel<WN, WK>), dim3(nb), dim3(64 * WN * WK),                   \
+                     (size_t)(2 * DwLdsCfg<WN, WK>::kBuf), s, dY, X, M, (int)N, (int)K,       \
+                     (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db, *al)
+    if (p.variant == 9) OB_DWL(3, 3);
+    else if (p.variant == 31) OB_DWL(3, 1);
+    else if (p.variant == 13) OB_DWL(1, 3);
+    else OB_DWL(1, 1);
+#undef OB_DWL
+    return;
+  }
   if (p.variant != 0) {
     const int64_t steps = p.rows_per_chunk / 128;
     if (steps == 16) OB_DW6(16);
@@ -490,6 +864,15 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
   }
 #undef OB_DW6
 #undef OB_DW
+}
+
+void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* part_db,
+                      int64_t n_db, const float* W, const float* alpha, int alpha_raw,
+                      const float* apart, int n_apart, float* dW, float* db, float* dalpha,
+                      hipStream_t s) {
+  const int64_t nb = ceil_div(nk + n_db, kThreads) + 1;  // + the alpha block
+  hipLaunchKernelGGL(dw_finish_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, chunks, nk,
+                     part_db, n_db, W, alpha, alpha_raw, apart, n_apart, dW, db, dalpha);
 }
 
 }  // namespace ob

@@ -131,10 +131,26 @@ struct DwPlan {
 };
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
 DwPlan plan_dw_passes(int64_t P, int64_t M_per_pass, int64_t N, int64_t K);
-// Also zeroes *ticket (for the ste_reduce launch that follows on the same stream).
+// Alpha-gradient inputs of the LDS dW path (variant >= 9): each dW block writes its share
+// of sum_e G[e] term[e] (at its pass's bitwidth) to apart[logical block].
+struct DwAlpha {
+  const float* W;
+  const float* alpha;
+  int alpha_raw;
+  int bits;               // one pass: bitwidth, or read from bits_dev when set
+  const int* bits_dev;
+  const int* pass_bits;   // stacked passes: DEVICE int32 [P]
+  float* apart;           // [tiles * chunks]
+};
+// Variants < 9 also zero *ticket (for the ste_reduce launch that follows on the same
+// stream); variants >= 9 need `al` and are finished by launch_dw_finish.
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
-                       hipStream_t s);
+                       hipStream_t s, const DwAlpha* al = nullptr);
+void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* part_db,
+                      int64_t n_db, const float* W, const float* alpha, int alpha_raw,
+                      const float* apart, int n_apart, float* dW, float* db, float* dalpha,
+                      hipStream_t s);
 
 // tgemm_i8.hip (opt-in absmax-int8 activations x ternary codes on the i8 matrix cores)
 bool ternary_gemm_i8_supported(int64_t K, int64_t N);

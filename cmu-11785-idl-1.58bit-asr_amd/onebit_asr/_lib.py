@@ -18,7 +18,7 @@ from pathlib import Path
 import torch  # noqa: F401  (must precede the CDLL: shares torch's HIP runtime)
 
 LIB_NAME = "libonebit_hip.so"
-LIB_PATH = Path(os.environ.get("ONEBIT_HIP_LIB", Path(__file__).with_name(LIB_NAME)))
+LIB_PATH = Path(os.environ.get("ONEBIT_HIP_LIB") or Path(__file__).with_name(LIB_NAME))
 
 OB_OK = 0
 OB_ERR_BITWIDTH = -3
