@@ -392,6 +392,63 @@ int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, siz
 }
 
 namespace {
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+int subsample_check(int64_t B, int64_t T, int64_t F, int64_t C) {
+  if (B < 1 || B > 65535 || T > (1 << 20) || F > (1 << 16)) return OB_ERR_SHAPE;
+  if (B * ((T - 3) / 2 + 1) * ((F - 3) / 2 + 1) * C >= ((int64_t)1 << 30)) return OB_ERR_SHAPE;
+  if (!subsample_supported(T, F, C)) return OB_ERR_SHAPE;
+  return OB_OK;
+}
+}  // namespace
+
+size_t ob_subsample_image_bytes(int64_t C) {
+  return subsample_supported(7, 7, C) ? subsample_image_bytes(C) : 0;
+}
+
+int ob_subsample_pack(const float* W2, int64_t C, void* img, void* stream) {
+  if (!subsample_supported(7, 7, C)) return OB_ERR_SHAPE;
+  if (!W2 || !img) return OB_ERR_NULL;
+  if (!aligned4(W2) || !aligned16(img)) return OB_ERR_ALIGN;
+  launch_subsample_pack(W2, C, img, as_stream(stream));
+  return launched();
+}
+
+int ob_subsample_fwd(const float* X, int64_t B, int64_t T, int64_t F, int64_t C,
+                     const float* W0, const float* b0, const void* img, const float* b2,
+                     float* Y1, float* Y2, void* stream) {
+  if (const int st = subsample_check(B, T, F, C)) return st;
+  if (!X || !W0 || !b0 || !img || !b2 || !Y1 || !Y2) return OB_ERR_NULL;
+  if (!aligned4(X) || !aligned4(W0) || !aligned4(b0) || !aligned4(b2) || !aligned16(img) ||
+      !aligned16(Y1) || !aligned16(Y2))
+    return OB_ERR_ALIGN;
+  launch_subsample_fwd(X, B, T, F, C, W0, b0, img, b2, Y1, Y2, as_stream(stream));
+  return launched();
+}
+
+size_t ob_subsample_bwd_workspace(int64_t B, int64_t T, int64_t F, int64_t C) {
+  return subsample_check(B, T, F, C) ? 0 : subsample_bwd_workspace(B, T, F, C);
+}
+
+int ob_subsample_bwd(const float* X, const float* W0, const float* b0, const float* Y1,
+                     const float* Y2, const float* dY2, int64_t B, int64_t T, int64_t F, int64_t C,
+                     const void* img, float* dW0,
+                     float* db0, float* dW2, float* db2, void* ws, size_t ws_bytes,
+                     void* stream) {
+  if (const int st = subsample_check(B, T, F, C)) return st;
+  if (!X || !W0 || !b0 || !Y1 || !Y2 || !dY2 || !img || !dW0 || !db0 || !dW2 || !db2 || !ws)
+    return OB_ERR_NULL;
+  if (ws_bytes < subsample_bwd_workspace(B, T, F, C)) return OB_ERR_WORKSPACE;
+  if (!aligned4(X) || !aligned4(W0) || !aligned4(b0) || !aligned16(Y1) || !aligned16(Y2) ||
+      !aligned16(dY2) || !aligned16(img) ||
+      !aligned16(ws) || !aligned4(dW0) || !aligned4(db0) || !aligned4(dW2) || !aligned4(db2))
+    return OB_ERR_ALIGN;
+  if (B * ((T - 3) / 2 + 1) * ((F - 3) / 2 + 1) * C * 4 >= ((int64_t)1 << 31)) return OB_ERR_SHAPE;
+  launch_subsample_bwd(X, W0, b0, Y1, Y2, dY2, B, T, F, C, img, dW0, db0, dW2, db2, ws,
+                       as_stream(stream));
+  return launched();
+}
+
+namespace {
 int convmod_check(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K) {
   if (P < 1 || Bt < 0 || T < 0 || C < 1 || K < 1 || Bt % P || Bt > 65535) return OB_ERR_SHAPE;
   if (!convmod_supported(C, K) || Bt * T * 2 * C > ((int64_t)1 << 40)) return OB_ERR_SHAPE;

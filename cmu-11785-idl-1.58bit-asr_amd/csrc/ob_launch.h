@@ -231,4 +231,18 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
 void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,
                                  hipStream_t s);
 
+// subsample.hip (Conv2dSubsampling, channels-last implicit GEMMs)
+bool subsample_supported(int64_t T, int64_t F, int64_t C);
+size_t subsample_image_bytes(int64_t C);
+void launch_subsample_pack(const float* W2, int64_t C, void* img, hipStream_t s);
+void launch_subsample_fwd(const float* X, int64_t B, int64_t T, int64_t F, int64_t C,
+                          const float* W0, const float* b0, const void* img, const float* b2,
+                          float* Y1, float* Y2, hipStream_t s);
+size_t subsample_bwd_workspace(int64_t B, int64_t T, int64_t F, int64_t C);
+void launch_subsample_bwd(const float* X, const float* W0, const float* b0, const float* Y1,
+                          const float* Y2, const float* dY2, int64_t B, int64_t T, int64_t F,
+                          int64_t C, const void* img,
+                          float* dW0, float* db0, float* dW2, float* db2, void* ws,
+                          hipStream_t s);
+
 }  // namespace ob

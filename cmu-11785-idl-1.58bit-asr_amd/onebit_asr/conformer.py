@@ -29,7 +29,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .attention import fused_attention_supported, rel_pos_attention
-from .conv import conv2d_bias_relu, conv_module_fused, conv_module_supported, depthwise_conv1d
+from .conv import (conv2d_bias_relu, conv_module_fused, conv_module_supported, depthwise_conv1d,
+                   subsample_convs, subsample_supported)
 from .embedding import embedding
 from .fused import ffn_residual, fused_supported, linear_residual
 from .layernorm import layer_norm, layer_norm_fork
@@ -310,6 +311,13 @@ class Conv2dSubsampling(nn.Module):
         self.out = nn.Linear(d_model * f_out, d_model)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if subsample_supported(x, self.conv[0], self.conv[2]):
+            # channels-last implicit GEMMs (csrc/subsample.hip): y [B, T', F', C]; the
+            # Linear's columns are permuted to that order instead of transposing y
+            y = subsample_convs(x, self.conv[0], self.conv[2])
+            bsz, tsub, fsub, ch = y.shape
+            w = self.out.weight.view(-1, ch, fsub).transpose(1, 2).reshape(-1, fsub * ch)
+            return linear(y.view(bsz, tsub, fsub * ch), w, self.out.bias)
         if x.is_cuda and x.dtype == torch.float32:  # bias + ReLU fused (conv.py)
             y = conv2d_bias_relu(conv2d_bias_relu(x.unsqueeze(1), self.conv[0]), self.conv[2])
         else:

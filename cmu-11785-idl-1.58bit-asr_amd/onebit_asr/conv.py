@@ -242,6 +242,80 @@ def conv2d_bias_relu(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     return _BiasReluFn.apply(y.contiguous(), conv.bias)
 
 
+class _SubsampleFn(torch.autograd.Function):
+    """Conv2dSubsampling's convolutions (conformer.py:183-186) in csrc/subsample.hip,
+    channels-last: [B, T, F] feats -> Y2 [B, T2, F2, C] = relu(conv(relu(conv(x)))). The
+    second conv's weight is re-split into its bf16 MFMA images each forward; backward gives
+    the four weight / bias gradients (the feats get none)."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w2, b2):
+        lib = _lib.load()
+        bsz, t, f = x.shape
+        c = w0.shape[0]
+        t1, f1 = (t - 3) // 2 + 1, (f - 3) // 2 + 1
+        t2, f2 = (t1 - 3) // 2 + 1, (f1 - 3) // 2 + 1
+        img = torch.empty((lib.ob_subsample_image_bytes(c),), dtype=torch.uint8,
+                          device=x.device)
+        y1 = torch.empty((bsz, t1, f1, c), dtype=torch.float32, device=x.device)
+        y2 = torch.empty((bsz, t2, f2, c), dtype=torch.float32, device=x.device)
+        st = _lib.stream_of(x)
+        _lib.check(lib.ob_subsample_pack(w2.data_ptr(), c, img.data_ptr(), st),
+                   "ob_subsample_pack")
+        _lib.check(lib.ob_subsample_fwd(x.data_ptr(), bsz, t, f, c, w0.data_ptr(),
+                                        b0.data_ptr(), img.data_ptr(), b2.data_ptr(),
+                                        y1.data_ptr(), y2.data_ptr(), st), "ob_subsample_fwd")
+        ctx.save_for_backward(x, w0, b0, y1, y2, img)
+        return y2
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("Conv2dSubsampling HIP path: no gradient for the feats")
+        x, w0, b0, y1, y2, img = ctx.saved_tensors
+        g = g.contiguous()
+        bsz, t, f = x.shape
+        c = y1.shape[-1]
+        lib = _lib.load()
+        wsb = lib.ob_subsample_bwd_workspace(bsz, t, f, c)
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=x.device)
+        dw0 = torch.empty((c, 1, 3, 3), dtype=torch.float32, device=x.device)
+        db0 = torch.empty((c,), dtype=torch.float32, device=x.device)
+        dw2 = torch.empty((c, c, 3, 3), dtype=torch.float32, device=x.device)
+        db2 = torch.empty((c,), dtype=torch.float32, device=x.device)
+        _lib.check(lib.ob_subsample_bwd(x.data_ptr(), w0.data_ptr(), b0.data_ptr(), y1.data_ptr(),
+                                        y2.data_ptr(), g.data_ptr(),
+                                        bsz, t, f, c, img.data_ptr(), dw0.data_ptr(),
+                                        db0.data_ptr(), dw2.data_ptr(), db2.data_ptr(),
+                                        ws.data_ptr(), wsb, _lib.stream_of(g)),
+                   "ob_subsample_bwd")
+        return None, dw0, db0, dw2, db2
+
+
+def _std_conv(conv: nn.Conv2d) -> bool:
+    return (conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (0, 0)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is not None
+            and conv.weight.dtype == torch.float32)
+
+
+def subsample_supported(x: torch.Tensor, conv0: nn.Conv2d, conv2: nn.Conv2d) -> bool:
+    """csrc/subsample.hip applies: CUDA fp32 [B, T, F] feats that need no gradient, the
+    reference's two 3x3 / stride-2 convolutions, a supported channel count."""
+    if os.environ.get("OB_SUBSAMPLE", "hip") != "hip":
+        return False
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and not x.requires_grad
+            and _std_conv(conv0) and _std_conv(conv2) and conv0.in_channels == 1
+            and conv2.in_channels == conv2.out_channels == conv0.out_channels):
+        return False
+    return _lib.load().ob_subsample_bwd_workspace(x.size(0), x.size(1), x.size(2),
+                                                  conv0.out_channels) > 0
+
+
+def subsample_convs(x: torch.Tensor, conv0: nn.Conv2d, conv2: nn.Conv2d) -> torch.Tensor:
+    """[B, T, F] -> [B, T2, F2, C] (channels last) = relu(conv2(relu(conv0(x))))."""
+    return _SubsampleFn.apply(x.contiguous(), conv0.weight, conv0.bias, conv2.weight, conv2.bias)
+
+
 def _pointwise(x: torch.Tensor, conv: nn.Conv1d) -> torch.Tensor:
     c_in = x.shape[-1]
     y = _PointwiseFn.apply(x.reshape(-1, c_in), conv.weight.view(conv.out_channels, c_in),

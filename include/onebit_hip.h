@@ -461,6 +461,31 @@ OB_API int ob_convmod_bwd(const float* dv, const float* u, const float* z, const
                           int64_t K, float* du, float* dw_dw, float* db_dw, float* dgamma,
                           float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Conv2dSubsampling's two convolutions (conformer.py:170-208: Conv2d(1, C, 3, 2) -> ReLU ->
+ * Conv2d(C, C, 3, 2) -> ReLU; replaces the torch.nn.Conv2d / cuDNN calls the module makes),
+ * channels-last so the flatten + Linear that follows needs no transpose:
+ *   X  [B][T][F] feats;  W0 [C][1][3][3], b0 [C];  W2 [C][C][3][3], b2 [C] (torch layouts)
+ *   Y1 [B][T1][F1][C] = relu(conv(X, W0) + b0),  T1 = (T-3)/2+1, F1 = (F-3)/2+1
+ *   Y2 [B][T2][F2][C] = relu(conv(Y1, W2) + b2), T2 = (T1-3)/2+1, F2 = (F1-3)/2+1
+ * ob_subsample_pack re-splits W2 into the bf16 hi/mid/lo images the fp32-exact MFMA
+ * GEMMs read (call it whenever W2 changes; ob_subsample_image_bytes(C) bytes, 16-aligned).
+ * bwd: from dY2 = dL/dY2 (before the ReLU mask) and the forward's X, W0, b0, Y1, Y2: dW0,
+ * db0, dW2, db2 (overwritten; dX is not produced: the feats need no gradient). Deterministic; C in {48, 64, 96, 144},
+ * T, F >= 7; ob_subsample_bwd_workspace() == 0 means unsupported.
+ * ------------------------------------------------------------------------------------ */
+OB_API size_t ob_subsample_image_bytes(int64_t C);
+OB_API int ob_subsample_pack(const float* W2, int64_t C, void* img, void* stream);
+OB_API int ob_subsample_fwd(const float* X, int64_t B, int64_t T, int64_t F, int64_t C,
+                            const float* W0, const float* b0, const void* img,
+                            const float* b2, float* Y1, float* Y2, void* stream);
+OB_API size_t ob_subsample_bwd_workspace(int64_t B, int64_t T, int64_t F, int64_t C);
+OB_API int ob_subsample_bwd(const float* X, const float* W0, const float* b0, const float* Y1,
+                            const float* Y2, const float* dY2, int64_t B, int64_t T, int64_t F,
+                            int64_t C, const void* img,
+                            float* dW0, float* db0, float* dW2, float* db2, void* ws,
+                            size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
