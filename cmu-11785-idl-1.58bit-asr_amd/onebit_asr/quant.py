@@ -476,6 +476,9 @@ class QuantizedLinear(nn.Module):
         else:
             self.register_parameter("bias", None)
         self._codes_cache: dict = {}
+        # packed-ternary checkpoint (checkpoint.py): {bits: (codes, codes_t)} used as they are;
+        # the fp32 weight is then not meaningful (inference at bitwidth 1 / 2 only)
+        self._packed: Optional[dict] = None
 
     def extra_repr(self) -> str:
         extra = f", act_quant={self.act_quant!r}" if self.act_quant else ""
@@ -485,6 +488,11 @@ class QuantizedLinear(nn.Module):
     def _codes(self, bits: int):
         """Codes for the current (weight, alpha) values: repacked only when either
         parameter was modified in place (optimizer step, load_state_dict, DDP broadcast)."""
+        if self._packed is not None:
+            if bits not in self._packed:
+                raise KeyError(f"packed layer has no {bits}-bit codes "
+                               f"(checkpoint holds {sorted(self._packed)})")
+            return self._packed[bits]
         key = (self.weight.data_ptr(), self.weight._version, self.alpha.data_ptr(),
                self.alpha._version)
         hit = self._codes_cache.get(bits)
@@ -497,6 +505,8 @@ class QuantizedLinear(nn.Module):
     def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
         if self.quant_off is not None:  # configs[3] ceiling: no quantizer, library GEMM
             return linear(x, self.weight, self.bias, dtype=self.quant_off)
+        if self._packed is not None:
+            self._check_packed_use(bitwidth)
         if isinstance(bitwidth, PassBits):
             return self._forward_passes(x, bitwidth)
         bits = _check_bitwidth(bitwidth)
@@ -541,18 +551,41 @@ class QuantizedLinear(nn.Module):
                                      codes2, codes2_t, codes1, codes1_t)
         return y.view(*lead, self.out_features)
 
+    def install_packed(self, packed: dict) -> None:
+        """Use the given {bits: (codes, codes_t)} (a packed-ternary checkpoint,
+        checkpoint.load_packed) for every forward at those bitwidths: inference only."""
+        for b, (c, ct) in packed.items():
+            n, k = self.weight.shape
+            if b not in (1, 2) or tuple(c.shape) != (n, (k + 15) // 16) or \
+                    tuple(ct.shape) != (k, (n + 15) // 16):
+                raise ValueError(f"bad packed codes for bitwidth {b}")
+        self._packed = dict(packed)
+        self._codes_cache = {}
+
+    def _check_packed_use(self, bitwidth) -> None:
+        if isinstance(bitwidth, int) and bitwidth == 32:
+            raise RuntimeError("packed-ternary layer: the checkpoint holds no fp32 weights "
+                               "(bitwidth 32 needs an fp32 checkpoint)")
+        if torch.is_grad_enabled() and (self.alpha.requires_grad or self.weight.requires_grad):
+            raise RuntimeError("packed-ternary layers are inference-only: run under "
+                               "torch.no_grad() / torch.inference_mode()")
+
     def invalidate_codes(self) -> None:
         """Drop the cached 2-bit codes. Needed after writing ``weight`` / ``alpha`` through
         ``.data`` (such writes do not bump the version counter the cache is keyed on);
         optimizer steps, ``load_state_dict`` and in-place ops on the parameters do not need it."""
         self._codes_cache = {}
 
-    def _load_from_state_dict(self, *args, **kwargs):
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self._codes_cache = {}
-        return super()._load_from_state_dict(*args, **kwargs)
+        if prefix + "weight" in state_dict:  # an fp32 weight replaces packed codes
+            self._packed = None
+        return super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate cached codes
         self._codes_cache = {}
+        if self._packed is not None:  # packed codes follow the module (int: no dtype cast)
+            self._packed = {b: (fn(c), fn(ct)) for b, (c, ct) in self._packed.items()}
         return super()._apply(fn, *args, **kwargs)
 
 
@@ -572,7 +605,8 @@ class PackGroup:
 
     def __init__(self, module: nn.Module, bits=(2, 1)):
         self.layers = [m for m in module.modules()
-                       if isinstance(m, QuantizedLinear) and m.quant_off is None]
+                       if isinstance(m, QuantizedLinear) and m.quant_off is None
+                       and m._packed is None]  # packed layers keep their loaded codes
         self.bits = tuple(bits)
         self._ptrs = None
         self.table = None
