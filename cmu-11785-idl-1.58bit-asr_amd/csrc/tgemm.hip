@@ -30,6 +30,20 @@
 #include "ob_launch.h"
 #include "ob_quant.h"
 
+// Phase-pricing experiments (tools/variant.sh builds; all 0 in the product)
+#ifndef TG_EXP_NOSTORE
+#define TG_EXP_NOSTORE 0
+#endif
+#ifndef TG_EXP_NOMFMA
+#define TG_EXP_NOMFMA 0
+#endif
+#ifndef TG_EXP_NOA
+#define TG_EXP_NOA 0
+#endif
+#ifndef TG_EXP_PLAINEPI
+#define TG_EXP_PLAINEPI 0
+#endif
+
 namespace ob {
 
 namespace {
@@ -40,7 +54,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;  // 4 waves
 constexpr int kRows = 64;      // rows per row tile (16 per wave)
-constexpr size_t kMaxLds = 64 * 1024;
+constexpr size_t kMaxLds = 80 * 1024;  // B image + epilogue staging: 2 blocks per CU
 constexpr int kTargetBlocks = 512;  // 2 per CU
 
 __device__ __forceinline__ uint32_t code_bf16(uint32_t c) {
@@ -82,28 +96,40 @@ struct EpiArgs {
 
 // torch's silu and silu backward formulas: x / (1 + exp(-x)) and
 // (dy * s) * (1 + x * (1 - s)), s = 1 / (1 + exp(-x)), evaluated in that order.
-__device__ __forceinline__ float silu_f(float z) { return z / (1.0f + expf(-z)); }
+#ifndef TG_FASTMATH
+#define TG_FASTMATH 0
+#endif
+__device__ __forceinline__ float silu_f(float z) {
+  if (TG_FASTMATH) return __fdividef(z, 1.0f + __expf(-z));
+  return z / (1.0f + expf(-z));
+}
 __device__ __forceinline__ float silu_bwd_f(float dy, float z) {
-  const float s = 1.0f / (1.0f + expf(-z));
+  const float s = TG_FASTMATH ? __frcp_rn(1.0f + __expf(-z)) : 1.0f / (1.0f + expf(-z));
   return nc_mul(nc_mul(dy, s), 1.0f + z * (1.0f - s));
 }
 
 // Store y = a*acc + b through the fused epilogue. `c` is this element's output address,
 // grow its pass-inclusive row. Non-contracting ops (ob_fp.h) keep hipcc from contracting the unfused
 // reference sequence (y, then *scale, then +R) into an fma.
+#ifndef TG_EXP_NODROP
+#define TG_EXP_NODROP 0
+#endif
+#ifndef TG_EXP_NOLENS
+#define TG_EXP_NOLENS 0
+#endif
 template <int MODE>
 __device__ __forceinline__ void epi_store(const EpiArgs& ep, uint32_t dkey, float* c,
                                           int64_t grow, int col, int N, float y, float rv) {
   const int64_t i = grow * N + col;
   const float keep =
-      ep.dc.on ? (drop_hash(dkey, (uint64_t)i) >= ep.dc.thresh ? ep.dc.scale : 0.0f) : 1.0f;
+      (ep.dc.on && !TG_EXP_NODROP) ? (drop_hash(dkey, (uint64_t)i) >= ep.dc.thresh ? ep.dc.scale : 0.0f) : 1.0f;
   if constexpr (MODE == kEpiSwishDrop) {
     ep.C2[i] = y;
     const float sv = silu_f(y);
     *c = ep.dc.on ? nc_mul(sv, keep) : sv;
   } else if constexpr (MODE == kEpiResidual) {
     bool valid = true;
-    if (ep.lens) {
+    if (ep.lens && !TG_EXP_NOLENS) {
       const int64_t b = grow / ep.T;
       valid = (grow - b * ep.T) < ep.lens[b];
     }
@@ -131,6 +157,11 @@ __device__ __forceinline__ void load8(const float* __restrict__ arow, int k, int
                                       f32x4& b) {
   const int ka = k < K - 4 ? k : K - 4;
   const int kb = k + 4 < K - 4 ? k + 4 : K - 4;
+  if (TG_EXP_NOA) {
+    a = f32x4{0.5f, 0.25f, 0.125f, 1.0f} * (float)ka;
+    b = f32x4{0.5f, 0.25f, 0.125f, 1.0f} * (float)kb;
+    return;
+  }
   a = *reinterpret_cast<const f32x4*>(arow + ka);
   b = *reinterpret_cast<const f32x4*>(arow + kb);
 }
@@ -148,7 +179,57 @@ __device__ __forceinline__ void select_pass(const float* __restrict__& A, float*
   C += (int64_t)p * M * N;
 }
 
-template <int NT, int NCH, int EPI>
+// byte offset of the epilogue staging tiles (after the B image, 16-B aligned) and their size
+__host__ __device__ inline size_t epi_stage_off(int nt, int kpad) {
+  return ((size_t)2 * 16 * nt * (kpad + 8) + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t epi_stage_bytes(int nt) {
+  const int cw = nt < 4 ? nt : 4;
+  return (size_t)4 * 16 * (16 * cw + 4) * sizeof(float);
+}
+
+// The same epilogue for 4 consecutive columns of one row (col % 4 == 0, N % 4 == 0): R loaded
+// and C / C2 stored as dwordx4, so 16 lanes cover 256 contiguous bytes of the row.
+template <int MODE>
+__device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, float* c,
+                                           int64_t grow, int col, int N, f32x4 y, bool valid) {
+  const int64_t i = grow * N + col;
+  f32x4 keep = {1.f, 1.f, 1.f, 1.f};
+  if (ep.dc.on && !TG_EXP_NODROP) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      keep[e] = drop_hash(dkey, (uint64_t)(i + e)) >= ep.dc.thresh ? ep.dc.scale : 0.0f;
+  }
+  f32x4 out;
+  if constexpr (MODE == kEpiNone) {
+    out = y;
+  } else if constexpr (MODE == kEpiSwishDrop) {
+    *reinterpret_cast<f32x4*>(ep.C2 + i) = y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sv = silu_f(y[e]);
+      out[e] = ep.dc.on ? nc_mul(sv, keep[e]) : sv;
+    }
+  } else if constexpr (MODE == kEpiResidual) {
+    const f32x4 rv = *reinterpret_cast<const f32x4*>(ep.R + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = ep.dc.on ? nc_mul(y[e], keep[e]) : y[e];
+      v = valid ? v : nc_mul(v, 0.0f);
+      out[e] = nc_add(rv[e], ep.rscale == 1.0f ? v : nc_mul(ep.rscale, v));
+    }
+  } else {  // kEpiSwishDropBwd
+    const f32x4 rv = *reinterpret_cast<const f32x4*>(ep.R + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float dd = ep.dc.on ? nc_mul(y[e], keep[e]) : y[e];
+      out[e] = silu_bwd_f(dd, rv[e]);
+    }
+  }
+  *reinterpret_cast<f32x4*>(c) = out;
+}
+
+template <int NT, int NCH, int EPI, bool VEC_EPI>
 __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
@@ -161,6 +242,9 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
   const int stride = kpad + 8;
   const int kwp = kpad >> 4;
+  // row-coalesced epilogue (vec_epi): per-wave staging [16][kEpiCC + 4] after the B image
+  constexpr int kEpiCW = NT < 4 ? NT : 4, kEpiCC = 16 * kEpiCW, kEpiLd = kEpiCC + 4;
+  // VEC_EPI (host-checked: N % 4 == 0, C / C2 / R 16-B aligned): the row-coalesced epilogue
 
   const int L = xcd_logical(blockIdx.x, gridDim.x);
   const int ct = L % n_ct;
@@ -265,6 +349,12 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       split3(x0, x1, hi, mid, lo);
       // part-major: consecutive MFMAs update different accumulators (no back-to-back
       // dependence on the MFMA just issued)
+      if (TG_EXP_NOMFMA) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t][t & 3] += (float)lo[t & 7] * (float)bq[t][1] + (float)mid[1] * (float)hi[2];
+        return;
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(lo, bq[t], acc[t]);
 #pragma unroll
@@ -320,6 +410,54 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     // keep the epilogue's loads (residual / pre-activation) from being hoisted into the
     // main loop, where they would hold NT*4 VGPRs across it
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (VEC_EPI && !TG_EXP_NOSTORE) {
+      // Row-coalesced epilogue: each chunk of <= 4 column tiles goes through the wave's LDS
+      // staging tile, then every lane handles 4 consecutive columns of one row (dwordx4 R
+      // loads and C / C2 stores; 16 lanes = 256 contiguous bytes). The wave's LDS ops run
+      // in issue order; the waitcnt + sched barriers keep hipcc from reordering across them.
+      float* stg = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad)) + wave * 16 * kEpiLd;
+#pragma unroll
+      for (int c0 = 0; c0 < NT; c0 += kEpiCW) {
+#pragma unroll
+        for (int t = 0; t < kEpiCW; ++t) {
+          if (c0 + t >= NT) continue;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            stg[(4 * g + reg) * kEpiLd + 16 * t + r] = fmaf(a_eff, acc[c0 + t][reg], bcol[c0 + t]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int kQ = kEpiCC / 4;  // float4s per staged row
+#pragma unroll
+        for (int it = 0; it < kEpiCW; ++it) {
+          const int idx = it * 64 + lane, row = idx / kQ, c4 = idx - row * kQ;
+          const int64_t orow = m0 + row;
+          const int col = n0 + 16 * c0 + 4 * c4;
+          const f32x4 y = *reinterpret_cast<const f32x4*>(stg + row * kEpiLd + 4 * c4);
+          // (the last chunk of an NT that is not a multiple of 4 holds fewer columns)
+          if (orow < M && col < N && 4 * c4 < 16 * (NT - c0)) {
+            if constexpr (EPI == kEpiNone || TG_EXP_PLAINEPI) {
+              *reinterpret_cast<f32x4*>(C + orow * N + col) = y;
+              if (EPI == kEpiSwishDrop)
+                *reinterpret_cast<f32x4*>(ep.C2 + (rowbase + orow) * N + col) = y;
+            } else {
+              bool valid = true;
+              if (EPI == kEpiResidual && ep.lens && !TG_EXP_NOLENS) {
+                const int64_t grow = rowbase + orow;
+                const int64_t bb = grow / ep.T;
+                valid = (grow - bb * ep.T) < ep.lens[bb];
+              }
+              epi_store4<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, valid);
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
+    if constexpr (!VEC_EPI || TG_EXP_NOSTORE) {
+
     // epilogue operand: all NT*4 loads issued before any is used (one latency, not 4*NT)
     // epilogue operand (residual / pre-activation): rolling prefetch kPre tiles ahead, so at
     // most (kPre + 1) * 4 values are live (all NT * 4 at once spilled at NT = 12)
@@ -351,12 +489,19 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
         const int64_t orow = m0 + 4 * g + reg;
         if (orow >= M) continue;
         const float y = fmaf(a_eff, acc[t][reg], bcol[t]);
-        if constexpr (EPI == kEpiNone) C[orow * N + col] = y;
-        else epi_store<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, rv[t][reg]);
+        if (TG_EXP_NOSTORE) {
+          if (y == 1234.5f) C[orow * N + col] = y;
+        } else if constexpr (EPI == kEpiNone || TG_EXP_PLAINEPI) {
+          C[orow * N + col] = y;
+          if (EPI == kEpiSwishDrop) ep.C2[(rowbase + orow) * N + col] = y;
+        } else {
+          epi_store<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, rv[t][reg]);
+        }
       }
       // one tile's elementwise work at a time: hipcc would otherwise interleave all NT*4
       // exp/div sequences and spill
       if constexpr (EPI != kEpiNone) __builtin_amdgcn_sched_barrier(0);
+    }
     }
   }
 }
@@ -660,18 +805,16 @@ size_t bimg_bytes(int nt, int64_t K) {
   return sizeof(uint16_t) * (size_t)(16 * nt) * (size_t)(kpad + 8);
 }
 
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 // Widest column tile whose bf16 image fits the LDS budget, preferring tiles that divide N.
 // OB_TGEMM_NTMAX (tuning experiments) caps the width.
-// Fused epilogues: widths whose instantiation spills are excluded (hipcc's allocation of
-// the exp/div epilogues is erratic in NT; checked with -Rpass-analysis=kernel-resource-usage):
-// swish fwd <= 4 (NT 12 compiles spill-free but measured 49 vs 44 us at lin1), swish bwd
-// {6, <=4}, residual any at K <= 160; all <= 4 beyond.
+// Fused epilogues: widths whose instantiation spills are excluded (checked with
+// -Rpass-analysis=kernel-resource-usage on the row-coalesced (VEC_EPI) kernels: every
+// epilogue is spill-free up to NT 9 at K <= 160 and up to NT 4 beyond).
 bool epi_nt_ok(int nt, int64_t K, int epi_mode) {
   if (epi_mode == kEpiNone) return true;
-  if (K > 160) return nt <= 4;
-  if (epi_mode == kEpiSwishDrop) return nt <= 4;
-  if (epi_mode == kEpiSwishDropBwd) return nt == 6 || nt <= 4;
-  return true;
+  return K <= 160 ? nt <= 9 : nt <= 4;
 }
 
 int pick_nt(int64_t N, int64_t K, int epi_mode) {
@@ -687,11 +830,12 @@ int pick_nt(int64_t N, int64_t K, int epi_mode) {
     if (c <= cap) cands[nc++] = c;
   for (int i = nc; i < 7; ++i) cands[i] = 1;
   for (int nt : cands)
-    if (epi_nt_ok(nt, K, epi_mode) && N % (16 * nt) == 0 && bimg_bytes(nt, K) <= kMaxLds)
+    if (epi_nt_ok(nt, K, epi_mode) && N % (16 * nt) == 0 &&
+        bimg_bytes(nt, K) + 16 + epi_stage_bytes(nt) <= kMaxLds)
       return nt;
   for (int nt : cands)
     if (epi_nt_ok(nt, K, epi_mode) && 16 * nt <= ((N + 15) & ~int64_t(15)) &&
-        bimg_bytes(nt, K) <= kMaxLds)
+        bimg_bytes(nt, K) + 16 + epi_stage_bytes(nt) <= kMaxLds)
       return nt;
   return 0;
 }
@@ -711,12 +855,20 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
   if (rgroups < 1) rgroups = 1;
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
-  const size_t lds = bimg_bytes(NT, K);
+  const int kpad = (int)((K + 31) & ~int64_t(31));
+  const size_t lds = epi_stage_off(NT, kpad) + epi_stage_bytes(NT);
   const int KW = (int)ceil_div(K, 16);
+  const bool vec = (N % 4 == 0) && aligned16(C) && (ep.mode != kEpiSwishDrop || aligned16(ep.C2)) &&
+                   ((ep.mode != kEpiResidual && ep.mode != kEpiSwishDropBwd) || aligned16(ep.R));
 #define OB_TGEMM_E(NCH, E)                                                                     \
-  hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E>), grid, dim3(kThreads), lds, s, A, M,       \
-                     (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C,   \
-                     codes1, pass_bits, ep)
+  if (vec)                                                                                    \
+    hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E, true>), grid, dim3(kThreads), lds, s,  \
+                       A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,  \
+                       bias, C, codes1, pass_bits, ep);                                         \
+  else                                                                                        \
+    hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E, false>), grid, dim3(kThreads), lds, s, \
+                       A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,  \
+                       bias, C, codes1, pass_bits, ep)
 #define OB_TGEMM(NCH)                                                   \
   switch (ep.mode) {                                                    \
     case kEpiSwishDrop: OB_TGEMM_E(NCH, kEpiSwishDrop); break;          \
