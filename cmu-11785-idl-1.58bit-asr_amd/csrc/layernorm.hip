@@ -30,14 +30,15 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
-template <int NPL>  // columns per lane: d <= 16 * NPL
-__global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
-    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
-    int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
-    float* __restrict__ rstd_out) {
+// One row (16 lanes): y = LN(x) and the row's (mean, rstd); returns this lane's max|y|.
+template <int NPL>
+__device__ __forceinline__ float ln_row(const float* __restrict__ x,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ beta, int64_t row, int d,
+                                        float eps, float* __restrict__ y,
+                                        float* __restrict__ mean_out,
+                                        float* __restrict__ rstd_out) {
   const int j = threadIdx.x & (kLanesPerRow - 1);
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
-  if (row >= rows) return;
   const float* xr = x + row * d;
   float v[NPL];
   float s = 0.0f;
@@ -59,19 +60,64 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
   const float var = row_sum16(q) * inv_d;
   const float rstd = 1.0f / sqrtf(var + eps);
   float* yr = y + row * d;
+  float amx = 0.0f;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
     const int c = j + kLanesPerRow * i;
     if (c < d) {
       const float g = gamma ? gamma[c] : 1.0f;
       const float b = beta ? beta[c] : 0.0f;
-      yr[c] = fmaf((v[i] - mean) * rstd, g, b);
+      const float o = fmaf((v[i] - mean) * rstd, g, b);
+      yr[c] = o;
+      amx = fmaxf(amx, fabsf(o));
     }
   }
   if (j == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
   }
+  return amx;
+}
+
+template <int NPL>  // columns per lane: d <= 16 * NPL
+__global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out) {
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
+  if (row >= rows) return;
+  (void)ln_row<NPL>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
+}
+
+// The same rows plus the per-pass max|y| (the int8 activation scale of the BitLinear that
+// consumes y; passes = consecutive blocks of rows_per_pass rows). Blocks stride over the
+// rows; each keeps per-pass maxima in LDS (ds_max on the fp32 bit patterns: |y| >= 0 so
+// the unsigned order is the float order) and adds them to amax with one global atomicMax
+// per (block, pass) -- max is order-independent, so the result is deterministic. amax must
+// hold zeros (or smaller maxima) on entry.
+constexpr int kAmaxMaxPasses = 8;
+template <int NPL>
+__global__ __launch_bounds__(kThreads) void ln_fwd_amax_kernel(
+    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int64_t rows_per_pass, int P, uint32_t* __restrict__ amax) {
+  __shared__ uint32_t smax[kAmaxMaxPasses];
+  if (threadIdx.x < kAmaxMaxPasses) smax[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock; r0 < rows;
+       r0 += (int64_t)gridDim.x * kRowsPerBlock) {
+    const int64_t row = r0 + (threadIdx.x / kLanesPerRow);
+    if (row < rows) {
+      float m = ln_row<NPL>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      if ((threadIdx.x & (kLanesPerRow - 1)) == 0)
+        atomicMax(&smax[(int)(row / rows_per_pass)], __float_as_uint(m));
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < P && smax[threadIdx.x] != 0u)
+    atomicMax(amax + threadIdx.x, smax[threadIdx.x]);
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
@@ -237,6 +283,23 @@ void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta,
                      (int)d, eps, y, mean, rstd);
   OB_LN_NPL(OB_LNF)
 #undef OB_LNF
+}
+
+void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
+                               int64_t rows, int64_t d, float eps, float* y, float* mean,
+                               float* rstd, int P, float* amax, hipStream_t s) {
+  launch_zero_words(amax, P, s);
+  if (rows == 0) return;
+  const int npl = (int)ceil_div(d, kLanesPerRow);
+  int64_t nb = ceil_div(rows, kRowsPerBlock);
+  if (nb > 4096) nb = 4096;  // one LDS max + one global atomicMax per (block, pass)
+  const int64_t rpp = rows / P;
+#define OB_LNFA(N)                                                                           \
+  hipLaunchKernelGGL((ln_fwd_amax_kernel<N>), dim3((unsigned)nb), dim3(kThreads), 0, s, x,    \
+                     gamma, beta, rows, (int)d, eps, y, mean, rstd, rpp, P,                  \
+                     reinterpret_cast<uint32_t*>(amax));
+  OB_LN_NPL(OB_LNFA)
+#undef OB_LNFA
 }
 
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,

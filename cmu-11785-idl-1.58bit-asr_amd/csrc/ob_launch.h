@@ -168,11 +168,24 @@ bool launch_ternary_gemm_i8(const float* A, int P, int64_t M, int64_t K, const u
 void launch_ctc_greedy(const float* logits, const int64_t* lens, int64_t B, int64_t T, int64_t V,
                        int blank, int* ids, int* out, int* out_len, hipStream_t s);
 
+// fused epilogue (mode 1: C = silu(y), per-pass max|C| into amax_out (zeroed here);
+// mode 2: C = R + rscale * (valid ? y : 0*y) with lens / T row validity); N % 4 == 0
+bool launch_ternary_gemm_i8_epi(const float* A, int P, int64_t M, int64_t K,
+                                const uint32_t* codes, const uint32_t* codes1,
+                                const int* pass_bits, int64_t N, const float* alpha,
+                                int alpha_raw, const float* amax, const float* bias, float* C,
+                                int mode, const float* R, float rscale, const int* lens, int64_t T,
+                                float* amax_out, hipStream_t s);
+
 // layernorm.hip (LayerNorm over the last dim, d <= 512; deterministic dgamma/dbeta)
 bool layernorm_supported(int64_t d);
 size_t layernorm_bwd_workspace(int64_t rows, int64_t d);
 void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                           int64_t d, float eps, float* y, float* mean, float* rstd, hipStream_t s);
+// + per-pass max|y| into amax[P] (zeroed here first; rows % P == 0, P <= 8)
+void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
+                               int64_t rows, int64_t d, float eps, float* y, float* mean,
+                               float* rstd, int P, float* amax, hipStream_t s);
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                           const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx, float* dgamma,
                           float* dbeta, void* ws, hipStream_t s);

@@ -157,12 +157,40 @@ __global__ __launch_bounds__(kThreads) void act_dequant_kernel(const float* __re
   }
 }
 
-template <int NT, int NCH>
+// Fused epilogues of the inference call sites (the fp32 path's are in tgemm.hip):
+//   I8_SWISH     C = silu(y) and the per-pass max|C| into amax_out (the int8 scale of the
+//                next BitLinear, ff.lin2: conformer.py:36-45 at dropout 0);
+//   I8_RESIDUAL  C = R + rscale * (row valid ? y : 0*y)  (ff.lin2 / mhsa.out_proj + x).
+// Stores go row-coalesced through a per-wave LDS staging tile, as in tgemm.hip.
+constexpr int kI8Plain = 0, kI8Swish = 1, kI8Residual = 2;
+struct I8Epi {
+  const float* R;
+  float rscale;
+  const int* lens;
+  int T;
+  uint32_t* amax_out;
+};
+
+// torch's silu formula (x / (1 + exp(-x)), accurate expf and IEEE division): the fused
+// int8 FFN equals the unfused module path bit for bit (same values -> same absmax -> same
+// int8 quantization of ff.lin2's input).
+__device__ __forceinline__ float silu_ref(float z) { return z / (1.0f + expf(-z)); }
+
+__host__ __device__ inline size_t i8_stage_off(int nt, int nch) {
+  return (((size_t)(16 * nt) * (size_t)(64 * nch + 16)) + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t i8_stage_bytes(int nt) {
+  const int cw = nt < 4 ? nt : 4;
+  return (size_t)4 * 16 * (16 * cw + 4) * sizeof(float);
+}
+
+template <int NT, int NCH, int EPI>
 __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ amax, const float* __restrict__ bias, float* __restrict__ C,
-    const uint32_t* __restrict__ codes1, const int* __restrict__ pass_bits) {
+    const uint32_t* __restrict__ codes1, const int* __restrict__ pass_bits, I8Epi ep) {
+  const int64_t rowbase = pass_bits ? (int64_t)blockIdx.y * M : 0;
   int p = 0;
   if (pass_bits) {
     p = blockIdx.y;
@@ -170,6 +198,7 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
     A += (int64_t)p * M * K;
     C += (int64_t)p * M * N;
   }
+  (void)rowbase;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kpad = 64 * NCH;
   constexpr int stride = kpad + 16;  // bytes per image row
@@ -203,6 +232,7 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
     const int col = n0 + 16 * t + r;
     bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
   }
+  float amx = 0.0f;  // I8_SWISH: this lane's max|C|
 
   for (int rt = rg; rt < n_rt; rt += rgroups) {
     const int64_t m0 = (int64_t)rt * kRows + wave * 16;
@@ -240,15 +270,81 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[t], acc[t], 0, 0, 0);
     }
 
+    if constexpr (EPI == kI8Plain) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = n0 + 16 * t + r;
-      if (col >= N) continue;
+      for (int t = 0; t < NT; ++t) {
+        const int col = n0 + 16 * t + r;
+        if (col >= N) continue;
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int64_t orow = m0 + 4 * g + reg;
-        if (orow < M) C[orow * N + col] = epilogue(acc[t][reg], osc, bcol[t]);
+        for (int reg = 0; reg < 4; ++reg) {
+          const int64_t orow = m0 + 4 * g + reg;
+          if (orow < M) C[orow * N + col] = epilogue(acc[t][reg], osc, bcol[t]);
+        }
       }
+    } else {
+      // row-coalesced (host-checked: N % 4 == 0, C / R 16-B aligned)
+      constexpr int kCW = NT < 4 ? NT : 4, kCC = 16 * kCW, kLd = kCC + 4, kQ = kCC / 4;
+      float* stg = reinterpret_cast<float*>(smem + i8_stage_off(NT, NCH)) + wave * 16 * kLd;
+#pragma unroll
+      for (int c0 = 0; c0 < NT; c0 += kCW) {
+#pragma unroll
+        for (int t = 0; t < kCW; ++t) {
+          if (c0 + t >= NT) continue;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            stg[(4 * g + reg) * kLd + 16 * t + r] = epilogue(acc[c0 + t][reg], osc, bcol[c0 + t]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int it = 0; it < kCW; ++it) {
+          const int idx = it * 64 + lane, row = idx / kQ, c4 = idx - row * kQ;
+          const int64_t orow = m0 + row;
+          const int col = n0 + 16 * c0 + 4 * c4;
+          const f32x4 y = *reinterpret_cast<const f32x4*>(stg + row * kLd + 4 * c4);
+          if (orow < M && col < N && 4 * c4 < 16 * (NT - c0)) {
+            f32x4 out;
+            if constexpr (EPI == kI8Swish) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                out[e] = silu_ref(y[e]);
+                amx = fmaxf(amx, fabsf(out[e]));
+              }
+            } else {
+              bool valid = true;
+              if (ep.lens) {
+                const int64_t grow = rowbase + orow;
+                const int64_t bb = grow / ep.T;
+                valid = (grow - bb * ep.T) < ep.lens[bb];
+              }
+              const f32x4 rv = *reinterpret_cast<const f32x4*>(ep.R + (rowbase + orow) * N + col);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+#pragma clang fp contract(off)
+                const float v = valid ? y[e] : y[e] * 0.0f;
+                out[e] = rv[e] + (ep.rscale == 1.0f ? v : ep.rscale * v);
+              }
+            }
+            *reinterpret_cast<f32x4*>(C + orow * N + col) = out;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  if constexpr (EPI == kI8Swish) {
+    // the block's max|C| -> one atomicMax per block (order-independent: deterministic)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o));
+    __shared__ uint32_t bmax[kThreads / 64];
+    if (lane == 0) bmax[wave] = __float_as_uint(amx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t m = bmax[0];
+#pragma unroll
+      for (int w2 = 1; w2 < kThreads / 64; ++w2) m = max(m, bmax[w2]);
+      if (m != 0u) atomicMax(ep.amax_out + p, m);
     }
   }
 }
@@ -257,31 +353,41 @@ size_t i8_image_bytes(int nt, int64_t K) {
   return (size_t)(16 * nt) * (size_t)(64 * ceil_div(K, 64) + 16);
 }
 
-int pick_nt_i8(int64_t N, int64_t K) {
+// fused epilogues add the staging tiles; their total stays within 80 KB (2 blocks per CU)
+int pick_nt_i8(int64_t N, int64_t K, bool epi = false) {
   static const int cands[] = {12, 9, 6, 4, 3, 2, 1};
+  auto fits = [&](int nt) {
+    return epi ? i8_stage_off(nt, (int)ceil_div(K, 64)) + i8_stage_bytes(nt) <= 80 * 1024
+               : i8_image_bytes(nt, K) <= kMaxLds;
+  };
   for (int nt : cands)
-    if (N % (16 * nt) == 0 && i8_image_bytes(nt, K) <= kMaxLds) return nt;
+    if (N % (16 * nt) == 0 && fits(nt)) return nt;
   for (int nt : cands)
-    if (16 * nt <= ((N + 15) & ~int64_t(15)) && i8_image_bytes(nt, K) <= kMaxLds) return nt;
+    if (16 * nt <= ((N + 15) & ~int64_t(15)) && fits(nt)) return nt;
   return 0;
 }
 
 template <int NT>
 bool launch_i8_nt(const float* A, int P, int64_t M, int64_t K, const uint32_t* codes,
                   const uint32_t* codes1, const int* pass_bits, int64_t N, const float* alpha,
-                  int alpha_raw, const float* amax, const float* bias, float* C, hipStream_t s) {
+                  int alpha_raw, const float* amax, const float* bias, float* C, hipStream_t s,
+                  int mode = kI8Plain, const I8Epi& ep = I8Epi{}) {
   const int n_ct = (int)ceil_div(N, 16 * NT);
   const int n_rt = (int)ceil_div(M, kRows);
   int rgroups = kTargetBlocks / (n_ct * P);
   if (rgroups < 1) rgroups = 1;
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
-  const size_t lds = i8_image_bytes(NT, K);
   const int KW = (int)ceil_div(K, 16);
-#define OB_I8(NCH)                                                                          \
-  hipLaunchKernelGGL((tgemm_i8_kernel<NT, NCH>), grid, dim3(kThreads), lds, s, A, M, (int)K, \
-                     codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, amax, bias, C, \
-                     codes1, pass_bits);                                                     \
+#define OB_I8E(NCH, E)                                                                        \
+  hipLaunchKernelGGL((tgemm_i8_kernel<NT, NCH, E>), grid, dim3(kThreads),                     \
+                     i8_stage_off(NT, NCH) + (E == kI8Plain ? 0 : i8_stage_bytes(NT)), s, A, M, \
+                     (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, amax,     \
+                     bias, C, codes1, pass_bits, ep);
+#define OB_I8(NCH)                                                   \
+  if (mode == kI8Swish) { OB_I8E(NCH, kI8Swish) }                    \
+  else if (mode == kI8Residual) { OB_I8E(NCH, kI8Residual) }         \
+  else { OB_I8E(NCH, kI8Plain) }                                     \
   return true;
   switch (ceil_div(K, 64)) {
     case 1: OB_I8(1)
@@ -296,6 +402,7 @@ bool launch_i8_nt(const float* A, int P, int64_t M, int64_t K, const uint32_t* c
     default: return false;
   }
 #undef OB_I8
+#undef OB_I8E
 }
 
 }  // namespace
@@ -339,6 +446,32 @@ bool launch_ternary_gemm_i8(const float* A, int P, int64_t M, int64_t K, const u
     case 1: return launch_i8_nt<1>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
     default: return false;
   }
+}
+
+bool launch_ternary_gemm_i8_epi(const float* A, int P, int64_t M, int64_t K,
+                                const uint32_t* codes, const uint32_t* codes1,
+                                const int* pass_bits, int64_t N, const float* alpha,
+                                int alpha_raw, const float* amax, const float* bias, float* C,
+                                int mode, const float* R, float rscale, const int* lens, int64_t T,
+                                float* amax_out, hipStream_t s) {
+  I8Epi ep{R, rscale, lens, (int)(T > 0 ? T : 1), reinterpret_cast<uint32_t*>(amax_out)};
+  if (mode == kI8Swish) launch_zero_words(amax_out, P, s);
+  if (M == 0 || N == 0 || P == 0) return true;
+#define OB_I8NT(V)                                                                             \
+  case V:                                                                                      \
+    return launch_i8_nt<V>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, \
+                           C, s, mode, ep);
+  switch (pick_nt_i8(N, K, true)) {
+    OB_I8NT(12)
+    OB_I8NT(9)
+    OB_I8NT(6)
+    OB_I8NT(4)
+    OB_I8NT(3)
+    OB_I8NT(2)
+    OB_I8NT(1)
+    default: return false;
+  }
+#undef OB_I8NT
 }
 
 }  // namespace ob

@@ -32,8 +32,9 @@ from .attention import fused_attention_supported, rel_pos_attention
 from .conv import (conv2d_bias_relu, conv_module_fused, conv_module_supported, depthwise_conv1d,
                    subsample_convs, subsample_supported)
 from .embedding import embedding
-from .fused import ffn_residual, fused_supported, linear_residual
-from .layernorm import layer_norm, layer_norm_fork
+from .fused import (ffn_residual, ffn_residual_i8, fused_supported, i8_fused_supported,
+                    linear_residual, linear_residual_i8)
+from .layernorm import fused_layernorm_supported, layer_norm, layer_norm_amax, layer_norm_fork
 from .linear import linear
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
@@ -56,8 +57,14 @@ class LayerNorm(nn.Module):
     def __init__(self, d_model: int):
         super().__init__()
         self.ln = nn.LayerNorm(d_model)
+        # set by quant.set_act_quant on the LNs that feed int8 BitLinears: at inference the
+        # LN kernel also produces the consumer's per-tensor absmax (y._ob_amax)
+        self.emit_amax = False
 
     def forward(self, x):
+        if (self.emit_amax and not torch.is_grad_enabled()
+                and fused_layernorm_supported(x, x.shape[-1])):
+            return layer_norm_amax(x, self.ln.weight, self.ln.bias, self.ln.eps)
         return layer_norm(x, self.ln.weight, self.ln.bias, self.ln.eps)
 
     def fork(self, x):
@@ -82,7 +89,15 @@ class FeedForwardModule(nn.Module):
         self.lin2 = QuantizedLinear(d_ff, d_model)
         self.dropout = nn.Dropout(dropout)
 
+    # act_quant="absmax_int8" LN gets emit_amax (quant.set_act_quant)
+    int8_ln = True
+
     def forward(self, x, bitwidth: int, mask=None):
+        if mask is None and i8_fused_supported(x, self.lin1, self.lin2, bitwidth=bitwidth,
+                                               p_drop=self.dropout.p if self.training else 0.0):
+            # inference, int8 activations: LN (+absmax) -> lin1 i8 + swish (+absmax of its
+            # output) -> lin2 i8 + 0.5 * residual, no separate absmax / elementwise passes
+            return ffn_residual_i8(self.ln(x), x, self.lin1, self.lin2, bitwidth)
         if mask is None and fused_supported(x, self.lin1, self.lin2, bitwidth=bitwidth):
             # same computation, elementwise ops in the GEMM epilogues (onebit_asr/fused.py)
             p = self.dropout.p if self.training else 0.0
@@ -137,6 +152,8 @@ class MHSA(nn.Module):
     """Relative-position multi-head self-attention (conformer.py:79-138). Five BitLinear
     projections: q/k/v on LN(x), pos_proj on the batch-1 sinusoid table, out_proj."""
 
+    int8_ln = True  # act_quant="absmax_int8": the LN also emits the q/k/v absmax
+
     def __init__(self, d_model: int, n_heads: int, dropout: float):
         super().__init__()
         assert d_model % n_heads == 0
@@ -185,6 +202,9 @@ class MHSA(nn.Module):
             # out_proj -> dropout -> zero padded rows -> + x in the GEMM epilogue
             return linear_residual(ctx, x, self.out_proj, bitwidth, p, 1.0,
                                    None if mask is None else lens, tlen)
+        if i8_fused_supported(ctx, self.out_proj, bitwidth=bitwidth, p_drop=p):
+            return linear_residual_i8(ctx, x, self.out_proj, bitwidth, 1.0,
+                                      None if mask is None else lens, tlen)
         out = self.dropout(self.out_proj(ctx, bitwidth))
         return x + _pad_rows(out, mask)
 

@@ -31,7 +31,8 @@ import torch
 from . import _lib
 from .quant import PassBits, QuantizedLinear
 
-__all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step"]
+__all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
+           "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8"]
 
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
@@ -240,4 +241,77 @@ def linear_residual(inp: torch.Tensor, x: torch.Tensor, lin: QuantizedLinear, bi
     meta = (P, pb, bits, _codes(lin, P, bits), float(rscale), float(p_drop), rng, off, lens,
             int(frames))
     out = _LinearResidualFn.apply(i2, x2, lin.weight, lin.alpha, lin.bias, meta)
+    return out.view(x.shape)
+
+
+# ----------------------------------------------------------------------------------------
+# int8-activation inference (act_quant="absmax_int8", no autograd, dropout off): the same
+# call sites on the int8 matrix cores (csrc/tgemm_i8.hip) with the elementwise tails in the
+# GEMM epilogue, and each activation's per-tensor absmax taken from the kernel that
+# produced it (the LN kernel, lin1's swish epilogue) instead of a separate pass.
+
+def i8_fused_supported(x: torch.Tensor, *layers: QuantizedLinear, bitwidth=None,
+                       p_drop: float = 0.0) -> bool:
+    if os.environ.get("OB_FUSED", "1") == "0" or p_drop > 0.0 or torch.is_grad_enabled():
+        return False
+    if isinstance(bitwidth, PassBits) or bitwidth not in (1, 2):
+        return False
+    lib = _lib.load()
+    return (x.is_cuda and x.dtype == torch.float32
+            and all(m.act_quant == "absmax_int8" and m.quant_off is None
+                    and m.out_features % 4 == 0 and m.in_features % 16 == 0
+                    and m.in_features <= 576 for m in layers)
+            and lib is not None)
+
+
+def _i8_epi(a2: torch.Tensor, amax: torch.Tensor, lin: QuantizedLinear, bits: int, mode: int,
+            R: Optional[torch.Tensor] = None, rscale: float = 1.0,
+            lens: Optional[torch.Tensor] = None, frames: int = 0):
+    rows, k = a2.shape
+    n = lin.out_features
+    codes, _ = lin._codes(bits)
+    y = torch.empty((rows, n), dtype=torch.float32, device=a2.device)
+    amax_out = torch.empty((1,), dtype=torch.float32, device=a2.device) if mode == 1 else None
+    lib = _lib.load()
+    _lib.check(lib.ob_bitlinear_fwd_i8_epi(
+        a2.data_ptr(), 1, rows, k, codes.data_ptr(), None, None, lin.alpha.data_ptr(), 1,
+        amax.data_ptr(), _lib.ptr(lin.bias), n, mode, _lib.ptr(R), float(rscale), _lib.ptr(lens),
+        int(frames), _lib.ptr(amax_out), y.data_ptr(), _lib.stream_of(a2)),
+        "ob_bitlinear_fwd_i8_epi")
+    return y, amax_out
+
+
+def _amax_of(t: torch.Tensor) -> torch.Tensor:
+    from .quant import act_absmax
+
+    amax = getattr(t, "_ob_amax", None)
+    return amax if amax is not None and amax.numel() == 1 else act_absmax(t.contiguous(), 1)
+
+
+@torch.no_grad()
+def ffn_residual_i8(h: torch.Tensor, x: torch.Tensor, lin1: QuantizedLinear,
+                    lin2: QuantizedLinear, bitwidth) -> torch.Tensor:
+    """x + 0.5 * lin2(swish(lin1(h))) (conformer.py:36-45, eval) with int8 activations; h =
+    LN(x), ideally carrying its absmax (LayerNorm.emit_amax)."""
+    bits = int(bitwidth)
+    amax_h = _amax_of(h)
+    h2 = _flat(h, lin1.in_features).contiguous()
+    x2 = _flat(x, lin2.out_features).contiguous()
+    a, amax_a = _i8_epi(h2, amax_h, lin1, bits, 1)
+    out, _ = _i8_epi(a, amax_a, lin2, bits, 2, R=x2, rscale=0.5)
+    return out.view(x.shape)
+
+
+@torch.no_grad()
+def linear_residual_i8(inp: torch.Tensor, x: torch.Tensor, lin: QuantizedLinear, bitwidth,
+                       rscale: float = 1.0, lens: Optional[torch.Tensor] = None,
+                       frames: int = 0) -> torch.Tensor:
+    """x + rscale * pad_zero(lin(inp)) (conformer.py:131-138, eval) with int8 activations."""
+    bits = int(bitwidth)
+    i2 = _flat(inp, lin.in_features).contiguous()
+    x2 = _flat(x, lin.out_features).contiguous()
+    if lens is not None:
+        lens = lens.to(torch.int32).contiguous()
+    out, _ = _i8_epi(i2, _amax_of(i2), lin, bits, 2, R=x2, rscale=rscale, lens=lens,
+                     frames=frames)
     return out.view(x.shape)

@@ -14,7 +14,7 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["layer_norm", "layer_norm_fork", "fused_layernorm_supported"]
+__all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "fused_layernorm_supported"]
 
 
 def fused_layernorm_supported(x: torch.Tensor, d: int) -> bool:
@@ -66,6 +66,26 @@ def layer_norm(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.Tensor
     if not fused_layernorm_supported(x, d):
         return F.layer_norm(x, (d,), weight, bias, eps)
     return _LayerNormFn.apply(x, weight, bias, eps)
+
+
+@torch.no_grad()
+def layer_norm_amax(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.Tensor:
+    """Inference: LN(x) carrying its max|y| (device fp32 [1]) as ``y._ob_amax`` -- the
+    per-tensor int8 scale of the BitLinear that consumes it, produced by the LN kernel itself
+    (ob_layernorm_fwd_amax) instead of a separate absmax pass over y."""
+    d = x.shape[-1]
+    x2 = x.contiguous().view(-1, d)
+    rows = x2.shape[0]
+    y = torch.empty_like(x2)
+    amax = torch.empty((1,), dtype=torch.float32, device=x.device)
+    lib = _lib.load()
+    _lib.check(lib.ob_layernorm_fwd_amax(x2.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), rows,
+                                         d, float(eps), y.data_ptr(), None, None, 1,
+                                         amax.data_ptr(), _lib.stream_of(x2)),
+               "ob_layernorm_fwd_amax")
+    y = y.view(x.shape)
+    y._ob_amax = amax
+    return y
 
 
 class _LayerNormForkFn(torch.autograd.Function):

@@ -149,6 +149,8 @@ def set_act_quant(module: nn.Module, mode: Optional[str]) -> nn.Module:
     for m in module.modules():
         if isinstance(m, QuantizedLinear):
             m.act_quant = mode
+        if getattr(m, "int8_ln", False) and hasattr(getattr(m, "ln", None), "emit_amax"):
+            m.ln.emit_amax = mode == "absmax_int8"
     return module
 
 
@@ -333,13 +335,15 @@ class _BitLinearI8Fn(torch.autograd.Function):
     kernel), dW / dalpha / db from dY and the dequantized activations the forward used."""
 
     @staticmethod
-    def forward(ctx, x2d, weight, alpha, bias, bits, P, codes, codes_t, codes1, codes1_t):
+    def forward(ctx, x2d, weight, alpha, bias, bits, P, codes, codes_t, codes1, codes1_t,
+                amax=None):
         rows, k = x2d.shape
         m = rows // P
         n = weight.shape[0]
         lib = _lib.load()
         stream = _lib.stream_of(x2d)
-        amax = act_absmax(x2d, P)
+        if amax is None:  # (else the producer's: LN / swish epilogue, x._ob_amax)
+            amax = act_absmax(x2d, P)
         y = torch.empty((rows, n), dtype=torch.float32, device=x2d.device)
         pb = bits.tensor if isinstance(bits, PassBits) else None
         _lib.check(
@@ -399,7 +403,7 @@ class _BitLinearI8Fn(torch.autograd.Function):
                                              gw.data_ptr(), galpha.data_ptr(), _lib.ptr(gb),
                                              ws.data_ptr(), ws_bytes, stream)
             _lib.check(st, "ob_bitlinear_bwd_dw")
-        return gx, gw, galpha, gb, None, None, None, None, None, None
+        return gx, gw, galpha, gb, None, None, None, None, None, None, None
 
 
 class _QuantizeSTE(torch.autograd.Function):
@@ -525,8 +529,11 @@ class QuantizedLinear(nn.Module):
         else:
             codes, codes_t = self._codes(bits)
         if self.act_quant == "absmax_int8":
+            amax = getattr(x, "_ob_amax", None)  # the producer's (LN / swish epilogue) scale
+            if amax is not None and amax.numel() != 1:
+                amax = None
             y = _BitLinearI8Fn.apply(x2d, self.weight, self.alpha, self.bias, bits, 1, codes,
-                                     codes_t, None, None)
+                                     codes_t, None, None, amax)
             return y.view(*lead, self.out_features)
         y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bits, codes, codes_t)
         return y.view(*lead, self.out_features)

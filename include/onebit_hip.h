@@ -245,6 +245,20 @@ OB_API int ob_bitlinear_fwd_i8(const float* X, int64_t P, int64_t M, int64_t K,
                                const float* amax, const float* bias, int64_t N, float* Y,
                                void* stream);
 
+/* ob_bitlinear_fwd_i8 with the inference call sites' epilogues fused (conformer.py:36-45
+ * and :131-138 at dropout 0), N % 4 == 0, X / Y / R 16-byte aligned:
+ *   mode 1 (swish)    Y = silu(y) and amax_out[p] = max|Y_p| (amax_out zeroed first): the
+ *                     producer-side int8 scale of the next BitLinear (ff.lin2);
+ *   mode 2 (residual) Y = R + rscale * (valid ? y : 0*y), row r valid iff lens == NULL or
+ *                     (r % T) < lens[r / T] (padded frames zeroed, :137);
+ * where y = the ob_bitlinear_fwd_i8 output. */
+OB_API int ob_bitlinear_fwd_i8_epi(const float* X, int64_t P, int64_t M, int64_t K,
+                                   const uint32_t* codes, const uint32_t* codes1,
+                                   const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                   const float* amax, const float* bias, int64_t N, int mode,
+                                   const float* R, float rscale, const int32_t* lens, int64_t T,
+                                   float* amax_out, float* Y, void* stream);
+
 OB_API int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
                                       const uint32_t* codes2_t, const uint32_t* codes1_t,
                                       const int32_t* pass_bits, const float* alpha,
@@ -341,6 +355,11 @@ OB_API int ob_adamw_clip_step(const ob_adamw_tensor* table, int64_t n_tensors,
 OB_API int ob_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                             int64_t d, float eps, float* y, float* mean, float* rstd,
                             void* stream);
+/* ob_layernorm_fwd plus amax[p] = max|y| over pass p (rows split into P equal passes,
+ * P <= 8): the producer-side per-tensor scale of the int8 BitLinear that consumes y. */
+OB_API int ob_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
+                                 int64_t rows, int64_t d, float eps, float* y, float* mean,
+                                 float* rstd, int64_t P, float* amax, void* stream);
 OB_API size_t ob_layernorm_bwd_workspace(int64_t rows, int64_t d);
 OB_API int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma,
                             const float* mean, const float* rstd, int64_t rows, int64_t d,
