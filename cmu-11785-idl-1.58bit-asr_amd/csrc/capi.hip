@@ -710,15 +710,20 @@ int ob_layernorm_fwd(const float* x, const float* gamma, const float* beta, int6
   return launched();
 }
 
+size_t ob_layernorm_fwd_amax_workspace(int64_t P) {
+  return (P < 1 || P > 8) ? 0 : layernorm_fwd_amax_workspace(P);
+}
+
 int ob_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta, int64_t rows,
                           int64_t d, float eps, float* y, float* mean, float* rstd, int64_t P,
-                          float* amax, void* stream) {
+                          float* amax, void* ws, size_t ws_bytes, void* stream) {
   if (rows < 0 || !layernorm_supported(d) || !(eps >= 0.0f) || P < 1 || P > 8 || rows % P)
     return OB_ERR_SHAPE;
-  if ((rows > 0 && (!x || !y)) || !amax) return OB_ERR_NULL;
+  if ((rows > 0 && (!x || !y)) || !amax || !ws) return OB_ERR_NULL;
+  if (ws_bytes < layernorm_fwd_amax_workspace(P)) return OB_ERR_WORKSPACE;
   if (!aligned4(x) || !aligned4(y) || !aligned4(gamma) || !aligned4(beta) || !aligned4(amax))
     return OB_ERR_ALIGN;
-  launch_layernorm_fwd_amax(x, gamma, beta, rows, d, eps, y, mean, rstd, (int)P, amax,
+  launch_layernorm_fwd_amax(x, gamma, beta, rows, d, eps, y, mean, rstd, (int)P, amax, ws,
                             as_stream(stream));
   return launched();
 }

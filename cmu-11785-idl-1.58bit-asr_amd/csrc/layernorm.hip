@@ -92,15 +92,15 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
 // The same rows plus the per-pass max|y| (the int8 activation scale of the BitLinear that
 // consumes y; passes = consecutive blocks of rows_per_pass rows). Blocks stride over the
 // rows; each keeps per-pass maxima in LDS (ds_max on the fp32 bit patterns: |y| >= 0 so
-// the unsigned order is the float order) and adds them to amax with one global atomicMax
-// per (block, pass) -- max is order-independent, so the result is deterministic. amax must
-// hold zeros (or smaller maxima) on entry.
+// the unsigned order is the float order) and writes them as partials part[p][block]; a
+// one-wave launch reduces them (no same-address atomics: 1024 of those cost 10 us here).
+// Max is order-independent: deterministic.
 constexpr int kAmaxMaxPasses = 8;
 template <int NPL>
 __global__ __launch_bounds__(kThreads) void ln_fwd_amax_kernel(
     const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
-    float* __restrict__ rstd_out, int64_t rows_per_pass, int P, uint32_t* __restrict__ amax) {
+    float* __restrict__ rstd_out, int64_t rows_per_pass, int P, uint32_t* __restrict__ part) {
   __shared__ uint32_t smax[kAmaxMaxPasses];
   if (threadIdx.x < kAmaxMaxPasses) smax[threadIdx.x] = 0u;
   __syncthreads();
@@ -116,9 +116,31 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_amax_kernel(
     }
   }
   __syncthreads();
-  if ((int)threadIdx.x < P && smax[threadIdx.x] != 0u)
-    atomicMax(amax + threadIdx.x, smax[threadIdx.x]);
+  if ((int)threadIdx.x < P) part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = smax[threadIdx.x];
 }
+
+__global__ __launch_bounds__(kThreads) void ln_amax_final_kernel(
+    const uint32_t* __restrict__ part, int nparts, uint32_t* __restrict__ amax) {
+  __shared__ uint32_t red[kThreads / 64];
+  const int p = blockIdx.x;
+  const uint32_t* src = part + (int64_t)p * nparts;
+  uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 8 independent loads in flight per thread
+  for (int i0 = 0; i0 < nparts; i0 += 8 * kThreads) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * kThreads + threadIdx.x;
+      if (i < nparts) m[u] = max(m[u], src[i]);
+    }
+  }
+  uint32_t v = max(max(max(m[0], m[1]), max(m[2], m[3])), max(max(m[4], m[5]), max(m[6], m[7])));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) amax[p] = max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
+constexpr int kAmaxBlocks = 2048;
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
 template <int NPL>
@@ -285,21 +307,29 @@ void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta,
 #undef OB_LNF
 }
 
+size_t layernorm_fwd_amax_workspace(int64_t P) {
+  return sizeof(uint32_t) * (size_t)P * kAmaxBlocks;
+}
+
 void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
                                int64_t rows, int64_t d, float eps, float* y, float* mean,
-                               float* rstd, int P, float* amax, hipStream_t s) {
-  launch_zero_words(amax, P, s);
-  if (rows == 0) return;
+                               float* rstd, int P, float* amax, void* ws, hipStream_t s) {
+  if (rows == 0) {
+    launch_zero_words(amax, P, s);
+    return;
+  }
   const int npl = (int)ceil_div(d, kLanesPerRow);
   int64_t nb = ceil_div(rows, kRowsPerBlock);
-  if (nb > 4096) nb = 4096;  // one LDS max + one global atomicMax per (block, pass)
+  if (nb > kAmaxBlocks) nb = kAmaxBlocks;
   const int64_t rpp = rows / P;
+  uint32_t* part = static_cast<uint32_t*>(ws);
 #define OB_LNFA(N)                                                                           \
   hipLaunchKernelGGL((ln_fwd_amax_kernel<N>), dim3((unsigned)nb), dim3(kThreads), 0, s, x,    \
-                     gamma, beta, rows, (int)d, eps, y, mean, rstd, rpp, P,                  \
-                     reinterpret_cast<uint32_t*>(amax));
+                     gamma, beta, rows, (int)d, eps, y, mean, rstd, rpp, P, part);
   OB_LN_NPL(OB_LNFA)
 #undef OB_LNFA
+  hipLaunchKernelGGL(ln_amax_final_kernel, dim3((unsigned)P), dim3(kThreads), 0, s,
+                     (const uint32_t*)part, (int)nb, reinterpret_cast<uint32_t*>(amax));
 }
 
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,

@@ -182,10 +182,11 @@ bool layernorm_supported(int64_t d);
 size_t layernorm_bwd_workspace(int64_t rows, int64_t d);
 void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                           int64_t d, float eps, float* y, float* mean, float* rstd, hipStream_t s);
-// + per-pass max|y| into amax[P] (zeroed here first; rows % P == 0, P <= 8)
+// + per-pass max|y| into amax[P] (rows % P == 0, P <= 8; per-block partials in ws)
+size_t layernorm_fwd_amax_workspace(int64_t P);
 void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
                                int64_t rows, int64_t d, float eps, float* y, float* mean,
-                               float* rstd, int P, float* amax, hipStream_t s);
+                               float* rstd, int P, float* amax, void* ws, hipStream_t s);
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                           const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx, float* dgamma,
                           float* dbeta, void* ws, hipStream_t s);

@@ -79,10 +79,12 @@ def layer_norm_amax(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.T
     y = torch.empty_like(x2)
     amax = torch.empty((1,), dtype=torch.float32, device=x.device)
     lib = _lib.load()
+    wsb = lib.ob_layernorm_fwd_amax_workspace(1)
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=x.device)
     _lib.check(lib.ob_layernorm_fwd_amax(x2.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), rows,
                                          d, float(eps), y.data_ptr(), None, None, 1,
-                                         amax.data_ptr(), _lib.stream_of(x2)),
-               "ob_layernorm_fwd_amax")
+                                         amax.data_ptr(), ws.data_ptr(), wsb,
+                                         _lib.stream_of(x2)), "ob_layernorm_fwd_amax")
     y = y.view(x.shape)
     y._ob_amax = amax
     return y

@@ -356,10 +356,13 @@ OB_API int ob_layernorm_fwd(const float* x, const float* gamma, const float* bet
                             int64_t d, float eps, float* y, float* mean, float* rstd,
                             void* stream);
 /* ob_layernorm_fwd plus amax[p] = max|y| over pass p (rows split into P equal passes,
- * P <= 8): the producer-side per-tensor scale of the int8 BitLinear that consumes y. */
+ * P <= 8): the producer-side per-tensor scale of the int8 BitLinear that consumes y.
+ * ws: ob_layernorm_fwd_amax_workspace(P) bytes (per-block partial maxima). */
+OB_API size_t ob_layernorm_fwd_amax_workspace(int64_t P);
 OB_API int ob_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
                                  int64_t rows, int64_t d, float eps, float* y, float* mean,
-                                 float* rstd, int64_t P, float* amax, void* stream);
+                                 float* rstd, int64_t P, float* amax, void* ws,
+                                 size_t ws_bytes, void* stream);
 OB_API size_t ob_layernorm_bwd_workspace(int64_t rows, int64_t d);
 OB_API int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma,
                             const float* mean, const float* rstd, int64_t rows, int64_t d,
