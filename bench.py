@@ -229,7 +229,7 @@ def traffic_from(path, kernel):
 
 
 # ------------------------------------------------------------------------- cpu baseline
-def cpu_baseline(seconds: float, bsz: int = 4):
+def cpu_baseline(seconds: float, bsz: int = 4, progress=lambda msg: None):
     """The oracle step (CPU restatement) on a bounded sample of the same workload, on the
     host cores this process may run on (sched_getaffinity; os.cpu_count() is reported
     too). torch intra-op threads: the faster of all those cores and 16 (the box's CPU
@@ -268,6 +268,7 @@ def cpu_baseline(seconds: float, bsz: int = 4):
         t0 = time.perf_counter()
         one()
         trial[th] = time.perf_counter() - t0
+        progress(f"cpu baseline: {th} threads, one step {trial[th]:.1f} s")
     threads = min(trial, key=trial.get)
     torch.set_num_threads(threads)
     times = []
@@ -276,6 +277,7 @@ def cpu_baseline(seconds: float, bsz: int = 4):
         t0 = time.perf_counter()
         one()
         times.append(time.perf_counter() - t0)
+        progress(f"cpu baseline: step {len(times)} {times[-1]:.1f} s")
     t = sorted(times)[len(times) // 2]
     cpu = platform.processor() or platform.machine()
     try:
@@ -553,7 +555,11 @@ def main():
         roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
         out["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not quant_off:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        # (progress always on stderr: the CPU leg runs minutes without other output)
+        out["cpu_baseline"] = cpu_baseline(
+            args.cpu_seconds,
+            progress=lambda m: print(f"[bench {time.strftime('%H:%M:%S')}] {m}", file=sys.stderr,
+                                     flush=True))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

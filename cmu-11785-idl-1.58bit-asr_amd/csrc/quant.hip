@@ -210,6 +210,14 @@ __global__ __launch_bounds__(kThreads) void ste_reduce_kernel(
   // writes back the XCD L2 per block (measured 20 us for this kernel at Conformer-S).
   // `ticket` was zeroed by dw_partial (previous kernel on this stream) or a memset, and
   // is re-zeroed by the last block.
+  // ISA assumption (pinned by the #error below): on CDNA (gfx9-family) an agent-scope
+  // relaxed atomic store is a write-through (sc1) vector store counted by vmcnt, so the
+  // s_waitcnt vmcnt(0) orders it before the ticket; gfx10+ count stores in vscnt and would
+  // need a release / acquire pair here instead.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__) && \
+    !defined(__gfx941__) && !defined(__gfx940__) && !defined(__gfx90a__)
+#error "ste_reduce's last-block finish assumes CDNA (gfx9) store ordering; re-derive it for this target"
+#endif
   int last = 0;
   if (lane == 0) {
     __hip_atomic_store(&apart[blockIdx.x], prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
