@@ -107,7 +107,7 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
 
     lib = _lib.load()
     P = PASSES
-    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0], "dw_partial+ste_reduce": [0.0, 0.0, 0.0, 0]}
+    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0], "dw_lds+dw_finish": [0.0, 0.0, 0.0, 0]}
     # fam value: [total_time_us_per_step, total_bytes_per_step, total_flops_per_step, launches]
     detail = []
     side = torch.cuda.Stream(dev)
@@ -180,7 +180,7 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
         f[1] += count * by_f + n_dx * by_dx
         f[2] += (count + n_dx) * fl
         f[3] += count + n_dx
-        f = fam["dw_partial+ste_reduce"]
+        f = fam["dw_lds+dw_finish"]
         f[0] += count * t_dw
         f[1] += count * by_dw
         f[2] += count * fl

@@ -4,8 +4,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. gfx950 correction (MI355X_MICROARCH.md,
 HBM/rocprofv3 section): FETCH_SIZE reports half the bytes of a wide coalesced streaming
 read, so it is doubled; WRITE_SIZE is taken as is. Per (shape, op) the median over the
-timed dispatches of each kernel is used; one "launch" of the dW family is one dw_bf16x6
-dispatch plus its ste_reduce dispatch. Families are weighted by launches per training
+timed dispatches of each kernel is used; one "launch" of the dW family is one dw_lds
+dispatch plus its dw_finish dispatch. Families are weighted by launches per training
 step exactly as bench.py's roofline() weights its time and algorithmic bytes.
 
 usage: python tools/traffic_json.py gpurun_out/TAG > profiles/pmc_traffic.json"""
@@ -20,7 +20,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 # launches per step (bench.py ql_shapes at Conformer-S: 16 blocks, 2 FFNs, 4 q/k/v/out)
 COUNT = {"lin1": 32, "lin2": 32, "qkvo": 64, "pos": 16}
-KERNELS = {"fwd": ("tgemm",), "dx": ("tgemm",), "dw": ("dw_bf16x6", "ste_reduce")}
+KERNELS = {"fwd": ("tgemm",), "dx": ("tgemm",), "dw": ("dw_lds", "dw_finish")}
 
 
 def per_dispatch(path, sub):
@@ -52,7 +52,7 @@ def main():
                     raise SystemExit(f"missing counters for {shape} {op} {sub}")
                 tot += (2.0 * f + w) * 1024.0
             out[f"{shape}_{op}_hbm_bytes"] = int(tot)
-            key = "dw_partial+ste_reduce" if op == "dw" else "ternary_gemm"
+            key = "dw_lds+dw_finish" if op == "dw" else "ternary_gemm"
             b, n = fam.get(key, (0.0, 0))
             fam[key] = (b + cnt * tot, n + cnt)
     for key, (b, n) in fam.items():
