@@ -510,219 +510,6 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
 }
 
 // ---------------------------------------------------------------------------------
-// LDS-staged variant for K % 8 == 0, K <= 160 (the Conformer-S K = 144 launches): each
-// wave streams ITS OWN 16 A rows per row tile into a private LDS double buffer with
-// global_load_lds_dwordx4 (full 16-B-per-lane lines, no VGPR destination), one tile ahead
-// of the tile it computes, and reads its A fragments from LDS. No barrier in the tile loop
-// (the buffers are wave-private; the B image is read-only after the prologue), so the four
-// waves run decoupled; the prefetch needs no registers.
-// LDS row = K/4 + 1 granules of 16 B (the odd granule count makes the 16 rows of a fragment
-// read start on 16 distinct 4-bank groups); the padding granule and the tail of the last
-// instruction load a harmless in-row address. Granule s of the wave's tile image is
-// written by lane s % 64 of instruction s / 64 (LDS-DMA writes lane-linear; the per-lane
-// GLOBAL address realises the padded layout).
-// ---------------------------------------------------------------------------------
-constexpr int kLdsRows = 16;  // rows per wave per tile
-
-__host__ __device__ constexpr int glds_instr(int K) { return (kLdsRows * (K / 4 + 1) + 63) / 64; }
-constexpr int kLdsBufs = 3;  // per wave: the tile computed + two in flight
-__host__ __device__ constexpr size_t lds_abuf_bytes(int K) {
-  return (size_t)4 * kLdsBufs * glds_instr(K) * 1024;  // 4 waves x kLdsBufs buffers
-}
-
-template <int NT, int KC, int EPI>
-__global__ __launch_bounds__(kThreads, 1) void tgemm_lds_kernel(
-    const float* __restrict__ A, int64_t M, const uint32_t* __restrict__ codes, int KW, int N,
-    int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
-    const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
-    const int* __restrict__ pass_bits, EpiArgs ep) {
-  static_assert(KC % 8 == 0 && KC <= 160, "LDS-staged path: K % 8 == 0, K <= 160");
-  constexpr int K = KC;
-  constexpr int NCH = (K + 31) / 32;
-  constexpr int kInstr = glds_instr(K);
-  constexpr int G = K / 4;  // granules per row; G + 1 is odd (K % 8 == 0)
-  select_pass(A, C, codes, codes1, pass_bits, M, K, N);
-  const int64_t rowbase = pass_bits ? (int64_t)blockIdx.y * M : 0;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __bf16* bimg = reinterpret_cast<__bf16*>(smem);
-  constexpr int kpad = 32 * NCH;
-  constexpr int stride = kpad + 8;
-  constexpr int kwp = kpad >> 4;
-  const int L = xcd_logical(blockIdx.x, gridDim.x);
-  const int ct = L % n_ct;
-  const int rg = L / n_ct;
-  const int n0 = ct * (16 * NT);
-
-  // B image (as tgemm_bf16x3_kernel)
-  const int nwords = 16 * NT * kwp;
-  auto decode_store = [&](int idx, uint32_t word) {
-    const int nl = idx / kwp, w = idx - nl * kwp;
-    word = (n0 + nl < N && w < KW && idx < nwords) ? word : 0u;
-    u32x4 lo4, hi4;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      lo4[p] = code_bf16((word >> (4 * p)) & 3u) | (code_bf16((word >> (4 * p + 2)) & 3u) << 16);
-      hi4[p] = code_bf16((word >> (4 * p + 16)) & 3u) |
-               (code_bf16((word >> (4 * p + 18)) & 3u) << 16);
-    }
-    if (idx < nwords) {
-      u32x4* dst = reinterpret_cast<u32x4*>(bimg + nl * stride + 16 * w);
-      dst[0] = lo4;
-      dst[1] = hi4;
-    }
-  };
-  auto word_at = [&](int idx) -> uint32_t {
-    const int nl = idx / kwp, w = idx - nl * kwp;
-    int64_t n = n0 + nl;
-    n = n < N ? n : N - 1;
-    const int wc = w < KW ? w : KW - 1;
-    return codes[n * KW + wc];
-  };
-  {
-    constexpr int kWpt = (16 * NT * 2 * NCH + kThreads - 1) / kThreads;
-    uint32_t wv[kWpt];
-#pragma unroll
-    for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThreads);
-#pragma unroll
-    for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThreads, wv[i]);
-  }
-  __syncthreads();
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15;
-  const int g = lane >> 4;
-  const int kg = 8 * g;
-  const __bf16* brow = bimg + r * stride + kg;
-  // wave-private A buffers after the B image: [2][kInstr * 64] granules of 16 B
-  constexpr size_t bimg_bytes_al = ((size_t)16 * NT * stride * 2 + 1023) & ~(size_t)1023;
-  float* abuf =
-      reinterpret_cast<float*>(smem + bimg_bytes_al) + (size_t)wave * kLdsBufs * kInstr * 256;
-  // this lane's granule of each instruction -> (row, k offset) of the wave's 16-row tile;
-  // padding / tail granules re-read the row start (never used: B is zero for k >= K).
-  int goff[kInstr];
-#pragma unroll
-  for (int j = 0; j < kInstr; ++j) {
-    const int sg = 64 * j + lane;
-    int row = sg / (G + 1), q = sg - row * (G + 1);
-    if (row >= kLdsRows) { row = kLdsRows - 1; q = 0; }
-    if (q >= G) q = 0;
-    goff[j] = row * K + 4 * q;
-  }
-  const float a_eff = effective_alpha(alpha, alpha_raw);
-  const uint32_t dkey = (EPI != kEpiNone && ep.dc.on) ? drop_key(ep.rng[0], ep.rng[1] + ep.rng_off) : 0u;
-  float bcol[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int col = n0 + 16 * t + r;
-    bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
-  }
-
-  // issue the wave's tile rt into buffer b (rows past M re-read row M-1: never stored)
-  auto issue = [&](int rt, int b) {
-    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
-    const int64_t last = M - 1 - m0;  // rows of this sub-tile that exist: 0..last
-    float* dst = abuf + (size_t)b * kInstr * 256;
-#pragma unroll
-    for (int j = 0; j < kInstr; ++j) {
-      int off = goff[j];
-      const int row = off / K;  // small: rows 0..15
-      if (row > last) off -= (int)((row - last) * K);
-      __builtin_amdgcn_global_load_lds((const void*)(A + m0 * K + off),
-                                       (__attribute__((address_space(3))) void*)(dst + j * 256),
-                                       16, 0, 0);
-    }
-  };
-
-  // ring of kLdsBufs buffers: tiles it+1 and it+2 are in flight while tile it computes
-  int rt = rg;
-  if (rt < n_rt) issue(rt, 0);
-  if (rt + rgroups < n_rt) issue(rt + rgroups, 1);
-  constexpr int kW1 = kInstr, kW2 = 2 * kInstr;
-  for (int it = 0; rt < n_rt; ++it, rt += rgroups) {
-    const int buf = it % kLdsBufs;
-    const int ahead = (rt + 2 * rgroups < n_rt) ? 2 : ((rt + rgroups < n_rt) ? 1 : 0);
-    if (ahead == 2) {
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): reads of the buffer reused are done
-      issue(rt + 2 * rgroups, (it + 2) % kLdsBufs);
-      __builtin_amdgcn_s_waitcnt(0x0f70 | (kW2 & 0xf) | ((kW2 >> 4) << 14));  // vmcnt(2 tiles)
-    } else if (ahead == 1) {
-      __builtin_amdgcn_s_waitcnt(0x0f70 | (kW1 & 0xf) | ((kW1 >> 4) << 14));  // vmcnt(1 tile)
-    } else {
-      __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    }
-    const float* arow = abuf + (size_t)buf * kInstr * 256 + r * 4 * (G + 1);
-    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
-
-    f32x4 acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      bf16x8 bq[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        bq[t] = *reinterpret_cast<const bf16x8*>(brow + t * 16 * stride + 32 * c);
-      f32x4 x0 = *reinterpret_cast<const f32x4*>(arow + 32 * c + kg);
-      f32x4 x1 = *reinterpret_cast<const f32x4*>(arow + 32 * c + kg + 4);
-      if (c == NCH - 1) {  // k >= K holds padding / the next row: zero it (B is 0 there, but
-                           // a non-finite neighbour must not reach this row's output)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] = (32 * c + kg + e < K) ? x0[e] : 0.0f;
-          x1[e] = (32 * c + kg + 4 + e < K) ? x1[e] : 0.0f;
-        }
-      }
-      bf16x8 hi, mid, lo;
-      split3(x0, x1, hi, mid, lo);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(lo, bq[t], acc[t]);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(mid, bq[t], acc[t]);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(hi, bq[t], acc[t]);
-    }
-
-    __builtin_amdgcn_sched_barrier(0);
-    // epilogue operand (residual / pre-activation): rolling prefetch kPre tiles ahead, so at
-    // most (kPre + 1) * 4 values are live (all NT * 4 at once spilled at NT = 12)
-    constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
-    constexpr int kPre = 2;
-    float rv[NT][4];
-    auto load_r = [&](int t) {
-      const int col = min(n0 + 16 * t + r, N - 1);
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int64_t orow = min(m0 + 4 * g + reg, M - 1);
-        rv[t][reg] = ep.R[(rowbase + orow) * N + col];
-      }
-    };
-    if constexpr (kHasR) {
-#pragma unroll
-      for (int t = 0; t < kPre && t < NT; ++t) load_r(t);
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if constexpr (kHasR) {
-        if (t + kPre < NT) load_r(t + kPre);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      const int col = n0 + 16 * t + r;
-      if (col >= N) continue;
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int64_t orow = m0 + 4 * g + reg;
-        if (orow >= M) continue;
-        const float y = fmaf(a_eff, acc[t][reg], bcol[t]);
-        if constexpr (EPI == kEpiNone) C[orow * N + col] = y;
-        else epi_store<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, rv[t][reg]);
-      }
-      if constexpr (EPI != kEpiNone) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------
 // fp32-MFMA ternary GEMM (exact fp32 fma chain), 64 rows x 48 columns per block.
 // Per 16-wide k chunk a lane loads X[row][kc+4g .. kc+4g+3] and one code word per n tile;
 // byte g of that word holds the 4 codes of k = kc+4g+e, e = 0..3.
@@ -890,76 +677,6 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
 #undef OB_TGEMM_E
 }
 
-// LDS-staged kernel (K = 144 / 64): widest NT whose B image + the A buffers fit 160 KB.
-constexpr size_t kLdsBudget = 160 * 1024;
-
-int pick_nt_lds(int64_t N, int K, int epi_mode) {
-  const int cap = (epi_mode == kEpiSwishDrop || epi_mode == kEpiSwishDropBwd) ? 4 : 12;
-  static const int cands[] = {12, 9, 6, 4, 3};
-  const size_t abuf = lds_abuf_bytes(K);
-  for (int nt : cands) {
-    if (nt > cap || N % (16 * nt) != 0) continue;
-    const size_t bimg = ((size_t)16 * nt * ((K + 31) / 32 * 32 + 8) * 2 + 1023) & ~(size_t)1023;
-    if (bimg + abuf <= kLdsBudget) return nt;
-  }
-  return 0;
-}
-
-// Opt-in (OB_TGEMM_LDS=1): measured slower than the register-streamed kernel at
-// Conformer-S (qkvo 14.1 vs 10.5 us, lin1 fwd 32.0 vs 26.0 us with a 3-deep ring): one
-// block per CU (145 KB LDS) leaves 1 wave per SIMD, and 375 64-row tiles over 256 CUs
-// imbalance. Kept as the base for a 2-blocks-per-CU variant.
-bool lds_path_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("OB_TGEMM_LDS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-template <int NT, int KC>
-void launch_lds(const float* A, int64_t M, const uint32_t* codes, int64_t N, const float* alpha,
-                int alpha_raw, const float* bias, float* C, const uint32_t* codes1,
-                const int* pass_bits, int P, const EpiArgs& ep, hipStream_t s) {
-  const int n_ct = (int)ceil_div(N, 16 * NT);
-  const int n_rt = (int)ceil_div(M, kRows);
-  int rgroups = 256 / (n_ct * P);  // one block per CU (the LDS image allows one)
-  if (rgroups < 1) rgroups = 1;
-  if (rgroups > n_rt) rgroups = n_rt;
-  const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
-  constexpr int stride = (KC + 31) / 32 * 32 + 8;
-  const size_t lds = (((size_t)16 * NT * stride * 2 + 1023) & ~(size_t)1023) + lds_abuf_bytes(KC);
-  const int KW = (int)ceil_div(KC, 16);
-#define OB_TL(E)                                                                              \
-  hipLaunchKernelGGL((tgemm_lds_kernel<NT, KC, E>), grid, dim3(kThreads), lds, s, A, M, codes, KW, \
-                     (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, bias, C, codes1, pass_bits, ep)
-  switch (ep.mode) {
-    case kEpiSwishDrop:
-      if constexpr (NT <= 4) OB_TL(kEpiSwishDrop);
-      break;
-    case kEpiResidual: OB_TL(kEpiResidual); break;
-    case kEpiSwishDropBwd:
-      if constexpr (NT <= 4) OB_TL(kEpiSwishDropBwd);
-      break;
-    default: OB_TL(kEpiNone); break;
-  }
-#undef OB_TL
-}
-
-template <int KC>
-bool try_lds(const float* A, int64_t M, const uint32_t* codes, int64_t N, const float* alpha,
-             int alpha_raw, const float* bias, float* C, const uint32_t* codes1,
-             const int* pass_bits, int P, const EpiArgs& ep, hipStream_t s) {
-  switch (pick_nt_lds(N, KC, ep.mode)) {
-    case 12: launch_lds<12, KC>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); return true;
-    case 9: launch_lds<9, KC>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); return true;
-    case 6: launch_lds<6, KC>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); return true;
-    case 4: launch_lds<4, KC>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); return true;
-    case 3: launch_lds<3, KC>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); return true;
-    default: return false;
-  }
-}
-
 }  // namespace
 
 void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
@@ -982,14 +699,6 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
     ep.rng_off = epi->rng_off;
   }
   const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-  if (vec && !use_f32_gemm() && lds_path_enabled()) {
-    if (K == 144 && try_lds<144>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P,
-                                 ep, s))
-      return;
-    if (K == 64 && try_lds<64>(A, M, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P,
-                               ep, s))
-      return;
-  }
   const int nt = vec && !use_f32_gemm() ? pick_nt(N, K, ep.mode) : 0;
 #define OB_NT(V)                                                                            \
   case V:                                                                                   \
