@@ -5,7 +5,7 @@
 // element index mixed with a per-call key. The key folds (seed, counter) -- a device
 // int64[2] the host advances once per call -- so a captured HIP graph draws a fresh mask
 // on every replay, and a backward kernel regenerates its forward's mask from the same
-// (seed, counter) without storing it. ~8 VALU ops per element.
+// (seed, counter) without storing it. ~8 VALU ops (2 multiplies) per element.
 // The mask is not torch's Philox stream; no reference-visible quantity depends on it
 // (dropout is stochastic in the reference too, train.py:200; parity runs use p = 0).
 #pragma once
@@ -29,8 +29,12 @@ __device__ __forceinline__ uint32_t drop_key(uint64_t seed, uint64_t ctr) {
                 fmix32((uint32_t)ctr * 0x27D4EB2Fu + (uint32_t)(ctr >> 32)));
 }
 
+// Two 32-bit multiplies per element (the fmix32 avalanche; v_mul_lo_u32 is a
+// quarter-rate instruction, and this hash runs once per element of every fused dropout):
+// the index's high word is folded in by a rotate, not a multiply.
 __device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t idx) {
-  return fmix32(((uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x165667B1u)) * 0x9E3779B1u + key);
+  const uint32_t hi = (uint32_t)(idx >> 32);
+  return fmix32((uint32_t)idx ^ ((hi << 16) | (hi >> 16)) ^ key);
 }
 
 struct DropCfg {
