@@ -393,6 +393,51 @@ int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, siz
 
 namespace {
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+}  // namespace
+
+int ob_dense_supported(int64_t K, int64_t N) { return dense_gemm_supported(K, N) ? 1 : 0; }
+
+int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_trans,
+                  const float* bias, int64_t N, float* Y, void* stream) {
+  if (M < 0 || M > ((int64_t)1 << 40) || !dense_gemm_supported(K, N)) return OB_ERR_SHAPE;
+  if (!W || (M > 0 && (!X || !Y))) return OB_ERR_NULL;
+  if (!aligned16(X) || !aligned16(W) || !aligned16(Y) || !aligned4(bias)) return OB_ERR_ALIGN;
+  if (!launch_dense_gemm(X, M, K, W, w_trans, bias, N, Y, as_stream(stream))) return OB_ERR_SHAPE;
+  return launched();
+}
+
+size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N <= 0 || K <= 0 || N % 48 != 0 || K % 48 != 0) return 0;
+  if (plan_dw(M, N, K).variant < 9) return 0;  // the LDS bf16x6 tiles only
+  return dw_layout(1, M, N, K).total;
+}
+
+int ob_dense_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K, float* dW,
+                float* db, void* ws, size_t ws_bytes, void* stream) {
+  const size_t need = ob_dense_dw_workspace(M, N, K);
+  if (need == 0) return OB_ERR_SHAPE;
+  if (!dW || !ws || (M > 0 && (!dY || !X))) return OB_ERR_NULL;
+  if (ws_bytes < need) return OB_ERR_WORKSPACE;
+  if (!aligned16(dY) || !aligned16(X) || !aligned4(dW) || !aligned4(db)) return OB_ERR_ALIGN;
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    launch_zero_words(dW, N * K, s);
+    if (db) launch_zero_words(db, N, s);
+    return launched();
+  }
+  const DwWorkspace L = dw_layout(1, M, N, K);
+  const DwPlan p = plan_dw(M, N, K);
+  char* base = static_cast<char*>(ws);
+  float* part = reinterpret_cast<float*>(base);
+  float* part_db = db ? reinterpret_cast<float*>(base + L.part) : nullptr;
+  const DwAlpha al{nullptr, nullptr, 0, 2, nullptr, nullptr, nullptr};  // no alpha: dense
+  launch_dw_partial(dY, X, M, N, K, p, part, part_db, nullptr, s, &al);
+  launch_dw_finish(part, (int)p.chunks, N * K, part_db, db ? N : 0, nullptr, nullptr, 0, nullptr,
+                   0, dW, db, nullptr, s);
+  return launched();
+}
+
+namespace {
 int subsample_check(int64_t B, int64_t T, int64_t F, int64_t C) {
   if (B < 1 || B > 65535 || T > (1 << 20) || F > (1 << 16)) return OB_ERR_SHAPE;
   if (B * ((T - 3) / 2 + 1) * ((F - 3) / 2 + 1) * C >= ((int64_t)1 << 30)) return OB_ERR_SHAPE;

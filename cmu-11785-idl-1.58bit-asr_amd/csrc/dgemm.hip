@@ -1,0 +1,358 @@
+// dgemm.hip — the conv module's pointwise (kernel-size-1) Conv1d GEMMs on gfx950 matrix
+// cores, fp32 in and out (conformer.py:143,147; onebit_asr/conv.py _PointwiseFn).
+//
+//   forward  Y  = X . W^T + b     (W [N][K]: the Conv1d weight viewed [out][in])
+//   dgrad    dX = dY . W          (the same kernel, W read transposed: W [K][N])
+//
+// fp32 parity with the reference's fp32 conv: both operands are split exactly into three
+// bf16 parts (x = hi + mid + lo, 8+8+8 significand bits) and six v_mfma_f32_16x16x32_bf16
+// per k-step accumulate the products mm, lh, hl, mh, hm, hh in fp32. The dropped terms
+// (ml, lm, ll) are below 2^-25 of |x||w|: an fp32 GEMM up to summation order.
+//
+// Block = WAVES waves, 16*WAVES rows x BN = 16*NT columns. At entry the block splits its BN
+// columns of W (read straight from the fp32 weight, L2-resident) into a three-plane bf16
+// image in LDS ([BN][3][Kpad+8]; the pad keeps the B-fragment ds_read_b128 conflict-free),
+// then loops over its row tiles: each wave streams 16 rows of A (two dwordx4 per lane per
+// 32-wide k-chunk, a window of chunks in flight across row tiles), splits them in
+// registers and issues 6 MFMAs per 16-column tile. Blocks sharing a row tile are dealt to
+// the same XCD (one L2 serves their A reads).
+//
+// Fragment map of v_mfma_f32_16x16x32_bf16 (lane l, r = l&15, g = l>>4):
+//   A[i=r][kk=8g+j] (j<8), B[kk=8g+j][col=r], D[row=4g+reg][col=r].
+#include <algorithm>
+#include <cstdlib>
+
+#include "ob_launch.h"
+
+namespace ob {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr size_t kLdsCU = 160 * 1024;  // LDS per CU
+
+// x = hi + mid + lo exactly (RNE at each step; the residuals are exact in fp32).
+__device__ __forceinline__ void split3x8(const f32x4& a, const f32x4& b, bf16x8& hi, bf16x8& mid,
+                                         bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = j < 4 ? a[j] : b[j - 4];
+    const __bf16 h = (__bf16)x;
+    const float r1 = x - (float)h;
+    const __bf16 m = (__bf16)r1;
+    hi[j] = h;
+    mid[j] = m;
+    lo[j] = (__bf16)(r1 - (float)m);
+  }
+}
+
+__device__ __forceinline__ void split3x4(const f32x4& a, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 h = (__bf16)a[j];
+    const float r1 = a[j] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    hi[j] = h;
+    mid[j] = m;
+    lo[j] = (__bf16)(r1 - (float)m);
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Bijective XCD-aware remap: consecutive logical ids land on one XCD under round-robin
+// dispatch (cdna_hip_programming.md §5).
+__device__ __forceinline__ int xcd_logical(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// Two dwordx4 of one row at k and k+4, the address clamped into the row (an unguarded load
+// keeps the prefetch window in flight; clamped positions k >= K meet zero rows of the image).
+__device__ __forceinline__ void load8(const float* __restrict__ arow, int k, int K, f32x4& a,
+                                      f32x4& b) {
+  const int ka = k < K - 4 ? k : K - 4;
+  const int kb = k + 4 < K - 4 ? k + 4 : K - 4;
+  a = *reinterpret_cast<const f32x4*>(arow + ka);
+  b = *reinterpret_cast<const f32x4*>(arow + kb);
+}
+
+// products in the order they are accumulated (smallest first): plane of A, plane of B
+// (0 = hi, 1 = mid, 2 = lo)
+constexpr int kProdA[6] = {1, 2, 0, 1, 0, 0};
+constexpr int kProdB[6] = {1, 0, 2, 0, 1, 0};
+
+__host__ __device__ inline int dg_kpad(int K, int nch) { return nch > 0 ? 32 * nch : (K + 31) & ~31; }
+__host__ __device__ inline size_t dg_lds_bytes(int nt, int kpad) {
+  return (size_t)16 * nt * 3 * (kpad + 8) * sizeof(uint16_t);
+}
+
+template <int NT, int NCH, int WAVES, bool TRANS>
+__global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
+    const float* __restrict__ A, int64_t M, int K, const float* __restrict__ W, int N, int n_ct,
+    int n_rt, int rgroups, const float* __restrict__ bias, float* __restrict__ C) {
+  constexpr int kThr = 64 * WAVES, kRowsT = 16 * WAVES, BN = 16 * NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* bimg = reinterpret_cast<__bf16*>(smem);
+  const int kpad = dg_kpad(K, NCH);
+  const int stride = kpad + 8;   // bf16 per plane row
+  const int cpitch = 3 * stride;  // bf16 per image column (three planes)
+
+  const int L = xcd_logical(blockIdx.x, gridDim.x);
+  const int ct = L % n_ct;
+  const int rg = L / n_ct;
+  const int n0 = ct * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int kg = 8 * g;
+
+  // ---- B image: column c (output column n0 + c) holds W's values along k in 3 planes.
+  // Loader unit = 4 consecutive k of one column, stored as one 8-byte write per plane:
+  // !TRANS -> one dwordx4 of W row n (units column-major: a lane's 4 k are contiguous);
+  // TRANS -> 4 dwords of W column n (units k-major: consecutive lanes read consecutive
+  // columns of a W row, coalesced). Clamped loads; zeros selected for k >= K (K % 4 == 0,
+  // so a unit is all in or all out) and for columns >= N.
+  const int kq = kpad >> 2;
+  const int units = BN * kq;
+  auto unit_cols = [&](int u, int& c, int& k4) {
+    if constexpr (TRANS) {
+      k4 = u / BN;
+      c = u - k4 * BN;
+    } else {
+      c = u / kq;
+      k4 = u - c * kq;
+    }
+  };
+  auto unit_load = [&](int u) -> f32x4 {
+    u = u < units ? u : units - 1;
+    int c, k4;
+    unit_cols(u, c, k4);
+    const int n = n0 + c < N ? n0 + c : N - 1;
+    const int kk = 4 * k4 < K - 4 ? 4 * k4 : K - 4;
+    if constexpr (TRANS) {
+      const float* p = W + (int64_t)kk * N + n;
+      return f32x4{p[0], p[N], p[2 * N], p[3 * N]};
+    } else {
+      return *reinterpret_cast<const f32x4*>(W + (int64_t)n * K + kk);
+    }
+  };
+  auto unit_store = [&](int u, f32x4 v) {
+    if (u >= units) return;
+    int c, k4;
+    unit_cols(u, c, k4);
+    const bool ok = 4 * k4 < K && n0 + c < N;
+    const f32x4 x = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x4 h, m, l;
+    split3x4(x, h, m, l);
+    __bf16* col = bimg + c * cpitch + 4 * k4;
+    *reinterpret_cast<bf16x4*>(col) = h;
+    *reinterpret_cast<bf16x4*>(col + stride) = m;
+    *reinterpret_cast<bf16x4*>(col + 2 * stride) = l;
+  };
+  auto arow_of = [&](int rt) {
+    const int64_t m0 = (int64_t)rt * kRowsT + wave * 16;
+    const int64_t row = m0 + r < M ? m0 + r : M - 1;
+    return A + row * (int64_t)K;
+  };
+
+  constexpr int kWmax = NT > 6 ? 3 : 5;
+  constexpr int kWin = NCH > 0 ? (NCH < kWmax ? NCH : kWmax) : 1;
+  f32x4 buf[NCH > 0 ? NCH : 1][2];
+  if constexpr (NCH > 0) {
+    constexpr int kUnits = BN * 8 * NCH;
+    constexpr int kUpt = (kUnits + kThr - 1) / kThr;
+    f32x4 wv[kUpt];
+#pragma unroll
+    for (int i = 0; i < kUpt; ++i) wv[i] = unit_load(threadIdx.x + i * kThr);
+    const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
+#pragma unroll
+    for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < kUpt; ++i) unit_store(threadIdx.x + i * kThr, wv[i]);
+  } else {
+    for (int u = threadIdx.x; u < units; u += kThr) unit_store(u, unit_load(u));
+  }
+  __syncthreads();
+
+  const __bf16* brow = bimg + r * cpitch + kg;
+  float bcol[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = n0 + 16 * t + r;
+    bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
+  }
+
+  for (int rt = rg; rt < n_rt; rt += rgroups) {
+    const int64_t m0 = (int64_t)rt * kRowsT + wave * 16;
+    const float* arow = arow_of(rt);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // One k-chunk: the A split runs while the first group's B reads are in flight; tiles
+    // go in groups of three (9 fragments = 36 VGPRs live), product-major inside a group so
+    // consecutive MFMAs update different accumulators.
+    auto compute = [&](const f32x4& x0, const f32x4& x1, int kc) {
+      constexpr int kG = NT < 3 ? NT : 3;
+#pragma unroll
+      for (int t0 = 0; t0 < NT; t0 += kG) {
+        bf16x8 b[kG][3];
+#pragma unroll
+        for (int t = 0; t < kG; ++t)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            if (t0 + t < NT)
+              b[t][q] = *reinterpret_cast<const bf16x8*>(brow + (t0 + t) * 16 * cpitch +
+                                                          q * stride + kc);
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 a[3];
+        split3x8(x0, x1, a[0], a[1], a[2]);
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+          for (int t = 0; t < kG; ++t)
+            if (t0 + t < NT)
+              acc[t0 + t] = mfma_bf16(a[kProdA[p]], b[t][kProdB[p]], acc[t0 + t]);
+      }
+    };
+
+    if constexpr (NCH > 0) {
+      // Fully unrolled; kWin chunks in flight, the next row tile's first chunks issued
+      // while this tile computes its last ones (the last tile re-reads its own rows as the
+      // "next" tile: L2 hits, never used).
+      const int rt_next = rt + rgroups < n_rt ? rt + rgroups : rt;
+      const float* anext = arow_of(rt_next);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + kWin < NCH) load8(arow, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(buf[c][0], buf[c][1], 32 * c);
+        if (c + kWin >= NCH) {
+          load8(anext, 32 * (c + kWin - NCH) + kg, K, buf[c + kWin - NCH][0],
+                buf[c + kWin - NCH][1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+      // Generic K: three rotating register sets (no register copy of an in-flight load).
+      f32x4 r0a, r0b, r1a, r1b, r2a, r2b;
+      load8(arow, kg, K, r0a, r0b);
+      load8(arow, 32 + kg, K, r1a, r1b);
+      for (int kc = 0; kc < kpad; kc += 96) {
+        load8(arow, kc + 64 + kg, K, r2a, r2b);
+        compute(r0a, r0b, kc);
+        load8(arow, kc + 96 + kg, K, r0a, r0b);
+        if (kc + 32 < kpad) compute(r1a, r1b, kc + 32);
+        load8(arow, kc + 128 + kg, K, r1a, r1b);
+        if (kc + 64 < kpad) compute(r2a, r2b, kc + 64);
+      }
+    }
+
+    __builtin_amdgcn_sched_barrier(0);
+    // D[row = 4g + reg][col = r]: 16 lanes write 64 contiguous bytes of a row per store
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = n0 + 16 * t + r;
+      if (col >= N) continue;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t orow = m0 + 4 * g + reg;
+        if (orow < M) C[orow * N + col] = acc[t][reg] + bcol[t];
+      }
+    }
+  }
+}
+
+struct DgCfg {
+  int nt, waves;
+};
+
+// Widest column tile whose image fits one CU's LDS (8 waves) or half of it (4 waves, two
+// blocks per CU), preferring tiles that divide N. OB_DGEMM_NT / OB_DGEMM_WAVES: tuning.
+DgCfg pick_cfg(int64_t N, int64_t K) {
+  static const int env_nt = [] {
+    const char* e = getenv("OB_DGEMM_NT");
+    return e ? atoi(e) : 0;
+  }();
+  static const int env_w = [] {
+    const char* e = getenv("OB_DGEMM_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const int kpad = dg_kpad((int)K, 0);
+  const bool k_special = kpad == 160 || kpad == 288;
+  static const int cands[] = {9, 6, 3, 2, 1};
+  for (int pass = 0; pass < 2; ++pass)
+    for (int nt : cands) {
+      if (env_nt && nt != env_nt) continue;
+      if (pass == 0 && N % (16 * nt) != 0) continue;
+      if (16 * nt > ((N + 15) & ~int64_t(15))) continue;
+      // instantiated combinations (launch_dense_gemm's switch)
+      const bool inst = kpad == 160 ? (nt == 9 || nt == 6 || nt == 3)
+                        : kpad == 288 ? (nt == 3 || nt == 2 || nt == 1)
+                                      : (nt == 3 || nt == 1);
+      if (!inst && k_special) continue;
+      if (!k_special && !(nt == 3 || nt == 1)) continue;
+      const size_t lds = dg_lds_bytes(nt, kpad);
+      int waves = lds <= kLdsCU / 2 ? 4 : lds <= kLdsCU ? 8 : 0;
+      if (env_w && waves && lds <= kLdsCU / (env_w == 4 ? 2 : 1)) waves = env_w;
+      if (waves) return DgCfg{nt, waves};
+    }
+  return DgCfg{0, 0};
+}
+
+}  // namespace
+
+bool dense_gemm_supported(int64_t K, int64_t N) {
+  return K >= 4 && N >= 4 && K % 4 == 0 && N % 4 == 0 && K <= (1 << 20) && N <= (1 << 20) &&
+         pick_cfg(N, K).nt > 0;
+}
+
+bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int trans,
+                       const float* bias, int64_t N, float* C, hipStream_t s) {
+  if (!dense_gemm_supported(K, N)) return false;
+  if (M == 0) return true;
+  const DgCfg cfg = pick_cfg(N, K);
+  const int kpad = dg_kpad((int)K, 0);
+  const size_t lds = dg_lds_bytes(cfg.nt, kpad);
+  const int rows_t = 16 * cfg.waves;
+  const int n_ct = (int)ceil_div(N, 16 * cfg.nt);
+  const int n_rt = (int)ceil_div(M, rows_t);
+  const int per_cu = (int)std::min<size_t>(kLdsCU / lds, (size_t)(8 / cfg.waves));
+  int rgroups = 256 * per_cu / n_ct;
+  if (rgroups < 1) rgroups = 1;
+  if (rgroups > n_rt) rgroups = n_rt;
+  const dim3 grid((unsigned)(rgroups * n_ct));
+  const int nch = kpad == 160 ? 5 : kpad == 288 ? 9 : 0;
+#define OB_DG(NT, NCH, WV)                                                                       \
+  if (cfg.nt == NT && nch == NCH && cfg.waves == WV) {                                           \
+    if (trans)                                                                                   \
+      hipLaunchKernelGGL((dgemm_kernel<NT, NCH, WV, true>), grid, dim3(64 * WV), lds, s, A, M,    \
+                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C);                        \
+    else                                                                                         \
+      hipLaunchKernelGGL((dgemm_kernel<NT, NCH, WV, false>), grid, dim3(64 * WV), lds, s, A, M,   \
+                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C);                        \
+    return true;                                                                                 \
+  }
+#define OB_DG2(NT, NCH) OB_DG(NT, NCH, 4) OB_DG(NT, NCH, 8)
+  OB_DG2(9, 5)
+  OB_DG2(6, 5)
+  OB_DG2(3, 5)
+  OB_DG2(3, 9)
+  OB_DG2(2, 9)
+  OB_DG2(1, 9)
+  OB_DG2(3, 0)
+  OB_DG2(1, 0)
+#undef OB_DG2
+#undef OB_DG
+  return false;
+}
+
+}  // namespace ob

@@ -17,6 +17,7 @@
 // OB_GEMM=f32 selects the fp32 kernel (v_mfma_f32_16x16x4_f32, exact fp32 fma chain):
 // A[i=r][kk=g], B[kk=g][j=r]; every lane loads 4 contiguous fp32 (one dwordx4) of a row.
 #include <cstdlib>
+#include <type_traits>
 
 #include "ob_launch.h"
 #include "ob_quant.h"
@@ -649,33 +650,44 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   // k = k0 + 48wk + 16u + r. The same loop forms this block's share of the alpha gradient
   // (quant.py:84-91 is linear in G: sum_e G[e] term[e] = sum over chunks of the chunk
   // partial's dot with term), with the term at this chunk's pass bitwidth.
-  const float a = effective_alpha(al.alpha, al.alpha_raw);
-  int bits = al.pass_bits ? al.pass_bits[pass] : (al.bits_dev ? *al.bits_dev : al.bits);
+  // al.W == nullptr: a dense dW (dgemm.hip's pointwise convs) -- no alpha partials
+  const bool has_al = al.W != nullptr;
+  const float a = has_al ? effective_alpha(al.alpha, al.alpha_raw) : 1.0f;
+  int bits = !has_al ? 2 : al.pass_bits ? al.pass_bits[pass] : (al.bits_dev ? *al.bits_dev : al.bits);
   bits = bits == 1 ? 1 : 2;
   float* out = part + chunk * ((int64_t)N * K);
   float prod = 0.0f;
+  // two straight-line copies of the store loop (a per-element `if (has_al)` around the W
+  // loads makes hipcc branch and wait for each load in turn)
+  auto emit = [&](auto with_al) {
 #pragma unroll
-  for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int n = n0 + 48 * wn + 16 * t + 4 * g + reg;
+      for (int reg = 0; reg < 4; ++reg) {
+        const int n = n0 + 48 * wn + 16 * t + 4 * g + reg;
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int64_t e = (int64_t)n * K + k0 + 48 * wk + 16 * u + r;
-        if (!DW_EXP_NOOUT || acc[t][u][reg] == 12345.0f) out[e] = acc[t][u][reg];
-        prod += acc[t][u][reg] * alpha_term(al.W[e] / a, bits);
+        for (int u = 0; u < 3; ++u) {
+          const int64_t e = (int64_t)n * K + k0 + 48 * wk + 16 * u + r;
+          if (!DW_EXP_NOOUT || acc[t][u][reg] == 12345.0f) out[e] = acc[t][u][reg];
+          if constexpr (decltype(with_al)::value)
+            prod += acc[t][u][reg] * alpha_term(al.W[e] / a, bits);
+        }
       }
-    }
+  };
+  if (has_al) emit(std::true_type{});
+  else emit(std::false_type{});
+  if (has_al) {
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
-  float* wred = reinterpret_cast<float*>(lds) + 16 * C::BN;  // past the db scratch
-  __syncthreads();  // (the loop's last barrier already ended all LDS reads)
-  if (lane == 0) wred[wave] = prod;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.0f;
-    for (int w = 0; w < WN * WK; ++w) t += wred[w];
-    al.apart[L] = t;  // logical block id: the finish kernel sums these in order
+    for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
+    float* wred = reinterpret_cast<float*>(lds) + 16 * C::BN;  // past the db scratch
+    __syncthreads();  // (the loop's last barrier already ended all LDS reads)
+    if (lane == 0) wred[wave] = prod;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.0f;
+      for (int w = 0; w < WN * WK; ++w) t += wred[w];
+      al.apart[L] = t;  // logical block id: the finish kernel sums these in order
+    }
   }
   if (do_db) {
     // column sums: the 16 row pairs of each column quad, added in row-pair order via LDS
@@ -709,7 +721,7 @@ __global__ __launch_bounds__(kThreads) void dw_finish_kernel(
     const float* __restrict__ apart, int n_apart, float* __restrict__ dW, float* __restrict__ db,
     float* __restrict__ dalpha) {
   if (blockIdx.x == gridDim.x - 1) {  // alpha: fixed order over the dW blocks
-    if (threadIdx.x >= 64) return;
+    if (threadIdx.x >= 64 || !dalpha) return;  // (no alpha: a dense dW)
     float s2 = 0.0f;
     for (int i = threadIdx.x; i < n_apart; i += 64) s2 += apart[i];
 #pragma unroll
@@ -738,7 +750,9 @@ __global__ __launch_bounds__(kThreads) void dw_finish_kernel(
 #pragma unroll
     for (int u = 0; u < G; ++u) cur[u] = nxt[u];
   }
-  if (is_w) {
+  if (is_w && !W) {
+    dW[e] = g;  // dense dW (W == nullptr)
+  } else if (is_w) {
     const float a = effective_alpha(alpha, alpha_raw);
     dW[e] = g * ste_indicator(W[e] / a);  // quant.py:81-82
   } else {

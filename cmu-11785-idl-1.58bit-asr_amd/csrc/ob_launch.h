@@ -152,6 +152,11 @@ void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* pa
                       const float* apart, int n_apart, float* dW, float* db, float* dalpha,
                       hipStream_t s);
 
+// dgemm.hip (dense exact-fp32 GEMM of the pointwise convs): false = shape not taken
+bool dense_gemm_supported(int64_t K, int64_t N);
+bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int trans,
+                       const float* bias, int64_t N, float* C, hipStream_t s);
+
 // tgemm_i8.hip (opt-in absmax-int8 activations x ternary codes on the i8 matrix cores)
 bool ternary_gemm_i8_supported(int64_t K, int64_t N);
 size_t act_absmax_workspace(int P);

@@ -61,6 +61,10 @@ SIGNATURES = {
     "ob_relu_bias_bwd": (_int, [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_colsum_workspace": (_sz, [_i64]),
     "ob_colsum": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _sz, _c_f]),
+    "ob_dense_supported": (_int, [_i64, _i64]),
+    "ob_dense_gemm": (_int, [_c_f, _i64, _i64, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
+    "ob_dense_dw_workspace": (_sz, [_i64, _i64, _i64]),
+    "ob_dense_dw": (_int, [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_subsample_image_bytes": (_sz, [_i64]),
     "ob_subsample_pack": (_int, [_c_f, _i64, _c_f, _c_f]),
     "ob_subsample_fwd": (_int, [_c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _c_f,

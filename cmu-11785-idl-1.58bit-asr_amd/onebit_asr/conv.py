@@ -180,13 +180,42 @@ class _BlasPref:
 _PW_BLAS = os.environ.get("OB_PW_BLAS", "cublas")  # "cublas" selects rocBLAS on ROCm
 
 
+_PW = os.environ.get("OB_PW", "hip")  # "blas": the rocBLAS fp32 GEMMs (A/B checks)
+
+
+def _aligned(t: torch.Tensor) -> bool:
+    return t.data_ptr() % 16 == 0
+
+
+def _dense_ok(x2d: torch.Tensor, w: torch.Tensor) -> bool:
+    """csrc/dgemm.hip takes this pointwise conv (forward and both backward GEMMs)."""
+    if _PW != "hip" or not (x2d.is_cuda and x2d.dtype == torch.float32 == w.dtype):
+        return False
+    n, k = w.shape
+    lib = _lib.load()
+    return (x2d.is_contiguous() and w.is_contiguous() and _aligned(x2d) and _aligned(w)
+            and lib.ob_dense_supported(k, n) == 1 and lib.ob_dense_supported(n, k) == 1
+            and lib.ob_dense_dw_workspace(x2d.shape[0], n, k) > 0)
+
+
 class _PointwiseFn(torch.autograd.Function):
-    """A 1x1 Conv1d on channels-last rows: y = x W^T + b (conformer.py:143,147)."""
+    """A 1x1 Conv1d on channels-last rows: y = x W^T + b (conformer.py:143,147). Eligible
+    shapes run on csrc/dgemm.hip (exact-fp32 products on the bf16 matrix cores: forward,
+    dX = dY W, and dW / db through the dW kernel family); others on rocBLAS fp32."""
 
     @staticmethod
     def forward(ctx, x2d, w, b):
-        with _BlasPref(_PW_BLAS):
-            y = torch.addmm(b, x2d, w.t()) if b is not None else x2d @ w.t()
+        ctx.hip = _dense_ok(x2d, w)
+        if ctx.hip:
+            m, k = x2d.shape
+            n = w.shape[0]
+            y = torch.empty((m, n), dtype=torch.float32, device=x2d.device)
+            _lib.check(_lib.load().ob_dense_gemm(x2d.data_ptr(), m, k, w.data_ptr(), 0,
+                                                 _lib.ptr(b), n, y.data_ptr(),
+                                                 _lib.stream_of(x2d)), "ob_dense_gemm")
+        else:
+            with _BlasPref(_PW_BLAS):
+                y = torch.addmm(b, x2d, w.t()) if b is not None else x2d @ w.t()
         ctx.save_for_backward(x2d, w)
         ctx.has_b = b is not None
         return y
@@ -195,6 +224,27 @@ class _PointwiseFn(torch.autograd.Function):
     def backward(ctx, g):
         x2d, w = ctx.saved_tensors
         gx = gw = gb = None
+        g = g.contiguous()
+        if ctx.hip and _aligned(g):
+            lib = _lib.load()
+            m, k = x2d.shape
+            n = w.shape[0]
+            st = _lib.stream_of(g)
+            if ctx.needs_input_grad[0]:
+                gx = torch.empty_like(x2d)
+                _lib.check(lib.ob_dense_gemm(g.data_ptr(), m, n, w.data_ptr(), 1, None, k,
+                                             gx.data_ptr(), st), "ob_dense_gemm")
+            if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+                gw = torch.empty_like(w)
+                gb = (torch.empty((n,), dtype=torch.float32, device=g.device)
+                      if ctx.has_b and ctx.needs_input_grad[2] else None)
+                wsb = lib.ob_dense_dw_workspace(m, n, k)
+                ws = torch.empty((wsb,), dtype=torch.uint8, device=g.device)
+                _lib.check(lib.ob_dense_dw(g.data_ptr(), x2d.data_ptr(), m, n, k, gw.data_ptr(),
+                                           _lib.ptr(gb), ws.data_ptr(), wsb, st), "ob_dense_dw")
+                if not ctx.needs_input_grad[1]:
+                    gw = None
+            return gx, gw, gb
         with _BlasPref(_PW_BLAS):
             if ctx.needs_input_grad[0]:
                 gx = g @ w

@@ -457,6 +457,24 @@ OB_API int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* 
                      size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Dense fp32 GEMMs of the conv module's pointwise Conv1d(kernel 1) layers
+ * (conformer.py:143,147; replaces the fp32 matmuls / addmm of a 1x1 conv on channels-last
+ * rows). Exact-fp32 products on the bf16 matrix cores (6 MFMAs per k-step, csrc/dgemm.hip).
+ *   ob_dense_gemm: w_trans = 0: Y[M][N] = X[M][K] . W^T + bias, W [N][K] (the forward);
+ *                  w_trans = 1: Y[M][N] = X[M][K] . W,          W [K][N] (dX = dY . W).
+ *                  bias may be NULL. X, W, Y 16-byte aligned; K, N multiples of 4.
+ *   ob_dense_dw:   dW[N][K] = dY[M][N]^T . X[M][K], db[N] = column sums of dY (db may be
+ *                  NULL); N, K multiples of 48. Deterministic (fixed-order chunk sums).
+ * ob_dense_supported(K, N) / ob_dense_dw_workspace(M, N, K) == 0: the shape is not taken.
+ * ------------------------------------------------------------------------------------ */
+OB_API int ob_dense_supported(int64_t K, int64_t N);
+OB_API int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_trans,
+                         const float* bias, int64_t N, float* Y, void* stream);
+OB_API size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K);
+OB_API int ob_dense_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                       float* dW, float* db, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Conv module core (ConvModule, conformer.py:139-167; full precision), channels-last.
  * Rows = Bt*T frames (utterance b = rows [b*T, (b+1)*T)), channel fastest; P stacked
  * passes (Bt = P*B) keep per-pass BatchNorm statistics. pw1 / pw2 are plain GEMMs left to

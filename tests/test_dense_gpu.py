@@ -1,0 +1,150 @@
+"""GPU parity of the pointwise-conv GEMMs (csrc/dgemm.hip through ob_dense_gemm /
+ob_dense_dw; conformer.py:143,147 Conv1d(kernel 1) on channels-last rows) against fp64
+torch products of the same fp32 inputs.
+
+Bars (written here): forward / dX max|err| <= 2e-6 * (max row-norm product) -- the
+bf16x6 products are exact to < 2^-25 relative, the rest is fp32 summation order;
+dW / db rel-L2 <= 1e-6.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from onebit_asr import _lib
+
+    return _lib
+
+
+def _gemm(x, w, trans, bias=None):
+    L = _lib()
+    m, k = x.shape
+    n = w.shape[1] if trans else w.shape[0]
+    y = torch.full((m, n), float("nan"), device=x.device)
+    L.check(L.load().ob_dense_gemm(x.data_ptr(), m, k, w.data_ptr(), int(trans), L.ptr(bias), n,
+                                   y.data_ptr(), L.stream_of(x)), "ob_dense_gemm")
+    return y
+
+
+def _bound(x, w, trans):
+    wk = w if trans else w.t()  # [K][N]
+    return float(x.double().norm(dim=1).max() * wk.double().norm(dim=0).max())
+
+
+@pytest.mark.parametrize("m,k,n,trans", [
+    (23904, 144, 288, False),  # pw1 forward at Conformer-S (3 stacked passes x 32 x 249)
+    (23904, 144, 144, False),  # pw2 forward
+    (23904, 288, 144, True),   # pw1 dX
+    (23904, 144, 144, True),   # pw2 dX
+    (1000, 144, 288, False), (777, 288, 144, True), (65, 144, 144, True),
+    (1, 144, 288, False), (130, 64, 48, False), (100, 20, 36, True), (513, 96, 192, False),
+])
+def test_dense_gemm_matches_fp64(gpu, m, k, n, trans):
+    assert _lib().load().ob_dense_supported(k, n) == 1
+    g = torch.Generator(device=gpu).manual_seed(m + k + n)
+    x = torch.randn(m, k, device=gpu, generator=g) * 3.0
+    w = torch.randn((k, n) if trans else (n, k), device=gpu, generator=g) * 0.1
+    b = None if trans else torch.randn(n, device=gpu, generator=g)
+    y = _gemm(x, w, trans, b)
+    wk = w.double() if trans else w.double().t()
+    ref = x.double() @ wk
+    if b is not None:
+        ref = ref + b.double()
+    assert torch.isfinite(y).all()
+    err = float((y.double() - ref).abs().max())
+    assert err <= 2e-6 * _bound(x, w, trans) + 1e-6, err
+
+
+def test_dense_gemm_special_values(gpu):
+    """Zero rows stay exactly zero (+ bias), tiny / huge magnitudes keep fp32 relative accuracy."""
+    m, k, n = 300, 144, 144
+    x = torch.randn(m, k, device=gpu)
+    x[5] = 0.0
+    x[7] *= 1e-30
+    x[9] *= 1e30
+    w = torch.randn(n, k, device=gpu) * 0.05
+    b = torch.randn(n, device=gpu)
+    y = _gemm(x, w, False, b)
+    assert torch.equal(y[5], b)
+    ref = x.double() @ w.double().t() + b.double()
+    for r in (7, 9, 11):
+        rel = float((y[r].double() - ref[r]).abs().max() / ref[r].abs().max())
+        assert rel <= 1e-5, (r, rel)
+
+
+def _dw(dy, x, with_db=True):
+    L = _lib()
+    lib = L.load()
+    m, n = dy.shape
+    k = x.shape[1]
+    wsb = lib.ob_dense_dw_workspace(m, n, k)
+    assert wsb > 0
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=dy.device)
+    dw = torch.full((n, k), float("nan"), device=dy.device)
+    db = torch.full((n,), float("nan"), device=dy.device) if with_db else None
+    L.check(lib.ob_dense_dw(dy.data_ptr(), x.data_ptr(), m, n, k, dw.data_ptr(), L.ptr(db),
+                            ws.data_ptr(), wsb, L.stream_of(dy)), "ob_dense_dw")
+    return dw, db
+
+
+@pytest.mark.parametrize("m,n,k", [(23904, 288, 144), (23904, 144, 144), (777, 144, 288),
+                                   (33, 48, 96), (1, 144, 144)])
+def test_dense_dw_matches_fp64(gpu, m, n, k):
+    g = torch.Generator(device=gpu).manual_seed(m * 3 + n)
+    dy = torch.randn(m, n, device=gpu, generator=g)
+    x = torch.randn(m, k, device=gpu, generator=g) * 2.0
+    dw, db = _dw(dy, x)
+    ref = dy.double().t() @ x.double()
+    rel = float((dw.double() - ref).norm() / ref.norm())
+    assert rel <= 1e-6, rel
+    rdb = dy.double().sum(0)
+    assert float((db.double() - rdb).norm() / rdb.norm()) <= 1e-6
+    dw2, _ = _dw(dy, x, with_db=False)
+    assert torch.equal(dw, dw2)  # deterministic, db optional
+
+
+def test_dense_dw_zero_rows(gpu):
+    dy = torch.empty(0, 144, device=gpu)
+    x = torch.empty(0, 144, device=gpu)
+    dw, db = _dw(dy, x)
+    assert torch.equal(dw, torch.zeros_like(dw)) and torch.equal(db, torch.zeros_like(db))
+
+
+def test_dense_abi_errors(gpu):
+    L = _lib()
+    lib = L.load()
+    assert lib.ob_dense_supported(142, 144) == 0  # K % 4
+    assert lib.ob_dense_supported(144, 30) == 0   # N % 4
+    assert lib.ob_dense_dw_workspace(10, 144, 100) == 0  # K % 48
+    x = torch.randn(8, 144, device=gpu)
+    w = torch.randn(144, 144, device=gpu)
+    y = torch.empty(8, 144, device=gpu)
+    st = L.stream_of(x)
+    assert lib.ob_dense_gemm(x.data_ptr(), 8, 144, None, 0, None, 144, y.data_ptr(), st) == -1
+    assert lib.ob_dense_gemm(x.data_ptr() + 4, 8, 144, w.data_ptr(), 0, None, 144, y.data_ptr(),
+                             st) == -5
+    assert lib.ob_dense_gemm(x.data_ptr(), 8, 142, w.data_ptr(), 0, None, 144, y.data_ptr(),
+                             st) == -2
+
+
+def test_pointwise_fn_hip_vs_blas(gpu, monkeypatch):
+    """_PointwiseFn (conv.py) on the HIP path equals the rocBLAS path: forward, dX, dW, db."""
+    from onebit_asr import conv
+
+    torch.manual_seed(3)
+    x = torch.randn(2000, 144, device=gpu)
+    w = torch.randn(288, 144, device=gpu) * 0.1
+    b = torch.randn(288, device=gpu)
+    gy = torch.randn(2000, 288, device=gpu)
+    outs = {}
+    for mode in ("hip", "blas"):
+        monkeypatch.setattr(conv, "_PW", mode)
+        xx, ww, bb = (t.clone().requires_grad_(True) for t in (x, w, b))
+        y = conv._PointwiseFn.apply(xx, ww, bb)
+        y.backward(gy)
+        outs[mode] = (y.detach(), xx.grad, ww.grad, bb.grad)
+    for a, r in zip(outs["hip"], outs["blas"]):
+        rel = float((a.double() - r.double()).norm() / r.double().norm())
+        assert rel <= 1e-6, rel
