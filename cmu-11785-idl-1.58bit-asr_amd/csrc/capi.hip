@@ -804,6 +804,30 @@ int ob_layernorm_bwd_res(const float* dy, const float* x, const float* gamma, co
   return launched();
 }
 
+int ob_layernorm_bwd_ex(const float* dy, const float* x, const float* gamma, const float* mean,
+                        const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx,
+                        float* dgamma, float* dbeta, void* ws, size_t ws_bytes, float* dy2,
+                        float rscale, float p_drop, const uint64_t* rng, int64_t rng_offset,
+                        const int32_t* lens, int64_t T, void* stream) {
+  if (rows < 0 || !layernorm_supported(d)) return OB_ERR_SHAPE;
+  if (rows > 0 && (!dy || !x || !mean || !rstd || !dx)) return OB_ERR_NULL;
+  if ((dgamma || dbeta) && !ws) return OB_ERR_NULL;
+  if ((dgamma || dbeta) && ws_bytes < layernorm_bwd_workspace(rows, d)) return OB_ERR_WORKSPACE;
+  if (!aligned4(dy) || !aligned4(x) || !aligned4(dx) || !aligned4(dres) || !aligned4(dy2) ||
+      !aligned4(lens))
+    return OB_ERR_ALIGN;
+  if (dy2) {
+    if (!(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+    if (lens && (T < 1 || T > 0x7fffffff || rows % T)) return OB_ERR_SHAPE;
+    if (p_drop > 0.0f && !rng) return OB_ERR_NULL;
+  }
+  LnGradScale gs{dy2, rscale, p_drop, rng, (uint64_t)rng_offset,
+                 reinterpret_cast<const int*>(lens), (int)T};
+  launch_layernorm_bwd(dy, x, gamma, mean, rstd, rows, d, dres, dx, dgamma, dbeta, ws,
+                       as_stream(stream), &gs);
+  return launched();
+}
+
 namespace {
 int relattn_check(int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop) {
   if (Bt < 1 || P < 1 || Bt % P != 0 || H < 1 || !relattn_supported(T, d)) return OB_ERR_SHAPE;
@@ -815,12 +839,13 @@ int relattn_check(int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float 
 int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                    const float* u, const float* vb, const int32_t* lens, int64_t Bt, int64_t P,
                    int64_t T, int64_t H, int64_t d, float p_drop, const int64_t* rng,
-                   float* probs, float* ctx, void* stream) {
+                   int64_t rng_offset, float* probs, float* ctx, void* stream) {
   if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
   if (!q || !k || !v || !pos || !u || !vb || !lens || !ctx || (p_drop > 0.0f && !rng))
     return OB_ERR_NULL;
   launch_relattn_fwd(q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop,
-                     reinterpret_cast<const uint64_t*>(rng), probs, ctx, as_stream(stream));
+                     reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset, probs, ctx,
+                     as_stream(stream));
   return launched();
 }
 
@@ -832,25 +857,26 @@ size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
 int ob_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
                    const float* pos, const float* u, const float* vb, const int32_t* lens,
                    int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                   const int64_t* rng, const float* probs, float* dq, float* dk, float* dv,
-                   float* dpos, float* du, float* dvb, void* ws, size_t ws_bytes, void* stream) {
+                   const int64_t* rng, int64_t rng_offset, const float* probs, float* dq,
+                   float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
+                   size_t ws_bytes, void* stream) {
   if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
   if (!dctx || !q || !k || !v || !pos || !u || !vb || !lens || !probs || !dq || !dk || !dv ||
       !dpos || !du || !dvb || !ws || (p_drop > 0.0f && !rng))
     return OB_ERR_NULL;
   if (ws_bytes < ob_relattn_bwd_workspace(Bt, T, H, d)) return OB_ERR_WORKSPACE;
   launch_relattn_bwd(dctx, q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop,
-                     reinterpret_cast<const uint64_t*>(rng), probs, dq, dk, dv, dpos, du, dvb, ws,
-                     as_stream(stream));
+                     reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset, probs, dq, dk,
+                     dv, dpos, du, dvb, ws, as_stream(stream));
   return launched();
 }
 
-int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, uint8_t* out,
-                            void* stream) {
+int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, int64_t rng_offset,
+                            uint8_t* out, void* stream) {
   if (n < 0 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
   if ((n > 0 && !out) || (p_drop > 0.0f && !rng)) return OB_ERR_NULL;
-  launch_relattn_dropout_mask(n, p_drop, reinterpret_cast<const uint64_t*>(rng), out,
-                              as_stream(stream));
+  launch_relattn_dropout_mask(n, p_drop, reinterpret_cast<const uint64_t*>(rng),
+                              (uint64_t)rng_offset, out, as_stream(stream));
   return launched();
 }
 

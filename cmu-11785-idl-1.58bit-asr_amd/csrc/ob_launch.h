@@ -192,9 +192,20 @@ size_t layernorm_fwd_amax_workspace(int64_t P);
 void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
                                int64_t rows, int64_t d, float eps, float* y, float* mean,
                                float* rstd, int P, float* amax, void* ws, hipStream_t s);
+// Optional second output of the backward: dy2 = rscale * rowvalid * drop(dx) (the residual
+// dropout backward of the module whose output this LN normalises; lens/T as TgemmEpi).
+struct LnGradScale {
+  float* dy2;
+  float rscale;
+  float p_drop;
+  const uint64_t* rng;
+  uint64_t rng_off;
+  const int* lens;
+  int T;
+};
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                           const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx, float* dgamma,
-                          float* dbeta, void* ws, hipStream_t s);
+                          float* dbeta, void* ws, hipStream_t s, const LnGradScale* gsc = nullptr);
 
 // dwconv.hip (depthwise Conv1d of the conv module, odd kernel width, 'same' padding)
 bool dwconv_supported(int KT);
@@ -241,14 +252,15 @@ size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
 void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                         const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
                         int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
-                        float* probs, float* ctx, hipStream_t s);
+                        uint64_t rng_off, float* probs, float* ctx, hipStream_t s);
 void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
                         const float* pos, const float* u, const float* vb, const int* lens,
                         int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                        const uint64_t* rng, const float* probs, float* dq, float* dk, float* dv,
-                        float* dpos, float* du, float* dvb, void* ws, hipStream_t s);
-void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,
-                                 hipStream_t s);
+                        const uint64_t* rng, uint64_t rng_off, const float* probs, float* dq,
+                        float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
+                        hipStream_t s);
+void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint64_t rng_off,
+                                 uint8_t* out, hipStream_t s);
 
 // subsample.hip (Conv2dSubsampling, channels-last implicit GEMMs)
 bool subsample_supported(int64_t T, int64_t F, int64_t C);

@@ -146,7 +146,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ pos, const float* __restrict__ u, const float* __restrict__ vbias,
     const int* __restrict__ lens, int Bp, int T, int H, float inv_sqrt_d, DropCfg dc,
-    const uint64_t* __restrict__ rng, float* __restrict__ probs, float* __restrict__ ctx) {
+    const uint64_t* __restrict__ rng, uint64_t rng_off, float* __restrict__ probs,
+    float* __restrict__ ctx) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   extern __shared__ float xs[];
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
   const float rsum = 1.0f / sum;
-  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
   const size_t prow_off = (((size_t)b * H + h) * T + qic) * T;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
@@ -361,8 +362,9 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     const float* __restrict__ dctx, const float* __restrict__ q, const float* __restrict__ k,
     const float* __restrict__ v, const float* __restrict__ pos, const float* __restrict__ u,
     const float* __restrict__ vbias, const int* __restrict__ lens, int Bp, int T, int H,
-    float inv_sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, const float* __restrict__ probs,
-    float* __restrict__ dq, float* __restrict__ dsg, float* __restrict__ du_part,
+    float inv_sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off,
+    const float* __restrict__ probs, float* __restrict__ dq, float* __restrict__ dsg,
+    float* __restrict__ du_part,
     float* __restrict__ dvb_part) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* dob = dctx + bo;
   const float* pb = pos + (size_t)pass * T * C + h * D;
   const float* prb = probs + ((size_t)b * H + h) * T * T;
-  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
   const size_t pbase = ((size_t)b * H + h) * T * T;
   auto keep_scale = [&](int i, int j) -> float {
     if (!dc.on) return 1.0f;
@@ -652,7 +654,8 @@ template <int DQ>
 __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     const float* __restrict__ dsg, const float* __restrict__ probs, const float* __restrict__ q,
     const float* __restrict__ dctx, const float* __restrict__ u, const float* __restrict__ vbias,
-    int T, int H, DropCfg dc, const uint64_t* __restrict__ rng, float* __restrict__ dk,
+    int T, int H, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off,
+    float* __restrict__ dk,
     float* __restrict__ dv, float* __restrict__ dp_part) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   const float* vbb = vbias + h * D;
   const float* dsb = dsg + ((size_t)b * H + h) * T * T;
   const float* prb = probs + ((size_t)b * H + h) * T * T;
-  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1]) : 0u;
+  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
   const size_t pbase = ((size_t)b * H + h) * T * T;
 
   // pad columns of the B tiles stay zero (their MFMA columns are discarded anyway)
@@ -822,17 +825,21 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
 }
 
 // du, dvb [H][D]: sum over (batch row, query tile) of the per-tile partials. Block = one
-// (which, head) x 64 columns x 16 slices (slice s: pairs s, s+16, ...), slices added in
-// order through LDS (fixed order). A thread per output with a serial loop over the
-// Bt*nqt partials measured 170 us at Conformer-S (one dependent load chain per thread).
-constexpr int kBiasSlices = 16;
+// (which, head) x 4 columns x 64 slices (slice s: pairs s, s+64, ..., four accumulators),
+// the slices added in order through LDS (fixed order). 2*H*ceil(D/4) blocks: each thread
+// has a few independent loads in flight (one block per (which, head) with a serial chain of
+// 24 partials per thread measured 15 us at Conformer-S).
+constexpr int kBiasCols = 4, kBiasSlices = kThreads / kBiasCols;
 
-__global__ __launch_bounds__(64 * kBiasSlices) void relattn_bias_reduce_kernel(
+__global__ __launch_bounds__(kThreads) void relattn_bias_reduce_kernel(
     const float* __restrict__ du_part, const float* __restrict__ dvb_part, int Bt, int H, int D,
     int nqt, float* __restrict__ du, float* __restrict__ dvb) {
-  __shared__ float red[kBiasSlices][64];
-  const int which = blockIdx.x / H, h = blockIdx.x - which * H;
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  __shared__ float red[kBiasSlices][kBiasCols];
+  const int ncg = (D + kBiasCols - 1) / kBiasCols;
+  const int cg = blockIdx.x % ncg, wh = blockIdx.x / ncg;
+  const int which = wh / H, h = wh - which * H;
+  const int cl = threadIdx.x % kBiasCols, sl = threadIdx.x / kBiasCols;
+  const int c = cg * kBiasCols + cl;
   const float* src = which == 0 ? du_part : dvb_part;
   const int pairs = Bt * nqt;
   float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -843,12 +850,12 @@ __global__ __launch_bounds__(64 * kBiasSlices) void relattn_bias_reduce_kernel(
       a[u & 3] += src[(((size_t)b * H + h) * nqt + qt) * D + c];
     }
   }
-  red[sl][c] = (a[0] + a[1]) + (a[2] + a[3]);
+  red[sl][cl] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   if (sl == 0 && c < D) {
     float t = 0.0f;
-#pragma unroll
-    for (int q = 0; q < kBiasSlices; ++q) t += red[q][c];
+#pragma unroll 8
+    for (int q = 0; q < kBiasSlices; ++q) t += red[q][cl];
     (which == 0 ? du : dvb)[h * D + c] = t;
   }
 }
@@ -884,10 +891,11 @@ __global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
 
 __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropCfg dc,
                                                                 const uint64_t* __restrict__ rng,
+                                                                uint64_t rng_off,
                                                                 uint8_t* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e >= n) return;
-  out[e] = (!dc.on || drop_hash(drop_key(rng[0], rng[1]), (uint64_t)e) >= dc.thresh) ? 1 : 0;
+  out[e] = (!dc.on || drop_hash(drop_key(rng[0], rng[1] + rng_off), (uint64_t)e) >= dc.thresh) ? 1 : 0;
 }
 
 
@@ -923,14 +931,14 @@ size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
 void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                         const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
                         int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
-                        float* probs, float* ctx, hipStream_t s) {
+                        uint64_t rng_off, float* probs, float* ctx, hipStream_t s) {
   const dim3 grid((unsigned)(((T + kTile - 1) / kTile) * H * Bt));
   const DropCfg dc = make_drop(p_drop);
   const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
   const size_t lds = lds_bytes((int)T);
 #define OB_RA_FWD(DQ, NTT)                                                                 \
   hipLaunchKernelGGL((relattn_fwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, q, k, v, pos, \
-                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, probs, ctx)
+                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, ctx)
   OB_RA_DISPATCH(OB_RA_FWD);
 #undef OB_RA_FWD
 }
@@ -938,8 +946,9 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
 void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
                         const float* pos, const float* u, const float* vb, const int* lens,
                         int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                        const uint64_t* rng, const float* probs, float* dq, float* dk, float* dv,
-                        float* dpos, float* du, float* dvb, void* ws, hipStream_t s) {
+                        const uint64_t* rng, uint64_t rng_off, const float* probs, float* dq,
+                        float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
+                        hipStream_t s) {
   const int nqt = (int)((T + kTile - 1) / kTile);
   const dim3 grid((unsigned)(nqt * H * Bt));
   const DropCfg dc = make_drop(p_drop);
@@ -951,17 +960,18 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
   float* dvb_part = du_part + (size_t)Bt * H * nqt * d;
 #define OB_RA_BWD(DQ, NTT)                                                                     \
   hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, q, k, v,  \
-                     pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, probs, dq, \
+                     pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, dq, \
                      dsg, du_part, dvb_part)
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
 #define OB_RA_KV(DQ, NTT)                                                                       \
   hipLaunchKernelGGL((relattn_bwd_kv_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg, \
-                     probs, q, dctx, u, vb, (int)T, (int)H, dc, rng, dk, dv, dp_part)
+                     probs, q, dctx, u, vb, (int)T, (int)H, dc, rng, rng_off, dk, dv, dp_part)
   OB_RA_DISPATCH(OB_RA_KV);
 #undef OB_RA_KV
   const int64_t C = H * d;
-  hipLaunchKernelGGL(relattn_bias_reduce_kernel, dim3((unsigned)(2 * H)), dim3(64 * kBiasSlices),
+  hipLaunchKernelGGL(relattn_bias_reduce_kernel,
+                     dim3((unsigned)(2 * H * ((d + kBiasCols - 1) / kBiasCols))), dim3(kThreads),
                      0, s, (const float*)du_part, (const float*)dvb_part, (int)Bt, (int)H, (int)d,
                      nqt, du, dvb);
   hipLaunchKernelGGL(relattn_dpos_reduce_kernel, dim3((unsigned)ceil_div(P * T * C, 64)),
@@ -969,11 +979,11 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
                      (int)d, 1, dpos);
 }
 
-void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint8_t* out,
-                                 hipStream_t s) {
+void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint64_t rng_off,
+                                 uint8_t* out, hipStream_t s) {
   if (n == 0) return;
   hipLaunchKernelGGL(relattn_mask_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, s, n, make_drop(p_drop), rng, out);
+                     dim3(kThreads), 0, s, n, make_drop(p_drop), rng, rng_off, out);
 }
 
 }  // namespace ob

@@ -113,6 +113,9 @@ SIGNATURES = {
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_layernorm_bwd_res": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_layernorm_bwd_ex": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f,
+               _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f]),
     "ob_act_absmax_workspace": (_sz, [_i64]),
     "ob_act_absmax": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _sz, _c_f]),
     "ob_act_dequant_i8": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _c_f]),
@@ -129,12 +132,12 @@ SIGNATURES = {
                _sz, _c_f]),
     "ob_relattn_fwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32, _c_f,
-               _c_f, _c_f, _c_f]),
+               _i64, _c_f, _c_f, _c_f]),
     "ob_relattn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64]),
     "ob_relattn_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32,
-               _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
-    "ob_relattn_dropout_mask": (_int, [_i64, _f32, _c_f, _c_f, _c_f]),
+               _c_f, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_relattn_dropout_mask": (_int, [_i64, _f32, _c_f, _i64, _c_f, _c_f]),
     "ob_embedding_bwd": (_int, [_c_f, _i64, _c_f, _i64, _i64, _i64, _c_f, _c_f]),
     "ob_adamw_plan": (_i64, [_c_f, _i64, _c_f]),
     "ob_adamw_workspace": (_sz, [_i64]),

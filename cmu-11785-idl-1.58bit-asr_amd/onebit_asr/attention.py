@@ -7,14 +7,16 @@ projection outputs in their natural [B, T, H*d] layout and returns the context i
 layout out_proj consumes, with one forward kernel and one backward kernel (+ a small
 reduction); see csrc/relattn.hip. Gradients flow to q, k, v, pos, pos_bias_u, pos_bias_v.
 
-Dropout uses the kernels' counter-based hash (seed, counter) per device; the counter
-advances on the device each call, so a captured step draws a fresh mask on every replay.
-The mask is not torch's RNG stream (no reference-visible quantity depends on it).
+Dropout uses the kernels' counter-based hash of (seed, counter + offset): the device state
+and per-call host offsets are the fused BitLinear call sites' (fused._rng), whose counter
+``fused.advance_step`` moves once per step, so a captured step draws fresh masks on every
+replay without a per-call device update (two launches per call before). The mask is not
+torch's RNG stream (no reference-visible quantity depends on it).
 """
 from __future__ import annotations
 
 import os
-from typing import Dict
+from typing import Dict, Tuple
 
 import torch
 
@@ -22,7 +24,8 @@ from . import _lib
 
 __all__ = ["rel_pos_attention", "fused_attention_supported", "dropout_mask"]
 
-_RNG: Dict[torch.device, torch.Tensor] = {}
+# device -> (rng tensor, offset) of the latest call with dropout (tests read the mask back)
+LAST_RNG: Dict[torch.device, Tuple[torch.Tensor, int]] = {}
 
 
 def fused_attention_supported(q: torch.Tensor, d_head: int) -> bool:
@@ -32,18 +35,9 @@ def fused_attention_supported(q: torch.Tensor, d_head: int) -> bool:
             and d_head in (16, 32, 36, 64))
 
 
-def _rng_state(device: torch.device) -> torch.Tensor:
-    st = _RNG.get(device)
-    if st is None:
-        seed = int(torch.initial_seed()) & ((1 << 62) - 1)
-        st = torch.tensor([seed, 0], dtype=torch.int64, device=device)
-        _RNG[device] = st
-    return st
-
-
 class _RelAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, pos, u, vb, lens, n_heads, p_drop, rng):
+    def forward(ctx, q, k, v, pos, u, vb, lens, n_heads, p_drop, rng, rng_off):
         bt, t, c = q.shape
         P = pos.size(0)
         d = c // n_heads
@@ -54,11 +48,11 @@ class _RelAttnFn(torch.autograd.Function):
         _lib.check(
             lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt, P, t, n_heads, d,
-                               p_drop, _lib.ptr(rng), _lib.ptr(probs), out.data_ptr(),
+                               p_drop, _lib.ptr(rng), rng_off, _lib.ptr(probs), out.data_ptr(),
                                _lib.stream_of(q)),
             "ob_relattn_fwd",
         )
-        ctx.meta = (n_heads, p_drop)
+        ctx.meta = (n_heads, p_drop, rng_off)
         if need:
             ctx.save_for_backward(q, k, v, pos, u, vb, lens, probs, rng)
         return out
@@ -66,7 +60,7 @@ class _RelAttnFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         q, k, v, pos, u, vb, lens, probs, rng = ctx.saved_tensors
-        n_heads, p_drop = ctx.meta
+        n_heads, p_drop, rng_off = ctx.meta
         g = g.contiguous()
         bt, t, c = q.shape
         P = pos.size(0)
@@ -80,13 +74,13 @@ class _RelAttnFn(torch.autograd.Function):
         _lib.check(
             lib.ob_relattn_bwd(g.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt,
-                               P, t, n_heads, d, p_drop, _lib.ptr(rng), probs.data_ptr(),
+                               P, t, n_heads, d, p_drop, _lib.ptr(rng), rng_off, probs.data_ptr(),
                                dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(),
                                du.data_ptr(), dvb.data_ptr(), ws.data_ptr(), wsb,
                                _lib.stream_of(g)),
             "ob_relattn_bwd",
         )
-        return dq, dk, dv, dpos, du, dvb, None, None, None, None
+        return dq, dk, dv, dpos, du, dvb, None, None, None, None, None
 
 
 def rel_pos_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos: torch.Tensor,
@@ -96,22 +90,24 @@ def rel_pos_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos: to
     pos_bias_u/v [H, d]; lens int [Bt] valid frames. Returns the context [Bt, T, H*d]."""
     q, k, v, pos = (x.contiguous() for x in (q, k, v, pos))
     lens = lens.to(torch.int32).contiguous()
-    rng = None
+    rng, off = None, 0
     if dropout_p > 0:
-        st = _rng_state(q.device)
-        st[1:].add_(1)          # a fresh mask per call (also on graph replay)
-        rng = st.clone()        # the backward regenerates this call's mask
+        from .fused import _rng
+
+        rng, off = _rng(q.device)  # a distinct offset per call; the backward reuses it
+        LAST_RNG[q.device] = (rng, off)
     return _RelAttnFn.apply(q, k, v, pos, pos_bias_u.contiguous(), pos_bias_v.contiguous(), lens,
-                            n_heads, float(dropout_p), rng)
+                            n_heads, float(dropout_p), rng, off)
 
 
-def dropout_mask(shape, p: float, rng: torch.Tensor) -> torch.Tensor:
+def dropout_mask(shape, p: float, rng: torch.Tensor, rng_off: int = 0) -> torch.Tensor:
     """The keep-mask (uint8, 1 = kept) the kernels draw for probs of ``shape`` (tests)."""
     n = 1
     for s in shape:
         n *= s
     out = torch.empty(n, dtype=torch.uint8, device=rng.device)
     lib = _lib.load()
-    _lib.check(lib.ob_relattn_dropout_mask(n, float(p), rng.data_ptr(), out.data_ptr(),
-                                           _lib.stream_of(rng)), "ob_relattn_dropout_mask")
+    _lib.check(lib.ob_relattn_dropout_mask(n, float(p), rng.data_ptr(), int(rng_off),
+                                           out.data_ptr(), _lib.stream_of(rng)),
+               "ob_relattn_dropout_mask")
     return out.view(*shape)

@@ -33,7 +33,7 @@ from .conv import (conv2d_bias_relu, conv_module_fused, conv_module_supported, d
                    subsample_convs, subsample_supported)
 from .embedding import embedding
 from .fused import (ffn_residual, ffn_residual_i8, fused_supported, i8_fused_supported,
-                    linear_residual, linear_residual_i8)
+                    linear_residual, linear_residual_i8, qkv_projections)
 from .layernorm import fused_layernorm_supported, layer_norm, layer_norm_amax, layer_norm_fork
 from .linear import linear
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
@@ -180,12 +180,21 @@ class MHSA(nn.Module):
         """The same computation with the attention core in one HIP kernel per direction
         (onebit_asr/attention.py); used on a ROCm device for supported shapes."""
         bsz, tlen, width = x.shape
-        qp = self.q_proj(h, bitwidth)
-        kp = self.k_proj(h, bitwidth)
-        vp = self.v_proj(h, bitwidth)
+        if fused_supported(h, self.q_proj, self.k_proj, self.v_proj, bitwidth=bitwidth):
+            # one autograd node: dX of k / v accumulated in the GEMM epilogue (no adds)
+            qp, kp, vp = qkv_projections(h, self.q_proj, self.k_proj, self.v_proj, bitwidth)
+        else:
+            qp = self.q_proj(h, bitwidth)
+            kp = self.k_proj(h, bitwidth)
+            vp = self.v_proj(h, bitwidth)
         if isinstance(bitwidth, PassBits):
             P = bitwidth.passes
-            pe = pos_emb.expand(P, tlen, width).reshape(P * tlen, width)
+            # the P stacked copies of the table: formed once per forward (the same pos_emb
+            # tensor reaches every block), not once per block
+            pe = getattr(pos_emb, "_ob_rows", None)
+            if pe is None or pe.shape[0] != P * tlen:
+                pe = pos_emb.expand(P, tlen, width).reshape(P * tlen, width)
+                pos_emb._ob_rows = pe
             pp = self.pos_proj(pe, bitwidth).view(P, tlen, width)
         else:
             pp = self.pos_proj(pos_emb, bitwidth).view(1, tlen, width)

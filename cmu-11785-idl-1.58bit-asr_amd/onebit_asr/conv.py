@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .layernorm import GradScale, attach_grad_scale
 from .linear import colsum
 
 __all__ = ["depthwise_conv1d", "conv_module_supported", "conv_module_fused", "colsum",
@@ -127,7 +128,7 @@ class _ResidualDropFn(torch.autograd.Function):
     """x + dropout(y) (conformer.py:160-167) with the fused kernels' hash mask."""
 
     @staticmethod
-    def forward(ctx, x, y, p, rng, off):
+    def forward(ctx, x, y, p, rng, off, spec):
         x, y = x.contiguous(), y.contiguous()
         out = torch.empty_like(y)
         n = y.shape[-1]
@@ -135,20 +136,22 @@ class _ResidualDropFn(torch.autograd.Function):
         _lib.check(_lib.load().ob_residual_drop_fwd(x.data_ptr(), y.data_ptr(), rows, n, 1.0, p,
                                                     _lib.ptr(rng), off, None, 0, out.data_ptr(),
                                                     _lib.stream_of(y)), "ob_residual_drop_fwd")
-        ctx.meta = (p, rng, off)
+        ctx.meta = (p, rng, off, spec)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        p, rng, off = ctx.meta
+        p, rng, off, spec = ctx.meta
         g = g.contiguous()
         n = g.shape[-1]
         rows = g.numel() // n
-        gy = torch.empty_like(g)
-        _lib.check(_lib.load().ob_drop_scale_bwd(g.data_ptr(), rows, n, 1.0, p, _lib.ptr(rng), off,
-                                                 None, 0, gy.data_ptr(), _lib.stream_of(g)),
-                   "ob_drop_scale_bwd")
-        return g, gy, None, None, None
+        gy = spec.take(g)  # formed by the next LN's backward (layernorm.GradScale)
+        if gy is None:
+            gy = torch.empty_like(g)
+            _lib.check(_lib.load().ob_drop_scale_bwd(g.data_ptr(), rows, n, 1.0, p, _lib.ptr(rng),
+                                                     off, None, 0, gy.data_ptr(),
+                                                     _lib.stream_of(g)), "ob_drop_scale_bwd")
+        return g, gy, None, None, None, None
 
 
 class _BlasPref:
@@ -404,4 +407,6 @@ def conv_module_fused(x: torch.Tensor, h: torch.Tensor, module, passes: int, p_d
                           module.bn.weight, module.bn.bias, passes, t, float(module.bn.eps))
     o = module.pw2(v, bitwidth) if quant else _pointwise(v, module.pw2)
     rng, off = _rng(x.device) if p_drop > 0 else (None, 0)
-    return _ResidualDropFn.apply(x, o.view(bt, t, c), float(p_drop), rng, off)
+    spec = GradScale(1.0, p_drop, rng, off)
+    return attach_grad_scale(_ResidualDropFn.apply(x, o.view(bt, t, c), float(p_drop), rng, off,
+                                                   spec), spec)

@@ -29,10 +29,11 @@ from typing import Dict, Optional
 import torch
 
 from . import _lib
+from .layernorm import GradScale, attach_grad_scale
 from .quant import PassBits, QuantizedLinear
 
 __all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
-           "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8"]
+           "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8", "qkv_projections"]
 
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
@@ -120,7 +121,7 @@ class _FFNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, x, w1, a1, b1, w2, a2, b2, meta):
-        P, pb, bits, codes1, codes2, p, rng, off1, off2 = meta
+        P, pb, bits, codes1, codes2, p, rng, off1, off2, _ = meta
         rows, k = h.shape
         m = rows // P
         n1, n2 = w1.shape[0], w2.shape[0]
@@ -145,16 +146,19 @@ class _FFNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         h, pre, act, w1, a1, w2, a2 = ctx.saved_tensors
-        P, pb, bits, codes1, codes2, p, rng, off1, off2 = ctx.meta
+        P, pb, bits, codes1, codes2, p, rng, off1, off2, spec = ctx.meta
         gout = gout.contiguous()
         rows, k = h.shape
         m = rows // P
         n1, n2 = w1.shape[0], w2.shape[0]
         lib = _lib.load()
         stream = _lib.stream_of(gout)
-        dy2 = torch.empty_like(gout)
-        _lib.check(lib.ob_drop_scale_bwd(gout.data_ptr(), rows, n2, 0.5, p, _lib.ptr(rng), off2,
-                                         None, 0, dy2.data_ptr(), stream), "ob_drop_scale_bwd")
+        dy2 = spec.take(gout)  # formed by the next LN's backward (layernorm.GradScale)
+        if dy2 is None:
+            dy2 = torch.empty_like(gout)
+            _lib.check(lib.ob_drop_scale_bwd(gout.data_ptr(), rows, n2, 0.5, p, _lib.ptr(rng),
+                                             off2, None, 0, dy2.data_ptr(), stream),
+                       "ob_drop_scale_bwd")
         dpre = torch.empty((rows, n1), dtype=torch.float32, device=gout.device)
         _lib.check(lib.ob_bitlinear_bwd_dx_swish_drop(
             dy2.data_ptr(), P, m, n2, codes2[2].data_ptr(), codes2[3].data_ptr(), _lib.ptr(pb),
@@ -171,7 +175,7 @@ class _LinearResidualFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, resid, w, a, b, meta):
-        P, pb, bits, codes, rscale, p, rng, off, lens, T = meta
+        P, pb, bits, codes, rscale, p, rng, off, lens, T, _ = meta
         rows, k = x.shape
         m = rows // P
         n = w.shape[0]
@@ -189,20 +193,100 @@ class _LinearResidualFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         x, w, a = ctx.saved_tensors
-        P, pb, bits, codes, rscale, p, rng, off, lens, T = ctx.meta
+        P, pb, bits, codes, rscale, p, rng, off, lens, T, spec = ctx.meta
         gout = gout.contiguous()
         rows, k = x.shape
         m = rows // P
         n = w.shape[0]
         lib = _lib.load()
         stream = _lib.stream_of(gout)
-        dy = torch.empty_like(gout)
-        _lib.check(lib.ob_drop_scale_bwd(gout.data_ptr(), rows, n, rscale, p, _lib.ptr(rng), off,
-                                         _lib.ptr(lens), T, dy.data_ptr(), stream),
-                   "ob_drop_scale_bwd")
+        dy = spec.take(gout)  # formed by the next LN's backward (layernorm.GradScale)
+        if dy is None:
+            dy = torch.empty_like(gout)
+            _lib.check(lib.ob_drop_scale_bwd(gout.data_ptr(), rows, n, rscale, p, _lib.ptr(rng),
+                                             off, _lib.ptr(lens), T, dy.data_ptr(), stream),
+                       "ob_drop_scale_bwd")
         gx = _dx(lib, dy, P, m, n, codes, pb, a, k, stream) if ctx.needs_input_grad[0] else None
         gw, ga, gb = _dw(lib, dy, x, P, m, n, k, w, a, ctx.has_bias, pb, bits, stream)
         return gx, gout, gw, ga, gb, None
+
+
+class _QKVFn(torch.autograd.Function):
+    """The three projections of one input (conformer.py:111-113: q/k/v_proj(x) on the same
+    LN output) as one autograd node: three GEMMs forward; backward, dX of q plain and the dX
+    GEMMs of k and v accumulated into it through the GEMM's residual epilogue (C = R + y,
+    in place), instead of autograd's two separate adds over [rows, d]; three dW GEMMs."""
+
+    @staticmethod
+    def forward(ctx, h, wq, aq, bq, wk, ak, bk, wv, av, bv, meta):
+        P, pb, bits, codes = meta
+        rows, k = h.shape
+        m = rows // P
+        lib = _lib.load()
+        stream = _lib.stream_of(h)
+        outs = []
+        for w, a, b, c in ((wq, aq, bq, codes[0]), (wk, ak, bk, codes[1]), (wv, av, bv, codes[2])):
+            n = w.shape[0]
+            y = torch.empty((rows, n), dtype=torch.float32, device=h.device)
+            st = (lib.ob_bitlinear_fwd_passes(h.data_ptr(), P, m, k, c[0].data_ptr(),
+                                              c[1].data_ptr(), pb.data_ptr(), a.data_ptr(), 1,
+                                              _lib.ptr(b), n, y.data_ptr(), stream)
+                  if pb is not None else
+                  lib.ob_bitlinear_fwd(h.data_ptr(), m, k, c[0].data_ptr(), a.data_ptr(), 1,
+                                       _lib.ptr(b), n, y.data_ptr(), stream))
+            _lib.check(st, "ob_bitlinear_fwd")
+            outs.append(y)
+        ctx.meta = meta
+        ctx.has_bias = (bq is not None, bk is not None, bv is not None)
+        ctx.save_for_backward(h, wq, aq, wk, ak, wv, av)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, gq, gk, gv):
+        h, wq, aq, wk, ak, wv, av = ctx.saved_tensors
+        P, pb, bits, codes = ctx.meta
+        rows, k = h.shape
+        m = rows // P
+        lib = _lib.load()
+        stream = _lib.stream_of(h)
+        layers = [(g.contiguous(), w, a, c, hb) for g, w, a, c, hb in
+                  zip((gq, gk, gv), (wq, wk, wv), (aq, ak, av), codes, ctx.has_bias)
+                  if g is not None]
+        gh = None
+        if ctx.needs_input_grad[0]:
+            for g, w, a, c, _ in layers:
+                n = w.shape[0]
+                if gh is None:
+                    gh = _dx(lib, g, P, m, n, c, pb, a, k, stream)
+                    continue
+                # gh += a * g . Q  (the dX GEMM with C = R = gh: each element read, then written,
+                # by one lane)
+                _lib.check(lib.ob_bitlinear_fwd_residual(
+                    g.data_ptr(), P, m, n, c[2].data_ptr(), c[3].data_ptr(), _lib.ptr(pb),
+                    a.data_ptr(), 1, None, k, gh.data_ptr(), 1.0, 0.0, None, 0, None, 0,
+                    gh.data_ptr(), stream), "ob_bitlinear_fwd_residual (dX accumulate)")
+        grads = {}
+        for i, (g, w, a, c, hb) in zip(range(3), layers):
+            grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream)
+        out = [gh]
+        for w in (wq, wk, wv):
+            out.extend(grads.get(id(w), (None, None, None)))
+        return (*out, None)
+
+
+def qkv_projections(h: torch.Tensor, q_proj: QuantizedLinear, k_proj: QuantizedLinear,
+                    v_proj: QuantizedLinear, bitwidth):
+    """(q_proj(h), k_proj(h), v_proj(h)) as one autograd node (_QKVFn)."""
+    P, pb, bits = _bits_args(bitwidth)
+    h2 = _flat(h, q_proj.in_features)
+    if h2.shape[0] % P:
+        raise ValueError(f"{h2.shape[0]} rows do not split into {P} passes")
+    meta = (P, pb, bits, tuple(_codes(l, P, bits) for l in (q_proj, k_proj, v_proj)))
+    q, k, v = _QKVFn.apply(h2, q_proj.weight, q_proj.alpha, q_proj.bias, k_proj.weight,
+                           k_proj.alpha, k_proj.bias, v_proj.weight, v_proj.alpha, v_proj.bias,
+                           meta)
+    lead = h.shape[:-1]
+    return (q.view(*lead, -1), k.view(*lead, -1), v.view(*lead, -1))
 
 
 def _flat(t: torch.Tensor, width: int) -> torch.Tensor:
@@ -219,11 +303,12 @@ def ffn_residual(h: torch.Tensor, x: torch.Tensor, lin1: QuantizedLinear, lin2: 
         raise ValueError(f"{h2.shape[0]} rows do not split into {P} passes")
     rng, off1 = _rng(h.device) if p_drop > 0 else (None, 0)
     off2 = _rng(h.device)[1] if p_drop > 0 else 0
+    spec = GradScale(0.5, p_drop, rng, off2)
     meta = (P, pb, bits, _codes(lin1, P, bits), _codes(lin2, P, bits), float(p_drop), rng,
-            off1, off2)
+            off1, off2, spec)
     out = _FFNFn.apply(h2, x2, lin1.weight, lin1.alpha, lin1.bias, lin2.weight, lin2.alpha,
                        lin2.bias, meta)
-    return out.view(x.shape)
+    return attach_grad_scale(out.view(x.shape), spec)
 
 
 def linear_residual(inp: torch.Tensor, x: torch.Tensor, lin: QuantizedLinear, bitwidth,
@@ -238,10 +323,11 @@ def linear_residual(inp: torch.Tensor, x: torch.Tensor, lin: QuantizedLinear, bi
     rng, off = _rng(inp.device) if p_drop > 0 else (None, 0)
     if lens is not None:
         lens = lens.to(torch.int32).contiguous()
+    spec = GradScale(rscale, p_drop, rng, off, lens, frames)
     meta = (P, pb, bits, _codes(lin, P, bits), float(rscale), float(p_drop), rng, off, lens,
-            int(frames))
+            int(frames), spec)
     out = _LinearResidualFn.apply(i2, x2, lin.weight, lin.alpha, lin.bias, meta)
-    return out.view(x.shape)
+    return attach_grad_scale(out.view(x.shape), spec)
 
 
 # ----------------------------------------------------------------------------------------

@@ -14,7 +14,60 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "fused_layernorm_supported"]
+__all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "fused_layernorm_supported",
+           "GradScale", "attach_grad_scale"]
+
+_GSCALE = os.environ.get("OB_LN_GSCALE", "1") != "0"  # 0: consumers run ob_drop_scale_bwd
+
+
+class GradScale:
+    """Hand-off between a residual tail "R + rscale * rowvalid * dropout(y)" (the fused FFN,
+    out_proj and conv-module outputs, conformer.py:39-45, :131-138, :160-167) and the LN that
+    normalises that output next. The tail's backward needs dy = rscale * rowvalid *
+    drop(gout), gout being exactly the LN backward's dx (the tail's output feeds only that
+    LN); the LN backward forms it as a second output (ob_layernorm_bwd_ex) while dx is in
+    registers, instead of the tail running ob_drop_scale_bwd over dx afterwards. The tail
+    takes the result only if its incoming gradient IS that dx (same storage); anything else
+    (another consumer's gradient added in, hooks) falls back to the separate kernel."""
+
+    __slots__ = ("rscale", "p", "rng", "off", "lens", "T", "dx_ptr", "dy2")
+
+    def __init__(self, rscale: float, p: float, rng, off: int, lens=None, T: int = 0):
+        self.rscale, self.p, self.rng, self.off = float(rscale), float(p), rng, int(off)
+        self.lens, self.T = lens, int(T)
+        self.dx_ptr, self.dy2 = 0, None
+
+    def take(self, gout: torch.Tensor):
+        dy2, self.dy2 = self.dy2, None
+        if dy2 is not None and gout.data_ptr() == self.dx_ptr and gout.numel() == dy2.numel():
+            return dy2.view(gout.shape)
+        return None
+
+
+def attach_grad_scale(out: torch.Tensor, spec: GradScale) -> torch.Tensor:
+    if _GSCALE and torch.is_grad_enabled():
+        out._ob_gscale = spec
+    return out
+
+
+def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, wsb, spec, stream):
+    if spec is None:
+        if dres is None:
+            return lib.ob_layernorm_bwd(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
+                                        mean.data_ptr(), rstd.data_ptr(), rows, d, dx.data_ptr(),
+                                        _lib.ptr(dw), _lib.ptr(db), ws.data_ptr(), wsb, stream)
+        return lib.ob_layernorm_bwd_res(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
+                                        mean.data_ptr(), rstd.data_ptr(), rows, d,
+                                        dres.data_ptr(), dx.data_ptr(), _lib.ptr(dw),
+                                        _lib.ptr(db), ws.data_ptr(), wsb, stream)
+    dy2 = torch.empty_like(dx)
+    st = lib.ob_layernorm_bwd_ex(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight), mean.data_ptr(),
+                                 rstd.data_ptr(), rows, d, _lib.ptr(dres), dx.data_ptr(),
+                                 _lib.ptr(dw), _lib.ptr(db), ws.data_ptr(), wsb, dy2.data_ptr(),
+                                 spec.rscale, spec.p, _lib.ptr(spec.rng), spec.off,
+                                 _lib.ptr(spec.lens), spec.T, stream)
+    spec.dx_ptr, spec.dy2 = dx.data_ptr(), dy2
+    return st
 
 
 def fused_layernorm_supported(x: torch.Tensor, d: int) -> bool:
@@ -25,8 +78,9 @@ def fused_layernorm_supported(x: torch.Tensor, d: int) -> bool:
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, spec=None):
         d = x.shape[-1]
+        ctx.spec = spec
         x2 = x.contiguous().view(-1, d)
         rows = x2.shape[0]
         y = torch.empty_like(x2)
@@ -54,18 +108,16 @@ class _LayerNormFn(torch.autograd.Function):
         lib = _lib.load()
         wsb = lib.ob_layernorm_bwd_workspace(rows, d)
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
-        _lib.check(lib.ob_layernorm_bwd(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
-                                        mean.data_ptr(), rstd.data_ptr(), rows, d, dx.data_ptr(),
-                                        _lib.ptr(dw), _lib.ptr(db), ws.data_ptr(), wsb,
-                                        _lib.stream_of(g2)), "ob_layernorm_bwd")
-        return dx.view(gy.shape), dw, db, None
+        _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, None, dx, dw, db, ws, wsb,
+                             ctx.spec, _lib.stream_of(g2)), "ob_layernorm_bwd")
+        return dx.view(gy.shape), dw, db, None, None
 
 
 def layer_norm(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.Tensor:
     d = x.shape[-1]
     if not fused_layernorm_supported(x, d):
         return F.layer_norm(x, (d,), weight, bias, eps)
-    return _LayerNormFn.apply(x, weight, bias, eps)
+    return _LayerNormFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None))
 
 
 @torch.no_grad()
@@ -96,8 +148,8 @@ class _LayerNormForkFn(torch.autograd.Function):
     instead of autograd's separate add over the [rows, d] tensor."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
-        y = _LayerNormFn.forward(ctx, x, weight, bias, eps)
+    def forward(ctx, x, weight, bias, eps, spec=None):
+        y = _LayerNormFn.forward(ctx, x, weight, bias, eps, spec)
         return y, x.view_as(x)
 
     @staticmethod
@@ -107,7 +159,7 @@ class _LayerNormForkFn(torch.autograd.Function):
         x2, weight, mean, rstd = ctx.saved_tensors
         rows, d = x2.shape
         if gy is None:
-            return gres, None, None, None
+            return gres, None, None, None, None
         g2 = gy.contiguous().view(rows, d)
         r2 = gres.contiguous().view(rows, d)
         dx = torch.empty_like(x2)
@@ -117,12 +169,9 @@ class _LayerNormForkFn(torch.autograd.Function):
         lib = _lib.load()
         wsb = lib.ob_layernorm_bwd_workspace(rows, d)
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
-        _lib.check(lib.ob_layernorm_bwd_res(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
-                                            mean.data_ptr(), rstd.data_ptr(), rows, d,
-                                            r2.data_ptr(), dx.data_ptr(), _lib.ptr(dw),
-                                            _lib.ptr(db), ws.data_ptr(), wsb,
-                                            _lib.stream_of(g2)), "ob_layernorm_bwd_res")
-        return dx.view(gy.shape), dw, db, None
+        _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, r2, dx, dw, db, ws, wsb,
+                             ctx.spec, _lib.stream_of(g2)), "ob_layernorm_bwd_res")
+        return dx.view(gy.shape), dw, db, None, None
 
 
 def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):
@@ -131,4 +180,4 @@ def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):
     d = x.shape[-1]
     if not fused_layernorm_supported(x, d) or not torch.is_grad_enabled() or not x.requires_grad:
         return layer_norm(x, weight, bias, eps), x
-    return _LayerNormForkFn.apply(x, weight, bias, eps)
+    return _LayerNormForkFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None))

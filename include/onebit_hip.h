@@ -282,25 +282,29 @@ OB_API int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P
  *   lens : DEVICE int32 [Bt]   (valid frames; the encoder's prefix masks)
  *   probs : [Bt][H][T][T]      softmax before dropout; written by fwd when non-NULL,
  *                              required by bwd
- *   rng : DEVICE int64 [2] (seed, counter); dropout keeps element e of probs when
- *         hash(seed, counter, e) >= p_drop * 2^32 (fwd and bwd regenerate the same mask;
- *         ob_relattn_dropout_mask writes it out). Unused when p_drop == 0.
+ *   rng : DEVICE int64 [2] (seed, counter), rng_offset a host offset added to the counter
+ *         (the fused BitLinear entries' convention: one device state, a distinct offset per
+ *         call site, the counter advanced once per step); dropout keeps element e of probs
+ *         when hash(seed, counter + rng_offset, e) >= p_drop * 2^32 (fwd and bwd regenerate
+ *         the same mask; ob_relattn_dropout_mask writes it out). Unused when p_drop == 0.
  * Supported: 1 <= T <= 512, d in {16, 32, 36, 64}.
  * ------------------------------------------------------------------------------------ */
 OB_API int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                           const float* u, const float* vb, const int32_t* lens, int64_t Bt,
                           int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                          const int64_t* rng, float* probs, float* ctx, void* stream);
+                          const int64_t* rng, int64_t rng_offset, float* probs, float* ctx,
+                          void* stream);
 OB_API size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
 OB_API int ob_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
                           const float* pos, const float* u, const float* vb,
                           const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H,
-                          int64_t d, float p_drop, const int64_t* rng, const float* probs,
+                          int64_t d, float p_drop, const int64_t* rng, int64_t rng_offset,
+                          const float* probs,
                           float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb,
                           void* ws, size_t ws_bytes, void* stream);
 /* The dropout keep-mask (1 = kept) the attention kernels use, for n elements of probs. */
-OB_API int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, uint8_t* out,
-                                   void* stream);
+OB_API int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng,
+                                   int64_t rng_offset, uint8_t* out, void* stream);
 
 /* Token-embedding backward of the decoder (conformer.py:279-299, nn.Embedding with
  * padding_idx): grad_weight[v] = sum over n ascending with indices[n] == v of grad[n]
@@ -375,6 +379,18 @@ OB_API int ob_layernorm_bwd_res(const float* dy, const float* x, const float* ga
                                 const float* mean, const float* rstd, int64_t rows, int64_t d,
                                 const float* dres, float* dx, float* dgamma, float* dbeta,
                                 void* ws, size_t ws_bytes, void* stream);
+/* ob_layernorm_bwd / _res (dres may be NULL) with an optional second output for the module
+ * whose output this LN normalises: dy2 = rscale * rowvalid * drop(dx), element for element
+ * ob_drop_scale_bwd(dx, rows, d, rscale, p_drop, rng, rng_offset, lens, T) -- the backward
+ * of that module's residual tail "R + rscale * rowvalid * dropout(y)" (conformer.py:39-45,
+ * :131-138, :160-167), formed while dx is in registers instead of in a pass of its own.
+ * dy2 == NULL: plain ob_layernorm_bwd_res. */
+OB_API int ob_layernorm_bwd_ex(const float* dy, const float* x, const float* gamma,
+                               const float* mean, const float* rstd, int64_t rows, int64_t d,
+                               const float* dres, float* dx, float* dgamma, float* dbeta,
+                               void* ws, size_t ws_bytes, float* dy2, float rscale,
+                               float p_drop, const uint64_t* rng, int64_t rng_offset,
+                               const int32_t* lens, int64_t T, void* stream);
 
 /*
  * Batched greedy CTC decode (inference path). Replaces onebit_asr/metrics.py:51-60

@@ -92,7 +92,10 @@ def test_s_literal_matches_stacked_and_replays(s_model, gpu, stacked_ref):
     med = med[len(med) // 2]
     for k, e in errs.items():
         if any(z in k for z in ZERO_GRAD):
-            assert (g_l[k] - g_s[k]).abs().max().item() <= 1e-7, (k, e)
+            # true gradient 0: both sides are rounding residuals (the BatchNorm backward's
+            # mean projection over 23904 rows; the softmax shift invariance); observed
+            # |residual| <= 1.2e-7 on either side
+            assert (g_l[k] - g_s[k]).abs().max().item() <= 5e-7, (k, e)
         elif k.endswith(".alpha"):
             d = abs(g_l[k].item() - g_s[k].item())
             assert d <= max(2e-3 * abs(g_s[k].item()), 1e-3 * med), (k, g_l[k], g_s[k], med)

@@ -96,9 +96,7 @@ def test_ffn_fused_stacked_passes(gpu, monkeypatch):
 def _mask(rng_state, off, n, p, gpu):
     from onebit_asr.attention import dropout_mask
 
-    r = rng_state.clone()
-    r[1] += off
-    return dropout_mask((n,), p, r).bool()
+    return dropout_mask((n,), p, rng_state, off).bool()
 
 
 def test_ffn_dropout_matches_torch_restatement(gpu, monkeypatch):
@@ -230,3 +228,45 @@ def test_subsampling_bias_relu_and_colsum(gpu):
     assert _rel(got[2], conv.bias.grad) <= 1e-6
     m = torch.randn(1000, 77, device=gpu)
     assert _rel(colsum(m), m.double().sum(0)) <= 1e-6
+
+
+@pytest.mark.parametrize("stacked", [False, True])
+def test_qkv_projections_match_separate_layers(gpu, stacked):
+    """fused.qkv_projections (one autograd node, dX of k / v accumulated in the GEMM
+    epilogue) == q_proj(h), k_proj(h), v_proj(h) as three module calls: outputs bit-exact,
+    dh and every weight / alpha / bias gradient within fp32 summation-order noise."""
+    from onebit_asr.fused import qkv_projections
+    from onebit_asr.quant import QuantizedLinear, StackedBits
+
+    torch.manual_seed(0)
+    layers = [QuantizedLinear(144, 144).to(gpu) for _ in range(3)]
+    with torch.no_grad():
+        for m in layers:
+            m.bias.normal_()
+    if stacked:
+        bits = StackedBits(1, gpu)
+        bits.set([1])
+        bw = bits[0]
+    else:
+        bw = 1
+    rows = (3 if stacked else 1) * 2 * 249
+    h = torch.randn(rows, 144, device=gpu, requires_grad=True)
+    gouts = [torch.randn(rows, 144, device=gpu) for _ in range(3)]
+
+    def run(fused):
+        for m in layers:
+            for p in m.parameters():
+                p.grad = None
+        h.grad = None
+        outs = qkv_projections(h, *layers, bw) if fused else [m(h, bw) for m in layers]
+        torch.autograd.backward(outs, gouts)
+        return ([o.detach().clone() for o in outs], h.grad.clone(),
+                [p.grad.clone() for m in layers for p in (m.weight, m.alpha, m.bias)])
+
+    o0, dh0, g0 = run(False)
+    o1, dh1, g1 = run(True)
+    for a, b in zip(o0, o1):
+        assert torch.equal(a, b)
+    assert (dh0 - dh1).abs().max().item() <= 1e-6 * dh0.abs().max().item()
+    for a, b in zip(g0, g1):
+        assert (a - b).abs().max().item() <= 1e-6 * max(a.abs().max().item(), 1e-30), (a, b)

@@ -74,12 +74,11 @@ def test_relattn_matches_reference(gpu, bt, P, t, H, d, lens, p):
     q, k, v, pos, u, vb = _inputs(bt, P, t, H, d, seed=bt * 1000 + t)
     lens_t = torch.tensor(lens)
     dev = [x.to(gpu).requires_grad_() for x in (q, k, v, pos, u, vb)]
-    at._RNG.pop(torch.device(gpu), None)
     ctx = at.rel_pos_attention(*dev, lens_t.to(gpu), H, dropout_p=p)
     keep = None
     if p > 0:
-        rng = at._rng_state(torch.device(gpu)).clone()  # the state this call used
-        keep = at.dropout_mask((bt, H, t, t), p, rng).cpu()
+        rng, off = at.LAST_RNG[torch.device(gpu)]  # the state + offset this call used
+        keep = at.dropout_mask((bt, H, t, t), p, rng, off).cpu()
     gout = torch.randn(bt, t, H * d, generator=torch.Generator().manual_seed(7))
     ctx.backward(gout.to(gpu))
 
@@ -104,7 +103,7 @@ def test_relattn_probs_and_determinism(gpu):
         ctx = torch.empty_like(q)
         _lib.check(lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                       u.data_ptr(), vb.data_ptr(), lens.to(gpu).data_ptr(), bt, P,
-                                      t, H, d, 0.0, None, probs.data_ptr(), ctx.data_ptr(),
+                                      t, H, d, 0.0, None, 0, probs.data_ptr(), ctx.data_ptr(),
                                       _lib.stream_of(q)), "fwd")
         outs.append((probs.clone(), ctx.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
@@ -122,6 +121,8 @@ def test_relattn_dropout_mask_rate(gpu):
     rng2 = torch.tensor([12345, 8], dtype=torch.int64, device=gpu)
     m2 = at.dropout_mask((4, 4, 249, 249), 0.1, rng2).float()
     assert (m != m2).float().mean().item() > 0.1  # the counter changes the mask
+    # the host offset is added to the device counter: (7, +1) draws (8, +0)'s mask
+    assert torch.equal(at.dropout_mask((4, 4, 249, 249), 0.1, rng, 1).float(), m2)
 
 
 def test_mhsa_fused_matches_torch_path(gpu, monkeypatch):

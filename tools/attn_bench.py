@@ -43,12 +43,12 @@ def main():
     def fwd(s):
         return lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                   u.data_ptr(), vb.data_ptr(), lens.data_ptr(), Bt, P, T, H, d, a.p,
-                                  rng.data_ptr(), probs.data_ptr(), ctx.data_ptr(), s)
+                                  rng.data_ptr(), 0, probs.data_ptr(), ctx.data_ptr(), s)
 
     def bwd(s):
         return lib.ob_relattn_bwd(do.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                   pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), Bt,
-                                  P, T, H, d, a.p, rng.data_ptr(), probs.data_ptr(), dq.data_ptr(),
+                                  P, T, H, d, a.p, rng.data_ptr(), 0, probs.data_ptr(), dq.data_ptr(),
                                   dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(), du.data_ptr(),
                                   dvb.data_ptr(), ws.data_ptr(), wsb, s)
 
