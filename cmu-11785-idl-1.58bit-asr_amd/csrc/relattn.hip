@@ -21,8 +21,11 @@
 // Layout: q, k, v, ctx, dq, dk, dv [Bt][T][H*d]; pos, dpos [P][T][H*d] (batch row b uses
 // pass b / (Bt/P)); u, vb, du, dvb [H][d]; probs [Bt][H][T][T]; lens int32 [Bt].
 // Products on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, like torch's fp32 matmul).
-// Dropout keeps (i, j) when hash(key(seed, counter), index) >= p * 2^32 (a counter hash:
-// the backward regenerates the same mask; torch's own RNG stream is not reproduced).
+// Dropout keeps (i, j) when hash(key(seed, counter + offset), index) >= p * 2^32 (a
+// counter hash; torch's own RNG stream is not reproduced). The forward stores each kept
+// probability as P and each dropped one as -P (P >= 0, so the sign bit is free): both
+// backward kernels read the keep bit back with the probability instead of hashing the
+// T x T matrix again (16 us per key-side call at Conformer-S).
 #include <math.h>
 
 #include "ob_drop.h"
@@ -59,6 +62,12 @@
 #endif
 #ifndef RB_EXP_NOPROBS
 #define RB_EXP_NOPROBS 0
+#endif
+#ifndef RA_EXP_NOROW64
+#define RA_EXP_NOROW64 0
+#endif
+#ifndef RB_EXP_NOROW
+#define RB_EXP_NOROW 0
 #endif
 #ifndef RK_EXP_NOMFMA
 #define RK_EXP_NOMFMA 0
@@ -217,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   // the first key group of the scores phase, in flight over the row-64 work and barrier
   load_group<DQ>(kb, C, 0, r, g, T, opa);
   // row 64: the next tile's first query (fp32 fma chain on the VALU)
-  if (i0 + kTile < T) {
+  if (!RA_EXP_NOROW64 && i0 + kTile < T) {
     const float* qe = qb + (size_t)(i0 + kTile) * C;
     for (int m = threadIdx.x; m < T; m += kThreads) {
       float pr[D];
@@ -297,12 +306,15 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     for (int j = 0; j < 4; ++j) {
       const int jj = 16 * t + 4 * g + j;
       const float pr = row_live ? sreg[t][j] * rsum : 0.0f;
-      if (!RA_EXP_NOPROBS && probs && qi < T && jj < T) probs[prow_off + jj] = pr;
       float pd = pr;
+      bool keep = true;
       if (dc.on && !RA_EXP_NODROP) {
-        const bool keep = drop_hash(dkey, prow_off + jj) >= dc.thresh;
+        keep = drop_hash(dkey, prow_off + jj) >= dc.thresh;
         pd = keep ? pr * dc.scale : 0.0f;
       }
+      // the keep decision rides in the sign bit (P >= 0): the backward kernels read it
+      // back instead of re-hashing every element
+      if (!RA_EXP_NOPROBS && probs && qi < T && jj < T) probs[prow_off + jj] = keep ? pr : -pr;
       sreg[t][j] = pd;
     }
   }
@@ -385,11 +397,12 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* dob = dctx + bo;
   const float* pb = pos + (size_t)pass * T * C + h * D;
   const float* prb = probs + ((size_t)b * H + h) * T * T;
-  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
-  const size_t pbase = ((size_t)b * H + h) * T * T;
-  auto keep_scale = [&](int i, int j) -> float {
+  (void)rng;
+  (void)rng_off;
+  // dropout backward factor from a stored probability's sign bit (the forward's keep bit)
+  auto keep_scale = [&](float pv) -> float {
     if (!dc.on) return 1.0f;
-    return drop_hash(dkey, pbase + (size_t)i * T + j) >= dc.thresh ? dc.scale : 0.0f;
+    return __builtin_signbit(pv) ? 0.0f : dc.scale;
   };
 
   const int qi = i0 + 16 * w + r;
@@ -439,9 +452,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int jj = 16 * t + 4 * g + j;
-      const float p = RB_EXP_NOPROBS ? 0.5f : pp[j];
-      const float dp = acc[j] * keep_scale(qic, jj);  // dropout backward
+      const float p = RB_EXP_NOPROBS ? 0.5f : fabsf(pp[j]);
+      const float dp = acc[j] * keep_scale(pp[j]);  // dropout backward
       dsr[t][j] = p;
       acc[j] = dp;
       rowdot += p * dp;
@@ -476,7 +488,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   }
 
   // row i0-1 (LDS row 0) on the VALU, the same formula
-  if (i0 > 0) {
+  if (!RB_EXP_NOROW && i0 > 0) {
     const int ip = i0 - 1;
     float part = 0.0f;
     for (int jj = threadIdx.x; jj < T; jj += kThreads) {
@@ -484,8 +496,9 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
       const float* drow = dob + (size_t)ip * C;
       float a = 0.0f;
       for (int c = 0; c < D; ++c) a = fmaf(vrow[c], drow[c], a);
-      const float dp = a * keep_scale(ip, jj);
-      const float p = prb[(size_t)ip * T + jj];
+      const float pv = prb[(size_t)ip * T + jj];
+      const float dp = a * keep_scale(pv);
+      const float p = fabsf(pv);
       ds[jj] = dp;
       part += p * dp;
     }
@@ -494,7 +507,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     __syncthreads();
     const float rd = ((rsum[0] + rsum[1]) + rsum[2]) + rsum[3];
     for (int jj = threadIdx.x; jj < T; jj += kThreads) {
-      const float p = prb[(size_t)ip * T + jj];
+      const float p = fabsf(prb[(size_t)ip * T + jj]);
       ds[jj] = (p * (ds[jj] - rd)) * inv_sqrt_d;
     }
   }
@@ -674,8 +687,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   const float* vbb = vbias + h * D;
   const float* dsb = dsg + ((size_t)b * H + h) * T * T;
   const float* prb = probs + ((size_t)b * H + h) * T * T;
-  const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
-  const size_t pbase = ((size_t)b * H + h) * T * T;
+  (void)rng;
+  (void)rng_off;
 
   // pad columns of the B tiles stay zero (their MFMA columns are discarded anyway)
   for (int e = threadIdx.x; e < kQ * St::kBP; e += kThreads) {
@@ -725,11 +738,11 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
         ra_p[hf][j] = (ok && (upper || ic >= 1)) ? x : 0.0f;
       }
     }
+    // Pd = P * keep * scale, the keep bit from the stored probability's sign
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int m = key0 + j;
-      if (!RK_EXP_NOHASH && dc.on && i < T && m < T)
-        ra_v[hf][j] = drop_hash(dkey, pbase + (size_t)i * T + m) >= dc.thresh ? ra_v[hf][j] * dc.scale : 0.0f;
+      if (!RK_EXP_NOHASH && dc.on)
+        ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
     }
     }
 #pragma unroll

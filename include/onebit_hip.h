@@ -281,7 +281,8 @@ OB_API int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P
  *   u, vb, du, dvb : [H][d]    (pos_bias_u / pos_bias_v)
  *   lens : DEVICE int32 [Bt]   (valid frames; the encoder's prefix masks)
  *   probs : [Bt][H][T][T]      softmax before dropout; written by fwd when non-NULL,
- *                              required by bwd
+ *                              required by bwd. With p_drop > 0 each element's sign bit
+ *                              is its dropout decision (dropped: -P; |probs| = softmax)
  *   rng : DEVICE int64 [2] (seed, counter), rng_offset a host offset added to the counter
  *         (the fused BitLinear entries' convention: one device state, a distinct offset per
  *         call site, the counter advanced once per step); dropout keeps element e of probs
