@@ -34,8 +34,33 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// VW consecutive columns of slot i of lane j: columns VW * (j + 16 i) + e, e < VW. VW = 4
+// (d % 4 == 0, 16-byte aligned rows): dwordx4 loads and stores, 256 contiguous bytes per 16
+// lanes; VW = 1: 64-byte segments.
+template <int VW>
+__device__ __forceinline__ void load_cols(const float* __restrict__ p, int c0, int d,
+                                          float (&out)[VW]) {
+  if constexpr (VW == 4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 v = c0 < d ? *reinterpret_cast<const f4*>(p + c0) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = v[e];
+  } else {
+    out[0] = c0 < d ? p[c0] : 0.0f;
+  }
+}
+template <int VW>
+__device__ __forceinline__ void store_cols(float* __restrict__ p, int c0, const float (&v)[VW]) {
+  if constexpr (VW == 4) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<f4*>(p + c0) = f4{v[0], v[1], v[2], v[3]};
+  } else {
+    p[c0] = v[0];
+  }
+}
+
 // One row (16 lanes): y = LN(x) and the row's (mean, rstd); returns this lane's max|y|.
-template <int NPL>
+template <int NPL, int VW = 1>
 __device__ __forceinline__ float ln_row(const float* __restrict__ x,
                                         const float* __restrict__ gamma,
                                         const float* __restrict__ beta, int64_t row, int d,
@@ -44,36 +69,42 @@ __device__ __forceinline__ float ln_row(const float* __restrict__ x,
                                         float* __restrict__ rstd_out) {
   const int j = threadIdx.x & (kLanesPerRow - 1);
   const float* xr = x + row * d;
-  float v[NPL];
+  float v[NPL][VW];
   float s = 0.0f;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
-    const int c = j + kLanesPerRow * i;
-    v[i] = c < d ? xr[c] : 0.0f;
-    s += v[i];
+    load_cols<VW>(xr, VW * (j + kLanesPerRow * i), d, v[i]);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s += v[i][e];
   }
   const float inv_d = 1.0f / (float)d;
   const float mean = row_sum16(s) * inv_d;
   float q = 0.0f;
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    const int c = j + kLanesPerRow * i;
-    const float t = c < d ? v[i] - mean : 0.0f;
-    q = fmaf(t, t, q);
-  }
+  for (int i = 0; i < NPL; ++i)
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      const int c = VW * (j + kLanesPerRow * i) + e;
+      const float t = c < d ? v[i][e] - mean : 0.0f;
+      q = fmaf(t, t, q);
+    }
   const float var = row_sum16(q) * inv_d;
   const float rstd = 1.0f / sqrtf(var + eps);
   float* yr = y + row * d;
   float amx = 0.0f;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
-    const int c = j + kLanesPerRow * i;
-    if (c < d) {
-      const float g = gamma ? gamma[c] : 1.0f;
-      const float b = beta ? beta[c] : 0.0f;
-      const float o = fmaf((v[i] - mean) * rstd, g, b);
-      yr[c] = o;
-      amx = fmaxf(amx, fabsf(o));
+    const int c0 = VW * (j + kLanesPerRow * i);
+    if (c0 < d) {
+      float g[VW], b[VW], o[VW];
+      if (gamma) load_cols<VW>(gamma, c0, d, g);
+      if (beta) load_cols<VW>(beta, c0, d, b);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        o[e] = fmaf((v[i][e] - mean) * rstd, gamma ? g[e] : 1.0f, beta ? b[e] : 0.0f);
+        amx = fmaxf(amx, fabsf(o[e]));
+      }
+      store_cols<VW>(yr, c0, o);
     }
   }
   if (j == 0) {
@@ -83,14 +114,14 @@ __device__ __forceinline__ float ln_row(const float* __restrict__ x,
   return amx;
 }
 
-template <int NPL>  // columns per lane: d <= 16 * NPL
+template <int NPL, int VW>  // columns per lane: d <= 16 * NPL * VW
 __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
     float* __restrict__ rstd_out) {
   const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
   if (row >= rows) return;
-  (void)ln_row<NPL>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
+  (void)ln_row<NPL, VW>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
 }
 
 // The same rows plus the per-pass max|y| (the int8 activation scale of the BitLinear that
@@ -100,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
 // one-wave launch reduces them (no same-address atomics: 1024 of those cost 10 us here).
 // Max is order-independent: deterministic.
 constexpr int kAmaxMaxPasses = 8;
-template <int NPL>
+template <int NPL, int VW>
 __global__ __launch_bounds__(kThreads) void ln_fwd_amax_kernel(
     const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
@@ -112,7 +143,7 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_amax_kernel(
        r0 += (int64_t)gridDim.x * kRowsPerBlock) {
     const int64_t row = r0 + (threadIdx.x / kLanesPerRow);
     if (row < rows) {
-      float m = ln_row<NPL>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
+      float m = ln_row<NPL, VW>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
       if ((threadIdx.x & (kLanesPerRow - 1)) == 0)
@@ -160,24 +191,28 @@ struct GScale {
 };
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * gamma
-template <int NPL>
+template <int NPL, int VW>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows, int d,
     int rows_per_block, const float* __restrict__ dres, float* __restrict__ dx,
     float* __restrict__ part_g, float* __restrict__ part_b, GScale gs) {
-  __shared__ float red_g[kRowsPerBlock][kLanesPerRow * NPL];
-  __shared__ float red_b[kRowsPerBlock][kLanesPerRow * NPL];
+  __shared__ float red_g[kRowsPerBlock][kLanesPerRow * NPL * VW];
+  __shared__ float red_b[kRowsPerBlock][kLanesPerRow * NPL * VW];
   const int j = threadIdx.x & (kLanesPerRow - 1);
   const int sub = threadIdx.x / kLanesPerRow;
   const float inv_d = 1.0f / (float)d;
-  float gam[NPL], acc_g[NPL], acc_b[NPL];
+  float gam[NPL][VW], acc_g[NPL][VW], acc_b[NPL][VW];
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
-    const int c = j + kLanesPerRow * i;
-    gam[i] = (gamma && c < d) ? gamma[c] : (c < d ? 1.0f : 0.0f);
-    acc_g[i] = 0.0f;
-    acc_b[i] = 0.0f;
+    const int c0 = VW * (j + kLanesPerRow * i);
+    if (gamma) load_cols<VW>(gamma, c0, d, gam[i]);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      if (!gamma) gam[i][e] = c0 + e < d ? 1.0f : 0.0f;
+      acc_g[i][e] = 0.0f;
+      acc_b[i][e] = 0.0f;
+    }
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
@@ -186,27 +221,28 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const float mu = mean_in[row], rs = rstd_in[row];
     const float* xr = x + row * d;
     const float* gr = dy + row * d;
-    float xh[NPL], g[NPL], res[NPL];
+    float xh[NPL][VW], g[NPL][VW], res[NPL][VW];
     float s1 = 0.0f, s2 = 0.0f;
     const float* rr = dres ? dres + row * d : nullptr;
     if (rr) {  // issued with x / dy, not after the row reductions (one latency, not two)
 #pragma unroll
-      for (int i = 0; i < NPL; ++i) {
-        const int c = j + kLanesPerRow * i;
-        res[i] = c < d ? rr[c] : 0.0f;
-      }
+      for (int i = 0; i < NPL; ++i) load_cols<VW>(rr, VW * (j + kLanesPerRow * i), d, res[i]);
     }
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
-      const int c = j + kLanesPerRow * i;
-      const float xv = c < d ? xr[c] : 0.0f;
-      const float dv = c < d ? gr[c] : 0.0f;
-      xh[i] = (xv - mu) * rs;
-      acc_g[i] = fmaf(dv, xh[i], acc_g[i]);
-      acc_b[i] += dv;
-      g[i] = dv * gam[i];
-      s1 += g[i];
-      s2 = fmaf(g[i], xh[i], s2);
+      const int c0 = VW * (j + kLanesPerRow * i);
+      float xv[VW], dv[VW];
+      load_cols<VW>(xr, c0, d, xv);
+      load_cols<VW>(gr, c0, d, dv);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        xh[i][e] = (xv[e] - mu) * rs;
+        acc_g[i][e] = fmaf(dv[e], xh[i][e], acc_g[i][e]);
+        acc_b[i][e] += dv[e];
+        g[i][e] = dv[e] * gam[i][e];
+        s1 += g[i][e];
+        s2 = fmaf(g[i][e], xh[i][e], s2);
+      }
     }
     const float m1 = row_sum16(s1) * inv_d;
     const float m2 = row_sum16(s2) * inv_d;
@@ -218,30 +254,36 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     }
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
-      const int c = j + kLanesPerRow * i;
-      if (c < d) {
-        // explicit roundings: identical with and without dres (hipcc may contract the two
-        // loop versions differently otherwise)
-        const float v = nc_mul(rs, nc_sub(nc_sub(g[i], m1), nc_mul(xh[i], m2)));
-        // + the residual branch's gradient (the add autograd would do), not contracted
-        const float o = rr ? nc_add(v, res[i]) : v;
-        dr[c] = o;
-        if (gs.dy2) {  // the same operation sequence as drop_scale_bwd_kernel
-          float w = o;
+      const int c0 = VW * (j + kLanesPerRow * i);
+      if (c0 < d) {
+        float o[VW], w2[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) {
+          // explicit roundings: identical with and without dres (hipcc may contract the
+          // two loop versions differently otherwise)
+          const float v = nc_mul(rs, nc_sub(nc_sub(g[i][e], m1), nc_mul(xh[i][e], m2)));
+          // + the residual branch's gradient (the add autograd would do), not contracted
+          o[e] = rr ? nc_add(v, res[i][e]) : v;
+          // the same operation sequence as drop_scale_bwd_kernel
+          float w = o[e];
           if (gs.dc.on)
-            w = nc_mul(w, drop_hash(dkey, (uint64_t)(row * d + c)) >= gs.dc.thresh ? gs.dc.scale : 0.0f);
+            w = nc_mul(w, drop_hash(dkey, (uint64_t)(row * d + c0 + e)) >= gs.dc.thresh ? gs.dc.scale : 0.0f);
           if (!rvalid) w = nc_mul(w, 0.0f);
-          gs.dy2[row * d + c] = gs.rscale == 1.0f ? w : nc_mul(gs.rscale, w);
+          w2[e] = gs.rscale == 1.0f ? w : nc_mul(gs.rscale, w);
         }
+        store_cols<VW>(dr, c0, o);
+        if (gs.dy2) store_cols<VW>(gs.dy2 + row * d, c0, w2);
       }
     }
   }
   if (!part_g) return;
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    red_g[sub][j + kLanesPerRow * i] = acc_g[i];
-    red_b[sub][j + kLanesPerRow * i] = acc_b[i];
-  }
+  for (int i = 0; i < NPL; ++i)
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      red_g[sub][VW * (j + kLanesPerRow * i) + e] = acc_g[i][e];
+      red_b[sub][VW * (j + kLanesPerRow * i) + e] = acc_b[i][e];
+    }
   __syncthreads();
   for (int c = threadIdx.x; c < d; c += kThreads) {
     float sg = 0.0f, sb = 0.0f;
@@ -325,18 +367,34 @@ size_t layernorm_bwd_workspace(int64_t rows, int64_t d) {
 #define OB_LN_NPL(MACRO) \
   if (npl <= 4) MACRO(4) else if (npl <= 9) MACRO(9) else if (npl <= 16) MACRO(16) \
   else MACRO(32)
+// 4-column slots (d % 4 == 0, 16-byte aligned operands): d <= 64 * NPL
+#define OB_LN_NPL4(MACRO) \
+  if (npl4 <= 1) MACRO(1) else if (npl4 <= 2) MACRO(2) else if (npl4 <= 3) MACRO(3) \
+  else if (npl4 <= 4) MACRO(4) else MACRO(8)
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                           int64_t d, float eps, float* y, float* mean, float* rstd,
                           hipStream_t s) {
   if (rows == 0) return;
   const int npl = (int)ceil_div(d, kLanesPerRow);
+  const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
   const dim3 grid((unsigned)ceil_div(rows, kRowsPerBlock));
+  const bool vec = d % 4 == 0 && al16(x) && al16(y) && al16(gamma) && al16(beta);
 #define OB_LNF(N)                                                                             \
-  hipLaunchKernelGGL((ln_fwd_kernel<N>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
+  hipLaunchKernelGGL((ln_fwd_kernel<N, 1>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
                      (int)d, eps, y, mean, rstd);
-  OB_LN_NPL(OB_LNF)
+#define OB_LNF4(N)                                                                            \
+  hipLaunchKernelGGL((ln_fwd_kernel<N, 4>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
+                     (int)d, eps, y, mean, rstd);
+  if (vec) {
+    OB_LN_NPL4(OB_LNF4)
+  } else {
+    OB_LN_NPL(OB_LNF)
+  }
 #undef OB_LNF
+#undef OB_LNF4
 }
 
 size_t layernorm_fwd_amax_workspace(int64_t P) {
@@ -355,11 +413,22 @@ void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* 
   if (nb > kAmaxBlocks) nb = kAmaxBlocks;
   const int64_t rpp = rows / P;
   uint32_t* part = static_cast<uint32_t*>(ws);
-#define OB_LNFA(N)                                                                           \
-  hipLaunchKernelGGL((ln_fwd_amax_kernel<N>), dim3((unsigned)nb), dim3(kThreads), 0, s, x,    \
+  // (the same column slots as launch_layernorm_fwd: y bit-identical to the plain forward)
+  const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
+  const bool vec = d % 4 == 0 && al16(x) && al16(y) && al16(gamma) && al16(beta);
+#define OB_LNFA(N)                                                                              \
+  hipLaunchKernelGGL((ln_fwd_amax_kernel<N, 1>), dim3((unsigned)nb), dim3(kThreads), 0, s, x,    \
                      gamma, beta, rows, (int)d, eps, y, mean, rstd, rpp, P, part);
-  OB_LN_NPL(OB_LNFA)
+#define OB_LNFA4(N)                                                                             \
+  hipLaunchKernelGGL((ln_fwd_amax_kernel<N, 4>), dim3((unsigned)nb), dim3(kThreads), 0, s, x,    \
+                     gamma, beta, rows, (int)d, eps, y, mean, rstd, rpp, P, part);
+  if (vec) {
+    OB_LN_NPL4(OB_LNFA4)
+  } else {
+    OB_LN_NPL(OB_LNFA)
+  }
 #undef OB_LNFA
+#undef OB_LNFA4
   hipLaunchKernelGGL(ln_amax_final_kernel, dim3((unsigned)P), dim3(kThreads), 0, s,
                      (const uint32_t*)part, (int)nb, reinterpret_cast<uint32_t*>(amax));
 }
@@ -384,14 +453,25 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
   const int nb = rows > 0 ? bwd_blocks(rows, &rpb) : 0;
   float* part_b = part_g + (size_t)nb * d;
   const bool params = dgamma || dbeta;
+  const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
+  const bool vec = d % 4 == 0 && al16(dy) && al16(x) && al16(gamma) && al16(dres) && al16(dx) &&
+                   al16(gs.dy2);
   if (rows > 0) {
-#define OB_LNB(N)                                                                           \
-  hipLaunchKernelGGL((ln_bwd_kernel<N>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
-                     gamma, mean, rstd, rows, (int)d, rpb, dres, dx,                        \
-                     params ? part_g : nullptr,                                             \
-                     part_b, gs);
-    OB_LN_NPL(OB_LNB)
+#define OB_LNB(N)                                                                              \
+  hipLaunchKernelGGL((ln_bwd_kernel<N, 1>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
+                     gamma, mean, rstd, rows, (int)d, rpb, dres, dx,                           \
+                     params ? part_g : nullptr, part_b, gs);
+#define OB_LNB4(N)                                                                             \
+  hipLaunchKernelGGL((ln_bwd_kernel<N, 4>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
+                     gamma, mean, rstd, rows, (int)d, rpb, dres, dx,                           \
+                     params ? part_g : nullptr, part_b, gs);
+    if (vec) {
+      OB_LN_NPL4(OB_LNB4)
+    } else {
+      OB_LN_NPL(OB_LNB)
+    }
 #undef OB_LNB
+#undef OB_LNB4
   }
   if (params)
     hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, kRedCols)), dim3(kThreads), 0,

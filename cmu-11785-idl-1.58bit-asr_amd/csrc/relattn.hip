@@ -628,11 +628,22 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   // dS' rows of this tile to global for the key-side kernel (row-contiguous copy of the
   // LDS image: wave w copies rows 16w .. 16w+15, 64 consecutive columns per instruction)
   float* dsb = dsg + ((size_t)b * H + h) * T * T;
+  // (4 consecutive floats per lane: one unaligned dwordx4 store, 16 per wave and row
+  // quarter instead of 64 dword stores)
   for (int rr = 0; rr < 16; ++rr) {
     const int qrow = i0 + 16 * w + rr;
     if (qrow >= T) break;
     const float* src = ds + (1 + 16 * w + rr) * ldx;
-    for (int jj = lane; jj < T; jj += 64) if (!RB_EXP_NODSG) dsb[(size_t)qrow * T + jj] = src[jj];
+    float* dst = dsb + (size_t)qrow * T;
+    for (int j4 = 4 * lane; j4 < T; j4 += 256) {
+      if (RB_EXP_NODSG) break;
+      if (j4 + 3 < T) {
+        const f32x4 v4 = {src[j4], src[j4 + 1], src[j4 + 2], src[j4 + 3]};
+        *(f32x4u*)(dst + j4) = v4;
+      } else {
+        for (int e = j4; e < T; ++e) dst[e] = src[e];
+      }
+    }
   }
 }
 

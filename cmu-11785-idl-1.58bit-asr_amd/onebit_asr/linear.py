@@ -13,8 +13,15 @@ library GEMMs (hipBLASLt / rocBLAS), and the bias gradient is the fixed-order co
 
 ``dtype`` (optional) computes the GEMMs in that type (BASELINE configs[3]: bf16
 ``nn.Linear``); inputs, outputs and gradients stay fp32.
+
+fp32 forward (and dX) GEMMs whose shape csrc/dgemm.hip takes (K, N multiples of 4, the
+split weight image within LDS) run there: exact-fp32 products on the bf16 matrix cores
+(six MFMAs per k-step), bias in the epilogue. At Conformer-S the CTC head's forward
+([23904 x 144] x [144 x 5004]) is the large one. OB_DENSE_LINEAR=0: library GEMMs only.
 """
 from __future__ import annotations
+
+import os
 
 from typing import Optional
 
@@ -24,6 +31,23 @@ import torch.nn.functional as F
 from . import _lib
 
 __all__ = ["linear", "colsum"]
+
+_DENSE = os.environ.get("OB_DENSE_LINEAR", "1") != "0"
+
+
+def _dense_ok(x: torch.Tensor, k: int, n: int) -> bool:
+    return (_DENSE and k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
+            and _lib.load().ob_dense_supported(k, n) == 1)
+
+
+def _dense(x2d: torch.Tensor, w: torch.Tensor, trans: int, bias, n: int) -> torch.Tensor:
+    """x2d [M, K] . (w^T if trans == 0 else w) (+ bias) on csrc/dgemm.hip."""
+    m, k = x2d.shape
+    y = torch.empty((m, n), dtype=torch.float32, device=x2d.device)
+    _lib.check(_lib.load().ob_dense_gemm(x2d.data_ptr(), m, k, w.data_ptr(), trans,
+                                         _lib.ptr(bias), n, y.data_ptr(), _lib.stream_of(x2d)),
+               "ob_dense_gemm")
+    return y
 
 
 def colsum(x2d: torch.Tensor) -> torch.Tensor:
@@ -44,7 +68,10 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, dtype):
         k = x.shape[-1]
         x2d = x.reshape(-1, k)
-        if dtype is None:
+        n = weight.shape[0]
+        if dtype is None and x2d.is_contiguous() and weight.is_contiguous() and _dense_ok(x2d, k, n):
+            y = _dense(x2d, weight, 0, bias, n)
+        elif dtype is None:
             y = torch.addmm(bias, x2d, weight.t()) if bias is not None else x2d @ weight.t()
         else:
             wd = weight.to(dtype)
@@ -65,7 +92,11 @@ class _LinearFn(torch.autograd.Function):
         gx = gw = gb = None
         if dtype is None:
             if ctx.needs_input_grad[0]:
-                gx = (g2 @ weight).view(xshape)
+                k = weight.shape[1]
+                if weight.is_contiguous() and _dense_ok(g2, weight.shape[0], k):
+                    gx = _dense(g2, weight, 1, None, k).view(xshape)
+                else:
+                    gx = (g2 @ weight).view(xshape)
             if ctx.needs_input_grad[1]:
                 gw = g2.t() @ x2d
         else:

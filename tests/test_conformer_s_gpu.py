@@ -8,7 +8,8 @@ configs[1] -- the measured training step, dropout 0:
   * the stacked step == the reference's literal three forwards (train.py:82-111): loss rel
     <= 1e-5, parts rtol 1e-5, every parameter gradient rel-L2 <= 1e-4 (parameters whose true
     gradient is zero -- the depthwise bias before BatchNorm, the key biases under softmax
-    shift invariance -- within 1e-7 absolute instead; alpha gradients, single
+    shift invariance -- within 5e-7 absolute instead; pos_bias_u/v rel-L2 <= 5e-4; alpha
+    gradients, single
     cancellation-prone sums over N*K, within max(2e-3 relative, 1e-3 x the model's median
     alpha gradient));
   * the literal step replays too (it used to be refused by GraphedTrainStep).
@@ -99,6 +100,10 @@ def test_s_literal_matches_stacked_and_replays(s_model, gpu, stacked_ref):
         elif k.endswith(".alpha"):
             d = abs(g_l[k].item() - g_s[k].item())
             assert d <= max(2e-3 * abs(g_s[k].item()), 1e-3 * med), (k, g_l[k], g_s[k], med)
+        elif k.endswith(("pos_bias_u", "pos_bias_v")):
+            # like alpha: one column sum over all 23904 query rows of dQ (csrc/relattn.hip
+            # bias reduce), summed in a different order in the two layouts (seen 1.3e-4)
+            assert e <= 5e-4, (k, e)
         else:
             assert e <= 1e-4, (k, e)
 

@@ -148,3 +148,31 @@ def test_pointwise_fn_hip_vs_blas(gpu, monkeypatch):
     for a, r in zip(outs["hip"], outs["blas"]):
         rel = float((a.double() - r.double()).norm() / r.double().norm())
         assert rel <= 1e-6, rel
+
+
+@pytest.mark.parametrize("m,k,n", [(2000, 144, 5004), (600, 256, 1024), (600, 1024, 256),
+                                   (333, 256, 5004)])
+def test_linear_dense_path_matches_float64(gpu, m, k, n):
+    """onebit_asr.linear.linear (the full-precision linears: CTC head, decoder, subsampling
+    out) forward and dX on csrc/dgemm.hip when the shape is taken, vs float64 F.linear:
+    max|err| <= 1e-5 * max|ref|; dW / db as before (library GEMM, fixed-order colsum)."""
+    from onebit_asr import _lib
+    from onebit_asr.linear import linear
+
+    g = torch.Generator().manual_seed(m + k + n)
+    x = torch.randn(m, k, generator=g)
+    w = torch.randn(n, k, generator=g) * 0.05
+    b = torch.randn(n, generator=g)
+    gy = torch.randn(m, n, generator=g)
+    xd, wd, bd = (t.to(gpu).requires_grad_() for t in (x, w, b))
+    y = linear(xd, wd, bd)
+    y.backward(gy.to(gpu))
+    xr, wr, br = (t.double().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(gy.double())
+    for got, ref in ((y.detach(), yr.detach()), (xd.grad, xr.grad), (wd.grad, wr.grad),
+                     (bd.grad, br.grad)):
+        err = (got.double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item(), err
+    lib = _lib.load()
+    assert lib.ob_dense_supported(k, n) == 1  # the forward took the HIP kernel
