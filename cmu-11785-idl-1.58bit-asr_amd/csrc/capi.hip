@@ -733,6 +733,52 @@ int ob_ctc_loss_bwd_groups(const float* log_probs, const int64_t* targets,
   return launched();
 }
 
+size_t ob_ctc_logits_workspace(int64_t B, int64_t T, int64_t S) {
+  if (B < 0 || T < 0 || S < 0) return 0;
+  return align_up(ctc_logits_workspace_bytes(B, T, S));
+}
+
+namespace {
+int ctc_logits_check(const float* x, const int64_t* targets, const int64_t* input_lengths,
+                     const int64_t* target_lengths, int64_t G, int64_t B, int64_t T, int64_t V,
+                     int64_t S, int blank, const void* out, void* ws, size_t ws_bytes) {
+  if (G < 1 || G > 64 || B < 1 || B % G || T < 0 || V < 1 || V > INT32_MAX || S < 0 ||
+      blank < 0 || blank >= V || !ctc_supported(S) || B * T > INT32_MAX)
+    return OB_ERR_SHAPE;
+  if (!x || !input_lengths || !target_lengths || !out || !ws || (S > 0 && !targets))
+    return OB_ERR_NULL;
+  if (ws_bytes < ob_ctc_logits_workspace(B, T, S)) return OB_ERR_WORKSPACE;
+  if ((V & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15)) return OB_ERR_ALIGN;
+  return OB_OK;
+}
+}  // namespace
+
+int ob_ctc_loss_logits_fwd_groups(const float* logits, const int64_t* targets,
+                                  const int64_t* input_lengths, const int64_t* target_lengths,
+                                  int64_t G, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                                  float* loss, void* ws, size_t ws_bytes, void* stream) {
+  if (int st = ctc_logits_check(logits, targets, input_lengths, target_lengths, G, B, T, V, S,
+                                blank, loss, ws, ws_bytes))
+    return st;
+  launch_ctc_logits_fwd(logits, targets, input_lengths, target_lengths, B, T, V, S, blank, G,
+                        loss, ws, as_stream(stream));
+  return launched();
+}
+
+int ob_ctc_loss_logits_bwd_groups(const float* logits, const int64_t* targets,
+                                  const int64_t* input_lengths, const int64_t* target_lengths,
+                                  int64_t G, int64_t B, int64_t T, int64_t V, int64_t S, int blank,
+                                  const float* grad_out, float* grad, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  if (int st = ctc_logits_check(logits, targets, input_lengths, target_lengths, G, B, T, V, S,
+                                blank, grad, ws, ws_bytes))
+    return st;
+  if ((V & 3) == 0 && (reinterpret_cast<uintptr_t>(grad) & 15)) return OB_ERR_ALIGN;
+  launch_ctc_logits_bwd(logits, targets, input_lengths, target_lengths, B, T, V, S, blank, G,
+                        grad_out, grad, ws, as_stream(stream));
+  return launched();
+}
+
 int ob_ctc_greedy_decode(const float* logits, const int64_t* lens, int64_t B, int64_t T,
                          int64_t V, int blank, int32_t* ids, int32_t* out, int32_t* out_len,
                          void* stream) {

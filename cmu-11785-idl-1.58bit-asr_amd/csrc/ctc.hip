@@ -42,12 +42,11 @@ __device__ __forceinline__ int64_t ext_label(const int64_t* tg, int s, int blank
 }
 
 // alpha[b][t][s] for t < T_b (log space); nll[b] = -log p(l | x).
-__global__ __launch_bounds__(kThreads) void ctc_alpha_kernel(
+__device__ __forceinline__ void ctc_alpha_body(
     const float* __restrict__ lp, const int64_t* __restrict__ targets,
     const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len, int T, int V, int S,
-    int blank, float* __restrict__ alpha, float* __restrict__ nll) {
+    int blank, float* __restrict__ alpha, float* __restrict__ nll, int b) {
   __shared__ float buf[2][kMaxStates + 2];
-  const int b = blockIdx.x;
   const int Tb = (int)min<int64_t>(in_len[b], T);
   const int L = (int)tg_len[b];
   const int NS = 2 * L + 1;
@@ -55,13 +54,21 @@ __global__ __launch_bounds__(kThreads) void ctc_alpha_kernel(
   const float* lpb = lp + (int64_t)b * T * V;
   float* ab = alpha + (int64_t)b * T * (2 * S + 1);
   const int SS = 2 * S + 1;
+  // NS <= kThreads (the common case): each thread owns one state and loads its next step's
+  // log-prob while the current step computes (the load is off the recursion's chain)
+  const bool one = NS <= kThreads;
+  const int s1 = threadIdx.x;
+  const int64_t lab1 = s1 < NS ? ext_label(tg, s1, blank) : 0;
+  float l_next = (one && s1 < NS && Tb > 0) ? lpb[lab1] : 0.0f;
   for (int t = 0; t < Tb; ++t) {
     const float* row = lpb + (int64_t)t * V;
     float* cur = buf[t & 1];
     const float* prev = buf[(t & 1) ^ 1];
+    const float l_cur = l_next;
+    if (one && s1 < NS && t + 1 < Tb) l_next = row[V + lab1];
     for (int s = threadIdx.x; s < NS; s += kThreads) {
       const int64_t lab = ext_label(tg, s, blank);
-      const float l = row[lab];
+      const float l = one ? l_cur : row[lab];
       float a;
       if (t == 0) {
         a = (s <= 1) ? l : -INFINITY;
@@ -87,13 +94,19 @@ __global__ __launch_bounds__(kThreads) void ctc_alpha_kernel(
   }
 }
 
-// beta[b][t][s] for t < T_b (log space, includes lp[t] like alpha).
-__global__ __launch_bounds__(kThreads) void ctc_beta_kernel(
+__global__ __launch_bounds__(kThreads) void ctc_alpha_kernel(
     const float* __restrict__ lp, const int64_t* __restrict__ targets,
     const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len, int T, int V, int S,
-    int blank, float* __restrict__ beta) {
+    int blank, float* __restrict__ alpha, float* __restrict__ nll) {
+  ctc_alpha_body(lp, targets, in_len, tg_len, T, V, S, blank, alpha, nll, blockIdx.x);
+}
+
+// beta[b][t][s] for t < T_b (log space, includes lp[t] like alpha).
+__device__ __forceinline__ void ctc_beta_body(
+    const float* __restrict__ lp, const int64_t* __restrict__ targets,
+    const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len, int T, int V, int S,
+    int blank, float* __restrict__ beta, int b) {
   __shared__ float buf[2][kMaxStates + 2];
-  const int b = blockIdx.x;
   const int Tb = (int)min<int64_t>(in_len[b], T);
   const int L = (int)tg_len[b];
   const int NS = 2 * L + 1;
@@ -101,13 +114,19 @@ __global__ __launch_bounds__(kThreads) void ctc_beta_kernel(
   const float* lpb = lp + (int64_t)b * T * V;
   const int SS = 2 * S + 1;
   float* bb = beta + (int64_t)b * T * SS;
+  const bool one = NS <= kThreads;  // (as in the alpha kernel: next step's log-prob prefetched)
+  const int s1 = threadIdx.x;
+  const int64_t lab1 = s1 < NS ? ext_label(tg, s1, blank) : 0;
+  float l_next = (one && s1 < NS && Tb > 0) ? lpb[(int64_t)(Tb - 1) * V + lab1] : 0.0f;
   for (int t = Tb - 1; t >= 0; --t) {
     const float* row = lpb + (int64_t)t * V;
     float* cur = buf[t & 1];
     const float* nxt = buf[(t & 1) ^ 1];
+    const float l_cur = l_next;
+    if (one && s1 < NS && t > 0) l_next = row[lab1 - V];
     for (int s = threadIdx.x; s < NS; s += kThreads) {
       const int64_t lab = ext_label(tg, s, blank);
-      const float l = row[lab];
+      const float l = one ? l_cur : row[lab];
       float v;
       if (t == Tb - 1) {
         v = (s >= NS - 2) ? l : -INFINITY;
@@ -123,6 +142,25 @@ __global__ __launch_bounds__(kThreads) void ctc_beta_kernel(
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(kThreads) void ctc_beta_kernel(
+    const float* __restrict__ lp, const int64_t* __restrict__ targets,
+    const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len, int T, int V, int S,
+    int blank, float* __restrict__ beta) {
+  ctc_beta_body(lp, targets, in_len, tg_len, T, V, S, blank, beta, blockIdx.x);
+}
+
+// Both recursions in one launch (blocks 0..B-1 alpha, B..2B-1 beta): each is a chain of T
+// dependent steps on one block, so running them side by side halves the sequential time.
+__global__ __launch_bounds__(kThreads) void ctc_alpha_beta_kernel(
+    const float* __restrict__ lp, const int64_t* __restrict__ targets,
+    const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len, int B, int T, int V,
+    int S, int blank, float* __restrict__ alpha, float* __restrict__ nll, float* __restrict__ beta) {
+  if ((int)blockIdx.x < B)
+    ctc_alpha_body(lp, targets, in_len, tg_len, T, V, S, blank, alpha, nll, blockIdx.x);
+  else
+    ctc_beta_body(lp, targets, in_len, tg_len, T, V, S, blank, beta, blockIdx.x - B);
 }
 
 // Per-sample loss and gradient scale: 'mean' = mean_b(nll_b / max(L_b, 1)); zero_infinity.
@@ -192,6 +230,169 @@ __global__ __launch_bounds__(kThreads) void ctc_grad_fixup_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// CTC straight from the CTC head's logits (losses.py:41-47: log_softmax, then the CTC):
+// the recursion only reads log-probabilities at blank and at the utterance's labels, so
+// the [B*T][V] log_softmax tensor (478 MB at Conformer-S, V = 5004) is never formed.
+//   lse pass (one block per frame): m = max_v x, logs = log(sum_v exp(x - m)) (torch's
+//     LogSoftMax: lp = (x - m) - logs) and the compact log-probs
+//     lpc[frame][0] = lp[blank], lpc[frame][1 + u] = lp[target_u]; the t == 0 block of
+//     each utterance also writes its compact labels tgc[u] = 1 + (first u' with
+//     target_u' == target_u) (0 for a target equal to blank), so equal tokens keep equal
+//     labels for the recursion's skip rule.
+//   alpha / beta / reduce: the recursions above on lpc (V' = S + 1, blank' = 0, labels
+//     tgc), alpha and beta side by side in the forward's launch.
+//   gradient (one block per frame): dL/dx_v = scale * (softmax_v - gamma_v), written
+//     densely as scale * softmax_v, then the label columns overwritten with torch's own
+//     formula (exp(l) - exp(lcab + nll - l)) * scale. torch composes its log-prob gradient
+//     with the log_softmax backward g - softmax * sum(g); sum(g) = scale * (1 - sum gamma)
+//     is 0 up to rounding, the only difference.
+// ------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float block_reduce(float v, bool is_max, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float w = __shfl_xor(v, o);
+    v = is_max ? fmaxf(v, w) : v + w;
+  }
+  __syncthreads();  // red reused across calls
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < kThreads / 64; ++w) r = is_max ? fmaxf(r, red[w]) : r + red[w];
+  return r;
+}
+
+__global__ __launch_bounds__(kThreads) void ctc_lse_gather_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ targets,
+    const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len, int T, int V, int S,
+    int blank, float* __restrict__ mls, float* __restrict__ lpc, int64_t* __restrict__ tgc,
+    int* __restrict__ occ) {
+  __shared__ float red[kThreads / 64];
+  __shared__ int lab_s[kMaxStates];
+  const int64_t rowid = blockIdx.x;  // b * T + t
+  const int b = (int)(rowid / T), t = (int)(rowid % T);
+  const int64_t* tg = targets + (int64_t)b * S;
+  if (t == 0) {
+    // compact labels of utterance b, and per extended-label state s (frame-independent):
+    // occ[s] = the next state with the same compact label (-1: none), occ[SS + s] = 1 when s
+    // is the first state of its label; the gradient's label fix-up walks these chains
+    const int L = (int)tg_len[b];
+    const int NS = 2 * L + 1;
+    for (int u = threadIdx.x; u < S; u += kThreads) {
+      int c = 0;
+      if (u < L && tg[u] != blank) {
+        int f = u;
+        for (int q = 0; q < u; ++q)
+          if (tg[q] == tg[u]) { f = q; break; }
+        c = 1 + f;
+      }
+      tgc[(int64_t)b * S + u] = c;
+      if (u < L) lab_s[2 * u + 1] = c;
+    }
+    for (int st = 2 * threadIdx.x; st < NS; st += 2 * kThreads) lab_s[st] = 0;
+    __syncthreads();
+    int* ob = occ + (int64_t)b * 2 * (2 * S + 1);
+    for (int st = threadIdx.x; st < NS; st += kThreads) {
+      const int lab = lab_s[st];
+      bool first = true;
+      for (int q = 0; q < st; ++q)
+        if (lab_s[q] == lab) { first = false; break; }
+      int nx = -1;
+      for (int q = st + 1; q < NS; ++q)
+        if (lab_s[q] == lab) { nx = q; break; }
+      ob[st] = nx;
+      ob[2 * S + 1 + st] = first ? 1 : 0;
+    }
+  }
+  if (t >= in_len[b]) return;
+  const float* row = x + rowid * V;
+  const bool vec = (V & 3) == 0;
+  float m = -INFINITY;
+  if (vec) {
+    for (int q = threadIdx.x; q < V / 4; q += kThreads) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(row)[q];
+      m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += kThreads) m = fmaxf(m, row[v]);
+  }
+  m = block_reduce(m, true, red);
+  float sum = 0.0f;
+  if (vec) {
+    for (int q = threadIdx.x; q < V / 4; q += kThreads) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(row)[q];
+      sum += ((expf(v[0] - m) + expf(v[1] - m)) + expf(v[2] - m)) + expf(v[3] - m);
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += kThreads) sum += expf(row[v] - m);
+  }
+  sum = block_reduce(sum, false, red);
+  const float logs = logf(sum);
+  if (threadIdx.x == 0) {
+    mls[2 * rowid] = m;
+    mls[2 * rowid + 1] = logs;
+  }
+  for (int c = threadIdx.x; c <= S; c += kThreads) {
+    int64_t lab = c == 0 ? blank : tg[c - 1];
+    lab = lab < 0 ? 0 : (lab >= V ? V - 1 : lab);  // padded target slots: any valid column
+    lpc[rowid * (S + 1) + c] = (row[lab] - m) - logs;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void ctc_logits_grad_kernel(
+    const float* __restrict__ x, const float* __restrict__ mls, const float* __restrict__ lpc,
+    const int64_t* __restrict__ targets, const int64_t* __restrict__ tgc,
+    const int64_t* __restrict__ in_len, const int64_t* __restrict__ tg_len,
+    const float* __restrict__ alpha, const float* __restrict__ beta, const float* __restrict__ nll,
+    const float* __restrict__ scale, const int* __restrict__ occ, int T, int V, int S, int blank,
+    float* __restrict__ grad) {
+  const int64_t rowid = blockIdx.x;
+  const int b = (int)(rowid / T), t = (int)(rowid % T);
+  const bool live = t < in_len[b] && scale[b] != 0.0f;
+  const float* row = x + rowid * V;
+  float* g = grad + rowid * V;
+  const bool vec = (V & 3) == 0;
+  const float sc = live ? scale[b] : 0.0f;
+  const float m = live ? mls[2 * rowid] : 0.0f, logs = live ? mls[2 * rowid + 1] : 0.0f;
+  if (vec) {
+    for (int q = threadIdx.x; q < V / 4; q += kThreads) {
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+      if (live) {
+        const f32x4 v = reinterpret_cast<const f32x4*>(row)[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = expf((v[e] - m) - logs) * sc;
+      }
+      reinterpret_cast<f32x4*>(g)[q] = o;
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += kThreads)
+      g[v] = live ? expf((row[v] - m) - logs) * sc : 0.0f;
+  }
+  if (!live) return;
+  __syncthreads();  // the label columns below overwrite this block's dense values
+  const int L = (int)tg_len[b];
+  const int NS = 2 * L + 1;
+  const int SS = 2 * S + 1;
+  const int64_t* tgb = tgc + (int64_t)b * S;
+  const int* ob = occ + (int64_t)b * 2 * SS;
+  const float* a = alpha + rowid * SS;
+  const float* be = beta + rowid * SS;
+  const float n = nll[b];
+  for (int s = threadIdx.x; s < NS; s += kThreads) {
+    if (!ob[SS + s]) continue;  // not the first state of its label
+    const int64_t lab = ext_label(tgb, s, 0);  // compact label
+    // occurrences of the label in state order (lse2(-inf, x) == x: the chain's first step)
+    float acc = a[s] + be[s];
+    for (int q = ob[s]; q >= 0; q = ob[q]) acc = lse2(acc, a[q] + be[q]);
+    const float l = lpc[rowid * (S + 1) + lab];
+    const int64_t v = (s & 1) ? targets[(int64_t)b * S + (s >> 1)] : blank;  // vocabulary id
+    g[v] = (expf(l) - expf(acc + n - l)) * sc;
+  }
+}
+
 }  // namespace
 
 size_t ctc_workspace(int64_t B, int64_t T, int64_t S) {
@@ -229,6 +430,79 @@ void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_l
   hipLaunchKernelGGL(ctc_grad_fixup_kernel, dim3((unsigned)(B * T)), dim3(kThreads), 0, s, lp,
                      targets, in_len, tg_len, alpha, beta, nll, scale, (int)T, (int)V, (int)S,
                      blank, grad);
+}
+
+// logits path workspace: the CTC workspace, then lpc [B*T][S+1], mls [B*T][2], tgc [B][S]
+namespace {
+struct LogitsWs {
+  float* ctc;
+  float* lpc;
+  float* mls;
+  int64_t* tgc;
+  int* occ;
+};
+LogitsWs split_logits_ws(void* ws, int64_t B, int64_t T, int64_t S) {
+  LogitsWs w;
+  char* p = static_cast<char*>(ws);
+  w.ctc = reinterpret_cast<float*>(p);
+  p += (ctc_workspace(B, T, S) + 255) & ~size_t(255);
+  w.lpc = reinterpret_cast<float*>(p);
+  p += (sizeof(float) * (size_t)(B * T * (S + 1)) + 255) & ~size_t(255);
+  w.mls = reinterpret_cast<float*>(p);
+  p += (sizeof(float) * (size_t)(2 * B * T) + 255) & ~size_t(255);
+  w.tgc = reinterpret_cast<int64_t*>(p);
+  p += (sizeof(int64_t) * (size_t)(B * S + 8) + 255) & ~size_t(255);
+  w.occ = reinterpret_cast<int*>(p);
+  return w;
+}
+}  // namespace
+
+size_t ctc_logits_workspace_bytes(int64_t B, int64_t T, int64_t S) {
+  return ((ctc_workspace(B, T, S) + 255) & ~size_t(255)) +
+         ((sizeof(float) * (size_t)(B * T * (S + 1)) + 255) & ~size_t(255)) +
+         ((sizeof(float) * (size_t)(2 * B * T) + 255) & ~size_t(255)) +
+         ((sizeof(int64_t) * (size_t)(B * S + 8) + 255) & ~size_t(255)) +
+         sizeof(int) * (size_t)(2 * B * (2 * S + 1) + 8);
+}
+
+void launch_ctc_logits_fwd(const float* x, const int64_t* targets, const int64_t* in_len,
+                           const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S,
+                           int blank, int64_t G, float* loss, void* ws, hipStream_t s) {
+  const LogitsWs w = split_logits_ws(ws, B, T, S);
+  if (B * T > 0)
+    hipLaunchKernelGGL(ctc_lse_gather_kernel, dim3((unsigned)(B * T)), dim3(kThreads), 0, s, x,
+                       targets, in_len, tg_len, (int)T, (int)V, (int)S, blank, w.mls, w.lpc, w.tgc,
+                       w.occ);
+  // alpha and beta side by side (beta kept in the workspace for the backward)
+  const int64_t SS = 2 * S + 1;
+  float* alpha = w.ctc;
+  float* beta = w.ctc + B * T * SS;
+  float* nll = w.ctc + 2 * B * T * SS;
+  hipLaunchKernelGGL(ctc_alpha_beta_kernel, dim3((unsigned)(2 * B)), dim3(kThreads), 0, s,
+                     (const float*)w.lpc, (const int64_t*)w.tgc, in_len, tg_len, (int)B, (int)T,
+                     (int)(S + 1), (int)S, 0, alpha, nll, beta);
+  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(64), 0, s, (const float*)nll, tg_len, (int)B,
+                     (int)G, (const float*)nullptr, loss, (float*)nullptr);
+}
+
+void launch_ctc_logits_bwd(const float* x, const int64_t* targets, const int64_t* in_len,
+                           const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S,
+                           int blank, int64_t G, const float* grad_out, float* grad, void* ws,
+                           hipStream_t s) {
+  const LogitsWs w = split_logits_ws(ws, B, T, S);
+  const int64_t SS = 2 * S + 1;
+  float* alpha = w.ctc;
+  float* beta = w.ctc + B * T * SS;
+  float* nll = w.ctc + 2 * B * T * SS;
+  float* scale = nll + B;
+  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(64), 0, s, (const float*)nll, tg_len, (int)B,
+                     (int)G, grad_out, (float*)nullptr, scale);
+  if (B * T > 0)
+    hipLaunchKernelGGL(ctc_logits_grad_kernel, dim3((unsigned)(B * T)), dim3(kThreads), 0, s, x,
+                       (const float*)w.mls, (const float*)w.lpc, targets, (const int64_t*)w.tgc,
+                       in_len, tg_len, (const float*)alpha, (const float*)beta, (const float*)nll,
+                       (const float*)scale, (const int*)w.occ, (int)T, (int)V, (int)S, blank,
+                       grad);
 }
 
 }  // namespace ob

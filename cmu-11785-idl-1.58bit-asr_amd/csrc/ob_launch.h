@@ -225,6 +225,16 @@ void launch_ctc_fwd(const float* lp, const int64_t* targets, const int64_t* in_l
 void launch_ctc_bwd(const float* lp, const int64_t* targets, const int64_t* in_len,
                     const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S, int blank, int64_t G,
                     const float* grad_out, float* grad, float* ws, hipStream_t s);
+// CTC from the head's logits x [B][T][V] (no log_softmax tensor): forward = lse pass +
+// alpha + reduce; backward = beta + reduce + dense softmax gradient with label fix-up.
+size_t ctc_logits_workspace_bytes(int64_t B, int64_t T, int64_t S);
+void launch_ctc_logits_fwd(const float* x, const int64_t* targets, const int64_t* in_len,
+                           const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S,
+                           int blank, int64_t G, float* loss, void* ws, hipStream_t s);
+void launch_ctc_logits_bwd(const float* x, const int64_t* targets, const int64_t* in_len,
+                           const int64_t* tg_len, int64_t B, int64_t T, int64_t V, int64_t S,
+                           int blank, int64_t G, const float* grad_out, float* grad, void* ws,
+                           hipStream_t s);
 
 // adamw.hip (clip_grad_norm_ + AdamW over a tensor table; layout = ob_adamw_tensor)
 struct AdamwTensor {

@@ -77,6 +77,12 @@ SIGNATURES = {
     "ob_ctc_loss_bwd_groups": (
         _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _sz,
                _c_f]),
+    "ob_ctc_logits_workspace": (_sz, [_i64, _i64, _i64]),
+    "ob_ctc_loss_logits_fwd_groups": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _sz, _c_f]),
+    "ob_ctc_loss_logits_bwd_groups": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _sz,
+               _c_f]),
     "ob_quant_dequant": (_int, [_c_f, _c_f, _int, _int, _i64, _c_f, _c_f]),
     "ob_quant_ste_bwd_workspace": (_sz, [_i64]),
     "ob_quant_ste_bwd": (_int, [_c_f, _c_f, _c_f, _int, _int, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),

@@ -48,13 +48,14 @@ def att_ce_loss(logits: torch.Tensor, targets: torch.Tensor, pad_id: int,
 
 def ctc_loss_from_logits(ctc_logits: torch.Tensor, feat_lens: torch.Tensor,
                          tokens: torch.Tensor, token_lens: torch.Tensor, blank_id: int):
-    """On a ROCm device: the HIP CTC (same loss and gradient, lengths read on device, no host
-    sync); elsewhere torch's nn.CTCLoss on the [T,B,V] transpose as in the reference."""
-    log_probs = F.log_softmax(ctc_logits, dim=-1)  # [B,T,V]
-    if log_probs.is_cuda and log_probs.dtype == torch.float32 and tokens.dim() == 2:
-        from .ctc import ctc_loss_mean
+    """On a ROCm device: the HIP CTC straight from the logits (same loss and gradient as
+    log_softmax + CTC, lengths read on device, no host sync, no log_softmax tensor);
+    elsewhere torch's nn.CTCLoss on the [T,B,V] transpose as in the reference."""
+    if ctc_logits.is_cuda and ctc_logits.dtype == torch.float32 and tokens.dim() == 2:
+        from .ctc import ctc_loss_logits_groups
 
-        return ctc_loss_mean(log_probs, tokens, feat_lens, token_lens, blank_id)
+        return ctc_loss_logits_groups(ctc_logits, tokens, feat_lens, token_lens, blank_id, 1)[0]
+    log_probs = F.log_softmax(ctc_logits, dim=-1)  # [B,T,V]
     return nn.CTCLoss(blank=blank_id, zero_infinity=True)(log_probs.transpose(0, 1), tokens,
                                                          feat_lens, token_lens)
 

@@ -159,7 +159,7 @@ class OneBitStep(nn.Module):
 
 
     def _forward_stacked(self, batch, bits):
-        from .ctc import ctc_loss_mean_groups
+        from .ctc import ctc_loss_logits_groups
 
         from .fused import advance_step
         from .quant import PackGroup
@@ -191,12 +191,11 @@ class OneBitStep(nn.Module):
             l_att = torch.stack([
                 F.nll_loss(logp[p].transpose(1, 2), t_out, ignore_index=sp["pad_id"])
                 for p in range(P)])
-        # CTC per pass (losses.py:41-47)
-        ctc_lp = F.log_softmax(ctc, dim=-1)
+        # CTC per pass (losses.py:41-47: log_softmax + CTC), straight from the head's logits
         in_lens = mask.sum(dim=1).long()
         # the P passes' CTC losses in one launch per direction (each pass its own mean)
-        l_ctc = ctc_loss_mean_groups(ctc_lp, batch["tokens"].repeat(P, 1), in_lens,
-                                     batch["token_lens"].repeat(P), sp["blank_id"], P)
+        l_ctc = ctc_loss_logits_groups(ctc, batch["tokens"].repeat(P, 1), in_lens,
+                                       batch["token_lens"].repeat(P), sp["blank_id"], P)
         l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
         # KL(teacher || student) for the student and SP passes (losses.py:50-59)
         with torch.no_grad():  # softmax of the detached teacher logits (train.py:101)

@@ -196,6 +196,25 @@ OB_API int ob_ctc_loss_bwd_groups(const float* log_probs, const int64_t* targets
                                   int64_t G, int64_t B, int64_t T, int64_t V, int64_t S,
                                   int blank, const float* grad_out, float* grad, void* ws,
                                   size_t ws_bytes, void* stream);
+/* The same grouped CTC loss taken straight from the CTC head's logits [B][T][V]
+ * (losses.py:41-47 is log_softmax then the CTC): the log-probabilities are read only at
+ * blank and the utterance's labels, and the backward returns d loss / d logits
+ * (= scale * (softmax - occupancy), torch's log-prob gradient composed with the log_softmax
+ * backward up to its rounding-level sum term), so no [B*T][V] log_softmax or log-prob
+ * gradient tensor exists. ws: ob_ctc_logits_workspace(B, T, S) bytes, kept from fwd to bwd.
+ * logits / grad 16-byte aligned when V % 4 == 0. */
+OB_API size_t ob_ctc_logits_workspace(int64_t B, int64_t T, int64_t S);
+OB_API int ob_ctc_loss_logits_fwd_groups(const float* logits, const int64_t* targets,
+                                         const int64_t* input_lengths,
+                                         const int64_t* target_lengths, int64_t G, int64_t B,
+                                         int64_t T, int64_t V, int64_t S, int blank, float* loss,
+                                         void* ws, size_t ws_bytes, void* stream);
+OB_API int ob_ctc_loss_logits_bwd_groups(const float* logits, const int64_t* targets,
+                                         const int64_t* input_lengths,
+                                         const int64_t* target_lengths, int64_t G, int64_t B,
+                                         int64_t T, int64_t V, int64_t S, int blank,
+                                         const float* grad_out, float* grad, void* ws,
+                                         size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Stacked passes. The reference's training step runs every BitLinear three times per
