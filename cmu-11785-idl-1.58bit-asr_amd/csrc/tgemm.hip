@@ -195,7 +195,8 @@ __host__ __device__ inline size_t epi_stage_bytes(int nt) {
 // and C / C2 stored as dwordx4, so 16 lanes cover 256 contiguous bytes of the row.
 template <int MODE>
 __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, float* c,
-                                           int64_t grow, int col, int N, f32x4 y, bool valid) {
+                                           int64_t grow, int col, int N, f32x4 y, bool valid,
+                                           const f32x4& rv) {
   const int64_t i = grow * N + col;
   f32x4 keep = {1.f, 1.f, 1.f, 1.f};
   if (ep.dc.on && !TG_EXP_NODROP) {
@@ -214,7 +215,6 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
       out[e] = ep.dc.on ? nc_mul(sv, keep[e]) : sv;
     }
   } else if constexpr (MODE == kEpiResidual) {
-    const f32x4 rv = *reinterpret_cast<const f32x4*>(ep.R + i);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float v = ep.dc.on ? nc_mul(y[e], keep[e]) : y[e];
@@ -222,7 +222,6 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
       out[e] = nc_add(rv[e], ep.rscale == 1.0f ? v : nc_mul(ep.rscale, v));
     }
   } else {  // kEpiSwishDropBwd
-    const f32x4 rv = *reinterpret_cast<const f32x4*>(ep.R + i);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float dd = ep.dc.on ? nc_mul(y[e], keep[e]) : y[e];
@@ -419,8 +418,23 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       // loads and C / C2 stores; 16 lanes = 256 contiguous bytes). The wave's LDS ops run
       // in issue order; the waitcnt + sched barriers keep hipcc from reordering across them.
       float* stg = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad)) + wave * 16 * kEpiLd;
+      constexpr int kQ = kEpiCC / 4;  // float4s per staged row
+      constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
 #pragma unroll
       for (int c0 = 0; c0 < NT; c0 += kEpiCW) {
+        // the chunk's residual / pre-activation operand, loaded unconditionally from clamped
+        // addresses before the LDS staging: its latency runs under the staging instead of
+        // one load-to-use wait per guarded store below
+        f32x4 rpre[kEpiCW];
+        if constexpr (kHasR && !TG_EXP_PLAINEPI) {
+#pragma unroll
+          for (int it = 0; it < kEpiCW; ++it) {
+            const int idx = it * 64 + lane, row = idx / kQ, c4 = idx - row * kQ;
+            const int64_t orow = m0 + row < M ? m0 + row : M - 1;
+            const int col = min(n0 + 16 * c0 + 4 * c4, N - 4);
+            rpre[it] = *reinterpret_cast<const f32x4*>(ep.R + (rowbase + orow) * N + col);
+          }
+        }
 #pragma unroll
         for (int t = 0; t < kEpiCW; ++t) {
           if (c0 + t >= NT) continue;
@@ -430,7 +444,6 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        constexpr int kQ = kEpiCC / 4;  // float4s per staged row
 #pragma unroll
         for (int it = 0; it < kEpiCW; ++it) {
           const int idx = it * 64 + lane, row = idx / kQ, c4 = idx - row * kQ;
@@ -450,7 +463,8 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
                 const int64_t bb = grow / ep.T;
                 valid = (grow - bb * ep.T) < ep.lens[bb];
               }
-              epi_store4<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, valid);
+              epi_store4<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, valid,
+                              rpre[it]);
             }
           }
         }
