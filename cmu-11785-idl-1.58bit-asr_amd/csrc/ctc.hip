@@ -310,21 +310,33 @@ __global__ __launch_bounds__(kThreads) void ctc_lse_gather_kernel(
   if (t >= in_len[b]) return;
   const float* row = x + rowid * V;
   const bool vec = (V & 3) == 0;
+  // one pass over the row: the thread's values stay in registers (V <= 8 * 4 * kThreads
+  // here: up to 8 float4 per thread) between the max and the sum
+  constexpr int kMaxQ = 8;
+  const int nq = vec ? V / 4 : 0;
+  f32x4 vals[kMaxQ];
   float m = -INFINITY;
-  if (vec) {
-    for (int q = threadIdx.x; q < V / 4; q += kThreads) {
-      const f32x4 v = reinterpret_cast<const f32x4*>(row)[q];
-      m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+  const bool regs = vec && nq <= kMaxQ * kThreads;
+  if (regs) {
+#pragma unroll
+    for (int i = 0; i < kMaxQ; ++i) {
+      const int q = threadIdx.x + i * kThreads;
+      vals[i] = q < nq ? reinterpret_cast<const f32x4*>(row)[q]
+                       : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      m = fmaxf(m, fmaxf(fmaxf(vals[i][0], vals[i][1]), fmaxf(vals[i][2], vals[i][3])));
     }
   } else {
     for (int v = threadIdx.x; v < V; v += kThreads) m = fmaxf(m, row[v]);
   }
   m = block_reduce(m, true, red);
   float sum = 0.0f;
-  if (vec) {
-    for (int q = threadIdx.x; q < V / 4; q += kThreads) {
-      const f32x4 v = reinterpret_cast<const f32x4*>(row)[q];
-      sum += ((expf(v[0] - m) + expf(v[1] - m)) + expf(v[2] - m)) + expf(v[3] - m);
+  if (regs) {
+#pragma unroll
+    for (int i = 0; i < kMaxQ; ++i) {
+      const int q = threadIdx.x + i * kThreads;
+      if (q < nq)
+        sum += ((expf(vals[i][0] - m) + expf(vals[i][1] - m)) + expf(vals[i][2] - m)) +
+               expf(vals[i][3] - m);
     }
   } else {
     for (int v = threadIdx.x; v < V; v += kThreads) sum += expf(row[v] - m);
@@ -372,7 +384,12 @@ __global__ __launch_bounds__(kThreads) void ctc_logits_grad_kernel(
       g[v] = live ? expf((row[v] - m) - logs) * sc : 0.0f;
   }
   if (!live) return;
-  __syncthreads();  // the label columns below overwrite this block's dense values
+  // alpha + beta of every state and the label chains into LDS (one parallel load each), so
+  // an owner's walk over its label's occurrences -- L + 1 of them for blank -- reads LDS
+  // instead of a dependent global load per step
+  __shared__ float xs[kMaxStates];
+  __shared__ int nx[kMaxStates];
+  __shared__ int own[kMaxStates];
   const int L = (int)tg_len[b];
   const int NS = 2 * L + 1;
   const int SS = 2 * S + 1;
@@ -380,13 +397,19 @@ __global__ __launch_bounds__(kThreads) void ctc_logits_grad_kernel(
   const int* ob = occ + (int64_t)b * 2 * SS;
   const float* a = alpha + rowid * SS;
   const float* be = beta + rowid * SS;
+  for (int s = threadIdx.x; s < NS; s += kThreads) {
+    xs[s] = a[s] + be[s];
+    nx[s] = ob[s];
+    own[s] = ob[SS + s];
+  }
+  __syncthreads();  // (also: the label columns below overwrite this block's dense values)
   const float n = nll[b];
   for (int s = threadIdx.x; s < NS; s += kThreads) {
-    if (!ob[SS + s]) continue;  // not the first state of its label
+    if (!own[s]) continue;  // not the first state of its label
     const int64_t lab = ext_label(tgb, s, 0);  // compact label
     // occurrences of the label in state order (lse2(-inf, x) == x: the chain's first step)
-    float acc = a[s] + be[s];
-    for (int q = ob[s]; q >= 0; q = ob[q]) acc = lse2(acc, a[q] + be[q]);
+    float acc = xs[s];
+    for (int q = nx[s]; q >= 0; q = nx[q]) acc = lse2(acc, xs[q]);
     const float l = lpc[rowid * (S + 1) + lab];
     const int64_t v = (s & 1) ? targets[(int64_t)b * S + (s >> 1)] : blank;  // vocabulary id
     g[v] = (expf(l) - expf(acc + n - l)) * sc;
