@@ -319,36 +319,31 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     }
   }
 
-  // ctx = A v: A = the lane's probabilities (row r, k = 4g+j of tile t), B = v rows
+  // ctx = A v: A = the lane's probabilities (row r, k = 4g+j of tile t), B = v rows.
+  // v [16 nt keys][D] of (b, h) is staged once per block into the X image (free once every
+  // wave has passed the scores phase) with coalesced dwordx4 loads; the MFMA operands then
+  // come from LDS (row pitch D: the 4 key rows a B fragment touches sit 16 banks apart)
+  // instead of 12 scalar L2 loads per lane and key tile in each of the 4 waves.
+  __syncthreads();
+  float* vs = xs;
+  for (int e = threadIdx.x; e < 16 * nt * DQ; e += kThreads) {
+    const int key = e / DQ, c4 = 4 * (e - key * DQ);
+    const f32x4 v4 = key < T ? *(const f32x4u*)(vbp + (size_t)key * C + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(vs + key * D + c4) = v4;
+  }
+  __syncthreads();
   f32x4 o[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B operands of key tile t (v[16t+4g+j][16ct+r]); tile t+1's are loaded while tile t's
-  // MFMAs issue
-  float vb_cur[4][CT];
-  auto load_v = [&](int t, float (&dst)[4][CT]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* vrow = vbp + (size_t)min(16 * t + 4 * g + j, T - 1) * C;
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) dst[j][ct] = vrow[min(16 * ct + r, D - 1)];
-    }
-  };
-  load_v(0, vb_cur);
+  // (columns 16ct + r >= D read the next row: they only feed output columns never stored)
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     if (t >= nt) continue;
-    float vb_nxt[4][CT];
-    if (t + 1 < NTT && t + 1 < nt) load_v(t + 1, vb_nxt);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) {
+      const float* vrow = vs + (16 * t + 4 * g + j) * D + r;
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) if (!RA_EXP_NOCTX) o[ct] = mfma4(sreg[t][j], vb_cur[j][ct], o[ct]);
-    if (t + 1 < NTT) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) vb_cur[j][ct] = vb_nxt[j][ct];
+      for (int ct = 0; ct < CT; ++ct) if (!RA_EXP_NOCTX) o[ct] = mfma4(sreg[t][j], vrow[16 * ct], o[ct]);
     }
   }
 #pragma unroll
