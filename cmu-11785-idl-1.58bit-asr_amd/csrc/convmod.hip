@@ -49,6 +49,7 @@ __device__ __forceinline__ void conv_window(const float* __restrict__ tile, int 
 
 constexpr int kR = 8;  // frames per register window
 constexpr int kLB = 16;  // window elements loaded per thread and batch (all in flight)
+constexpr int kSB = 16;  // rows per batch of the per-channel statistics loops
 
 // ------------------------------------------------------------------ forward
 // Block = (time tile of TT frames, utterance). LDS holds g over [t0-P, t0+TT+P) x C and
@@ -139,13 +140,19 @@ __global__ __launch_bounds__(kThreads) void cm_stats_part_kernel(const float* __
   const float* xp = x + (size_t)p * rows_pp * C;
   for (int c = threadIdx.x; c < C; c += kThreads) {
     double s1 = 0.0, s2 = 0.0;
-#pragma unroll 4
-    for (int64_t r = r0; r < r1; ++r) {
-      const double v = xp[r * C + c];
-      s1 += v;
-      s2 += v * v;
+    // rows in batches of kSB loads in flight (clamped addresses, masked use)
+    for (int64_t rb = r0; rb < r1; rb += kSB) {
+      float v[kSB];
+#pragma unroll
+      for (int q = 0; q < kSB; ++q) v[q] = xp[min(rb + q, r1 - 1) * C + c];
+#pragma unroll
+      for (int q = 0; q < kSB; ++q)
+        if (rb + q < r1) {
+          s1 += (double)v[q];
+          s2 += (double)v[q] * v[q];
+        }
     }
-    double* o = part + (((size_t)p * S + s) * C + c) * 2;
+    double* o = part + (((size_t)p * C + c) * S + s) * 2;
     o[0] = s1;
     o[1] = s2;
   }
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(64) void cm_stats_final_kernel(const double* __rest
   const int p = i / C, c = i - p * C;
   double s1 = 0.0, s2 = 0.0;
   for (int s = threadIdx.x; s < S; s += 64) {
-    const double* o = part + (((size_t)p * S + s) * C + c) * 2;
+    const double* o = part + (((size_t)p * C + c) * S + s) * 2;
     s1 += o[0];
     s2 += o[1];
   }
@@ -220,14 +227,24 @@ __global__ __launch_bounds__(kThreads) void cm_bn_bwd_part_kernel(
     const float* st = stats + 2 * ((size_t)p * C + c);
     const float gm = gamma[c], bt = beta[c];
     double s1 = 0.0, s2 = 0.0;
-#pragma unroll 4
-    for (int64_t r = r0; r < r1; ++r) {
-      float xh;
-      const float d = bn_dy(dv[base + r * C + c], z[base + r * C + c], st, gm, bt, xh);
-      s1 += d;
-      s2 += (double)d * xh;
+    for (int64_t rb = r0; rb < r1; rb += kSB) {
+      float a[kSB], zz[kSB];
+#pragma unroll
+      for (int q = 0; q < kSB; ++q) {
+        const size_t e = base + min(rb + q, r1 - 1) * C + c;
+        a[q] = dv[e];
+        zz[q] = z[e];
+      }
+#pragma unroll
+      for (int q = 0; q < kSB; ++q)
+        if (rb + q < r1) {
+          float xh;
+          const float d = bn_dy(a[q], zz[q], st, gm, bt, xh);
+          s1 += d;
+          s2 += (double)d * xh;
+        }
     }
-    double* o = part + (((size_t)p * S + s) * C + c) * 2;
+    double* o = part + (((size_t)p * C + c) * S + s) * 2;
     o[0] = s1;
     o[1] = s2;
   }
@@ -243,7 +260,7 @@ __global__ __launch_bounds__(64) void cm_bn_bwd_final_kernel(
   for (int p = 0; p < P; ++p) {
     double s1 = 0.0, s2 = 0.0;
     for (int s = threadIdx.x; s < S; s += 64) {
-      const double* o = part + (((size_t)p * S + s) * C + c) * 2;
+      const double* o = part + (((size_t)p * C + c) * S + s) * 2;
       s1 += o[0];
       s2 += o[1];
     }
@@ -402,22 +419,50 @@ __global__ __launch_bounds__(kThreads) void cm_glu_bwd_kernel(const float* __res
 
 // dw_dw[c][j] = sum over blocks (fixed order) of the partials; db_dw[c] likewise.
 // One wave per output: lanes take blocks k = lane, lane + 64, ... (fp64 lane sums).
-__global__ __launch_bounds__(64) void cm_wgrad_final_kernel(const float* __restrict__ wpart,
-                                                            int nblk, int C, int K,
-                                                            float* __restrict__ dw,
-                                                            float* __restrict__ db) {
-  const int i = blockIdx.x;  // c * (K + 1) + j
-  const int c = i / (K + 1), j = i - c * (K + 1);
+// Block = 64 consecutive outputs (c, j) x 16 block-slices (slice q: partials q, q+16, ...,
+// 8 loads in flight), fp64, the slices added in order through LDS (fixed order). Lanes read
+// consecutive outputs of one partial: coalesced (one wave per output walked the partials
+// 18 KB apart: a cache line per 4-byte value, 16 us per launch).
+constexpr int kWfSlices = 16;
+__global__ __launch_bounds__(64 * kWfSlices) void cm_wgrad_final_kernel(
+    const float* __restrict__ wpart, int nblk, int C, int K, float* __restrict__ dw,
+    float* __restrict__ db) {
+  __shared__ double red[kWfSlices][64];
+  const int n = C * (K + 1);
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;  // c * (K + 1) + j
+  const int ic = i < n ? i : n - 1;
   double acc = 0.0;
-  for (int k = threadIdx.x; k < nblk; k += 64) acc += wpart[(size_t)k * C * (K + 1) + i];
-  acc = wave_sum(acc);
-  if (threadIdx.x == 0) {
-    if (j < K) dw[(size_t)c * K + j] = (float)acc;
-    else if (db) db[c] = (float)acc;
+  for (int k0 = sl; k0 < nblk; k0 += 8 * kWfSlices) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u * kWfSlices;
+      v[u] = wpart[(size_t)(k < nblk ? k : nblk - 1) * n + ic];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + u * kWfSlices < nblk) acc += (double)v[u];
   }
+  red[sl][lane] = acc;
+  __syncthreads();
+  if (sl != 0 || i >= n) return;
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < kWfSlices; ++q) t += red[q][lane];
+  const int c = i / (K + 1), j = i - c * (K + 1);
+  if (j < K) dw[(size_t)c * K + j] = (float)t;
+  else if (db) db[c] = (float)t;
 }
 
-int stats_chunks(int64_t rows_pp) { return (int)(rows_pp < 128 ? (rows_pp > 0 ? rows_pp : 1) : 128); }
+// Row chunks per pass of the BatchNorm statistics / backward sums: ~16 rows per block at
+// Conformer-S (one batch of kSB loads in flight per thread), at most 512 chunks. Partials
+// are laid out [pass][channel][chunk][2] so the final kernels' lanes (consecutive chunks)
+// read consecutive 16-byte pairs.
+int stats_chunks(int64_t rows_pp) {
+  const int64_t s = (rows_pp + kSB - 1) / kSB;
+  return (int)(s < 1 ? 1 : (s > 512 ? 512 : s));
+}
 
 size_t lds_fwd(int C, int K, int TT) { return sizeof(float) * ((size_t)(TT + K - 1) * C + (size_t)C * K); }
 size_t lds_bwd(int C, int K, int TT) {
@@ -514,7 +559,8 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
                        (const float*)dz, g, wdw, (int)T, (int)C, (int)K, TT, dg, wpart);
   hipLaunchKernelGGL(cm_glu_bwd_kernel, dim3((unsigned)eblocks), dim3(kThreads), 0, s,
                      (const float*)dg, u, (int)C, total, du);
-  hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)(C * (K + 1))), dim3(64), 0, s,
+  hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)ceil_div(C * (K + 1), 64)),
+                     dim3(64 * kWfSlices), 0, s,
                      (const float*)wpart, (int)(Bt * ntt), (int)C, (int)K, dwdw, dbdw);
 }
 
