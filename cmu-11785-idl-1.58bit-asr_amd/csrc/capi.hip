@@ -779,6 +779,50 @@ int ob_ctc_loss_logits_bwd_groups(const float* logits, const int64_t* targets,
   return launched();
 }
 
+size_t ob_att_kl_workspace(int64_t P, int64_t BU) {
+  if (P < 1 || BU < 0) return 0;
+  return align_up(att_kl_workspace(P, BU));
+}
+
+namespace {
+int att_kl_check(const float* x, const int64_t* tgt, const uint8_t* pad, int64_t P, int64_t BU,
+                 int64_t V, float ls, const void* out, size_t ws_bytes, const void* ws) {
+  if (P < 1 || P > 64 || BU < 1 || !att_kl_supported(V) || P * BU > INT32_MAX ||
+      !(ls > 0.0f && ls < 1.0f))
+    return OB_ERR_SHAPE;
+  if (!x || !tgt || !pad || !out || !ws) return OB_ERR_NULL;
+  if (ws_bytes < ob_att_kl_workspace(P, BU)) return OB_ERR_WORKSPACE;
+  if (reinterpret_cast<uintptr_t>(x) & 15) return OB_ERR_ALIGN;
+  return OB_OK;
+}
+}  // namespace
+
+int ob_att_kl_loss_fwd(const float* logits, const int64_t* tgt_out, const uint8_t* tgt_pad,
+                       int64_t P, int64_t BU, int64_t V, int pad_id, float label_smoothing,
+                       float* l_att, float* l_kl, void* ws, size_t ws_bytes, void* stream) {
+  if (int st = att_kl_check(logits, tgt_out, tgt_pad, P, BU, V, label_smoothing, l_att, ws_bytes,
+                            ws))
+    return st;
+  if (P > 1 && !l_kl) return OB_ERR_NULL;
+  launch_att_kl_fwd(logits, tgt_out, tgt_pad, P, BU, V, pad_id, label_smoothing, l_att, l_kl, ws,
+                    as_stream(stream));
+  return launched();
+}
+
+int ob_att_kl_loss_bwd(const float* logits, const int64_t* tgt_out, const uint8_t* tgt_pad,
+                       int64_t P, int64_t BU, int64_t V, float label_smoothing,
+                       const float* g_att, const float* g_kl, float* grad, const void* ws,
+                       size_t ws_bytes, void* stream) {
+  if (int st = att_kl_check(logits, tgt_out, tgt_pad, P, BU, V, label_smoothing, grad, ws_bytes,
+                            ws))
+    return st;
+  if (!g_att || (P > 1 && !g_kl)) return OB_ERR_NULL;
+  if (reinterpret_cast<uintptr_t>(grad) & 15) return OB_ERR_ALIGN;
+  launch_att_kl_bwd(logits, tgt_out, tgt_pad, P, BU, V, label_smoothing, g_att, g_kl, grad, ws,
+                    as_stream(stream));
+  return launched();
+}
+
 int ob_ctc_greedy_decode(const float* logits, const int64_t* lens, int64_t B, int64_t T,
                          int64_t V, int blank, int32_t* ids, int32_t* out, int32_t* out_len,
                          void* stream) {

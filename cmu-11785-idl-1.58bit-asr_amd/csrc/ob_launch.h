@@ -236,6 +236,17 @@ void launch_ctc_logits_bwd(const float* x, const int64_t* targets, const int64_t
                            int blank, int64_t G, const float* grad_out, float* grad, void* ws,
                            hipStream_t s);
 
+// seqloss.hip: label-smoothed attention CE + KL(teacher || student) over the stacked decoder
+// logits x [P*BU][V] (pass-major; the teacher's row of position q is row q).
+bool att_kl_supported(int64_t V);
+size_t att_kl_workspace(int64_t P, int64_t BU);
+void launch_att_kl_fwd(const float* x, const int64_t* tgt, const uint8_t* pad, int64_t P,
+                       int64_t BU, int64_t V, int pad_id, float ls, float* l_att, float* l_kl,
+                       void* ws, hipStream_t s);
+void launch_att_kl_bwd(const float* x, const int64_t* tgt, const uint8_t* pad, int64_t P,
+                       int64_t BU, int64_t V, float ls, const float* g_att, const float* g_kl,
+                       float* grad, const void* ws, hipStream_t s);
+
 // adamw.hip (clip_grad_norm_ + AdamW over a tensor table; layout = ob_adamw_tensor)
 struct AdamwTensor {
   float* param;

@@ -83,6 +83,11 @@ SIGNATURES = {
     "ob_ctc_loss_logits_bwd_groups": (
         _int, [_c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _sz,
                _c_f]),
+    "ob_att_kl_workspace": (_sz, [_i64, _i64]),
+    "ob_att_kl_loss_fwd": (
+        _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _int, _f32, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_att_kl_loss_bwd": (
+        _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _f32, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_quant_dequant": (_int, [_c_f, _c_f, _int, _int, _i64, _c_f, _c_f]),
     "ob_quant_ste_bwd_workspace": (_sz, [_i64]),
     "ob_quant_ste_bwd": (_int, [_c_f, _c_f, _c_f, _int, _int, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),

@@ -14,6 +14,7 @@ generator seeded identically on all ranks (train.py:56-59 draws from the global 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -21,6 +22,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .losses import att_ce_loss, ctc_loss_from_logits, kl_logits, make_att_targets
+from .seqloss import att_kl_losses, att_kl_supported
+
+_ATT_KL = os.environ.get("OB_ATT_KL", "1") != "0"  # 0: the torch loss expressions
 
 __all__ = ["OneBitStep", "WarmupCosine", "sample_sp_mask", "train_step", "SPECIAL_IDS",
            "make_optimizer"]
@@ -158,6 +162,32 @@ class OneBitStep(nn.Module):
         return loss, parts
 
 
+    def _att_kl_torch(self, logits, t_out, t_pad, P):
+        """The decoder losses as torch expressions (the path when csrc/seqloss.hip does not
+        apply: CPU, label smoothing 0, V % 4 != 0)."""
+        pad_id = self.special["pad_id"]
+        vocab, u1 = logits.size(-1), logits.size(1)
+        bsz = logits.size(0) // P
+        logp = F.log_softmax(logits, dim=-1).view(P, bsz, u1, vocab)
+        if self.label_smoothing > 0:
+            off = self.label_smoothing / (vocab - 1)
+            tgt = t_out.unsqueeze(0).expand(P, bsz, u1).unsqueeze(-1)
+            tgt_logp = logp.gather(-1, tgt).squeeze(-1)
+            per_pos = -(off * logp.sum(dim=-1) + (1.0 - self.label_smoothing - off) * tgt_logp)
+            l_mean = per_pos.reshape(P, -1).mean(dim=1)
+            m = (t_out != pad_id).float()
+            l_att = (l_mean[:, None] * m.reshape(1, -1)).sum(dim=1) / m.sum().clamp_min(1.0)
+        else:
+            l_att = torch.stack([F.nll_loss(logp[p].transpose(1, 2), t_out, ignore_index=pad_id)
+                                 for p in range(P)])
+        with torch.no_grad():  # softmax of the detached teacher logits (train.py:101)
+            p_t = F.softmax(logits[:bsz].detach(), dim=-1)
+        kl = F.kl_div(logp[1:], p_t.unsqueeze(0).expand(P - 1, -1, -1, -1),
+                      reduction="none").sum(dim=-1)
+        keep = (~t_pad).float()
+        l_kl = (kl * keep.unsqueeze(0)).sum(dim=(1, 2)) / keep.sum().clamp_min(1.0)
+        return l_att, l_kl
+
     def _forward_stacked(self, batch, bits):
         from .ctc import ctc_loss_logits_groups
 
@@ -175,35 +205,20 @@ class OneBitStep(nn.Module):
         # the encoder repeats the (pass-independent) subsampling output P times itself
         enc, mask, ctc = self.model(batch, precision=2, sp_mask=bits)
         logits = self.model.decode_logits(enc, mask, t_inp.repeat(P, 1), t_pad.repeat(P, 1))
-        vocab = logits.size(-1)
-        u1 = logits.size(1)
-        # attention CE per pass (losses.py:22-35, label smoothing, scalar-mean quirk)
-        logp = F.log_softmax(logits, dim=-1).view(P, bsz, u1, vocab)
-        if self.label_smoothing > 0:
-            off = self.label_smoothing / (vocab - 1)
-            tgt = t_out.unsqueeze(0).expand(P, bsz, u1).unsqueeze(-1)
-            tgt_logp = logp.gather(-1, tgt).squeeze(-1)
-            per_pos = -(off * logp.sum(dim=-1) + (1.0 - self.label_smoothing - off) * tgt_logp)
-            l_mean = per_pos.reshape(P, -1).mean(dim=1)
-            m = (t_out != sp["pad_id"]).float()
-            l_att = (l_mean[:, None] * m.reshape(1, -1)).sum(dim=1) / m.sum().clamp_min(1.0)
+        # attention CE per pass (losses.py:22-35, label smoothing, scalar-mean quirk) and
+        # KL(teacher || student) for the student and SP passes (losses.py:50-59)
+        if _ATT_KL and att_kl_supported(logits, self.label_smoothing):
+            # csrc/seqloss.hip: both losses, one row pass per direction
+            l_att, l_kl = att_kl_losses(logits, t_out, t_pad, P, sp["pad_id"],
+                                        self.label_smoothing)
         else:
-            l_att = torch.stack([
-                F.nll_loss(logp[p].transpose(1, 2), t_out, ignore_index=sp["pad_id"])
-                for p in range(P)])
+            l_att, l_kl = self._att_kl_torch(logits, t_out, t_pad, P)
         # CTC per pass (losses.py:41-47: log_softmax + CTC), straight from the head's logits
         in_lens = mask.sum(dim=1).long()
         # the P passes' CTC losses in one launch per direction (each pass its own mean)
         l_ctc = ctc_loss_logits_groups(ctc, batch["tokens"].repeat(P, 1), in_lens,
                                        batch["token_lens"].repeat(P), sp["blank_id"], P)
         l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
-        # KL(teacher || student) for the student and SP passes (losses.py:50-59)
-        with torch.no_grad():  # softmax of the detached teacher logits (train.py:101)
-            p_t = F.softmax(logits[:bsz].detach(), dim=-1)
-        kl = F.kl_div(logp[1:], p_t.unsqueeze(0).expand(P - 1, -1, -1, -1),
-                      reduction="none").sum(dim=-1)
-        keep = (~t_pad).float()
-        l_kl = (kl * keep.unsqueeze(0)).sum(dim=(1, 2)) / keep.sum().clamp_min(1.0)
         loss = l_int[0] + self.lambda1 * (l_int[1] + l_int[2]) + self.lambda2 * (l_kl[0] + l_kl[1])
         parts = torch.stack([l_int[0], l_int[1], l_int[2], l_kl[0], l_kl[1],
                              l_ctc[0], l_ctc[1], l_ctc[2]]).detach()

@@ -216,6 +216,26 @@ OB_API int ob_ctc_loss_logits_bwd_groups(const float* logits, const int64_t* tar
                                          const float* grad_out, float* grad, void* ws,
                                          size_t ws_bytes, void* stream);
 
+/* Decoder losses of the stacked step (replaces the torch expression of
+ * onebit_asr/losses.py:22-35 att_ce_loss with label smoothing and :50-59 kl_logits, as
+ * train.py:82-111 calls them per pass). logits [P][BU][V] fp32 (pass-major, P <= 64, pass 0 =
+ * the teacher, detached for the KL); tgt_out [BU] int64 (tgt_out != pad_id marks the CE
+ * positions); tgt_pad [BU] uint8 (1 = padded decoder input, dropped from the KL).
+ * fwd: l_att[P] = mean_q(per-position smoothed CE) * msum / max(msum, 1) (the reference's
+ * scalar-mean quirk) and l_kl[P-1] = sum_{q kept} KL(softmax(teacher_q) || softmax(x_pq)) /
+ * max(kept, 1). bwd: grad [P][BU][V] from g_att[P], g_kl[P-1] (the teacher rows get only
+ * their CE gradient). 0 < label_smoothing < 1; V % 4 == 0, V <= 8192; logits / grad 16-byte
+ * aligned. ws: ob_att_kl_workspace(P, BU) bytes, kept from fwd to bwd. */
+OB_API size_t ob_att_kl_workspace(int64_t P, int64_t BU);
+OB_API int ob_att_kl_loss_fwd(const float* logits, const int64_t* tgt_out,
+                              const uint8_t* tgt_pad, int64_t P, int64_t BU, int64_t V,
+                              int pad_id, float label_smoothing, float* l_att, float* l_kl,
+                              void* ws, size_t ws_bytes, void* stream);
+OB_API int ob_att_kl_loss_bwd(const float* logits, const int64_t* tgt_out,
+                              const uint8_t* tgt_pad, int64_t P, int64_t BU, int64_t V,
+                              float label_smoothing, const float* g_att, const float* g_kl,
+                              float* grad, const void* ws, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Stacked passes. The reference's training step runs every BitLinear three times per
  * batch -- 2-bit teacher, 1-bit student and the stochastic-precision pass
