@@ -17,7 +17,11 @@ library GEMMs (hipBLASLt / rocBLAS), and the bias gradient is the fixed-order co
 fp32 forward (and dX) GEMMs whose shape csrc/dgemm.hip takes (K, N multiples of 4, the
 split weight image within LDS) run there: exact-fp32 products on the bf16 matrix cores
 (six MFMAs per k-step), bias in the epilogue. At Conformer-S the CTC head's forward
-([23904 x 144] x [144 x 5004]) is the large one. OB_DENSE_LINEAR=0: library GEMMs only.
+([23904 x 144] x [144 x 5004]) is the large one. Weight gradients whose N and K are
+multiples of 48 (the decoder's projections and feed-forward, the subsampling output layer)
+run on the dW kernel family (``ob_dense_dw``: exact-fp32 products, fixed-order chunk sums,
+the bias gradient from the same pass). OB_DENSE_LINEAR=0: library GEMMs only;
+OB_DENSE_LINEAR_DW=0: library weight gradients.
 """
 from __future__ import annotations
 
@@ -33,11 +37,21 @@ from . import _lib
 __all__ = ["linear", "colsum"]
 
 _DENSE = os.environ.get("OB_DENSE_LINEAR", "1") != "0"
+_DENSE_DW = _DENSE and os.environ.get("OB_DENSE_LINEAR_DW", "1") != "0"
 
 
 def _dense_ok(x: torch.Tensor, k: int, n: int) -> bool:
     return (_DENSE and k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
             and _lib.load().ob_dense_supported(k, n) == 1)
+
+
+def _dense_dw_ws(g2: torch.Tensor, x2d: torch.Tensor, w: torch.Tensor) -> int:
+    """Workspace bytes of ob_dense_dw for this linear's weight gradient, 0 if not taken
+    (N, K multiples of 48; 16-byte aligned operands)."""
+    if not (_DENSE_DW and g2.is_cuda and x2d.is_contiguous() and w.is_contiguous()
+            and g2.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0):
+        return 0
+    return int(_lib.load().ob_dense_dw_workspace(g2.shape[0], w.shape[0], w.shape[1]))
 
 
 def _dense(x2d: torch.Tensor, w: torch.Tensor, trans: int, bias, n: int) -> torch.Tensor:
@@ -97,6 +111,17 @@ class _LinearFn(torch.autograd.Function):
                     gx = _dense(g2, weight, 1, None, k).view(xshape)
                 else:
                     gx = (g2 @ weight).view(xshape)
+            wsb = _dense_dw_ws(g2, x2d, weight) if ctx.needs_input_grad[1] else 0
+            if wsb:  # dW (and db) on the dW kernel family: exact-fp32 products, fixed order
+                m, n, k = g2.shape[0], weight.shape[0], weight.shape[1]
+                gw = torch.empty_like(weight)
+                if has_b and ctx.needs_input_grad[2]:
+                    gb = torch.empty((n,), dtype=torch.float32, device=g2.device)
+                ws = torch.empty((wsb,), dtype=torch.uint8, device=g2.device)
+                _lib.check(_lib.load().ob_dense_dw(g2.data_ptr(), x2d.data_ptr(), m, n, k,
+                                                   gw.data_ptr(), _lib.ptr(gb), ws.data_ptr(),
+                                                   wsb, _lib.stream_of(g2)), "ob_dense_dw")
+                return gx, gw, gb, None
             if ctx.needs_input_grad[1]:
                 gw = g2.t() @ x2d
         else:
