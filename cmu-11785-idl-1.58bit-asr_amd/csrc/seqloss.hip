@@ -97,15 +97,17 @@ __global__ __launch_bounds__(kThreads) void att_kl_fwd_kernel(
   load_row(x + (size_t)q * V, nq, yv);
   float mt, logst, syt;
   row_stats(yv, nq, red, mt, logst, syt);
+  // log pt - log p = (y - x) + c with the row constant c = (m - mt) + (logs - logst): the
+  // O(1) difference is rounded instead of two O(log V) log-probabilities (4x less error)
+  const float c = (m - mt) + (logs - logst);
   float acc = 0.0f;
 #pragma unroll
   for (int i = 0; i < kMaxQ; ++i) {
     if ((int)threadIdx.x + i * kThreads >= nq) continue;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float lpt = (yv[i][e] - mt) - logst;
-      const float pt = expf(lpt);
-      acc += pt == 0.0f ? 0.0f : pt * (lpt - ((xv[i][e] - m) - logs));
+      const float pt = expf((yv[i][e] - mt) - logst);
+      acc += pt == 0.0f ? 0.0f : pt * ((yv[i][e] - xv[i][e]) + c);
     }
   }
   acc = block_sum(acc, red, false);

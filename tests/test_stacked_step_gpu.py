@@ -1,5 +1,6 @@
 """The stacked three-pass step (OneBitStep(stacked=True)) against the reference's literal
-three forwards (stacked=False) on cfg1, dropout 0: same loss and loss parts (rel <= 1e-5),
+three forwards (stacked=False) on cfg1, dropout 0: same loss and loss parts (rel <= 1e-5,
+parts atol 2e-6 for the small KL parts),
 same gradients for every parameter (max|err| <= 2e-4 * max|g| + 1e-7, scalar alpha
 gradients 1e-3; only the order in which the passes' contributions are summed differs)."""
 import pytest
@@ -35,7 +36,10 @@ def test_stacked_equals_literal(gpu, sp_mask):
                                                   if p.grad is not None})
     (l0, p0, g0), (l1, p1, g1) = res[False], res[True]
     assert abs(l1 - l0) <= 1e-5 * abs(l0), (l1, l0)
-    torch.testing.assert_close(p1, p0, rtol=1e-5, atol=1e-7)
+    # atol: a KL part (~0.04 here) carries the fp32 rounding of log-probabilities of size
+    # log V ~ 8.5 (ulp 9.5e-7) in torch's literal form; the stacked kernel rounds O(1)
+    # differences instead (csrc/seqloss.hip), so the two differ by up to ~1e-6 (seen 7.5e-7)
+    torch.testing.assert_close(p1, p0, rtol=1e-5, atol=2e-6)
     assert g0.keys() == g1.keys()
     scale = max(g.abs().max().item() for g in g0.values())
     for k in g0:
