@@ -22,6 +22,7 @@ reference (conv module "kept full-precision per paper recommendation", :225; sub
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -434,6 +435,27 @@ class ConformerEncoder(nn.Module):
         return self.ln_out(x), key_mask
 
 
+_DEC_RESDROP = os.environ.get("OB_DEC_RESDROP", "1") != "0"  # 0: torch dropout + add
+
+
+def _residual_dropout(x: torch.Tensor, y: torch.Tensor, p: float, training: bool):
+    """x + dropout(y) of a post-norm decoder sublayer (nn.TransformerDecoderLayer's
+    ``norm_k(x + dropout_k(sublayer(x)))``) in one kernel with the fused call sites' hash
+    mask (conv.py _ResidualDropFn); the dropout backward is formed by the following
+    LayerNorm's backward (layernorm.GradScale) instead of a pass of its own."""
+    if not (training and p > 0):
+        return x + y
+    if not (_DEC_RESDROP and x.is_cuda and x.shape == y.shape):
+        return x + F.dropout(y, p, training)
+    from .conv import _ResidualDropFn
+    from .fused import _rng
+    from .layernorm import GradScale, attach_grad_scale
+
+    rng, off = _rng(x.device)
+    spec = GradScale(1.0, p, rng, off)
+    return attach_grad_scale(_ResidualDropFn.apply(x, y, float(p), rng, off, spec), spec)
+
+
 class TransformerDecoder(nn.Module):
     """Stock 2-layer nn.TransformerDecoder head (conformer.py:275-299), full precision.
 
@@ -486,12 +508,13 @@ class TransformerDecoder(nn.Module):
         tr = self.training
         n1, n2, n3 = lyr.norm1, lyr.norm2, lyr.norm3
         sa = self._attention(lyr.self_attn, x, None, self_bias, tr)
-        x = layer_norm(x + F.dropout(sa, lyr.dropout1.p, tr), n1.weight, n1.bias, n1.eps)
+        x = layer_norm(_residual_dropout(x, sa, lyr.dropout1.p, tr), n1.weight, n1.bias, n1.eps)
         ca = self._attention(lyr.multihead_attn, x, mem, cross_bias, tr)
-        x = layer_norm(x + F.dropout(ca, lyr.dropout2.p, tr), n2.weight, n2.bias, n2.eps)
+        x = layer_norm(_residual_dropout(x, ca, lyr.dropout2.p, tr), n2.weight, n2.bias, n2.eps)
         ff = linear(F.dropout(F.relu(linear(x, lyr.linear1.weight, lyr.linear1.bias)),
                               lyr.dropout.p, tr), lyr.linear2.weight, lyr.linear2.bias)
-        return layer_norm(x + F.dropout(ff, lyr.dropout3.p, tr), n3.weight, n3.bias, n3.eps)
+        return layer_norm(_residual_dropout(x, ff, lyr.dropout3.p, tr), n3.weight, n3.bias,
+                          n3.eps)
 
     def forward(self, tgt_inp, memory, memory_mask, tgt_key_padding_mask):
         tt = tgt_inp.size(1)

@@ -270,3 +270,38 @@ def test_qkv_projections_match_separate_layers(gpu, stacked):
     assert (dh0 - dh1).abs().max().item() <= 1e-6 * dh0.abs().max().item()
     for a, b in zip(g0, g1):
         assert (a - b).abs().max().item() <= 1e-6 * max(a.abs().max().item(), 1e-30), (a, b)
+
+
+def test_decoder_residual_dropout(gpu):
+    """conformer._residual_dropout (decoder post-norm sublayers): out = x + keep * y / (1-p)
+    with a keep rate ~ 1-p, dy = keep / (1-p) * gout and dx = gout -- both directly and with
+    the dropout backward formed by the following LayerNorm's backward (GradScale hand-off),
+    bit for bit; identity when not training."""
+    from onebit_asr.conformer import _residual_dropout
+    from onebit_asr.layernorm import layer_norm
+
+    p = 0.1
+    g = torch.Generator().manual_seed(3)
+    x = torch.zeros(6, 41, 144, device=gpu, requires_grad=True)  # out - x exact
+    y = torch.ones(6, 41, 144, device=gpu, requires_grad=True)
+    out = _residual_dropout(x, y, p, True)
+    d = (out - x).detach()
+    scale = torch.tensor(1.0 / (1.0 - p), device=gpu)
+    assert bool(((d == 0) | (d == scale)).all())
+    keep = (d != 0).float().mean().item()
+    assert abs(keep - (1 - p)) < 0.01, keep
+    gout = torch.randn(out.shape, generator=g).to(gpu)
+    out.backward(gout)
+    assert torch.equal(x.grad, gout)
+    assert torch.equal(y.grad, torch.where(d != 0, gout * scale, torch.zeros_like(gout)))
+    # through the LN hand-off: y's gradient == the separate dropout backward of LN's dx
+    w = torch.randn(144, generator=g).to(gpu)
+    b = torch.randn(144, generator=g).to(gpu)
+    x = torch.randn(6, 41, 144, generator=g).to(gpu).requires_grad_()
+    y.grad = None
+    ln = layer_norm(_residual_dropout(x, y, p, True), w, b, 1e-5)
+    ln.backward(gout)
+    gx, gy = x.grad.clone(), y.grad.clone()
+    d2 = gy != 0
+    assert torch.equal(torch.where(d2, gx * scale, torch.zeros_like(gx)), gy)
+    assert torch.equal(_residual_dropout(x, y, p, False), x + y)
