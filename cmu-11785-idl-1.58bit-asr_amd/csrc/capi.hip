@@ -160,7 +160,8 @@ namespace {
 int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N, int64_t K,
                 const float* W, const float* alpha, int alpha_raw, int bits,
                 const int32_t* bits_dev, const int32_t* pass_bits, float* dW, float* dalpha,
-                float* db, void* ws, size_t ws_bytes, void* stream) {
+                float* db, void* ws, size_t ws_bytes, void* stream,
+                DwFinish* defer = nullptr) {
   if (M < 0 || N < 0 || K < 0 || P < 1 || P > kMaxPasses) return OB_ERR_SHAPE;
   if (!alpha || !dalpha || !ws || (N * K > 0 && (!W || !dW)) || (M > 0 && (!dY || (K > 0 && !X))))
     return OB_ERR_NULL;
@@ -191,8 +192,14 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N
     const DwAlpha al{W, alpha, alpha_raw, bits, reinterpret_cast<const int*>(bits_dev),
                      reinterpret_cast<const int*>(pass_bits), apart};
     launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s, &al);
-    launch_dw_finish(part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, apart,
-                     (int)(p.tiles_n * p.tiles_k * p.chunks), dW, db, dalpha, s);
+    const DwFinish fin{part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, apart,
+                       (int)(p.tiles_n * p.tiles_k * p.chunks), dW, db, dalpha};
+    if (defer) {  // the caller launches it (grouped with other layers' finishes)
+      *defer = fin;
+      return launched();
+    }
+    launch_dw_finish(fin.part, fin.chunks, fin.nk, fin.part_db, fin.n_db, fin.W, fin.alpha,
+                     fin.alpha_raw, fin.apart, fin.n_apart, fin.dW, fin.db, fin.dalpha, s);
     return launched();
   } else {
     launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s);
@@ -639,6 +646,44 @@ int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P, int64
   if (!pass_bits) return OB_ERR_NULL;
   return bwd_dw_impl(dY, X, P, M, N, K, W, alpha, alpha_raw, 2, nullptr, pass_bits, dW, dalpha,
                      db, ws, ws_bytes, stream);
+}
+
+size_t ob_bitlinear_bwd_dw_passes_group_workspace(int64_t G, int64_t P, int64_t M, int64_t N,
+                                                  int64_t K) {
+  if (G < 1 || G > kMaxDwGroup) return 0;
+  const size_t one = ob_bitlinear_bwd_dw_passes_workspace(P, M, N, K);
+  return one ? (size_t)G * align_up(one) : 0;
+}
+
+int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, const float* X,
+                                     int64_t P, int64_t M, int64_t N, int64_t K,
+                                     const float* const* W, const float* const* alpha,
+                                     int alpha_raw, const int32_t* pass_bits, float* const* dW,
+                                     float* const* dalpha, float* const* db, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (G < 1 || G > kMaxDwGroup) return OB_ERR_SHAPE;
+  if (!dY || !W || !alpha || !dW || !dalpha || !db || !pass_bits || !ws) return OB_ERR_NULL;
+  const size_t need = ob_bitlinear_bwd_dw_passes_group_workspace(G, P, M, N, K);
+  if (need == 0) return OB_ERR_SHAPE;
+  if (ws_bytes < need) return OB_ERR_WORKSPACE;
+  const size_t one = need / (size_t)G;
+  DwFinish fin[kMaxDwGroup];
+  bool deferred[kMaxDwGroup] = {false, false, false};
+  for (int64_t i = 0; i < G; ++i) {
+    fin[i].part = nullptr;
+    const int st = bwd_dw_impl(dY[i], X, P, M, N, K, W[i], alpha[i], alpha_raw, 2, nullptr,
+                               pass_bits, dW[i], dalpha[i], db[i],
+                               static_cast<char*>(ws) + i * one, one, stream, &fin[i]);
+    if (st != OB_OK) return st;
+    deferred[i] = fin[i].part != nullptr;
+  }
+  // the LDS path deferred its finish (every layer, at one shape); others finished already
+  int nd = 0;
+  DwFinish grp[kMaxDwGroup];
+  for (int64_t i = 0; i < G; ++i)
+    if (deferred[i]) grp[nd++] = fin[i];
+  if (nd) launch_dw_finish_group(grp, nd, as_stream(stream));
+  return launched();
 }
 
 int ob_dwconv1d_fwd(const float* x, const float* w, const float* bias, int64_t B, int64_t C,

@@ -717,26 +717,25 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
 // thread (82 blocks for a 144 x 144 weight left most CUs idle: 6.4 us per launch).
 // ---------------------------------------------------------------------------------
 constexpr int kFinSlices = 4, kFinElems = kThreads / kFinSlices;
-__global__ __launch_bounds__(kThreads) void dw_finish_kernel(
-    const float* __restrict__ part, int chunks, int64_t nk, const float* __restrict__ part_db,
-    int64_t n_db, const float* __restrict__ W, const float* __restrict__ alpha, int alpha_raw,
-    const float* __restrict__ apart, int n_apart, float* __restrict__ dW, float* __restrict__ db,
-    float* __restrict__ dalpha) {
-  if (blockIdx.x == gridDim.x - 1) {  // alpha: fixed order over the dW blocks
-    if (threadIdx.x >= 64 || !dalpha) return;  // (no alpha: a dense dW)
+// One finish (chunk sum + STE mask, db, dalpha) as block `bid` of `nb` blocks.
+__device__ __forceinline__ void dw_finish_body(const DwFinish& a, int bid, int nb) {
+  if (bid == nb - 1) {  // alpha: fixed order over the dW blocks
+    if (threadIdx.x >= 64 || !a.dalpha) return;  // (no alpha: a dense dW)
     float s2 = 0.0f;
-    for (int i = threadIdx.x; i < n_apart; i += 64) s2 += apart[i];
+    for (int i = threadIdx.x; i < a.n_apart; i += 64) s2 += a.apart[i];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off, 64);
-    if (threadIdx.x == 0) dalpha[0] = s2 * alpha_chain(alpha, alpha_raw);
+    if (threadIdx.x == 0) a.dalpha[0] = s2 * alpha_chain(a.alpha, a.alpha_raw);
     return;
   }
   __shared__ float red[kFinSlices][kFinElems];
   const int el = threadIdx.x % kFinElems, sl = threadIdx.x / kFinElems;
-  const int64_t e = (int64_t)blockIdx.x * kFinElems + el;
+  const int64_t nk = a.nk, n_db = a.n_db;
+  const int chunks = a.chunks;
+  const int64_t e = (int64_t)bid * kFinElems + el;
   const bool is_w = e < nk;
   const bool live = e < nk + n_db;
-  const float* src = is_w ? part + e : part_db + (live ? e - nk : 0);
+  const float* src = is_w ? a.part + e : a.part_db + (live ? e - nk : 0);
   const int64_t stride = is_w ? nk : n_db;
   constexpr int G = 8;
   float cur[G], nxt[G];
@@ -761,14 +760,35 @@ __global__ __launch_bounds__(kThreads) void dw_finish_kernel(
   __syncthreads();
   if (sl != 0 || !live) return;
   g = (red[0][el] + red[1][el]) + (red[2][el] + red[3][el]);
-  if (is_w && !W) {
-    dW[e] = g;  // dense dW (W == nullptr)
+  if (is_w && !a.W) {
+    a.dW[e] = g;  // dense dW (W == nullptr)
   } else if (is_w) {
-    const float a = effective_alpha(alpha, alpha_raw);
-    dW[e] = g * ste_indicator(W[e] / a);  // quant.py:81-82
+    const float al = effective_alpha(a.alpha, a.alpha_raw);
+    a.dW[e] = g * ste_indicator(a.W[e] / al);  // quant.py:81-82
   } else {
-    db[e - nk] = g;
+    a.db[e - nk] = g;
   }
+}
+
+int64_t finish_blocks(const DwFinish& a) { return ceil_div(a.nk + a.n_db, kFinElems) + 1; }
+
+__global__ __launch_bounds__(kThreads) void dw_finish_kernel(DwFinish a) {
+  dw_finish_body(a, blockIdx.x, gridDim.x);
+}
+
+// Several layers' finishes in one launch (the q/k/v projections of one input): block ranges
+// [start[i], start[i+1]) belong to layer i; each layer's arithmetic is unchanged.
+struct DwFinishGroup {
+  DwFinish g[kMaxDwGroup];
+  int start[kMaxDwGroup + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(kThreads) void dw_finish_group_kernel(DwFinishGroup G) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < G.n && b >= G.start[i + 1]) ++i;
+  dw_finish_body(G.g[i], b - G.start[i], G.start[i + 1] - G.start[i]);
 }
 
 bool use_reg_dw() {  // OB_DW=reg: the register-only bf16x6 kernel (A/B experiments)
@@ -895,9 +915,23 @@ void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* pa
                       int64_t n_db, const float* W, const float* alpha, int alpha_raw,
                       const float* apart, int n_apart, float* dW, float* db, float* dalpha,
                       hipStream_t s) {
-  const int64_t nb = ceil_div(nk + n_db, kFinElems) + 1;  // + the alpha block
-  hipLaunchKernelGGL(dw_finish_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, part, chunks, nk,
-                     part_db, n_db, W, alpha, alpha_raw, apart, n_apart, dW, db, dalpha);
+  const DwFinish a{part, chunks, nk, part_db, n_db, W, alpha, alpha_raw, apart, n_apart,
+                   dW, db, dalpha};
+  const int64_t nb = finish_blocks(a);  // + the alpha block
+  hipLaunchKernelGGL(dw_finish_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, a);
+}
+
+void launch_dw_finish_group(const DwFinish* a, int n, hipStream_t s) {
+  DwFinishGroup G{};
+  G.n = n;
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    G.g[i] = a[i];
+    G.start[i] = (int)total;
+    total += finish_blocks(a[i]);
+  }
+  G.start[n] = (int)total;
+  hipLaunchKernelGGL(dw_finish_group_kernel, dim3((unsigned)total), dim3(kThreads), 0, s, G);
 }
 
 }  // namespace ob

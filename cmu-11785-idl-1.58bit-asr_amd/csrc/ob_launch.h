@@ -152,6 +152,26 @@ void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* pa
                       const float* apart, int n_apart, float* dW, float* db, float* dalpha,
                       hipStream_t s);
 
+// The finish of one LDS-path dW (arguments of launch_dw_finish); a group of up to
+// kMaxDwGroup of them runs as one launch (block ranges per layer, same arithmetic).
+struct DwFinish {
+  const float* part;
+  int chunks;
+  int64_t nk;
+  const float* part_db;
+  int64_t n_db;
+  const float* W;
+  const float* alpha;
+  int alpha_raw;
+  const float* apart;
+  int n_apart;
+  float* dW;
+  float* db;
+  float* dalpha;
+};
+constexpr int kMaxDwGroup = 3;
+void launch_dw_finish_group(const DwFinish* a, int n, hipStream_t s);
+
 // dgemm.hip (dense exact-fp32 GEMM of the pointwise convs): false = shape not taken
 bool dense_gemm_supported(int64_t K, int64_t N);
 bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int trans,

@@ -141,6 +141,10 @@ SIGNATURES = {
     "ob_bitlinear_bwd_dw_passes": (
         _int, [_c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f, _c_f,
                _sz, _c_f]),
+    "ob_bitlinear_bwd_dw_passes_group_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "ob_bitlinear_bwd_dw_passes_group": (  # pointer arrays: host addresses (ptr_array)
+        _int, [_i64, _c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f,
+               _c_f, _sz, _c_f]),
     "ob_relattn_fwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32, _c_f,
                _i64, _c_f, _c_f, _c_f]),
@@ -185,6 +189,12 @@ def load() -> ctypes.CDLL:
         raise OneBitHipError(f"ABI mismatch: library {lib.ob_abi_version()} != {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+def ptr_array(ptrs):
+    """A host array of device addresses for the C ABI's ``T* const*`` arguments; keep the
+    returned object alive across the call and pass ``ctypes.addressof`` of it."""
+    return (ctypes.c_void_p * len(ptrs))(*[p or None for p in ptrs])
 
 
 def check(status: int, what: str) -> None:

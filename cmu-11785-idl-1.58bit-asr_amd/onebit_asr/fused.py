@@ -23,6 +23,7 @@ from the same (seed, counter + offset).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Dict, Optional
 
@@ -35,6 +36,7 @@ from .quant import PassBits, QuantizedLinear
 __all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
            "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8", "qkv_projections"]
 
+_DW_GROUP = os.environ.get("OB_DW_GROUP", "1") != "0"  # 0: q/k/v dW finishes one by one
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
 
@@ -266,8 +268,31 @@ class _QKVFn(torch.autograd.Function):
                     a.data_ptr(), 1, None, k, gh.data_ptr(), 1.0, 0.0, None, 0, None, 0,
                     gh.data_ptr(), stream), "ob_bitlinear_fwd_residual (dX accumulate)")
         grads = {}
+        if _DW_GROUP and pb is not None and len(layers) == 3 and \
+                len({w.shape for _, w, _, _, _ in layers}) == 1:
+            # the three dW GEMMs share X = h: their finishes in one launch
+            n = layers[0][1].shape[0]
+            wsb = lib.ob_bitlinear_bwd_dw_passes_group_workspace(3, P, m, n, k)
+            if wsb:
+                outs = [(torch.empty_like(w), torch.empty((), dtype=torch.float32, device=h.device),
+                         torch.empty((n,), dtype=torch.float32, device=h.device) if hb else None)
+                        for _, w, _, _, hb in layers]
+                ws = torch.empty((wsb,), dtype=torch.uint8, device=h.device)
+                arrs = [_lib.ptr_array(v) for v in (
+                    [g.data_ptr() for g, _, _, _, _ in layers],
+                    [w.data_ptr() for _, w, _, _, _ in layers],
+                    [a.data_ptr() for _, _, a, _, _ in layers],
+                    [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs],
+                    [_lib.ptr(o[2]) for o in outs])]
+                ad = [ctypes.addressof(x) for x in arrs]
+                _lib.check(lib.ob_bitlinear_bwd_dw_passes_group(
+                    3, ad[0], h.data_ptr(), P, m, n, k, ad[1], ad[2], 1, pb.data_ptr(), ad[3],
+                    ad[4], ad[5], ws.data_ptr(), wsb, stream), "ob_bitlinear_bwd_dw_passes_group")
+                for (_, w, _, _, _), o in zip(layers, outs):
+                    grads[id(w)] = o
         for i, (g, w, a, c, hb) in zip(range(3), layers):
-            grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream)
+            if id(w) not in grads:
+                grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream)
         out = [gh]
         for w in (wq, wk, wv):
             out.extend(grads.get(id(w), (None, None, None)))

@@ -308,6 +308,19 @@ OB_API int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P
                                       int alpha_raw, const int32_t* pass_bits, float* dW,
                                       float* dalpha, float* db, void* ws, size_t ws_bytes,
                                       void* stream);
+/* G (<= 3) layers of the same input X and shape (the q/k/v projections of one LayerNorm
+ * output, conformer.py:111-113): ob_bitlinear_bwd_dw_passes of each, their finishes (chunk
+ * sum, STE mask, db, dalpha) in ONE launch. Same arithmetic per layer. Arrays of G device
+ * pointers (host arrays); db[i] may be NULL. ws: ..._group_workspace(G, P, M, N, K) bytes. */
+OB_API size_t ob_bitlinear_bwd_dw_passes_group_workspace(int64_t G, int64_t P, int64_t M,
+                                                         int64_t N, int64_t K);
+OB_API int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, const float* X,
+                                            int64_t P, int64_t M, int64_t N, int64_t K,
+                                            const float* const* W, const float* const* alpha,
+                                            int alpha_raw, const int32_t* pass_bits,
+                                            float* const* dW, float* const* dalpha,
+                                            float* const* db, void* ws, size_t ws_bytes,
+                                            void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Relative-position attention core of MHSA.forward (onebit_asr/conformer.py:115-127),

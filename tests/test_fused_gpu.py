@@ -270,6 +270,16 @@ def test_qkv_projections_match_separate_layers(gpu, stacked):
     assert (dh0 - dh1).abs().max().item() <= 1e-6 * dh0.abs().max().item()
     for a, b in zip(g0, g1):
         assert (a - b).abs().max().item() <= 1e-6 * max(a.abs().max().item(), 1e-30), (a, b)
+    # stacked: the three dW finishes run as one grouped launch; the same bits as one by one
+    from onebit_asr import fused
+
+    prev, fused._DW_GROUP = fused._DW_GROUP, False
+    try:
+        _, _, g2 = run(True)
+    finally:
+        fused._DW_GROUP = prev
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
 
 
 def test_decoder_residual_dropout(gpu):
