@@ -70,6 +70,9 @@ def parse():
                     help="opt-in ternary conv-module pw1/pw2 (north_star; not reference math)")
     ap.add_argument("--conv-find", action="store_true",
                     help="torch.backends.cudnn.benchmark (MIOpen Find) for the subsampling convs")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 exchange: nccl (= RCCL, one GPU per rank) or gloo (ranks may "
+                         "share a GPU: the -m gpu test of the multi-rank bench on a 1-GPU box)")
     args = ap.parse_args()
     if args.conv_find:
         torch.backends.cudnn.benchmark = True
@@ -439,18 +442,72 @@ def log(args, msg):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def spawn_ranks(args) -> int:
+    """``bench.py --gpus N`` started as ONE process (no WORLD_SIZE in the environment): start
+    the N ranks as fresh child processes under torch.distributed.run -- before this process
+    has touched the GPU (nothing above initialises HIP; no exec) -- and print rank 0's JSON
+    line. Fails loudly when the line does not report N ranks."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           str(Path(__file__).resolve())] + sys.argv[1:]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    for ln in r.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if r.returncode != 0:
+        print(f"bench: {args.gpus}-rank run failed (exit {r.returncode})", file=sys.stderr)
+        return r.returncode or 1
+    if len(lines) != 1:
+        print(f"bench: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    if json.loads(lines[0]).get("n_gpus") != args.gpus:
+        print(f"bench: the line reports n_gpus != --gpus {args.gpus}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+def replicas_equal(model, dev) -> bool:
+    """After the timed steps: are the N replicas' parameters bitwise identical? (elementwise
+    max == min over ranks of every parameter)."""
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).to(dev)
+    hi, lo = flat.clone(), flat.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo))
+
+
 def main():
     args = parse()
     if args.mode.startswith("infer"):
         return run_infer(args)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE {world} != --gpus {args.gpus}")
     distributed = world > 1
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local >= n_dev:
+        raise SystemExit(f"bench: rank {rank} needs GPU {local} but only {n_dev} are visible "
+                         "(RCCL takes one GPU per rank; --dist-backend gloo shares one)")
+    dev = torch.device("cuda", local % max(n_dev, 1))
     if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     if os.environ.get("OB_BLAS_ALL"):  # A/B experiments: one BLAS library for every GEMM
         torch.backends.cuda.preferred_blas_library(os.environ["OB_BLAS_ALL"])
 
@@ -480,7 +537,7 @@ def main():
         if distributed:
             from torch.nn.parallel import DistributedDataParallel as DDP
 
-            step_mod = DDP(step_mod, device_ids=[local], broadcast_buffers=False,
+            step_mod = DDP(step_mod, device_ids=[dev.index], broadcast_buffers=False,
                            gradient_as_bucket_view=True)
         opt = make_optimizer(model.parameters())
         sched = WarmupCosine(opt, warmup_steps=4000, total_steps=100000)
@@ -524,6 +581,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     loss_val = float(loss.item())
+    same = replicas_equal(model, dev) if distributed else None
 
     frames_total = world * args.batch * args.frames * args.steps
     value = frames_total / elapsed
@@ -546,12 +604,18 @@ def main():
                    "execution": "eager" if args.eager else "hip-graph",
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
                    "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
-                   "parallelism": f"dp{world}", "passes": "teacher 2-bit + student 1-bit + SP",
+                   "parallelism": f"dp{world}",
+                   "exchange": (f"one flat fp32 gradient all-reduce per step over "
+                                f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'}"
+                                if distributed else None),
+                   "passes": "teacher 2-bit + student 1-bit + SP",
                    "subsampling": "computed once, shared by the 3 stacked passes (exact: no "
                                   "dropout, full-precision weights; the reference runs it 3x)",
                    "conv_pointwise": "ternary (opt-in)" if args.conv_pw_ternary else "fp32 (reference)"},
         "final_loss": round(loss_val, 4),
     }
+    if distributed:
+        out["replicas_bitwise_equal"] = same
     if quant_off:  # no ternary kernel runs: the line is the ceiling the 1.58-bit step is read against
         out["roofline"] = None
     elif rank == 0 and world == 1 and not args.no_roofline:

@@ -51,6 +51,25 @@ def _rng(device: torch.device):
     return st[0], off
 
 
+def rng_snapshot(device: torch.device):
+    """The fused call sites' dropout state on ``device`` ({seed, counter} tensor + the host
+    offset), for undoing warm-up steps (graph_step.GraphedTrainStep)."""
+    st = _STATE.get(device)
+    return None if st is None else (st[0].clone(), st[1])
+
+
+def rng_restore(device: torch.device, snap) -> None:
+    if snap is None:
+        _STATE.pop(device, None)
+        return
+    st = _STATE.get(device)
+    if st is None:
+        _STATE[device] = [snap[0].clone(), snap[1]]
+    else:
+        st[0].copy_(snap[0])  # in place: captured kernels keep reading this tensor
+        st[1] = snap[1]
+
+
 def advance_step(device: torch.device) -> None:
     """New dropout masks for every fused call site of the next step (one tiny kernel)."""
     st = _STATE.get(device)
@@ -63,6 +82,9 @@ def fused_supported(x: torch.Tensor, *layers: QuantizedLinear, bitwidth=None) ->
         return False
     if not (isinstance(bitwidth, PassBits) or bitwidth in (1, 2)):
         return False  # 32 (F.linear), DynamicBitwidth and invalid values take the module path
+    for m in layers:  # packed-ternary layers are inference-only: training raises here too
+        if m._packed is not None:
+            m._check_packed_use(bitwidth)
     return x.is_cuda and x.dtype == torch.float32 and all(
         m.act_quant is None and m.quant_off is None for m in layers)
 
@@ -367,6 +389,9 @@ def i8_fused_supported(x: torch.Tensor, *layers: QuantizedLinear, bitwidth=None,
         return False
     if isinstance(bitwidth, PassBits) or bitwidth not in (1, 2):
         return False
+    for m in layers:
+        if m._packed is not None:
+            m._check_packed_use(bitwidth)
     lib = _lib.load()
     return (x.is_cuda and x.dtype == torch.float32
             and all(m.act_quant == "absmax_int8" and m.quant_off is None

@@ -161,18 +161,35 @@ class GraphedTrainStep:
         for _ in range(self.warmup_iters):
             self.loss, self.parts = self._eager()
 
-    def _snapshot(self):
-        return [p.detach().clone() for p in self.params]
+    def _rng_snapshot(self):
+        from .fused import rng_snapshot
+
+        cuda = self.device.type == "cuda"
+        return (rng_snapshot(self.device),
+                torch.cuda.get_rng_state(self.device) if cuda else torch.get_rng_state())
+
+    def _snapshot(self, rng):
+        return [p.detach().clone() for p in self.params], rng
 
     @torch.no_grad()
     def _restore(self, snap):
         """Undo the warm-up: parameters back to their values, optimizer state and schedule
         back to a fresh start (AdamW's state starts at zero with step 0), so that the
-        first ``step()`` performs exactly one update (train.py:114-120). In-place writes
-        keep every address the captured graph will use and bump the parameters' versions
-        (which invalidates version-keyed code caches)."""
-        for p, s in zip(self.params, snap):
+        first ``step()`` performs exactly one update (train.py:114-120); the dropout
+        streams (the fused call sites' hash counter and host offsets, torch's generator)
+        back to where they were, so the first real step draws the masks an un-warmed run
+        would. In-place writes keep every address the captured graph will use and bump the
+        parameters' versions (which invalidates version-keyed code caches)."""
+        from .fused import rng_restore
+
+        params, (rng, torch_rng) = snap
+        for p, s in zip(self.params, params):
             p.copy_(s)
+        rng_restore(self.device, rng)
+        if self.device.type == "cuda":
+            torch.cuda.set_rng_state(torch_rng, self.device)
+        else:
+            torch.set_rng_state(torch_rng)
         if self.fused:
             self.opt.reset_state()
         else:
@@ -191,7 +208,8 @@ class GraphedTrainStep:
     def prime(self, batch, sp_mask):
         """Static inputs, flat grads, optimizer; ``warmup_iters`` eager steps on a side stream
         (library heuristics, allocator) whose effects are then undone; then capture. The
-        warm-up leaves no trace: the model, optimizer and schedule are restored."""
+        warm-up leaves no trace: the model, optimizer, schedule and dropout streams are
+        restored."""
         self._set_batch(batch)
         self.bits.set(sp_mask)
         if self.device.type != "cuda":  # host path (gloo tests of the exchange logic)
@@ -201,8 +219,9 @@ class GraphedTrainStep:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
+            rng = self._rng_snapshot()  # before the discovery pass draws any mask
             self._discover_params()
-            snap = self._snapshot()
+            snap = self._snapshot(rng)
             self._warm()
             self._restore(snap)
         torch.cuda.current_stream(self.device).wait_stream(side)

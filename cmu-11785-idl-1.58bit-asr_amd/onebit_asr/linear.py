@@ -40,9 +40,11 @@ _DENSE = os.environ.get("OB_DENSE_LINEAR", "1") != "0"
 _DENSE_DW = _DENSE and os.environ.get("OB_DENSE_LINEAR_DW", "1") != "0"
 
 
-def _dense_ok(x: torch.Tensor, k: int, n: int) -> bool:
+def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
+    """ob_dense_gemm's preconditions (capi.hip: aligned16 of BOTH operands), so an operand
+    it would refuse takes the library path instead of raising."""
     return (_DENSE and k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
-            and _lib.load().ob_dense_supported(k, n) == 1)
+            and w.data_ptr() % 16 == 0 and _lib.load().ob_dense_supported(k, n) == 1)
 
 
 def _dense_dw_ws(g2: torch.Tensor, x2d: torch.Tensor, w: torch.Tensor) -> int:
@@ -83,7 +85,7 @@ class _LinearFn(torch.autograd.Function):
         k = x.shape[-1]
         x2d = x.reshape(-1, k)
         n = weight.shape[0]
-        if dtype is None and x2d.is_contiguous() and weight.is_contiguous() and _dense_ok(x2d, k, n):
+        if dtype is None and x2d.is_contiguous() and weight.is_contiguous() and _dense_ok(x2d, weight, k, n):
             y = _dense(x2d, weight, 0, bias, n)
         elif dtype is None:
             y = torch.addmm(bias, x2d, weight.t()) if bias is not None else x2d @ weight.t()
@@ -107,7 +109,7 @@ class _LinearFn(torch.autograd.Function):
         if dtype is None:
             if ctx.needs_input_grad[0]:
                 k = weight.shape[1]
-                if weight.is_contiguous() and _dense_ok(g2, weight.shape[0], k):
+                if weight.is_contiguous() and _dense_ok(g2, weight, weight.shape[0], k):
                     gx = _dense(g2, weight, 1, None, k).view(xshape)
                 else:
                     gx = (g2 @ weight).view(xshape)

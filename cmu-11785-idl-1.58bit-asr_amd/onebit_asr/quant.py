@@ -583,6 +583,15 @@ class QuantizedLinear(nn.Module):
         optimizer steps, ``load_state_dict`` and in-place ops on the parameters do not need it."""
         self._codes_cache = {}
 
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        """A packed layer's ``weight`` is a placeholder (the codes came from a packed
+        checkpoint): it is left out, so that the state dict cannot be mistaken for an fp32
+        checkpoint (a strict load of it reports the missing weight; a packed model is
+        saved with checkpoint.save_packed's source model or re-exported from its file)."""
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        if self._packed is not None:
+            destination.pop(prefix + "weight", None)
+
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self._codes_cache = {}
         if prefix + "weight" in state_dict:  # an fp32 weight replaces packed codes

@@ -54,3 +54,22 @@ def test_conformer_s_packed_size(gpu, tmp_path):
     codes = sum(v.numel() * 4 for k, v in tensors.items() if ".codes" in k)
     assert codes <= qw * 2 / 8 * 1.13  # 2 bits per weight (+ row padding to 16)
     assert len(_quant_layers(model)) >= 16 * 4
+
+
+def test_packed_model_refuses_training_on_fused_paths(gpu, tmp_path):
+    """the fused FFN / q-k-v / out_proj call sites check the packed layers too, so
+    a forward with grad enabled raises instead of training on placeholder weights."""
+    from onebit_asr.checkpoint import load_packed, save_packed
+    from onebit_asr.data import CFG1, synthetic_batch
+
+    src = _build(CFG1, gpu, 0)
+    f = tmp_path / "cfg1.safetensors"
+    save_packed(src, f)
+    dst = load_packed(_build(CFG1, gpu, 1), f, device=gpu).train()
+    batch = synthetic_batch([400, 300], [20, 10], seed=3, device=gpu)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        dst(batch, precision=2)
+    # the packed layers' placeholder weights stay out of the state dict
+    sd = dst.state_dict()
+    assert "encoder.blocks.0.ff1.lin1.weight" not in sd
+    assert "encoder.blocks.0.ff1.lin1.alpha" in sd

@@ -1,0 +1,116 @@
+"""Conformer-S (BASELINE configs[1] architecture) against the CPU oracle, not against itself.
+
+Full model: 16 blocks, d_model 144, 4 heads (d_head 36), d_ff 576, conv kernel 31, the 2-layer
+decoder, V = 5004, dropout 0. Batch: 4 utterances x 1000 frames (T' = 249), 40 tokens each --
+the S kernel paths (ternary GEMM K = 576 tiles, attention at d_head 36 / T' 249, dW at
+144-wide tiles, conv module at C = 144, subsampling at C = 144) that the cfg1 test
+(tests/test_model_gpu.py) never takes.
+
+Bars (the cfg1 bars of tests/test_model_gpu.py):
+  * forward at precision 2, precision 1 and an SP mask: CTC logits max|err| <= 1e-3, the
+    frame masks equal, the CTC loss rel <= 1e-4;
+  * the stacked three-pass step (train.py:82-111) vs ``oracle_step_loss`` (the reference's
+    literal three forwards): loss rel <= 1e-4, every loss part rtol 1e-4;
+  * EVERY parameter gradient rel-L2 <= 1e-3 (alpha <= 2e-3); parameters whose true gradient
+    is zero (key biases, the depthwise bias before BatchNorm, the key third of the
+    decoder's in_proj_bias) within 1e-6 absolute.
+Reference: onebit_asr/conformer.py:243-272,315-319, onebit_asr/train.py:82-111.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+S_ORACLE = dict(input_dim=80, vocab_size=5004, d_model=144, n_layers=16, n_heads=4, d_ff=576,
+                conv_kernel=31, dec_layers=2, dec_heads=4, dec_d_ff=1024, dropout=0.0)
+SP_MASK = [1, 0, 1, 1, 0, 0, 1, 0, 1, 0, 0, 1, 1, 0, 1, 0]
+ZERO_GRAD = ("k_proj.bias", "conv.dw.bias", "in_proj_bias")
+BAR_ALPHA = 2e-3
+BAR = 1e-3
+
+
+@pytest.fixture(scope="module")
+def s_pair(gpu):
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CONFORMER_S
+    from oracle.conformer_oracle import OracleConformer
+
+    cfg = dict(CONFORMER_S, enc_dropout=0.0, dec_dropout=0.0)
+    torch.manual_seed(4242)
+    prod = ConformerASR(80, 5004, **cfg).to(gpu)
+    orc = OracleConformer(prod.state_dict(), **S_ORACLE)
+    return prod, orc
+
+
+@pytest.fixture(scope="module")
+def s_batch():
+    from onebit_asr.data import synthetic_batch
+
+    return synthetic_batch([1000] * 4, [40] * 4, seed=77)
+
+
+def _to(b, dev):
+    return {k: v.to(dev) for k, v in b.items()}
+
+
+@pytest.mark.parametrize("precision,sp_mask", [(2, None), (1, None), (2, SP_MASK)])
+def test_s_forward_matches_oracle(s_pair, s_batch, gpu, precision, sp_mask):
+    from onebit_asr.losses import ctc_loss_from_logits
+
+    prod, orc = s_pair
+    with torch.no_grad():
+        _, mask_p, lg_p = prod(_to(s_batch, gpu), precision, sp_mask)
+        _, mask_o, lg_o = orc(s_batch, precision, sp_mask)
+    assert lg_p.shape == (4, 249, 5004)
+    assert torch.equal(mask_p.cpu(), mask_o)
+    err = (lg_p.cpu() - lg_o).abs().max().item()
+    assert err <= 1e-3, err
+    lp = ctc_loss_from_logits(lg_p, mask_p.sum(1).long(), s_batch["tokens"].to(gpu),
+                              s_batch["token_lens"].to(gpu), 3).item()
+    lo = ctc_loss_from_logits(lg_o, mask_o.sum(1).long(), s_batch["tokens"],
+                              s_batch["token_lens"], 3).item()
+    assert abs(lp - lo) <= 1e-4 * abs(lo), (lp, lo)
+
+
+def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
+    from onebit_asr.train_step import OneBitStep
+    from oracle.conformer_oracle import oracle_step_loss
+
+    prod, orc = s_pair
+    step = OneBitStep(prod, n_layers=16, stacked=True)
+    prod.zero_grad(set_to_none=True)
+    orc.zero_grad(set_to_none=True)
+    loss_p, parts_p = step(_to(s_batch, gpu), SP_MASK)
+    loss_p.backward()
+    loss_o, parts_o = oracle_step_loss(orc, s_batch, SP_MASK)
+    loss_o.backward()
+    assert abs(loss_p.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item()), (loss_p, loss_o)
+    np.testing.assert_allclose(parts_p.cpu().numpy(), parts_o.numpy(), rtol=1e-4, atol=1e-6)
+    ref = dict(orc.named_reference_parameters())
+    names = [n for n, _ in prod.named_parameters()]
+    assert set(names) == set(ref), set(names) ^ set(ref)
+    checked = 0
+    worst = (None, 0.0)
+    for name, p in prod.named_parameters():
+        g_p = p.grad.detach().cpu().double()
+        g_o = ref[name].grad.detach().double()
+        d = g_p - g_o
+        if any(z in name for z in ZERO_GRAD):
+            if name.endswith("in_proj_bias"):  # only the key third is zero in truth
+                e = g_o.numel() // 3
+                for part in (slice(0, e), slice(2 * e, 3 * e)):
+                    rel = d[part].norm().item() / max(g_o[part].norm().item(), 1e-12)
+                    assert rel <= BAR, (name, rel)
+                d = d[e:2 * e]
+            assert d.abs().max().item() <= 1e-6, (name, d.abs().max().item())
+            continue
+        rel = d.norm().item() / max(g_o.norm().item(), 1e-12)
+        bar = BAR_ALPHA if name.endswith(".alpha") else BAR
+        assert rel <= bar or d.abs().max().item() <= 1e-7, (name, rel, bar)
+        if rel > worst[1]:
+            worst = (name, rel)
+        checked += 1
+    # 16 blocks x (9 BitLinears x 3 params + LNs, conv module, pos biases) + the rest
+    assert checked > 700, checked
+    print("worst gradient rel-L2:", worst)
