@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kThreads) void drop_scale_bwd_kernel(
   auto one = [&](int64_t i, float g) -> float {
     const int64_t row = i / N;
     float v = g;
-    if (dc.on) v = nc_mul(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
+    if (dc.on) v = nc_mul(v, drop_keep(dkey, (uint64_t)i, dc.thresh) ? dc.scale : 0.0f);
     if (lens) {
       const int64_t b = row / T;
       if (row - b * T >= lens[b]) v = nc_mul(v, 0.0f);
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kThreads) void residual_drop_fwd_kernel(
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < total; i += stride) {
     float v = Y[i];
-    if (dc.on) v = nc_mul(v, drop_hash(dkey, (uint64_t)i) >= dc.thresh ? dc.scale : 0.0f);
+    if (dc.on) v = nc_mul(v, drop_keep(dkey, (uint64_t)i, dc.thresh) ? dc.scale : 0.0f);
     if (lens) {
       const int64_t row = i / N, b = row / T;
       if (row - b * T >= lens[b]) v = nc_mul(v, 0.0f);

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
           // the same operation sequence as drop_scale_bwd_kernel
           float w = o[e];
           if (gs.dc.on)
-            w = nc_mul(w, drop_hash(dkey, (uint64_t)(row * d + c0 + e)) >= gs.dc.thresh ? gs.dc.scale : 0.0f);
+            w = nc_mul(w, drop_keep(dkey, (uint64_t)(row * d + c0 + e), gs.dc.thresh) ? gs.dc.scale : 0.0f);
           if (!rvalid) w = nc_mul(w, 0.0f);
           w2[e] = gs.rscale == 1.0f ? w : nc_mul(gs.rscale, w);
         }

@@ -1,11 +1,17 @@
 // ob_drop.h — the counter-based dropout keep-hash shared by every fused-dropout kernel
 // (attention probabilities, BitLinear epilogues, the dropout-backward scale kernel).
 //
-// keep(i) = drop_hash(drop_key(seed, ctr), i) >= thresh: a 32-bit murmur3-fmix hash of the
-// element index mixed with a per-call key. The key folds (seed, counter) -- a device
+// keep(i) = the 16-bit field (i & 1) of drop_hash(drop_key(seed, ctr), i >> 1) >= thresh:
+// one 32-bit murmur3-fmix hash of the element-PAIR index, mixed with a per-call key, draws
+// two elements (its low and high halves). The key folds (seed, counter) -- a device
 // int64[2] the host advances once per call -- so a captured HIP graph draws a fresh mask
 // on every replay, and a backward kernel regenerates its forward's mask from the same
-// (seed, counter) without storing it. ~8 VALU ops (2 multiplies) per element.
+// (seed, counter) without storing it. ~8 VALU ops (2 multiplies) per PAIR of elements.
+// Mask quality: fmix32 is a bijection whose every output bit depends on every input bit
+// (full avalanche), so the two 16-bit halves of one hash are as independent as two hashes
+// of nearby indices; the drop probability is thresh / 2^16 with thresh = round(p * 2^16),
+// |p_eff - p| <= 2^-17 (p = 0.1: 6554 / 65536 = 0.100006), and the keep scale stays the
+// reference's 1 / (1 - p).
 // The mask is not torch's Philox stream; no reference-visible quantity depends on it
 // (dropout is stochastic in the reference too, train.py:200; parity runs use p = 0).
 #pragma once
@@ -38,7 +44,7 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t idx) {
 }
 
 struct DropCfg {
-  uint32_t thresh;  // keep iff hash >= thresh
+  uint32_t thresh;  // keep iff the element's 16-bit field >= thresh
   float scale;      // 1 / (1 - p)
   int on;
 };
@@ -46,11 +52,27 @@ struct DropCfg {
 inline DropCfg make_drop(float p_drop) {
   DropCfg dc;
   dc.on = p_drop > 0.0f ? 1 : 0;
-  double t = (double)p_drop * 4294967296.0;
-  if (t > 4294967295.0) t = 4294967295.0;
+  double t = (double)p_drop * 65536.0 + 0.5;
+  if (t > 65536.0) t = 65536.0;  // p = 1: every field (< 2^16) drops
   dc.thresh = (uint32_t)t;
-  dc.scale = p_drop > 0.0f ? (float)(1.0 / (1.0 - (double)p_drop)) : 1.0f;
+  dc.scale = p_drop > 0.0f && p_drop < 1.0f ? (float)(1.0 / (1.0 - (double)p_drop)) : 1.0f;
   return dc;
+}
+
+// keep bit of element i (one hash per element pair; pairs (2j, 2j+1))
+__device__ __forceinline__ bool drop_keep(uint32_t key, uint64_t i, uint32_t thresh) {
+  const uint32_t h = drop_hash(key, i >> 1);
+  return ((i & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thresh;
+}
+
+// keep scales of elements i .. i+3 (i % 4 == 0): two hashes
+__device__ __forceinline__ void drop_scale4(uint32_t key, uint64_t i, const DropCfg& dc,
+                                            float (&out)[4]) {
+  const uint32_t h0 = drop_hash(key, i >> 1), h1 = drop_hash(key, (i >> 1) + 1);
+  out[0] = (h0 & 0xFFFFu) >= dc.thresh ? dc.scale : 0.0f;
+  out[1] = (h0 >> 16) >= dc.thresh ? dc.scale : 0.0f;
+  out[2] = (h1 & 0xFFFFu) >= dc.thresh ? dc.scale : 0.0f;
+  out[3] = (h1 >> 16) >= dc.thresh ? dc.scale : 0.0f;
 }
 
 }  // namespace ob

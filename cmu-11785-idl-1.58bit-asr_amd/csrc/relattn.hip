@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       float pd = pr;
       bool keep = true;
       if (dc.on && !RA_EXP_NODROP) {
-        keep = drop_hash(dkey, prow_off + jj) >= dc.thresh;
+        keep = drop_keep(dkey, prow_off + jj, dc.thresh);
         pd = keep ? pr * dc.scale : 0.0f;
       }
       // the keep decision rides in the sign bit (P >= 0): the backward kernels read it
@@ -914,7 +914,7 @@ __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropC
                                                                 uint8_t* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e >= n) return;
-  out[e] = (!dc.on || drop_hash(drop_key(rng[0], rng[1] + rng_off), (uint64_t)e) >= dc.thresh) ? 1 : 0;
+  out[e] = (!dc.on || drop_keep(drop_key(rng[0], rng[1] + rng_off), (uint64_t)e, dc.thresh)) ? 1 : 0;
 }
 
 

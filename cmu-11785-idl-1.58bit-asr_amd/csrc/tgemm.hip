@@ -125,7 +125,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ep, uint32_t dkey, floa
                                           int64_t grow, int col, int N, float y, float rv) {
   const int64_t i = grow * N + col;
   const float keep =
-      (ep.dc.on && !TG_EXP_NODROP) ? (drop_hash(dkey, (uint64_t)i) >= ep.dc.thresh ? ep.dc.scale : 0.0f) : 1.0f;
+      (ep.dc.on && !TG_EXP_NODROP) ? (drop_keep(dkey, (uint64_t)i, ep.dc.thresh) ? ep.dc.scale : 0.0f) : 1.0f;
   if constexpr (MODE == kEpiSwishDrop) {
     ep.C2[i] = y;
     const float sv = silu_f(y);
@@ -198,12 +198,8 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
                                            int64_t grow, int col, int N, f32x4 y, bool valid,
                                            const f32x4& rv) {
   const int64_t i = grow * N + col;
-  f32x4 keep = {1.f, 1.f, 1.f, 1.f};
-  if (ep.dc.on && !TG_EXP_NODROP) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      keep[e] = drop_hash(dkey, (uint64_t)(i + e)) >= ep.dc.thresh ? ep.dc.scale : 0.0f;
-  }
+  float keep[4] = {1.f, 1.f, 1.f, 1.f};
+  if (ep.dc.on && !TG_EXP_NODROP) drop_scale4(dkey, (uint64_t)i, ep.dc, keep);  // i % 4 == 0
   f32x4 out;
   if constexpr (MODE == kEpiNone) {
     out = y;

@@ -40,11 +40,14 @@ _DW_GROUP = os.environ.get("OB_DW_GROUP", "1") != "0"  # 0: q/k/v dW finishes on
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
 
+def _seed() -> int:
+    return (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + 0x5851F42D) & ((1 << 62) - 1)
+
+
 def _rng(device: torch.device):
     st = _STATE.get(device)
     if st is None:
-        seed = (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + 0x5851F42D) & ((1 << 62) - 1)
-        st = [torch.tensor([seed, 0], dtype=torch.int64, device=device), 0]
+        st = [torch.tensor([_seed(), 0], dtype=torch.int64, device=device), 0]
         _STATE[device] = st
     off = st[1]
     st[1] = (st[1] + 1) & ((1 << 32) - 1)
@@ -59,10 +62,14 @@ def rng_snapshot(device: torch.device):
 
 
 def rng_restore(device: torch.device, snap) -> None:
-    if snap is None:
-        _STATE.pop(device, None)
-        return
+    """Back to ``snap``; ``None`` (no state existed) = the state a first draw would create,
+    written in place (a capture that follows must not allocate)."""
     st = _STATE.get(device)
+    if snap is None:
+        if st is not None:
+            st[0].copy_(torch.tensor([_seed(), 0], dtype=torch.int64))
+            st[1] = 0
+        return
     if st is None:
         _STATE[device] = [snap[0].clone(), snap[1]]
     else:

