@@ -989,28 +989,34 @@ size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
   return align_up(relattn_bwd_workspace(Bt, T, H, d));
 }
 
-int ob_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
-                   const float* pos, const float* u, const float* vb, const int32_t* lens,
-                   int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                   const int64_t* rng, int64_t rng_offset, const float* probs, float* dq,
-                   float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
+int64_t ob_relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
+  if (Bt < 1 || H < 1 || T < 1) return 0;
+  return relattn_probs_elems(Bt, T, H);
+}
+
+int ob_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
+                   const float* v, const float* pos, const float* u, const float* vb,
+                   const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d,
+                   float p_drop, const int64_t* rng, int64_t rng_offset, const float* probs,
+                   float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
                    size_t ws_bytes, void* stream) {
   if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
-  if (!dctx || !q || !k || !v || !pos || !u || !vb || !lens || !probs || !dq || !dk || !dv ||
-      !dpos || !du || !dvb || !ws || (p_drop > 0.0f && !rng))
+  if (!dctx || !ctx || !q || !k || !v || !pos || !u || !vb || !lens || !probs || !dq || !dk ||
+      !dv || !dpos || !du || !dvb || !ws)
     return OB_ERR_NULL;
+  (void)rng;  // the forward's keep bits ride in probs' sign bits
+  (void)rng_offset;
   if (ws_bytes < ob_relattn_bwd_workspace(Bt, T, H, d)) return OB_ERR_WORKSPACE;
-  launch_relattn_bwd(dctx, q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop,
-                     reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset, probs, dq, dk,
-                     dv, dpos, du, dvb, ws, as_stream(stream));
+  launch_relattn_bwd(dctx, ctx, q, k, v, pos, u, vb, Bt, P, T, H, d, p_drop, probs, dq, dk, dv,
+                     dpos, du, dvb, ws, as_stream(stream));
   return launched();
 }
 
-int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng, int64_t rng_offset,
-                            uint8_t* out, void* stream) {
-  if (n < 0 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+int ob_relattn_dropout_mask(int64_t n, int64_t row_len, float p_drop, const int64_t* rng,
+                            int64_t rng_offset, uint8_t* out, void* stream) {
+  if (n < 0 || row_len < 1 || !(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
   if ((n > 0 && !out) || (p_drop > 0.0f && !rng)) return OB_ERR_NULL;
-  launch_relattn_dropout_mask(n, p_drop, reinterpret_cast<const uint64_t*>(rng),
+  launch_relattn_dropout_mask(n, row_len, p_drop, reinterpret_cast<const uint64_t*>(rng),
                               (uint64_t)rng_offset, out, as_stream(stream));
   return launched();
 }

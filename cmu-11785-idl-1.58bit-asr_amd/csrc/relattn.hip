@@ -14,73 +14,29 @@
 // per-query-tile partials), plus two small fixed-order reductions (du/dvb over tiles,
 // dpos over the pass's batch rows).
 //
-// rel_shift as a gather: with X = (q + v) p^T,
-//   bd[i][j] = X[i][T-1-i+j]   (j <= i);   0   (j == i+1);   X[i+1][j-i-2]   (j >= i+2)
-// and its adjoint: dX[i][m] = dbd[i][m-T+1+i] (m >= T-1-i), else dbd[i-1][m+i+1] (i >= 1).
+// rel_shift as a FLAT re-reading (conformer.py:97-103 pads a zero column on the left of X =
+// (q + v) p^T, views the [T][T+1] result as [T+1][T] and drops the first row): with
+// Xpad[r] = [0, X[r][0 .. T-1]] stored row after row at pitch T+1,
+//   bd[i][j] = Xpad.flat[T + i*T + j]
+// so the forward reads bd at a lane base + an immediate offset (no per-element branch), and
+// the adjoint is the same map backwards: dX[r][m] = dS'.flat[r*(T+1) + m + 1 - T] (0 where
+// that index is negative, i.e. only in row 0), read from a row-major dS' band at pitch T.
 //
 // Layout: q, k, v, ctx, dq, dk, dv [Bt][T][H*d]; pos, dpos [P][T][H*d] (batch row b uses
-// pass b / (Bt/P)); u, vb, du, dvb [H][d]; probs [Bt][H][T][T]; lens int32 [Bt].
+// pass b / (Bt/P)); u, vb, du, dvb [H][d]; lens int32 [Bt].
+// probs: MFMA-fragment tiles [Bt*H][nt][nt][64 lanes][4], nt = ceil(T/16): tile (a, t) holds
+// P[16a + r][16t + 4g + e] in lane r + 16g, element e -- the layout the forward's scores
+// are in, so every lane writes (and the query-side backward reads) one dwordx4 per 16x16
+// tile, 1 KB contiguous per wave instruction. Rows / keys >= T hold 0.
 // Products on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, like torch's fp32 matmul).
-// Dropout keeps (i, j) when hash(key(seed, counter + offset), index) >= p * 2^32 (a
-// counter hash; torch's own RNG stream is not reproduced). The forward stores each kept
-// probability as P and each dropped one as -P (P >= 0, so the sign bit is free): both
-// backward kernels read the keep bit back with the probability instead of hashing the
-// T x T matrix again (16 us per key-side call at Conformer-S).
+// Dropout keeps (i, j) by the pair hash of ob_drop.h on index (bh*T + i)*Te + j, Te = T
+// rounded up to even (so the two keys of a pair share a row); the forward stores each kept
+// probability as P and each dropped one as -P (P >= 0, so the sign bit is free), and the
+// backward kernels read the keep bit back with the probability.
 #include <math.h>
 
 #include "ob_drop.h"
 #include "ob_launch.h"
-
-// Profiling switches (tools/variant.sh builds; all 0 in the product): drop one phase of
-// the forward to price it. Results are wrong with any of them set.
-#ifndef RA_EXP_NOX
-#define RA_EXP_NOX 0
-#endif
-#ifndef RA_EXP_NOAC
-#define RA_EXP_NOAC 0
-#endif
-#ifndef RA_EXP_NOCTX
-#define RA_EXP_NOCTX 0
-#endif
-#ifndef RA_EXP_NOPROBS
-#define RA_EXP_NOPROBS 0
-#endif
-#ifndef RA_EXP_NODROP
-#define RA_EXP_NODROP 0
-#endif
-#ifndef RB_EXP_NODP
-#define RB_EXP_NODP 0
-#endif
-#ifndef RB_EXP_NODQU
-#define RB_EXP_NODQU 0
-#endif
-#ifndef RB_EXP_NODQV
-#define RB_EXP_NODQV 0
-#endif
-#ifndef RB_EXP_NODSG
-#define RB_EXP_NODSG 0
-#endif
-#ifndef RB_EXP_NOPROBS
-#define RB_EXP_NOPROBS 0
-#endif
-#ifndef RA_EXP_NOROW64
-#define RA_EXP_NOROW64 0
-#endif
-#ifndef RB_EXP_NOROW
-#define RB_EXP_NOROW 0
-#endif
-#ifndef RK_EXP_NOMFMA
-#define RK_EXP_NOMFMA 0
-#endif
-#ifndef RK_EXP_NOFETCH
-#define RK_EXP_NOFETCH 0
-#endif
-#ifndef RK_EXP_NOHASH
-#define RK_EXP_NOHASH 0
-#endif
-#ifndef RK_EXP_NODX
-#define RK_EXP_NODX 0
-#endif
 
 namespace ob {
 
@@ -145,10 +101,29 @@ __device__ __forceinline__ BlockId block_id(int nqt, int H) {
   return id;
 }
 
+// first float of probs fragment tile (a, t) of (batch row, head) bh
+__device__ __forceinline__ size_t frag_off(int bh, int a, int t, int nt) {
+  return (((size_t)bh * nt + a) * nt + t) * 256;
+}
+
+__device__ __forceinline__ uint64_t drop_row_base(int bh, int T, int i) {  // even
+  return ((uint64_t)bh * T + i) * (uint64_t)(T + (T & 1));
+}
+
+// keep bits of keys 16t+4g .. +3 of a row (idx even: the two pairs of a dwordx4 group)
+__device__ __forceinline__ void keep4(uint32_t key, uint64_t idx, const DropCfg& dc,
+                                      bool (&keep)[4]) {
+  const uint32_t h0 = drop_hash(key, idx >> 1), h1 = drop_hash(key, (idx >> 1) + 1);
+  keep[0] = (h0 & 0xFFFFu) >= dc.thresh;
+  keep[1] = (h0 >> 16) >= dc.thresh;
+  keep[2] = (h1 & 0xFFFFu) >= dc.thresh;
+  keep[3] = (h1 >> 16) >= dc.thresh;
+}
 
 // ------------------------------------------------------------------------------------
-// Forward: block = (query tile of 64, head, batch row). X rows i0 .. i0+64 live in LDS
-// (row 64 = the next tile's first query, needed by the j >= i+2 branch of rel_shift).
+// Forward: block = (query tile of 64, head, batch row). The Xpad image of rows i0 .. i0+64
+// lives in LDS (row 64 = the next tile's first query, read by the last rows' j >= i+2
+// entries), then the same space holds v for the context product.
 // ------------------------------------------------------------------------------------
 template <int DQ, int NTT>
 __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
@@ -159,13 +134,12 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     float* __restrict__ ctx) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
-  extern __shared__ float xs[];
+  extern __shared__ float img[];
   const int nt = (T + 15) >> 4;
-  // pitch = 2 mod 32: the rel_shift gather below reads lanes r at stride ldx - 1 (bank
-  // r + 4g, 2-way) -- a pitch of 16nt+1 put all 16 rows of a lane group on one bank
-  const int ldx = 16 * nt + 2;
+  const int ldi = T + 1;  // Xpad pitch
   const BlockId bid = block_id((T + kTile - 1) / kTile, H);
   const int b = bid.b, h = bid.h, i0 = bid.qt * kTile;
+  const int bh = b * H + h;
   const int pass = b / Bp;
   const int C = H * D;
   const int L = min(lens[b], T);
@@ -177,7 +151,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   const float* ub = u + h * D;
   const float* vbb = vbias + h * D;
 
-  const int qi = i0 + 16 * w + r;  // this lane's query row (scores phase)
+  const int ir = 16 * w + r;  // this lane's query row in the tile (scores phase)
+  const int qi = i0 + ir;
   const int qic = min(qi, T - 1);
   float qu[DQ], qv[DQ];
   {
@@ -191,10 +166,9 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     }
   }
 
-  // X = (q + v) p^T for the wave's 16 rows: D[m][query] with A = p rows, B = (q+v)
-  // four key tiles at a time, s-major: consecutive MFMAs feed different accumulators
-  // (per-accumulator order unchanged). The next group's p rows are loaded (unaligned
-  // dwordx4 runs) while the current group's MFMAs issue.
+  // X = (q + v) p^T for the wave's 16 rows: D[pos][query] with A = p rows, B = (q+v),
+  // four position tiles at a time (next group's p rows loading meanwhile), stored as
+  // Xpad rows: img[ir][1 + m] = X[qi][m], img[ir][0] = 0.
   float opa[4][DQ];
   load_group<DQ>(pb, C, 0, r, g, T, opa);
 #pragma unroll
@@ -204,29 +178,32 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(pb, C, t0 + 4, r, g, T, opn);
     f32x4 acc[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int uu = 0; uu < 4; ++uu) acc[uu] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) if (!RA_EXP_NOX) acc[u] = mfma4(opa[u][s], qv[s], acc[u]);
+      for (int uu = 0; uu < 4; ++uu) acc[uu] = mfma4(opa[uu][s], qv[s], acc[uu]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (t0 + u >= nt) continue;
-      float* dst = xs + (16 * w + r) * ldx + 16 * (t0 + u) + 4 * g;
+    for (int uu = 0; uu < 4; ++uu) {
+      const int t = t0 + uu;
+      if (t >= nt) continue;
+      float* dst = img + ir * ldi + 1 + 16 * t + 4 * g;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dst[j] = acc[u][j];
+      for (int j = 0; j < 4; ++j)
+        if (16 * t + 4 * g + j < T) dst[j] = acc[uu][j];  // (m >= T: the next row's zero)
     }
     if (t0 + 4 < NTT) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
-        for (int s2 = 0; s2 < DQ; ++s2) opa[u][s2] = opn[u][s2];
+        for (int s2 = 0; s2 < DQ; ++s2) opa[uu][s2] = opn[uu][s2];
     }
   }
+  if (g == 0) img[ir * ldi] = 0.0f;
   // the first key group of the scores phase, in flight over the row-64 work and barrier
   load_group<DQ>(kb, C, 0, r, g, T, opa);
-  // row 64: the next tile's first query (fp32 fma chain on the VALU)
-  if (!RA_EXP_NOROW64 && i0 + kTile < T) {
+  // Xpad row 64: the next tile's first query (fp32 fma chain on the VALU)
+  if (i0 + kTile < T) {
     const float* qe = qb + (size_t)(i0 + kTile) * C;
     for (int m = threadIdx.x; m < T; m += kThreads) {
       float pr[D];
@@ -234,15 +211,17 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       float a = 0.0f;
 #pragma unroll
       for (int c = 0; c < D; ++c) a = fmaf(qe[c] + vbb[c], pr[c], a);
-      xs[kTile * ldx + m] = a;
+      img[kTile * ldi + 1 + m] = a;
     }
+    if (threadIdx.x == 0) img[kTile * ldi] = 0.0f;
   }
   __syncthreads();
 
-  // scores for (query r, keys 16t+4g+j): ac by MFMA (A = k rows, B = q+u), bd gathered
+  // scores for (query qi, keys 16t+4g+j): ac by MFMA (A = k rows, B = q+u); bd read flat
   float sreg[NTT][4];
   float mx = -INFINITY;
-  const float* xrow = xs + (16 * w + r) * ldx;
+  const float* bdp = img + (T + ir * T + 4 * g - i0);  // bd[qi][16t+4g+j] = bdp[16t + j]
+  const int Lq = qi < L ? L : 0;                        // valid keys of this row
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
@@ -250,82 +229,73 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(kb, C, t0 + 4, r, g, T, opn);
     f32x4 acc4[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int uu = 0; uu < 4; ++uu) acc4[uu] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) if (!RA_EXP_NOAC) acc4[u] = mfma4(opa[u][s], qu[s], acc4[u]);
+      for (int uu = 0; uu < 4; ++uu) acc4[uu] = mfma4(opa[uu][s], qu[s], acc4[uu]);
     if (t0 + 4 < NTT) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
-        for (int s2 = 0; s2 < DQ; ++s2) opa[u][s2] = opn[u][s2];
+        for (int s2 = 0; s2 < DQ; ++s2) opa[uu][s2] = opn[uu][s2];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-    const int t = t0 + u;
-    if (t >= nt) continue;
-    const f32x4 acc = acc4[u];
+    for (int uu = 0; uu < 4; ++uu) {
+      const int t = t0 + uu;
+      if (t >= nt) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int jj = 16 * t + 4 * g + j;
-      // bd = X[qi][T-1-qi+jj] (jj <= qi), 0 (jj == qi+1), X[qi+1][jj-qi-2] (jj >= qi+2):
-      // one LDS read at a select-computed offset (always inside the 65-row image)
-      const float xv = xrow[jj - qi + (jj <= qi ? T - 1 : ldx - 2)];
-      const float bd = jj == qi + 1 ? 0.0f : xv;
-      const float sc = (acc[j] + bd) * inv_sqrt_d;
-      const bool valid = qi < L && jj < L;
-      sreg[t][j] = valid ? sc : -INFINITY;
-      mx = fmaxf(mx, sreg[t][j]);
-    }
+      for (int j = 0; j < 4; ++j) {
+        const float sc = (acc4[uu][j] + bdp[16 * t + j]) * inv_sqrt_d;
+        sreg[t][j] = 16 * t + 4 * g + j < Lq ? sc : -INFINITY;
+        mx = fmaxf(mx, sreg[t][j]);
+      }
     }
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16));
   mx = fmaxf(mx, __shfl_xor(mx, 32));
-  float sum = 0.0f;
   const bool row_live = mx != -INFINITY;  // all -inf -> softmax NaN -> nan_to_num 0
+  const float mxs = row_live ? mx : 0.0f;
+  float sum = 0.0f;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     if (t >= nt) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float e = row_live ? __expf(sreg[t][j] - mx) : 0.0f;
+      const float e = __expf(sreg[t][j] - mxs);  // exp(-inf) = 0
       sreg[t][j] = e;
       sum += e;
     }
   }
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
-  const float rsum = 1.0f / sum;
+  const float rsum = row_live ? 1.0f / sum : 0.0f;
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
-  const size_t prow_off = (((size_t)b * H + h) * T + qic) * T;
+  const uint64_t didx = drop_row_base(bh, T, qi) + 4 * g;  // + 16t
+  float* pf = probs ? probs + frag_off(bh, (i0 >> 4) + w, 0, nt) + 4 * lane : nullptr;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     if (t >= nt) continue;
+    bool keep[4] = {true, true, true, true};
+    if (dc.on) keep4(dkey, didx + 16 * t, dc, keep);
+    f32x4 st;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int jj = 16 * t + 4 * g + j;
-      const float pr = row_live ? sreg[t][j] * rsum : 0.0f;
-      float pd = pr;
-      bool keep = true;
-      if (dc.on && !RA_EXP_NODROP) {
-        keep = drop_keep(dkey, prow_off + jj, dc.thresh);
-        pd = keep ? pr * dc.scale : 0.0f;
-      }
+      const float pr = sreg[t][j] * rsum;
       // the keep decision rides in the sign bit (P >= 0): the backward kernels read it
       // back instead of re-hashing every element
-      if (!RA_EXP_NOPROBS && probs && qi < T && jj < T) probs[prow_off + jj] = keep ? pr : -pr;
-      sreg[t][j] = pd;
+      st[j] = keep[j] ? pr : -pr;
+      sreg[t][j] = dc.on ? (keep[j] ? pr * dc.scale : 0.0f) : pr;
     }
+    if (pf) *reinterpret_cast<f32x4*>(pf + 256 * t) = st;
   }
 
   // ctx = A v: A = the lane's probabilities (row r, k = 4g+j of tile t), B = v rows.
-  // v [16 nt keys][D] of (b, h) is staged once per block into the X image (free once every
+  // v [16 nt keys][D] of (b, h) is staged once per block into the image (free once every
   // wave has passed the scores phase) with coalesced dwordx4 loads; the MFMA operands then
-  // come from LDS (row pitch D: the 4 key rows a B fragment touches sit 16 banks apart)
-  // instead of 12 scalar L2 loads per lane and key tile in each of the 4 waves.
+  // come from LDS (row pitch D: the 4 key rows a B fragment touches sit 16 banks apart).
   __syncthreads();
-  float* vs = xs;
+  float* vs = img;
   for (int e = threadIdx.x; e < 16 * nt * DQ; e += kThreads) {
     const int key = e / DQ, c4 = 4 * (e - key * DQ);
     const f32x4 v4 = key < T ? *(const f32x4u*)(vbp + (size_t)key * C + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -343,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     for (int j = 0; j < 4; ++j) {
       const float* vrow = vs + (16 * t + 4 * g + j) * D + r;
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) if (!RA_EXP_NOCTX) o[ct] = mfma4(sreg[t][j], vrow[16 * ct], o[ct]);
+      for (int ct = 0; ct < CT; ++ct) o[ct] = mfma4(sreg[t][j], vrow[16 * ct], o[ct]);
     }
   }
 #pragma unroll
@@ -361,28 +331,27 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 // ------------------------------------------------------------------------------------
 // Backward, query side: block = (query tile, head, batch row). Writes dq (final), the
 // tile's du / dvb partials (summed by relattn_bias_reduce_kernel) and dS' = dS / sqrt(d)
-// to global for the key-side kernel. LDS holds dS' for query rows i0-1 .. i0+63 (row 0 =
-// i0-1, recomputed here on the VALU) -- the rows the rel_shift adjoint of the tile needs.
+// to global for the key-side kernel. The softmax backward's row term is
+//   delta_i = sum_j Pd_ij dPd_ij = dO_i . ctx_i
+// (ctx = Pd v), so each score's dS' is formed as soon as its dP tile is: no parking of dP.
+// LDS holds dS' rows i0-1 .. i0+63 at pitch T (band row 0 = query i0-1, recomputed here on
+// the VALU; zero when i0 == 0) -- the rows the rel_shift adjoint of the tile reads.
 // ------------------------------------------------------------------------------------
 template <int DQ, int NTT>
 __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
-    const float* __restrict__ dctx, const float* __restrict__ q, const float* __restrict__ k,
-    const float* __restrict__ v, const float* __restrict__ pos, const float* __restrict__ u,
-    const float* __restrict__ vbias, const int* __restrict__ lens, int Bp, int T, int H,
-    float inv_sqrt_d, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off,
-    const float* __restrict__ probs, float* __restrict__ dq, float* __restrict__ dsg,
-    float* __restrict__ du_part,
-    float* __restrict__ dvb_part) {
+    const float* __restrict__ dctx, const float* __restrict__ ctxo, const float* __restrict__ k,
+    const float* __restrict__ v, const float* __restrict__ pos, int Bp, int T, int H,
+    float inv_sqrt_d, DropCfg dc, const float* __restrict__ probs, float* __restrict__ dq,
+    float* __restrict__ dsg, float* __restrict__ du_part, float* __restrict__ dvb_part) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
-  extern __shared__ float ds[];
+  extern __shared__ float band[];
   __shared__ float red[kThreads / 64][2][64];
-  __shared__ float rsum[kThreads / 64];
   const int nt = (T + 15) >> 4;
-  const int ldx = 16 * nt + 1;
   const int nqt = (T + kTile - 1) / kTile;
   const BlockId bid = block_id(nqt, H);
   const int b = bid.b, h = bid.h, qt = bid.qt, i0 = qt * kTile;
+  const int bh = b * H + h;
   const int pass = b / Bp;
   const int C = H * D;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
@@ -390,25 +359,38 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* kb = k + bo;
   const float* vbp = v + bo;
   const float* dob = dctx + bo;
+  const float* cob = ctxo + bo;
   const float* pb = pos + (size_t)pass * T * C + h * D;
-  const float* prb = probs + ((size_t)b * H + h) * T * T;
-  (void)rng;
-  (void)rng_off;
   // dropout backward factor from a stored probability's sign bit (the forward's keep bit)
   auto keep_scale = [&](float pv) -> float {
     if (!dc.on) return 1.0f;
     return __builtin_signbit(pv) ? 0.0f : dc.scale;
   };
+  // the band's slack past its 65 rows (read only by rows >= T and padded positions)
+  if (threadIdx.x < 128) band[(kTile + 1) * T + threadIdx.x] = 0.0f;
 
-  const int qi = i0 + 16 * w + r;
+  const int ir = 16 * w + r;
+  const int qi = i0 + ir;
   const int qic = min(qi, T - 1);
   float dor[DQ];
   load_run<DQ>(dob + (size_t)qic * C + g * DQ, dor);
+  float delta;
+  {
+    float cr[DQ];
+    load_run<DQ>(cob + (size_t)qic * C + g * DQ, cr);
+    float a = 0.0f;
+#pragma unroll
+    for (int s = 0; s < DQ; ++s) a = fmaf(dor[s], cr[s], a);
+    a += __shfl_xor(a, 16);
+    a += __shfl_xor(a, 32);
+    delta = a;
+  }
 
-  // dPd[query r][key] = dO . v (A = v rows, B = dO row), P from the forward
+  // dPd[query qi][key] = dO . v (A = v rows, B = dO row); P from the fragment tiles;
+  // dS' = P (dPd * keep * scale - delta) / sqrt(d) (softmax backward, then the 1/sqrt(d))
+  const float* pf = probs + frag_off(bh, (i0 >> 4) + w, 0, nt) + 4 * lane;
+  float* brow = band + (1 + ir) * T + 4 * g;  // band row of query qi
   float dsr[NTT][4];
-  float rowdot = 0.0f;
-  // (v rows of the next four key tiles load while the current tiles' MFMAs issue)
   float opa[4][DQ];
   load_group<DQ>(vbp, C, 0, r, g, T, opa);
 #pragma unroll
@@ -416,97 +398,60 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     if (t0 >= nt) continue;
     float opn[4][DQ];
     if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(vbp, C, t0 + 4, r, g, T, opn);
+    f32x4 p4[4];
+#pragma unroll
+    for (int uu = 0; uu < 4; ++uu)
+      p4[uu] = t0 + uu < nt ? *reinterpret_cast<const f32x4*>(pf + 256 * (t0 + uu))
+                            : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc4[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int uu = 0; uu < 4; ++uu) acc4[uu] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) if (!RB_EXP_NODP) acc4[u] = mfma4(opa[u][s], dor[s], acc4[u]);
+      for (int uu = 0; uu < 4; ++uu) acc4[uu] = mfma4(opa[uu][s], dor[s], acc4[uu]);
     if (t0 + 4 < NTT) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
-        for (int s2 = 0; s2 < DQ; ++s2) opa[u][s2] = opn[u][s2];
+        for (int s2 = 0; s2 < DQ; ++s2) opa[uu][s2] = opn[uu][s2];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-    const int t = t0 + u;
-    if (t >= nt) continue;
-    f32x4 acc = acc4[u];
-    // the lane's four probabilities P[qi][16t+4g .. +3]: one unaligned dwordx4 when in range
-    float pp[4];
-    const int jb = 16 * t + 4 * g;
-    if (qi < T && jb + 3 < T) {
-      const f32x4 v4 = *(const f32x4u*)(prb + (size_t)qi * T + jb);
+    for (int uu = 0; uu < 4; ++uu) {
+      const int t = t0 + uu;
+      if (t >= nt) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pp[j] = v4[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pp[j] = (qi < T && jb + j < T) ? prb[(size_t)qi * T + jb + j] : 0.0f;
+      for (int j = 0; j < 4; ++j) {
+        const float pv = p4[uu][j];
+        const float dp = acc4[uu][j] * keep_scale(pv);  // dropout backward
+        const float ds = (fabsf(pv) * (dp - delta)) * inv_sqrt_d;
+        dsr[t][j] = ds;
+        if (16 * t + 4 * g + j < T) brow[16 * t + j] = ds;
+      }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float p = RB_EXP_NOPROBS ? 0.5f : fabsf(pp[j]);
-      const float dp = acc[j] * keep_scale(pp[j]);  // dropout backward
-      dsr[t][j] = p;
-      acc[j] = dp;
-      rowdot += p * dp;
-    }
-    // dS needs the row sum first: park dP in this lane's own LDS cells meanwhile
-    float* dst = ds + (1 + 16 * w + r) * ldx + 16 * t + 4 * g;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = acc[j];
-    }
-  }
-  rowdot += __shfl_xor(rowdot, 16);
-  rowdot += __shfl_xor(rowdot, 32);
-  // dS' = P (dP - rowdot) / sqrt(d)  (softmax backward, then the 1/sqrt(d) of :120)
-  const float* dprow = ds + (1 + 16 * w + r) * ldx;
-#pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int jj = 16 * t + 4 * g + j;
-      const float dp = dprow[jj];
-      dsr[t][j] = (dsr[t][j] * (dp - rowdot)) * inv_sqrt_d;
-    }
-  }
-  // (each lane rewrites exactly the LDS cells it wrote: no barrier needed in between)
-#pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
-    float* dst = ds + (1 + 16 * w + r) * ldx + 16 * t + 4 * g;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = dsr[t][j];
   }
 
-  // row i0-1 (LDS row 0) on the VALU, the same formula
-  if (!RB_EXP_NOROW && i0 > 0) {
+  // band row 0: query i0-1 on the VALU, the same formula (zero row when i0 == 0)
+  if (i0 > 0) {
     const int ip = i0 - 1;
-    float part = 0.0f;
+    const float* drow = dob + (size_t)ip * C;
+    const float* crow = cob + (size_t)ip * C;
+    float dl = 0.0f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) dl = fmaf(drow[c], crow[c], dl);
+    const float* pr = probs + frag_off(bh, ip >> 4, 0, nt) + 4 * (ip & 15);
     for (int jj = threadIdx.x; jj < T; jj += kThreads) {
-      const float* vrow = vbp + (size_t)jj * C;
-      const float* drow = dob + (size_t)ip * C;
+      float vr[D];
+      load_run<D>(vbp + (size_t)jj * C, vr);
       float a = 0.0f;
-      for (int c = 0; c < D; ++c) a = fmaf(vrow[c], drow[c], a);
-      const float pv = prb[(size_t)ip * T + jj];
-      const float dp = a * keep_scale(pv);
-      const float p = fabsf(pv);
-      ds[jj] = dp;
-      part += p * dp;
+#pragma unroll
+      for (int c = 0; c < D; ++c) a = fmaf(vr[c], drow[c], a);
+      const float pv = pr[256 * (jj >> 4) + 64 * ((jj & 15) >> 2) + (jj & 3)];
+      band[jj] = (fabsf(pv) * (a * keep_scale(pv) - dl)) * inv_sqrt_d;
     }
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) rsum[w] = part;
-    __syncthreads();
-    const float rd = ((rsum[0] + rsum[1]) + rsum[2]) + rsum[3];
-    for (int jj = threadIdx.x; jj < T; jj += kThreads) {
-      const float p = fabsf(prb[(size_t)ip * T + jj]);
-      ds[jj] = (p * (ds[jj] - rd)) * inv_sqrt_d;
-    }
+  } else {
+    for (int jj = threadIdx.x; jj < T; jj += kThreads) band[jj] = 0.0f;
   }
-  __syncthreads();
 
   // dQu = dS' k (A = dS' row r, k = 4g+j of tile t; B = k rows)
   f32x4 oq[CT];
@@ -532,7 +477,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) if (!RB_EXP_NODQU) oq[ct] = mfma4(dsr[t][j], kb_cur[j][ct], oq[ct]);
+        for (int ct = 0; ct < CT; ++ct) oq[ct] = mfma4(dsr[t][j], kb_cur[j][ct], oq[ct]);
       if (t + 1 < NTT) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -541,23 +486,28 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
       }
     }
   }
-  // dQv = dX p, dX gathered from LDS by the rel_shift adjoint
+  __syncthreads();  // the band is complete (row 0 and every wave's rows)
+
+  // dQv = dX p, dX read flat from the band: dX[qi][m] = dS'.flat[qi(T+1) + m + 1 - T]
+  // = band[i0 + 1 + ir(T+1) + m] (band row 0 = query i0-1, zero for the first tile).
+  // Positions m = 4mk+g go four MFMA steps at a time, the next four's p operands loading
+  // meanwhile; positions past T multiply p = 0.
   f32x4 ov[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) ov[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // dX[qi][m] = dS'[qi][m-T+1+qi] (m >= T-1-qi), else dS'[qi-1][m+qi+1] (qi >= 1): one LDS
-  // read at a select-computed offset (LDS row 1+16w+r holds dS' row qi, the row above it
-  // qi-1). Positions m = 4mk+g go four MFMA steps at a time, the next four's p operands
-  // loading meanwhile; steps past the end multiply zeros.
-  const float* row_i = ds + (1 + 16 * w + r) * ldx;
+  const float* xrow = band + i0 + 1 + ir * (T + 1) + g;  // dX[qi][4mk + g] = xrow[4mk]
   const int nk = (T + 3) >> 2;
   constexpr int kMK = 4;
   auto load_p = [&](int mk0, float (&dst)[kMK][CT]) {
 #pragma unroll
-    for (int q = 0; q < kMK; ++q) {
-      const float* prow = pb + (size_t)min(4 * (mk0 + q) + g, T - 1) * C;
+    for (int qq = 0; qq < kMK; ++qq) {
+      const int m = 4 * (mk0 + qq) + g;
+      const float* prow = pb + (size_t)min(m, T - 1) * C;
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) dst[q][ct] = prow[min(16 * ct + r, D - 1)];
+      for (int ct = 0; ct < CT; ++ct) {
+        const float x = prow[min(16 * ct + r, D - 1)];
+        dst[qq][ct] = m < T ? x : 0.0f;
+      }
     }
   };
   float pv_cur[kMK][CT];
@@ -565,23 +515,16 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   for (int mk0 = 0; mk0 < nk; mk0 += kMK) {
     float pv_nxt[kMK][CT];
     if (mk0 + kMK < nk) load_p(mk0 + kMK, pv_nxt);
-    float av[kMK];
 #pragma unroll
-    for (int q = 0; q < kMK; ++q) {
-      const int m = 4 * (mk0 + q) + g;
-      const int mm = min(m, T - 1);  // (clamped address; the value is masked below)
-      const bool upper = mm >= T - 1 - qic;
-      const float x = row_i[mm + qic + 1 - (upper ? T : ldx)];
-      av[q] = (qi < T && m < T && (upper || qi >= 1)) ? x : 0.0f;
+    for (int qq = 0; qq < kMK; ++qq) {
+      const float av = xrow[4 * (mk0 + qq)];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) ov[ct] = mfma4(av, pv_cur[qq][ct], ov[ct]);
     }
 #pragma unroll
-    for (int q = 0; q < kMK; ++q)
+    for (int qq = 0; qq < kMK; ++qq)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) if (!RB_EXP_NODQV) ov[ct] = mfma4(av[q], pv_cur[q][ct], ov[ct]);
-#pragma unroll
-    for (int q = 0; q < kMK; ++q)
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) pv_cur[q][ct] = pv_nxt[q][ct];
+      for (int ct = 0; ct < CT; ++ct) pv_cur[qq][ct] = pv_nxt[qq][ct];
   }
   // dq = dQu + dQv; per-tile column sums of dQu / dQv for du / dvb
   float su[CT], sv[CT];
@@ -620,24 +563,18 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     dvb_part[tile_id * D + c] = ((red[0][1][c] + red[1][1][c]) + red[2][1][c]) + red[3][1][c];
   }
 
-  // dS' rows of this tile to global for the key-side kernel (row-contiguous copy of the
-  // LDS image: wave w copies rows 16w .. 16w+15, 64 consecutive columns per instruction)
-  float* dsb = dsg + ((size_t)b * H + h) * T * T;
-  // (4 consecutive floats per lane: one unaligned dwordx4 store, 16 per wave and row
-  // quarter instead of 64 dword stores)
-  for (int rr = 0; rr < 16; ++rr) {
-    const int qrow = i0 + 16 * w + rr;
-    if (qrow >= T) break;
-    const float* src = ds + (1 + 16 * w + rr) * ldx;
-    float* dst = dsb + (size_t)qrow * T;
-    for (int j4 = 4 * lane; j4 < T; j4 += 256) {
-      if (RB_EXP_NODSG) break;
-      if (j4 + 3 < T) {
-        const f32x4 v4 = {src[j4], src[j4 + 1], src[j4 + 2], src[j4 + 3]};
-        *(f32x4u*)(dst + j4) = v4;
-      } else {
-        for (int e = j4; e < T; ++e) dst[e] = src[e];
-      }
+  // dS' rows of this tile to global for the key-side kernel: band rows 1 .. 64 are the
+  // global rows i0 .. i0+63 at the same pitch T, i.e. one contiguous run -- copied as
+  // dwordx4 (unaligned) by the whole block
+  float* dsb = dsg + (size_t)bh * T * T + (size_t)i0 * T;
+  const int n = min(kTile, T - i0) * T;
+  const float* src = band + T;
+  for (int e4 = 4 * threadIdx.x; e4 < n; e4 += 4 * kThreads) {
+    if (e4 + 3 < n) {
+      const f32x4 v4 = {src[e4], src[e4 + 1], src[e4 + 2], src[e4 + 3]};
+      *(f32x4u*)(dsb + e4) = v4;
+    } else {
+      for (int e = e4; e < n; ++e) dsb[e] = src[e];
     }
   }
 }
@@ -673,17 +610,18 @@ template <int DQ>
 __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     const float* __restrict__ dsg, const float* __restrict__ probs, const float* __restrict__ q,
     const float* __restrict__ dctx, const float* __restrict__ u, const float* __restrict__ vbias,
-    int T, int H, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off,
-    float* __restrict__ dk,
-    float* __restrict__ dv, float* __restrict__ dp_part) {
+    int T, int H, DropCfg dc, float* __restrict__ dk, float* __restrict__ dv,
+    float* __restrict__ dp_part) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   using St = KvStage<D>;
   constexpr int kQ = St::kQ;
   __shared__ St st;
+  const int nt = (T + 15) >> 4;
   const int nkt = (T + kTile - 1) / kTile;
   const BlockId bid = block_id(nkt, H);
   const int b = bid.b, h = bid.h, k0 = bid.qt * kTile;
+  const int bh = b * H + h;
   const int C = H * D;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
   const size_t bo = (size_t)b * T * C + h * D;
@@ -691,10 +629,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   const float* dob = dctx + bo;
   const float* ub = u + h * D;
   const float* vbb = vbias + h * D;
-  const float* dsb = dsg + ((size_t)b * H + h) * T * T;
-  const float* prb = probs + ((size_t)b * H + h) * T * T;
-  (void)rng;
-  (void)rng_off;
+  const float* dsb = dsg + (size_t)bh * T * T;
+  const float* prb = probs + frag_off(bh, 0, 0, nt);
 
   // pad columns of the B tiles stay zero (their MFMA columns are discarded anyway)
   for (int e = threadIdx.x; e < kQ * St::kBP; e += kThreads) {
@@ -707,30 +643,35 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   // B -- float4 slot e = t + 256 j: q (e < kBVec) or dO, row e/(D/4), columns 4(e%(D/4))..
   constexpr int kAH = kQ / 16;  // A rows per thread (ai, ai + 16, ...)
   const int ai = threadIdx.x >> 4, ax = 4 * (threadIdx.x & 15);
+  const int key0 = k0 + ax;
+  // P[i][key0 .. +3] is element 0..3 of lane (i & 15) + 16 ((key0 & 15) >> 2) of fragment
+  // tile (i / 16, key0 / 16): one aligned dwordx4
+  const size_t pcol = (size_t)256 * (key0 >> 4) + 64 * ((key0 & 15) >> 2);
   f32x4 ra_k[kAH], ra_v[kAH], ra_p[kAH], rb[St::kBSlots];
   auto fetch = [&](int i0) {
 #pragma unroll
     for (int hf = 0; hf < kAH; ++hf) {
     const int i = i0 + ai + 16 * hf;
-    const int key0 = k0 + ax;
     if (i < T && key0 + 3 < T) {
       ra_k[hf] = *(const f32x4u*)(dsb + (size_t)i * T + key0);
-      ra_v[hf] = *(const f32x4u*)(prb + (size_t)i * T + key0);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool ok = i < T && key0 + j < T;
         ra_k[hf][j] = ok ? dsb[(size_t)i * T + key0 + j] : 0.0f;
-        ra_v[hf][j] = ok ? prb[(size_t)i * T + key0 + j] : 0.0f;
       }
     }
+    ra_v[hf] = (i < T && key0 < 16 * nt)
+                   ? *reinterpret_cast<const f32x4*>(prb + (size_t)(i >> 4) * nt * 256 + pcol +
+                                                     4 * (i & 15))
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
     // dX[i][m0..m0+3]: one unaligned dwordx4 when the four positions sit in one branch of
     // the adjoint (upper: dS' row i from column m0-T+1+i; lower: row i-1 from m0+i+1)
     const int up0 = T - 1 - i;  // first upper position of row i
     if (i < T && key0 + 3 < T && (key0 >= up0 || (key0 + 3 < up0 && i >= 1))) {
       const float* src = key0 >= up0 ? dsb + (size_t)i * T + (key0 - up0)
                                      : dsb + (size_t)(i - 1) * T + (key0 + i + 1);
-      ra_p[hf] = RK_EXP_NODX ? f32x4{0.5f, 0.5f, 0.5f, 0.5f} : *(const f32x4u*)src;
+      ra_p[hf] = *(const f32x4u*)src;
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -740,15 +681,14 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
         const bool upper = mc >= T - 1 - ic;
         const size_t off = upper ? (size_t)ic * T + (mc - T + 1 + ic)
                                  : (size_t)max(ic - 1, 0) * T + min(mc + ic + 1, T - 1);
-        const float x = RK_EXP_NODX ? 0.5f : dsb[off];
+        const float x = dsb[off];
         ra_p[hf][j] = (ok && (upper || ic >= 1)) ? x : 0.0f;
       }
     }
     // Pd = P * keep * scale, the keep bit from the stored probability's sign
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (!RK_EXP_NOHASH && dc.on)
-        ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
+      if (dc.on) ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
     }
     }
 #pragma unroll
@@ -805,7 +745,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     __syncthreads();  // the previous chunk's LDS reads are done
     stage();
     __syncthreads();
-    if (!RK_EXP_NOFETCH && i0 + kQ < T) fetch(i0 + kQ);
+    if (i0 + kQ < T) fetch(i0 + kQ);
 #pragma unroll
     for (int s4 = 0; s4 < kQ / 4; ++s4) {
       const int qq = 4 * s4 + g;
@@ -813,12 +753,6 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const int col = 16 * ct + r;
-        if (RK_EXP_NOMFMA) {
-          ak[ct][0] += a_k * st.qu[qq][col];
-          av[ct][0] += a_v * st.dob[qq][col];
-          ap[ct][0] += a_p * st.qv[qq][col];
-          continue;
-        }
         ak[ct] = mfma4(a_k, st.qu[qq][col], ak[ct]);
         av[ct] = mfma4(a_v, st.dob[qq][col], av[ct]);
         ap[ct] = mfma4(a_p, st.qv[qq][col], ap[ct]);
@@ -863,10 +797,10 @@ __global__ __launch_bounds__(kThreads) void relattn_bias_reduce_kernel(
   const int pairs = Bt * nqt;
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < D) {
-    int u = 0;
-    for (int q = sl; q < pairs; q += kBiasSlices, ++u) {
-      const int b = q / nqt, qt = q - b * nqt;
-      a[u & 3] += src[(((size_t)b * H + h) * nqt + qt) * D + c];
+    int uu = 0;
+    for (int qq = sl; qq < pairs; qq += kBiasSlices, ++uu) {
+      const int b = qq / nqt, qt = qq - b * nqt;
+      a[uu & 3] += src[(((size_t)b * H + h) * nqt + qt) * D + c];
     }
   }
   red[sl][cl] = (a[0] + a[1]) + (a[2] + a[3]);
@@ -874,16 +808,16 @@ __global__ __launch_bounds__(kThreads) void relattn_bias_reduce_kernel(
   if (sl == 0 && c < D) {
     float t = 0.0f;
 #pragma unroll 8
-    for (int q = 0; q < kBiasSlices; ++q) t += red[q][cl];
+    for (int qq = 0; qq < kBiasSlices; ++qq) t += red[qq][cl];
     (which == 0 ? du : dvb)[h * D + c] = t;
   }
 }
 
-// dpos [P][T][H*D]: sum over the pass's Bp batch rows and the query tiles. Block = 64
-// consecutive output elements x 4 batch slices (slice s: rows s, s+4, ... of the pass);
-// the slices are added in slice order through LDS (fixed order: deterministic).
+// dpos [P][T][H*D]: sum over the pass's Bp batch rows. Block = 64 consecutive output
+// elements x 4 batch slices (slice s: rows s, s+4, ... of the pass); the slices are added
+// in slice order through LDS (fixed order: deterministic).
 __global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
-    const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D, int nqt,
+    const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D,
     float* __restrict__ dpos) {
   __shared__ float red[4][64];
   const int C = H * D;
@@ -897,10 +831,9 @@ __global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
     const int rem = (int)(f - (int64_t)p * T * C);
     const int t = rem / C, hc = rem - t * C, h = hc / D, c = hc - h * D;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
-    int u = 0;
-    for (int b = p * Bp + sl; b < (p + 1) * Bp; b += 4, ++u)
-      for (int qt = 0; qt < nqt; ++qt)
-        a[u & 3] += dp_part[(((((size_t)qt * Bt + b) * H + h) * T) + t) * D + c];
+    int uu = 0;
+    for (int b = p * Bp + sl; b < (p + 1) * Bp; b += 4, ++uu)
+      a[uu & 3] += dp_part[((((size_t)b * H + h) * T) + t) * D + c];
     s = (a[0] + a[1]) + (a[2] + a[3]);
   }
   red[sl][el] = s;
@@ -908,23 +841,35 @@ __global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
   if (sl == 0 && f < n_p) dpos[f] = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
 }
 
-__global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, DropCfg dc,
+// keep mask of n elements in rows of T (element e = row * T + j): the attention kernels'
+// index (row * Te + j); with T = n it is the flat index of the BitLinear / LayerNorm sites
+__global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, int64_t T, DropCfg dc,
                                                                 const uint64_t* __restrict__ rng,
                                                                 uint64_t rng_off,
                                                                 uint8_t* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e >= n) return;
-  out[e] = (!dc.on || drop_keep(drop_key(rng[0], rng[1] + rng_off), (uint64_t)e, dc.thresh)) ? 1 : 0;
+  const int64_t row = e / T, j = e - row * T;
+  const uint64_t idx = (uint64_t)row * (uint64_t)(T + (T & 1)) + (uint64_t)j;
+  out[e] = (!dc.on || drop_keep(drop_key(rng[0], rng[1] + rng_off), idx, dc.thresh)) ? 1 : 0;
 }
 
-
-// (the forward's pitch, 16nt+2; the backward uses 16nt+1)
-size_t lds_bytes(int T) { return sizeof(float) * (size_t)(kTile + 1) * (16 * ((T + 15) / 16) + 2); }
+size_t fwd_lds_bytes(int T, int D) {
+  const size_t img = (size_t)(kTile + 1) * (T + 1);
+  const size_t vst = (size_t)16 * ((T + 15) / 16) * D;
+  return sizeof(float) * (img > vst ? img : vst);
+}
+size_t bwd_lds_bytes(int T) { return sizeof(float) * ((size_t)(kTile + 1) * T + 128); }
 
 }  // namespace
 
 bool relattn_supported(int64_t T, int64_t d) {
   return T >= 1 && T <= 512 && (d == 16 || d == 32 || d == 36 || d == 64);
+}
+
+int64_t relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
+  const int64_t nt = (T + 15) / 16;
+  return Bt * H * nt * nt * 256;
 }
 
 // ws: dS' [Bt][H][T][T] | dpos per batch row [Bt][H][T][d] | du, dvb tile partials.
@@ -954,7 +899,7 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
   const dim3 grid((unsigned)(((T + kTile - 1) / kTile) * H * Bt));
   const DropCfg dc = make_drop(p_drop);
   const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
-  const size_t lds = lds_bytes((int)T);
+  const size_t lds = fwd_lds_bytes((int)T, (int)d);
 #define OB_RA_FWD(DQ, NTT)                                                                 \
   hipLaunchKernelGGL((relattn_fwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, q, k, v, pos, \
                      u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, ctx)
@@ -962,30 +907,29 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
 #undef OB_RA_FWD
 }
 
-void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
-                        const float* pos, const float* u, const float* vb, const int* lens,
+void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
+                        const float* v, const float* pos, const float* u, const float* vb,
                         int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                        const uint64_t* rng, uint64_t rng_off, const float* probs, float* dq,
-                        float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
-                        hipStream_t s) {
+                        const float* probs, float* dq, float* dk, float* dv, float* dpos,
+                        float* du, float* dvb, void* ws, hipStream_t s) {
   const int nqt = (int)((T + kTile - 1) / kTile);
   const dim3 grid((unsigned)(nqt * H * Bt));
   const DropCfg dc = make_drop(p_drop);
   const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
-  const size_t lds = lds_bytes((int)T);
+  const size_t lds = bwd_lds_bytes((int)T);
   float* dsg = (float*)ws;
   float* dp_part = dsg + (size_t)Bt * H * T * T;
   float* du_part = dp_part + (size_t)Bt * H * T * d;
   float* dvb_part = du_part + (size_t)Bt * H * nqt * d;
 #define OB_RA_BWD(DQ, NTT)                                                                     \
-  hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, q, k, v,  \
-                     pos, u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, dq, \
-                     dsg, du_part, dvb_part)
+  hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, ctx, k, \
+                     v, pos, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, probs, dq, dsg,        \
+                     du_part, dvb_part)
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
 #define OB_RA_KV(DQ, NTT)                                                                       \
   hipLaunchKernelGGL((relattn_bwd_kv_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg, \
-                     probs, q, dctx, u, vb, (int)T, (int)H, dc, rng, rng_off, dk, dv, dp_part)
+                     probs, q, dctx, u, vb, (int)T, (int)H, dc, dk, dv, dp_part)
   OB_RA_DISPATCH(OB_RA_KV);
 #undef OB_RA_KV
   const int64_t C = H * d;
@@ -995,14 +939,14 @@ void launch_relattn_bwd(const float* dctx, const float* q, const float* k, const
                      nqt, du, dvb);
   hipLaunchKernelGGL(relattn_dpos_reduce_kernel, dim3((unsigned)ceil_div(P * T * C, 64)),
                      dim3(kThreads), 0, s, (const float*)dp_part, (int)Bt, (int)P, (int)T, (int)H,
-                     (int)d, 1, dpos);
+                     (int)d, dpos);
 }
 
-void launch_relattn_dropout_mask(int64_t n, float p_drop, const uint64_t* rng, uint64_t rng_off,
-                                 uint8_t* out, hipStream_t s) {
+void launch_relattn_dropout_mask(int64_t n, int64_t T, float p_drop, const uint64_t* rng,
+                                 uint64_t rng_off, uint8_t* out, hipStream_t s) {
   if (n == 0) return;
   hipLaunchKernelGGL(relattn_mask_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, s, n, make_drop(p_drop), rng, rng_off, out);
+                     dim3(kThreads), 0, s, n, T, make_drop(p_drop), rng, rng_off, out);
 }
 
 }  // namespace ob

@@ -148,11 +148,12 @@ SIGNATURES = {
     "ob_relattn_fwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32, _c_f,
                _i64, _c_f, _c_f, _c_f]),
+    "ob_relattn_probs_elems": (_i64, [_i64, _i64, _i64]),
     "ob_relattn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64]),
     "ob_relattn_bwd": (
-        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32,
-               _c_f, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
-    "ob_relattn_dropout_mask": (_int, [_i64, _f32, _c_f, _i64, _c_f, _c_f]),
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64,
+               _f32, _c_f, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_relattn_dropout_mask": (_int, [_i64, _i64, _f32, _c_f, _i64, _c_f, _c_f]),
     "ob_embedding_bwd": (_int, [_c_f, _i64, _c_f, _i64, _i64, _i64, _c_f, _c_f]),
     "ob_adamw_plan": (_i64, [_c_f, _i64, _c_f]),
     "ob_adamw_workspace": (_sz, [_i64]),

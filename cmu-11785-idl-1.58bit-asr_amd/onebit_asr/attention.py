@@ -22,7 +22,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["rel_pos_attention", "fused_attention_supported", "dropout_mask"]
+__all__ = ["rel_pos_attention", "fused_attention_supported", "dropout_mask", "probs_dense"]
 
 # device -> (rng tensor, offset) of the latest call with dropout (tests read the mask back)
 LAST_RNG: Dict[torch.device, Tuple[torch.Tensor, int]] = {}
@@ -43,8 +43,9 @@ class _RelAttnFn(torch.autograd.Function):
         d = c // n_heads
         out = torch.empty_like(q)
         need = any(ctx.needs_input_grad[:6])
-        probs = torch.empty((bt, n_heads, t, t), dtype=torch.float32, device=q.device) if need else None
         lib = _lib.load()
+        probs = (torch.empty((lib.ob_relattn_probs_elems(bt, t, n_heads),), dtype=torch.float32,
+                             device=q.device) if need else None)
         _lib.check(
             lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt, P, t, n_heads, d,
@@ -54,12 +55,12 @@ class _RelAttnFn(torch.autograd.Function):
         )
         ctx.meta = (n_heads, p_drop, rng_off)
         if need:
-            ctx.save_for_backward(q, k, v, pos, u, vb, lens, probs, rng)
+            ctx.save_for_backward(q, k, v, pos, u, vb, lens, probs, rng, out)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        q, k, v, pos, u, vb, lens, probs, rng = ctx.saved_tensors
+        q, k, v, pos, u, vb, lens, probs, rng, out = ctx.saved_tensors
         n_heads, p_drop, rng_off = ctx.meta
         g = g.contiguous()
         bt, t, c = q.shape
@@ -72,7 +73,7 @@ class _RelAttnFn(torch.autograd.Function):
         wsb = lib.ob_relattn_bwd_workspace(bt, t, n_heads, d)
         ws = torch.empty((wsb,), dtype=torch.uint8, device=q.device)
         _lib.check(
-            lib.ob_relattn_bwd(g.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
+            lib.ob_relattn_bwd(g.data_ptr(), out.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt,
                                P, t, n_heads, d, p_drop, _lib.ptr(rng), rng_off, probs.data_ptr(),
                                dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(),
@@ -100,14 +101,24 @@ def rel_pos_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos: to
                             n_heads, float(dropout_p), rng, off)
 
 
+def probs_dense(probs: torch.Tensor, bt: int, n_heads: int, t: int) -> torch.Tensor:
+    """The forward's fragment-tiled probabilities (csrc/relattn.hip) as [Bt, H, T, T]."""
+    nt = (t + 15) // 16
+    x = probs.view(bt * n_heads, nt, nt, 4, 16, 4)  # [bh][a][t][g][r][e]
+    x = x.permute(0, 1, 4, 2, 3, 5).reshape(bt, n_heads, 16 * nt, 16 * nt)
+    return x[:, :, :t, :t]
+
+
 def dropout_mask(shape, p: float, rng: torch.Tensor, rng_off: int = 0) -> torch.Tensor:
-    """The keep-mask (uint8, 1 = kept) the kernels draw for probs of ``shape`` (tests)."""
+    """The keep-mask (uint8, 1 = kept) the kernels draw for a tensor of ``shape`` whose last
+    dim is the row the mask index runs along (attention: [.., T, T]; a flat BitLinear /
+    LayerNorm tensor: (n,)) (tests)."""
     n = 1
     for s in shape:
         n *= s
     out = torch.empty(n, dtype=torch.uint8, device=rng.device)
     lib = _lib.load()
-    _lib.check(lib.ob_relattn_dropout_mask(n, float(p), rng.data_ptr(), int(rng_off),
-                                           out.data_ptr(), _lib.stream_of(rng)),
+    _lib.check(lib.ob_relattn_dropout_mask(n, int(shape[-1]), float(p), rng.data_ptr(),
+                                           int(rng_off), out.data_ptr(), _lib.stream_of(rng)),
                "ob_relattn_dropout_mask")
     return out.view(*shape)

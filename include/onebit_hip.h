@@ -332,14 +332,19 @@ OB_API int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, c
  *   pos, dpos : [P][T][H*d]    (pass p = b / (Bt/P) for stacked passes; P = 1 otherwise)
  *   u, vb, du, dvb : [H][d]    (pos_bias_u / pos_bias_v)
  *   lens : DEVICE int32 [Bt]   (valid frames; the encoder's prefix masks)
- *   probs : [Bt][H][T][T]      softmax before dropout; written by fwd when non-NULL,
- *                              required by bwd. With p_drop > 0 each element's sign bit
- *                              is its dropout decision (dropped: -P; |probs| = softmax)
+ *   probs : MFMA-fragment tiles [Bt*H][nt][nt][64][4], nt = ceil(T/16), of the softmax
+ *           before dropout (ob_relattn_probs_elems floats): tile (a, t), lane r + 16g,
+ *           element e holds P[16a + r][16t + 4g + e] (rows / keys >= T: 0). Written by
+ *           fwd when non-NULL, required by bwd. With p_drop > 0 each element's sign bit is
+ *           its dropout decision (dropped: -P; |probs| = softmax)
+ *   ctx (bwd) : the forward's output (the softmax backward's row term is dO . ctx)
  *   rng : DEVICE int64 [2] (seed, counter), rng_offset a host offset added to the counter
  *         (the fused BitLinear entries' convention: one device state, a distinct offset per
- *         call site, the counter advanced once per step); dropout keeps element e of probs
- *         when hash(seed, counter + rng_offset, e) >= p_drop * 2^32 (fwd and bwd regenerate
- *         the same mask; ob_relattn_dropout_mask writes it out). Unused when p_drop == 0.
+ *         call site, the counter advanced once per step); dropout keeps element (i, j) of
+ *         row bh when the 16-bit field (j & 1) of hash(seed, counter + rng_offset,
+ *         ((bh*T + i)*Te + j) / 2) >= p_drop * 2^16, Te = T rounded up to even (the bwd
+ *         reads the forward's decision from probs; ob_relattn_dropout_mask writes the mask
+ *         out). Unused when p_drop == 0.
  * Supported: 1 <= T <= 512, d in {16, 32, 36, 64}.
  * ------------------------------------------------------------------------------------ */
 OB_API int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
@@ -347,16 +352,19 @@ OB_API int ob_relattn_fwd(const float* q, const float* k, const float* v, const 
                           int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
                           const int64_t* rng, int64_t rng_offset, float* probs, float* ctx,
                           void* stream);
+OB_API int64_t ob_relattn_probs_elems(int64_t Bt, int64_t T, int64_t H);
 OB_API size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
-OB_API int ob_relattn_bwd(const float* dctx, const float* q, const float* k, const float* v,
-                          const float* pos, const float* u, const float* vb,
+OB_API int ob_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
+                          const float* v, const float* pos, const float* u, const float* vb,
                           const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H,
                           int64_t d, float p_drop, const int64_t* rng, int64_t rng_offset,
                           const float* probs,
                           float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb,
                           void* ws, size_t ws_bytes, void* stream);
-/* The dropout keep-mask (1 = kept) the attention kernels use, for n elements of probs. */
-OB_API int ob_relattn_dropout_mask(int64_t n, float p_drop, const int64_t* rng,
+/* The dropout keep-mask (1 = kept) of n elements laid out in rows of row_len: the attention
+ * kernels' mask of [rows][T] probabilities with row_len = T, the BitLinear / LayerNorm /
+ * residual-dropout kernels' mask of a flat tensor with row_len = n. */
+OB_API int ob_relattn_dropout_mask(int64_t n, int64_t row_len, float p_drop, const int64_t* rng,
                                    int64_t rng_offset, uint8_t* out, void* stream);
 
 /* Token-embedding backward of the decoder (conformer.py:279-299, nn.Embedding with

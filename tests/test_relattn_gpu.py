@@ -97,15 +97,19 @@ def test_relattn_probs_and_determinism(gpu):
     q, k, v, pos, u, vb = (x.to(gpu) for x in _inputs(bt, P, t, H, d, seed=3))
     lens = torch.tensor([249, 120, 0, 249], dtype=torch.int32)
     lib = _lib.load()
+    from onebit_asr.attention import probs_dense
+
     outs = []
     for _ in range(2):
-        probs = torch.empty(bt, H, t, t, device=gpu)
+        probs = torch.full((lib.ob_relattn_probs_elems(bt, t, H),), float("nan"), device=gpu)
         ctx = torch.empty_like(q)
         _lib.check(lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                       u.data_ptr(), vb.data_ptr(), lens.to(gpu).data_ptr(), bt, P,
                                       t, H, d, 0.0, None, 0, probs.data_ptr(), ctx.data_ptr(),
                                       _lib.stream_of(q)), "fwd")
-        outs.append((probs.clone(), ctx.clone()))
+        # every padding slot of the fragment tiles is written (zero)
+        assert torch.isfinite(probs).all().item()
+        outs.append((probs_dense(probs, bt, H, t).clone(), ctx.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     _, rprobs = _ref(*(x.double().cpu() for x in (q, k, v, pos, u, vb)), lens.long(), H)
     _close(outs[0][0], rprobs, 0.0, 1e-6, "probs")

@@ -33,7 +33,7 @@ def main():
     u, vb = torch.randn(H, d, device=dev) * 0.01, torch.randn(H, d, device=dev) * 0.01
     lens = torch.full((Bt,), T, dtype=torch.int32, device=dev)
     rng = torch.tensor([1234, 1], dtype=torch.int64, device=dev)
-    probs = torch.empty(Bt, H, T, T, device=dev)
+    probs = torch.empty(lib.ob_relattn_probs_elems(Bt, T, H), device=dev)
     ctx = torch.empty_like(q)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     dpos, du, dvb = torch.empty_like(pos), torch.empty_like(u), torch.empty_like(vb)
@@ -46,7 +46,7 @@ def main():
                                   rng.data_ptr(), 0, probs.data_ptr(), ctx.data_ptr(), s)
 
     def bwd(s):
-        return lib.ob_relattn_bwd(do.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
+        return lib.ob_relattn_bwd(do.data_ptr(), ctx.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                   pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), Bt,
                                   P, T, H, d, a.p, rng.data_ptr(), 0, probs.data_ptr(), dq.data_ptr(),
                                   dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(), du.data_ptr(),
