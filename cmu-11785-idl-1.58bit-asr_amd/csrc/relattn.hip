@@ -272,7 +272,10 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   const float rsum = row_live ? 1.0f / sum : 0.0f;
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
   const uint64_t didx = drop_row_base(bh, T, qi) + 4 * g;  // + 16t
-  float* pf = probs ? probs + frag_off(bh, (i0 >> 4) + w, 0, nt) + 4 * lane : nullptr;
+  // this wave's row tile of probs (waves past the last row tile -- T not a multiple of
+  // 64 -- store nothing)
+  const int arow = (i0 >> 4) + w;
+  float* pf = probs && arow < nt ? probs + frag_off(bh, arow, 0, nt) + 4 * lane : nullptr;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     if (t >= nt) continue;
@@ -388,7 +391,9 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
 
   // dPd[query qi][key] = dO . v (A = v rows, B = dO row); P from the fragment tiles;
   // dS' = P (dPd * keep * scale - delta) / sqrt(d) (softmax backward, then the 1/sqrt(d))
-  const float* pf = probs + frag_off(bh, (i0 >> 4) + w, 0, nt) + 4 * lane;
+  // (waves past the last row tile of probs -- T not a multiple of 64 -- read zeros)
+  const bool arow_ok = (i0 >> 4) + w < nt;
+  const float* pf = probs + frag_off(bh, arow_ok ? (i0 >> 4) + w : 0, 0, nt) + 4 * lane;
   float* brow = band + (1 + ir) * T + 4 * g;  // band row of query qi
   float dsr[NTT][4];
   float opa[4][DQ];
@@ -401,8 +406,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     f32x4 p4[4];
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu)
-      p4[uu] = t0 + uu < nt ? *reinterpret_cast<const f32x4*>(pf + 256 * (t0 + uu))
-                            : f32x4{0.f, 0.f, 0.f, 0.f};
+      p4[uu] = arow_ok && t0 + uu < nt ? *reinterpret_cast<const f32x4*>(pf + 256 * (t0 + uu))
+                                       : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc4[4];
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) acc4[uu] = f32x4{0.f, 0.f, 0.f, 0.f};
