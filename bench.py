@@ -110,8 +110,9 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
 
     lib = _lib.load()
     P = PASSES
-    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0], "dw_lds+dw_finish": [0.0, 0.0, 0.0, 0]}
-    # fam value: [total_time_us_per_step, total_bytes_per_step, total_flops_per_step, launches]
+    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0, 0.0], "dw_lds+dw_finish": [0.0, 0.0, 0.0, 0, 0.0]}
+    # fam value: [total_time_us_per_step, total_bytes_per_step, total_flops_per_step, launches,
+    #             MFMA pipe cycles per step summed over SIMDs]
     detail = []
     side = torch.cuda.Stream(dev)
     bits_t = torch.tensor(PASS_BITS, dtype=torch.int32, device=dev)
@@ -178,21 +179,31 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
         by_dw = 4 * (rows * N + rows * K + 2 * N * K + N)   # dY, X, W, dW, db
         fl = 2.0 * rows * K * N
         n_dx = 0 if name == "pos" else count  # pos_emb needs no input gradient
+        # MFMA instructions the kernels issue: v_mfma_f32_16x16x32_bf16 (16 cycles per SIMD,
+        # MI355X_MICROARCH.md cycle constants), 3 per 16x16x32 block in the bf16x3 ternary
+        # GEMM (fwd: K padded to 32; dX: N padded), 6 in the bf16x6 dW
+        t16 = lambda a: -(-a // 16)  # noqa: E731
+        t32 = lambda a: -(-a // 32)  # noqa: E731
+        cyc_f = 16 * 3 * t16(rows) * t16(N) * t32(K)
+        cyc_dx = 16 * 3 * t16(rows) * t16(K) * t32(N)
+        cyc_dw = 16 * 6 * t16(N) * t16(K) * t32(rows)
         f = fam["ternary_gemm"]
         f[0] += count * t_f + n_dx * t_dx
         f[1] += count * by_f + n_dx * by_dx
         f[2] += (count + n_dx) * fl
         f[3] += count + n_dx
+        f[4] += count * cyc_f + n_dx * cyc_dx
         f = fam["dw_lds+dw_finish"]
         f[0] += count * t_dw
         f[1] += count * by_dw
         f[2] += count * fl
         f[3] += count
+        f[4] += count * cyc_dw
         detail.append({"layer": name, "M_per_pass": M, "passes": P, "K": K, "N": N,
                        "launches_per_step": count, "fwd_us": round(t_f, 2),
                        "dx_us": round(t_dx, 2), "dw_us": round(t_dw, 2)})
     dom = max(fam, key=lambda k: fam[k][0])
-    t_us, by, fl, n = fam[dom]
+    t_us, by, fl, n, cyc = fam[dom]
     avg_t = t_us / n
     gbs = (by / n) / (avg_t * 1e-6) / 1e9
     tfs = (fl / n) / (avg_t * 1e-6) / 1e12
@@ -208,7 +219,14 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
     else:
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(gbs / PEAK_HBM_GBS, 4)}
+    # MFMA-busy (north_star: "MFMA-busy against gfx950 peak"): the MFMA pipe cycles the
+    # family's instructions take, over the 1024 SIMDs x 2.4 GHz x its measured time
+    mfma_busy = cyc / 1024 / (t_us * 1e-6 * 2.4e9)
     roof.update({"kernel": dom, "avg_launch_us": round(avg_t, 3),
+                 "mfma_busy": round(mfma_busy, 4),
+                 "mfma_busy_basis": "issued v_mfma_f32_16x16x32_bf16 cycles (16/SIMD each: 3 per "
+                                    "block bf16x3, 6 bf16x6) / (1024 SIMDs x 2.4 GHz x time); "
+                                    "PMC SQ_VALU_MFMA_BUSY_CYCLES in profiles/r3/pmc_step_*.md",
                  "bytes_per_launch": int(by / n), "flops_per_launch": int(fl / n),
                  "achieved_GBs": round(gbs, 1), "achieved_TFLOPs": round(tfs, 2),
                  "ql_kernel_ms_per_step": {k: round(v[0] / 1e3, 3) for k, v in fam.items()},

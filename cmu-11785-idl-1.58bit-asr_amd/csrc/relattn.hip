@@ -78,6 +78,40 @@ __device__ __forceinline__ void load_group(const float* __restrict__ base, int C
     load_run<DQ>(base + (size_t)min(16 * (t0 + u) + r, T - 1) * C + g * DQ, dst[u]);
 }
 
+// Buffer descriptor over one (batch row or pass, head) slice of a [rows][H*d] tensor:
+// [base, base + bytes); loads past it return 0 (hardware range check), so rows >= T need no
+// clamp, and every offset is a 32-bit VGPR / SGPR / immediate sum (no 64-bit address math
+// per load).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const float* base, int T, int C,
+                                                             int D) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
+                                           (int)(((size_t)(T - 1) * C + D) * sizeof(float)),
+                                           0x00020000);
+}
+
+// A operands of key/position tiles t0 .. t0+3 for the 16x16x4 MFMA from a slice: lane
+// (r, g) takes columns g*DQ .. g*DQ+DQ-1 of row 16t+r (voff = (r*C + g*DQ) * 4; rows >= T
+// read 0).
+template <int DQ>
+__device__ __forceinline__ void load_group_buf(__amdgpu_buffer_rsrc_t rs, int voff, int C, int t0,
+                                               float (&dst)[4][DQ]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int soff = 64 * (t0 + u) * C;  // 16 rows
+#pragma unroll
+    for (int i = 0; i + 4 <= DQ; i += 4) {
+      const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 4 * i, soff, 0);
+      dst[u][i] = v[0];
+      dst[u][i + 1] = v[1];
+      dst[u][i + 2] = v[2];
+      dst[u][i + 3] = v[3];
+    }
+#pragma unroll
+    for (int i = DQ & ~3; i < DQ; ++i)
+      dst[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff + 4 * i, soff, 0));
+  }
+}
+
 // Bijective XCD-aware remap (hardware block b runs on XCD b % 8): consecutive logical ids
 // share an XCD, so the query tiles and heads of one batch row -- which read the same
 // q/k/v/pos cache lines (heads are column slices of one row) -- share one L2.
@@ -150,6 +184,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   const float* pb = pos + (size_t)pass * T * C + h * D;
   const float* ub = u + h * D;
   const float* vbb = vbias + h * D;
+  const __amdgpu_buffer_rsrc_t rs_p = slice_rsrc(pb, T, C, D), rs_k = slice_rsrc(kb, T, C, D);
+  const int voff_a = (r * C + g * DQ) * 4;  // this lane's A-operand run in a 16-row group
 
   const int ir = 16 * w + r;  // this lane's query row in the tile (scores phase)
   const int qi = i0 + ir;
@@ -169,13 +205,14 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   // X = (q + v) p^T for the wave's 16 rows: D[pos][query] with A = p rows, B = (q+v),
   // four position tiles at a time (next group's p rows loading meanwhile), stored as
   // Xpad rows: img[ir][1 + m] = X[qi][m], img[ir][0] = 0.
-  float opa[4][DQ];
-  load_group<DQ>(pb, C, 0, r, g, T, opa);
+  // (two operand buffers used alternately by the fully unrolled group loop: no copies)
+  float opb[2][4][DQ];
+  load_group_buf<DQ>(rs_p, voff_a, C, 0, opb[0]);
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
-    float opn[4][DQ];
-    if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(pb, C, t0 + 4, r, g, T, opn);
+    float (&opa)[4][DQ] = opb[(t0 >> 2) & 1];
+    if (t0 + 4 < NTT && t0 + 4 < nt) load_group_buf<DQ>(rs_p, voff_a, C, t0 + 4, opb[((t0 >> 2) + 1) & 1]);
     f32x4 acc[4];
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) acc[uu] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -188,20 +225,19 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       const int t = t0 + uu;
       if (t >= nt) continue;
       float* dst = img + ir * ldi + 1 + 16 * t + 4 * g;
+      if (16 * t + 15 < T) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (16 * t + 4 * g + j < T) dst[j] = acc[uu][j];  // (m >= T: the next row's zero)
-    }
-    if (t0 + 4 < NTT) {
+        for (int j = 0; j < 4; ++j) dst[j] = acc[uu][j];
+      } else {
 #pragma unroll
-      for (int uu = 0; uu < 4; ++uu)
-#pragma unroll
-        for (int s2 = 0; s2 < DQ; ++s2) opa[uu][s2] = opn[uu][s2];
+        for (int j = 0; j < 4; ++j)
+          if (16 * t + 4 * g + j < T) dst[j] = acc[uu][j];  // (m >= T: the next row's zero)
+      }
     }
   }
   if (g == 0) img[ir * ldi] = 0.0f;
   // the first key group of the scores phase, in flight over the row-64 work and barrier
-  load_group<DQ>(kb, C, 0, r, g, T, opa);
+  load_group_buf<DQ>(rs_k, voff_a, C, 0, opb[0]);
   // Xpad row 64: the next tile's first query (fp32 fma chain on the VALU)
   if (i0 + kTile < T) {
     const float* qe = qb + (size_t)(i0 + kTile) * C;
@@ -225,8 +261,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
-    float opn[4][DQ];
-    if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(kb, C, t0 + 4, r, g, T, opn);
+    float (&opa)[4][DQ] = opb[(t0 >> 2) & 1];
+    if (t0 + 4 < NTT && t0 + 4 < nt) load_group_buf<DQ>(rs_k, voff_a, C, t0 + 4, opb[((t0 >> 2) + 1) & 1]);
     f32x4 acc4[4];
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) acc4[uu] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -234,12 +270,6 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu) acc4[uu] = mfma4(opa[uu][s], qu[s], acc4[uu]);
-    if (t0 + 4 < NTT) {
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu)
-#pragma unroll
-        for (int s2 = 0; s2 < DQ; ++s2) opa[uu][s2] = opn[uu][s2];
-    }
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) {
       const int t = t0 + uu;
@@ -364,6 +394,9 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* dob = dctx + bo;
   const float* cob = ctxo + bo;
   const float* pb = pos + (size_t)pass * T * C + h * D;
+  const __amdgpu_buffer_rsrc_t rs_v = slice_rsrc(vbp, T, C, D), rs_k = slice_rsrc(kb, T, C, D),
+                               rs_p = slice_rsrc(pb, T, C, D);
+  const int voff_a = (r * C + g * DQ) * 4;  // this lane's A-operand run in a 16-row group
   // dropout backward factor from a stored probability's sign bit (the forward's keep bit)
   auto keep_scale = [&](float pv) -> float {
     if (!dc.on) return 1.0f;
@@ -396,13 +429,13 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* pf = probs + frag_off(bh, arow_ok ? (i0 >> 4) + w : 0, 0, nt) + 4 * lane;
   float* brow = band + (1 + ir) * T + 4 * g;  // band row of query qi
   float dsr[NTT][4];
-  float opa[4][DQ];
-  load_group<DQ>(vbp, C, 0, r, g, T, opa);
+  float opb[2][4][DQ];
+  load_group_buf<DQ>(rs_v, voff_a, C, 0, opb[0]);
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
-    float opn[4][DQ];
-    if (t0 + 4 < NTT && t0 + 4 < nt) load_group<DQ>(vbp, C, t0 + 4, r, g, T, opn);
+    float (&opa)[4][DQ] = opb[(t0 >> 2) & 1];
+    if (t0 + 4 < NTT && t0 + 4 < nt) load_group_buf<DQ>(rs_v, voff_a, C, t0 + 4, opb[((t0 >> 2) + 1) & 1]);
     f32x4 p4[4];
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu)
@@ -415,12 +448,6 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     for (int s = 0; s < DQ; ++s)
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu) acc4[uu] = mfma4(opa[uu][s], dor[s], acc4[uu]);
-    if (t0 + 4 < NTT) {
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu)
-#pragma unroll
-        for (int s2 = 0; s2 < DQ; ++s2) opa[uu][s2] = opn[uu][s2];
-    }
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) {
       const int t = t0 + uu;
@@ -431,7 +458,14 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
         const float dp = acc4[uu][j] * keep_scale(pv);  // dropout backward
         const float ds = (fabsf(pv) * (dp - delta)) * inv_sqrt_d;
         dsr[t][j] = ds;
-        if (16 * t + 4 * g + j < T) brow[16 * t + j] = ds;
+      }
+      if (16 * t + 15 < T) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) brow[16 * t + j] = dsr[t][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (16 * t + 4 * g + j < T) brow[16 * t + j] = dsr[t][j];
       }
     }
   }
@@ -463,32 +497,28 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) oq[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
   // (B operands k[16t+4g+j][16ct+r] of tile t+1 load while tile t's MFMAs issue)
-  auto load_b = [&](const float* base, int t, float (&dst)[4][CT]) {
+  // (rows >= T read 0; columns >= D of a head read the next head's values, which only
+  // feed output columns that are never stored)
+  const int voff_b = (4 * g * C + r) * 4;
+  auto load_b = [&](int t, float (&dst)[4][CT]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* row = base + (size_t)min(16 * t + 4 * g + j, T - 1) * C;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) dst[j][ct] = row[min(16 * ct + r, D - 1)];
-    }
+      for (int ct = 0; ct < CT; ++ct)
+        dst[j][ct] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   rs_k, voff_b + 4 * (j * C + 16 * ct), 64 * t * C, 0));
   };
   {
-    float kb_cur[4][CT];
-    load_b(kb, 0, kb_cur);
+    float kbb[2][4][CT];
+    load_b(0, kbb[0]);
 #pragma unroll
     for (int t = 0; t < NTT; ++t) {
       if (t >= nt) continue;
-      float kb_nxt[4][CT];
-      if (t + 1 < NTT && t + 1 < nt) load_b(kb, t + 1, kb_nxt);
+      if (t + 1 < NTT && t + 1 < nt) load_b(t + 1, kbb[(t + 1) & 1]);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) oq[ct] = mfma4(dsr[t][j], kb_cur[j][ct], oq[ct]);
-      if (t + 1 < NTT) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int ct = 0; ct < CT; ++ct) kb_cur[j][ct] = kb_nxt[j][ct];
-      }
+        for (int ct = 0; ct < CT; ++ct) oq[ct] = mfma4(dsr[t][j], kbb[t & 1][j][ct], oq[ct]);
     }
   }
   __syncthreads();  // the band is complete (row 0 and every wave's rows)
@@ -503,17 +533,15 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   const float* xrow = band + i0 + 1 + ir * (T + 1) + g;  // dX[qi][4mk + g] = xrow[4mk]
   const int nk = (T + 3) >> 2;
   constexpr int kMK = 4;
+  // p[4mk + g][16ct + r]: positions >= T read 0 (range check)
+  const int voff_pm = (g * C + r) * 4;
   auto load_p = [&](int mk0, float (&dst)[kMK][CT]) {
 #pragma unroll
-    for (int qq = 0; qq < kMK; ++qq) {
-      const int m = 4 * (mk0 + qq) + g;
-      const float* prow = pb + (size_t)min(m, T - 1) * C;
+    for (int qq = 0; qq < kMK; ++qq)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const float x = prow[min(16 * ct + r, D - 1)];
-        dst[qq][ct] = m < T ? x : 0.0f;
-      }
-    }
+      for (int ct = 0; ct < CT; ++ct)
+        dst[qq][ct] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    rs_p, voff_pm + 64 * ct, 16 * (mk0 + qq) * C, 0));
   };
   float pv_cur[kMK][CT];
   load_p(0, pv_cur);
@@ -569,17 +597,23 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   }
 
   // dS' rows of this tile to global for the key-side kernel: band rows 1 .. 64 are the
-  // global rows i0 .. i0+63 at the same pitch T, i.e. one contiguous run -- copied as
-  // dwordx4 (unaligned) by the whole block
+  // global rows i0 .. i0+63 at the same pitch T, i.e. one contiguous run -- copied by the
+  // whole block, consecutive lanes on consecutive floats (conflict-free LDS reads, 256-B
+  // store segments), 8 loads in flight per thread
   float* dsb = dsg + (size_t)bh * T * T + (size_t)i0 * T;
   const int n = min(kTile, T - i0) * T;
   const float* src = band + T;
-  for (int e4 = 4 * threadIdx.x; e4 < n; e4 += 4 * kThreads) {
-    if (e4 + 3 < n) {
-      const f32x4 v4 = {src[e4], src[e4 + 1], src[e4 + 2], src[e4 + 3]};
-      *(f32x4u*)(dsb + e4) = v4;
-    } else {
-      for (int e = e4; e < n; ++e) dsb[e] = src[e];
+  for (int e0 = 0; e0 < n; e0 += 8 * kThreads) {
+    float v8[8];
+#pragma unroll
+    for (int q8 = 0; q8 < 8; ++q8) {
+      const int e = e0 + q8 * kThreads + threadIdx.x;
+      v8[q8] = src[e < n ? e : 0];
+    }
+#pragma unroll
+    for (int q8 = 0; q8 < 8; ++q8) {
+      const int e = e0 + q8 * kThreads + threadIdx.x;
+      if (e < n) dsb[e] = v8[q8];
     }
   }
 }
@@ -653,57 +687,53 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   // tile (i / 16, key0 / 16): one aligned dwordx4
   const size_t pcol = (size_t)256 * (key0 >> 4) + 64 * ((key0 & 15) >> 2);
   f32x4 ra_k[kAH], ra_v[kAH], ra_p[kAH], rb[St::kBSlots];
+  // buffer descriptors: dS' of (b, h) [T][T], its probs fragment tiles, q / dO slices
+  // (loads past a descriptor return 0: rows >= T need no test)
+  const __amdgpu_buffer_rsrc_t rs_ds = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(dsb), (short)0, (int)((size_t)T * T * sizeof(float)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_pr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(prb), (short)0, (int)((size_t)nt * nt * 256 * sizeof(float)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_q = slice_rsrc(qb, T, C, D), rs_do = slice_rsrc(dob, T, C, D);
+  const bool kfull = key0 + 3 < T;  // this thread's 4 keys all < T (false only in the last tile)
   auto fetch = [&](int i0) {
 #pragma unroll
     for (int hf = 0; hf < kAH; ++hf) {
-    const int i = i0 + ai + 16 * hf;
-    if (i < T && key0 + 3 < T) {
-      ra_k[hf] = *(const f32x4u*)(dsb + (size_t)i * T + key0);
-    } else {
+      const int i = i0 + ai + 16 * hf;
+      // dS'[i][key0 .. +3] and dX[i][key0 .. +3] = dS'.flat[i(T+1) + key0 + 1 - T + j] (the
+      // rel_shift adjoint read flat; 0 where that index is negative: row 0 only)
+      const int fk = i * T + key0, fx = i * (T + 1) + key0 + 1 - T;
+      if (kfull && i < T && fx >= 0) {
+        ra_k[hf] = __builtin_amdgcn_raw_buffer_load_b128(rs_ds, 4 * fk, 0, 0);
+        ra_p[hf] = __builtin_amdgcn_raw_buffer_load_b128(rs_ds, 4 * fx, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = i < T && key0 + j < T;
+          const float xk = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_ds, 4 * (fk + j), 0, 0));
+          const float xp = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_ds, 4 * max(fx + j, 0), 0, 0));
+          ra_k[hf][j] = ok ? xk : 0.0f;
+          ra_p[hf][j] = ok && fx + j >= 0 ? xp : 0.0f;
+        }
+      }
+      // P[i][key0 .. +3]: one aligned dwordx4 of fragment tile (i/16, key0/16) (zeros past T)
+      ra_v[hf] = key0 < 16 * nt
+                     ? __builtin_amdgcn_raw_buffer_load_b128(
+                           rs_pr, 4 * (int)((size_t)(i >> 4) * nt * 256 + pcol + 4 * (i & 15)), 0, 0)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+      // Pd = P * keep * scale, the keep bit from the stored probability's sign
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bool ok = i < T && key0 + j < T;
-        ra_k[hf][j] = ok ? dsb[(size_t)i * T + key0 + j] : 0.0f;
+        if (dc.on) ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
       }
-    }
-    ra_v[hf] = (i < T && key0 < 16 * nt)
-                   ? *reinterpret_cast<const f32x4*>(prb + (size_t)(i >> 4) * nt * 256 + pcol +
-                                                     4 * (i & 15))
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
-    // dX[i][m0..m0+3]: one unaligned dwordx4 when the four positions sit in one branch of
-    // the adjoint (upper: dS' row i from column m0-T+1+i; lower: row i-1 from m0+i+1)
-    const int up0 = T - 1 - i;  // first upper position of row i
-    if (i < T && key0 + 3 < T && (key0 >= up0 || (key0 + 3 < up0 && i >= 1))) {
-      const float* src = key0 >= up0 ? dsb + (size_t)i * T + (key0 - up0)
-                                     : dsb + (size_t)(i - 1) * T + (key0 + i + 1);
-      ra_p[hf] = *(const f32x4u*)src;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = key0 + j;
-        const bool ok = i < T && m < T;
-        const int ic = min(i, T - 1), mc = min(m, T - 1);
-        const bool upper = mc >= T - 1 - ic;
-        const size_t off = upper ? (size_t)ic * T + (mc - T + 1 + ic)
-                                 : (size_t)max(ic - 1, 0) * T + min(mc + ic + 1, T - 1);
-        const float x = dsb[off];
-        ra_p[hf][j] = (ok && (upper || ic >= 1)) ? x : 0.0f;
-      }
-    }
-    // Pd = P * keep * scale, the keep bit from the stored probability's sign
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (dc.on) ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
-    }
     }
 #pragma unroll
     for (int sl = 0; sl < St::kBSlots; ++sl) {
       const int e = threadIdx.x + kThreads * sl;
       const int e2 = e < St::kBVec ? e : e - St::kBVec;
       const int row = i0 + e2 / DQ, c4 = 4 * (e2 % DQ);
-      if (e < 2 * St::kBVec && row < T) {
-        const float* src = (e < St::kBVec ? qb : dob) + (size_t)row * C + c4;
-        rb[sl] = *(const f32x4u*)src;
+      if (e < 2 * St::kBVec) {
+        rb[sl] = __builtin_amdgcn_raw_buffer_load_b128(e < St::kBVec ? rs_q : rs_do,
+                                                       4 * (row * C + c4), 0, 0);
       } else {
         rb[sl] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
