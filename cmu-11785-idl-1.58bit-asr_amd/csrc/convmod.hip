@@ -18,6 +18,8 @@
 // Reductions are fixed-order (deterministic); statistics accumulate in fp64.
 #include <math.h>
 
+#include <cstdlib>
+
 #include "ob_launch.h"
 
 namespace ob {
@@ -417,6 +419,184 @@ __global__ __launch_bounds__(kThreads) void cm_glu_bwd_kernel(const float* __res
   }
 }
 
+// ------------------------------------------------------------------ channel-split tiles
+// The kernels above give one block a [W][C] window (all channels: 94 x 144 x 2 floats of LDS
+// in the backward), so one block fits a CU and its window loads never overlap arithmetic
+// (PMC: 58% of wave time waiting). These split the channels: block = (64-frame tile,
+// utterance, CG-channel group), 256 threads, LDS [W][CG] per array -- several blocks per
+// CU. The backward also folds what were two more passes over HBM into the tile: dz (the
+// BatchNorm + swish backward) is formed while the window loads, and the GLU backward is
+// applied to dg in registers (du written directly; dz and dg never reach HBM). The
+// arithmetic is the kernels' above, operation for operation (bitwise identical outputs).
+constexpr int kTT = 64;  // frames per tile (pick_tt's choice at every shape these serve)
+
+template <int KT, int CG>
+__global__ __launch_bounds__(kThreads) void cm_fwd_tile_kernel(
+    const float* __restrict__ u, const float* __restrict__ wdw, const float* __restrict__ bdw,
+    int T, int C, float* __restrict__ z, float* __restrict__ gout) {
+  constexpr int P = KT / 2, W = kTT + KT - 1, NW = W * CG;
+  __shared__ float gs[NW];
+  const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
+  const size_t rb = (size_t)b * T;
+  for (int i0 = 0; i0 < NW; i0 += kLB * kThreads) {
+    float va[kLB], vb[kLB];
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const int i = i0 + threadIdx.x + q * kThreads;
+      const int tl = i / CG, c = i - tl * CG;
+      const int t = t0 - P + tl;
+      const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
+      const float* ur = u + (rb + tc) * (size_t)(2 * C) + c0;
+      const int cc = i < NW ? c : 0;
+      va[q] = ur[cc];
+      vb[q] = ur[C + cc];
+    }
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const int i = i0 + threadIdx.x + q * kThreads;
+      if (i >= NW) break;
+      const int t = t0 - P + i / CG;
+      gs[i] = (t >= 0 && t < T) ? va[q] * sigm(vb[q]) : 0.0f;
+    }
+  }
+  __syncthreads();
+  constexpr int nrb = kTT / kR;
+  for (int it = threadIdx.x; it < CG * nrb; it += kThreads) {
+    const int c = it % CG, tl0 = kR * (it / CG);
+    if (t0 + tl0 >= T) break;
+    float wt[KT], out[kR];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) wt[j] = wdw[(c0 + c) * KT + j];
+    conv_window<KT, kR>(gs, CG, c, tl0, wt, out);
+    const float bc = bdw ? bdw[c0 + c] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int t = t0 + tl0 + r;
+      if (t < T) {
+        z[(rb + t) * C + c0 + c] = out[r] + bc;
+        gout[(rb + t) * C + c0 + c] = gs[(tl0 + r + P) * CG + c];  // kept for the weight gradient
+      }
+    }
+  }
+}
+
+template <int KT, int CG>
+__global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
+    const float* __restrict__ dv, const float* __restrict__ z, const float* __restrict__ g,
+    const float* __restrict__ u, const float* __restrict__ stats, const float* __restrict__ coef,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ wdw, int64_t rows_pp, int T, int C, float* __restrict__ du,
+    float* __restrict__ wpart) {
+  constexpr int P = KT / 2, W = kTT + KT - 1, NW = W * CG;
+  __shared__ float dzs[NW];  // dz over frames [t0-P, t0+kTT+P), the group's channels
+  __shared__ float gs[NW];   // g over the same window
+  const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
+  const size_t rb = (size_t)b * T;
+  // window: dz = BatchNorm + swish backward (per-pass statistics, cm_dz_kernel's formula)
+  for (int i0 = 0; i0 < NW; i0 += kLB * kThreads) {
+    float va[kLB], vz[kLB], vg[kLB];
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const int i = i0 + threadIdx.x + q * kThreads;
+      const int tl = i / CG, c = i - tl * CG;
+      const int t = t0 - P + tl;
+      const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
+      const size_t e = (rb + tc) * C + c0 + (i < NW ? c : 0);
+      va[q] = dv[e];
+      vz[q] = z[e];
+      vg[q] = g[e];
+    }
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const int i = i0 + threadIdx.x + q * kThreads;
+      if (i >= NW) break;
+      const int tl = i / CG, c = i - tl * CG;
+      const int t = t0 - P + tl;
+      const bool in = t >= 0 && t < T;
+      const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
+      const int cg = c0 + c;
+      const size_t pc = 2 * ((size_t)((rb + tc) / rows_pp) * C + cg);
+      float xh;
+      const float dy = bn_dy(va[q], vz[q], stats + pc, gamma[cg], beta[cg], xh);
+      const float dzv = gamma[cg] * stats[pc + 1] * (dy - coef[pc] - xh * coef[pc + 1]);
+      dzs[i] = in ? dzv : 0.0f;
+      gs[i] = in ? vg[q] : 0.0f;
+    }
+  }
+  __syncthreads();
+  // dg[t] = sum_j w[j] dz[t - j + P] (flipped weights), then the GLU backward (cm_glu_bwd's
+  // formula) in registers: du = [dg * s, dg * a * s * (1 - s)], (a, b) = u, s = sigmoid(b)
+  constexpr int nrb = kTT / kR;
+  for (int it = threadIdx.x; it < CG * nrb; it += kThreads) {
+    const int c = it % CG, tl0 = kR * (it / CG);
+    if (t0 + tl0 >= T) break;
+    float wt[KT], out[kR];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) wt[j] = wdw[(c0 + c) * KT + (KT - 1 - j)];
+    conv_window<KT, kR>(dzs, CG, c, tl0, wt, out);
+    float ua[kR], ub[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int t = min(t0 + tl0 + r, T - 1);
+      const size_t a = (rb + t) * (size_t)(2 * C) + c0 + c;
+      ua[r] = u[a];
+      ub[r] = u[a + C];
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int t = t0 + tl0 + r;
+      if (t < T) {
+        const size_t a = (rb + t) * (size_t)(2 * C) + c0 + c;
+        const float sb = sigm(ub[r]);
+        du[a] = out[r] * sb;
+        du[a + C] = out[r] * ua[r] * sb * (1.0f - sb);
+      }
+    }
+  }
+  // weight-gradient partial over this tile's frames (cm_dw_bwd_kernel's loop): item =
+  // (channel, 8 consecutive taps j0..j0+7; tap K is the bias, g == 1)
+  const int n_t = min(kTT, T - t0);
+  float* wp = wpart + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * C * (KT + 1);
+  constexpr int ngrp = (KT + 1 + 7) / 8;
+  for (int it = threadIdx.x; it < CG * ngrp; it += kThreads) {
+    const int c = it % CG, j0 = 8 * (it / CG);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
+    float gr[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gr[q] = gs[min(j0 + q, W - 1) * CG + c];
+    for (int tl = 0; tl < n_t; ++tl) {
+      const float d = dzs[(tl + P) * CG + c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int j = j0 + q;
+        acc[q] = fmaf(d, j < KT ? gr[q] : (j == KT ? 1.0f : 0.0f), acc[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 7; ++q) gr[q] = gr[q + 1];
+      gr[7] = gs[min(tl + 1 + j0 + 7, W - 1) * CG + c];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (j0 + q <= KT) wp[(size_t)(c0 + c) * (KT + 1) + j0 + q] = acc[q];
+  }
+}
+
+// channel group of the tile kernels (0: none applies -- the whole-row kernels run).
+// OB_CM_TILE=0 in the environment forces the whole-row kernels (bitwise A/B test).
+int tile_cg(int64_t C, int64_t K) {
+  static const bool off = [] {
+    const char* e = getenv("OB_CM_TILE");
+    return e && e[0] == '0';
+  }();
+  if (off || K != 31) return 0;
+  if (C % 48 == 0) return 48;
+  if (C % 32 == 0) return 32;
+  if (C % 16 == 0) return 16;
+  return 0;
+}
+
 // dw_dw[c][j] = sum over blocks (fixed order) of the partials; db_dw[c] likewise.
 // One wave per output: lanes take blocks k = lane, lane + 64, ... (fp64 lane sums).
 // Block = 64 consecutive outputs (c, j) x 16 block-slices (slice q: partials q, q+16, ...,
@@ -510,7 +690,19 @@ void launch_convmod_fwd(const float* u, const float* wdw, const float* bdw, cons
   double* part = reinterpret_cast<double*>(ws);
   const int TT = pick_tt(C, K);
   const dim3 gdw((unsigned)ceil_div(T, TT), (unsigned)Bt);
-  if (K == 31)  // the Conformer width (reference default, every config here)
+  const int cg = TT == kTT ? tile_cg(C, K) : 0;
+  if (cg) {  // channel-split tiles (the Conformer width K = 31, C a multiple of 16)
+    const dim3 gt((unsigned)ceil_div(T, kTT), (unsigned)Bt, (unsigned)(C / cg));
+    if (cg == 48)
+      hipLaunchKernelGGL((cm_fwd_tile_kernel<31, 48>), gt, dim3(kThreads), 0, s, u, wdw, bdw,
+                         (int)T, (int)C, z, g);
+    else if (cg == 32)
+      hipLaunchKernelGGL((cm_fwd_tile_kernel<31, 32>), gt, dim3(kThreads), 0, s, u, wdw, bdw,
+                         (int)T, (int)C, z, g);
+    else
+      hipLaunchKernelGGL((cm_fwd_tile_kernel<31, 16>), gt, dim3(kThreads), 0, s, u, wdw, bdw,
+                         (int)T, (int)C, z, g);
+  } else if (K == 31)  // the Conformer width (reference default, every config here)
     hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<31>, gdw, dim3(dw_threads(C, K)), lds_fwd((int)C, (int)K, TT),
                        s, u, wdw, bdw, (int)T, (int)C, (int)K, TT, z, g);
   else
@@ -548,6 +740,21 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
                      dv, z, stats, gamma, beta, rows_pp, (int)C, S, part);
   hipLaunchKernelGGL(cm_bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, s,
                      (const double*)part, (int)P, (int)C, S, rows_pp, coef, dgamma, dbeta);
+  const int cg = TT == kTT ? tile_cg(C, K) : 0;
+  if (cg) {  // dz, dg and the GLU backward inside the channel-split tiles
+    const dim3 gt((unsigned)ntt, (unsigned)Bt, (unsigned)(C / cg));
+#define OB_CM_BWD_TILE(CG)                                                                      \
+  hipLaunchKernelGGL((cm_bwd_tile_kernel<31, CG>), gt, dim3(kThreads), 0, s, dv, z, g, u, stats, \
+                     (const float*)coef, gamma, beta, wdw, rows_pp, (int)T, (int)C, du, wpart)
+    if (cg == 48) OB_CM_BWD_TILE(48);
+    else if (cg == 32) OB_CM_BWD_TILE(32);
+    else OB_CM_BWD_TILE(16);
+#undef OB_CM_BWD_TILE
+    hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)ceil_div(C * (K + 1), 64)),
+                       dim3(64 * kWfSlices), 0, s,
+                       (const float*)wpart, (int)(Bt * ntt), (int)C, (int)K, dwdw, dbdw);
+    return;
+  }
   hipLaunchKernelGGL(cm_dz_kernel, dim3((unsigned)eblocks), dim3(kThreads), 0, s, dv, z, stats,
                      (const float*)coef, gamma, beta, rows_pp, (int)C, total, dz);
   const dim3 gdw((unsigned)ntt, (unsigned)Bt);

@@ -88,3 +88,43 @@ def test_convmod_abi_errors(gpu):
     assert lib.ob_convmod_workspace(2, 3, 10, 144, 31) == 0  # Bt not a multiple of P
     assert lib.ob_convmod_workspace(1, 2, 10, 4096, 31) == 0  # LDS tile cannot fit
     assert lib.ob_convmod_workspace(3, 6, 249, 144, 31) > 0
+
+
+@pytest.mark.parametrize("d,bt,t,passes", [(144, 6, 249, 3), (64, 2, 182, 1), (48, 3, 70, 3)])
+def test_conv_module_tiles_bitwise_equal_whole_row(gpu, d, bt, t, passes):
+    """The channel-split tile kernels (dz and the GLU backward folded in) == the whole-row
+    kernels bit for bit: the same operations in the same order (OB_CM_TILE=0 forces the
+    latter; the switch is read once per process, so each side runs in its own process)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    code = f"""
+import sys, torch
+sys.path[:0] = [{str(root)!r}, {str(root / 'cmu-11785-idl-1.58bit-asr_amd')!r}]
+from onebit_asr.conformer import ConvModule
+torch.manual_seed(7)
+m = ConvModule({d}, kernel_size=31, dropout=0.0).cuda().eval()
+with torch.no_grad():
+    m.bn.weight.uniform_(0.5, 1.5); m.bn.bias.uniform_(-0.2, 0.2)
+x = (torch.randn({bt}, {t}, {d}, device='cuda', generator=torch.Generator(device='cuda').manual_seed(3)) * 2 + 0.3).requires_grad_()
+y = m(x, passes={passes})
+g = torch.randn(y.shape, device='cuda', generator=torch.Generator(device='cuda').manual_seed(5))
+(y * g).sum().backward()
+out = {{'y': y.detach().cpu(), 'gx': x.grad.cpu()}}
+out.update({{n: q.grad.cpu() for n, q in m.named_parameters()}})
+torch.save(out, sys.argv[1])
+"""
+    res = []
+    for flag in ("1", "0"):
+        f = f"/tmp/cm_tile_{os.getpid()}_{flag}.pt"
+        env = dict(os.environ, OB_CM_TILE=flag, OB_FUSED="1")
+        r = subprocess.run([sys.executable, "-c", code, f], env=env, capture_output=True,
+                           text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(torch.load(f, weights_only=True))
+        os.unlink(f)
+    for k in res[0]:
+        assert torch.equal(res[0][k], res[1][k]), k
