@@ -29,7 +29,12 @@ namespace {
 constexpr int kThreads = 256;
 constexpr size_t kMaxLds = 160 * 1024;
 
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// sigmoid through v_exp_f32 and v_rcp_f32 (a few ulp from torch's expf-based sigmoid, far
+// inside the fused-vs-unfused bars of tests/test_convmod_gpu.py; the accurate expf and IEEE
+// division were ~35 VALU ops per element, most of the depthwise tiles' arithmetic)
+__device__ __forceinline__ float sigm(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+// swish y * sigmoid(y)
+__device__ __forceinline__ float swish(float y) { return y * sigm(y); }
 
 // out[r] = sum_j wt[j] * tile[(tl0 + r + j) * C + c], r < R: one channel, R consecutive
 // frames, the R + KT - 1 tile values held in registers (KT compile-time) -- 1 + (KT-1)/R LDS
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(kThreads) void cm_bn_swish_fwd_kernel(
     const int p = (int)(row / rows_pp);
     const float* st = stats + 2 * ((size_t)p * C + c);
     const float y = (z[i] - st[0]) * st[1] * gamma[c] + beta[c];
-    v[i] = y / (1.0f + expf(-y));
+    v[i] = swish(y);
   }
 }
 
@@ -583,6 +588,111 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
   }
 }
 
+// ------------------------------------------------------------------ row-vectorised passes
+// The per-element kernels above index with 64-bit divisions (i / C, row / rows_pp) and one
+// float per thread; these take a row's channels as float4 groups (C % 4 == 0): thread
+// (row lane, group) of a 256-thread block, kRL = 256 / (C/4) rows per block iteration, one
+// division per row, dwordx4 loads and stores.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// v = swish(gamma * (z - mean) * rstd + beta), pass-wise statistics (cm_bn_swish_fwd's formula)
+__global__ __launch_bounds__(kThreads) void cm_bn_swish_rows_kernel(
+    const float* __restrict__ z, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int rows_pp, int rows, int C, float* __restrict__ v) {
+  const int G = C / 4, rl = threadIdx.x / G, q = threadIdx.x - rl * G, RL = kThreads / G;
+  if (rl >= RL) return;
+  const int c = 4 * q;
+  const f32x4 gm = *reinterpret_cast<const f32x4*>(gamma + c);
+  const f32x4 bt = *reinterpret_cast<const f32x4*>(beta + c);
+  for (int row = blockIdx.x * RL + rl; row < rows; row += gridDim.x * RL) {
+    const int p = row / rows_pp;
+    const float* st = stats + 2 * ((size_t)p * C + c);
+    const f32x4 zz = *reinterpret_cast<const f32x4*>(z + (size_t)row * C + c);
+    f32x4 out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float y = (zz[e] - st[2 * e]) * st[2 * e + 1] * gm[e] + bt[e];
+      out[e] = swish(y);
+    }
+    *reinterpret_cast<f32x4*>(v + (size_t)row * C + c) = out;
+  }
+}
+
+// Per-(pass, chunk) partial sums (fp64) of x and x^2 (MODE 0: the statistics of z) or of
+// dy_bn and dy_bn * xhat (MODE 1: the BatchNorm backward's sums), per channel: block =
+// (chunk, pass); thread (row lane rl, group q) walks rows r0 + rl, r0 + rl + RL, ... of the
+// chunk; the RL row lanes are added in lane order through LDS (fixed order).
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void cm_sums_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ dv, const float* __restrict__ stats,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int64_t rows_pp, int C,
+    int S, double* __restrict__ part) {
+  __shared__ double red[kThreads][2 * 4];
+  const int G = C / 4, rl = threadIdx.x / G, q = threadIdx.x - rl * G, RL = kThreads / G;
+  const int s = blockIdx.x, p = blockIdx.y;
+  const int64_t r0 = rows_pp * s / S, r1 = rows_pp * (s + 1) / S;
+  const size_t base = (size_t)p * rows_pp * C;
+  const int c = 4 * q;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (rl < RL) {
+    f32x4 gm = {0.f, 0.f, 0.f, 0.f}, bt = gm;
+    const float* st = stats + 2 * ((size_t)p * C + c);
+    if (MODE == 1) {
+      gm = *reinterpret_cast<const f32x4*>(gamma + c);
+      bt = *reinterpret_cast<const f32x4*>(beta + c);
+    }
+    // rows in batches of 4 per lane, all loads of a batch issued first (clamped addresses,
+    // masked use)
+    for (int64_t rb = r0 + rl; rb < r1; rb += 4 * RL) {
+      f32x4 a[4], d[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t r = min(rb + k * RL, r1 - 1);
+        a[k] = *reinterpret_cast<const f32x4*>(x + base + r * C + c);
+        if (MODE == 1) d[k] = *reinterpret_cast<const f32x4*>(dv + base + r * C + c);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (rb + k * RL >= r1) break;
+        if (MODE == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s1[e] += (double)a[k][e];
+            s2[e] += (double)a[k][e] * a[k][e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float xh;
+            const float dd = bn_dy(d[k][e], a[k][e], st + 2 * e, gm[e], bt[e], xh);
+            s1[e] += dd;
+            s2[e] += (double)dd * xh;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[threadIdx.x][2 * e] = s1[e];
+    red[threadIdx.x][2 * e + 1] = s2[e];
+  }
+  __syncthreads();
+  if (rl == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      double t1 = 0.0, t2 = 0.0;
+      for (int l = 0; l < RL; ++l) {
+        t1 += red[l * G + q][2 * e];
+        t2 += red[l * G + q][2 * e + 1];
+      }
+      double* o = part + (((size_t)p * C + c + e) * S + s) * 2;
+      o[0] = t1;
+      o[1] = t2;
+    }
+  }
+}
+
 // channel group of the tile kernels (0: none applies -- the whole-row kernels run).
 // OB_CM_TILE=0 in the environment forces the whole-row kernels (bitwise A/B test).
 int tile_cg(int64_t C, int64_t K) {
@@ -639,6 +749,16 @@ __global__ __launch_bounds__(64 * kWfSlices) void cm_wgrad_final_kernel(
 // Conformer-S (one batch of kSB loads in flight per thread), at most 512 chunks. Partials
 // are laid out [pass][channel][chunk][2] so the final kernels' lanes (consecutive chunks)
 // read consecutive 16-byte pairs.
+// chunks of the row-vectorised sums: ~8 rows per row lane (kThreads / (C/4) lanes), at most
+// stats_chunks' count (the workspace is sized for that)
+int rows_chunks(int64_t rows_pp, int64_t C) {
+  const int64_t per = 8 * (kThreads / (C / 4));
+  const int64_t s = (rows_pp + per - 1) / per;
+  const int64_t cap = (rows_pp + kSB - 1) / kSB;
+  const int64_t m = cap < 512 ? cap : 512;
+  return (int)(s < 1 ? 1 : (s > m ? m : s));
+}
+
 int stats_chunks(int64_t rows_pp) {
   const int64_t s = (rows_pp + kSB - 1) / kSB;
   return (int)(s < 1 ? 1 : (s > 512 ? 512 : s));
@@ -708,15 +828,30 @@ void launch_convmod_fwd(const float* u, const float* wdw, const float* bdw, cons
   else
     hipLaunchKernelGGL(cm_glu_dw_fwd_kernel<0>, gdw, dim3(dw_threads(C, K)), lds_fwd((int)C, (int)K, TT),
                        s, u, wdw, bdw, (int)T, (int)C, (int)K, TT, z, g);
-  hipLaunchKernelGGL(cm_stats_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
-                     (const float*)z, rows_pp, (int)C, S, part);
+  const bool rowvec = C % 4 == 0 && C / 4 <= kThreads && Bt * T < (1ll << 31);
+  const int Sr = rowvec ? rows_chunks(rows_pp, C) : S;
+  if (rowvec)
+    hipLaunchKernelGGL(cm_sums_rows_kernel<0>, dim3((unsigned)Sr, (unsigned)P), dim3(kThreads), 0, s,
+                       (const float*)z, (const float*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, (const float*)nullptr, rows_pp, (int)C, Sr, part);
+  else
+    hipLaunchKernelGGL(cm_stats_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
+                       (const float*)z, rows_pp, (int)C, S, part);
   hipLaunchKernelGGL(cm_stats_final_kernel, dim3((unsigned)(P * C)), dim3(64), 0, s,
-                     (const double*)part, (int)P, (int)C, S, rows_pp, eps, stats);
+                     (const double*)part, (int)P, (int)C, Sr, rows_pp, eps, stats);
   const int64_t total = Bt * T * C;
   int64_t blocks = ceil_div(total, kThreads);
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(cm_bn_swish_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s,
-                     (const float*)z, (const float*)stats, gamma, beta, rows_pp, (int)C, total, v);
+  if (rowvec) {
+    const int rl = kThreads / (int)(C / 4);
+    const int64_t rb = ceil_div(Bt * T, rl);
+    hipLaunchKernelGGL(cm_bn_swish_rows_kernel, dim3((unsigned)(rb < 8192 ? rb : 8192)),
+                       dim3(kThreads), 0, s, (const float*)z, (const float*)stats, gamma, beta,
+                       (int)rows_pp, (int)(Bt * T), (int)C, v);
+  } else {
+    hipLaunchKernelGGL(cm_bn_swish_fwd_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s,
+                       (const float*)z, (const float*)stats, gamma, beta, rows_pp, (int)C, total, v);
+  }
 }
 
 void launch_convmod_bwd(const float* dv, const float* u, const float* z, const float* g,
@@ -736,10 +871,16 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
   const int64_t total = Bt * T * C;
   int64_t eblocks = ceil_div(total, kThreads);
   if (eblocks > 8192) eblocks = 8192;
-  hipLaunchKernelGGL(cm_bn_bwd_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
-                     dv, z, stats, gamma, beta, rows_pp, (int)C, S, part);
+  const bool rowvec = C % 4 == 0 && C / 4 <= kThreads;
+  const int Sr = rowvec ? rows_chunks(rows_pp, C) : S;
+  if (rowvec)
+    hipLaunchKernelGGL(cm_sums_rows_kernel<1>, dim3((unsigned)Sr, (unsigned)P), dim3(kThreads), 0, s,
+                       z, dv, stats, gamma, beta, rows_pp, (int)C, Sr, part);
+  else
+    hipLaunchKernelGGL(cm_bn_bwd_part_kernel, dim3((unsigned)S, (unsigned)P), dim3(kThreads), 0, s,
+                       dv, z, stats, gamma, beta, rows_pp, (int)C, S, part);
   hipLaunchKernelGGL(cm_bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, s,
-                     (const double*)part, (int)P, (int)C, S, rows_pp, coef, dgamma, dbeta);
+                     (const double*)part, (int)P, (int)C, Sr, rows_pp, coef, dgamma, dbeta);
   const int cg = TT == kTT ? tile_cg(C, K) : 0;
   if (cg) {  // dz, dg and the GLU backward inside the channel-split tiles
     const dim3 gt((unsigned)ntt, (unsigned)Bt, (unsigned)(C / cg));
