@@ -424,6 +424,19 @@ __global__ __launch_bounds__(kThreads) void cm_glu_bwd_kernel(const float* __res
   }
 }
 
+// 32-bit offsets into one utterance slice through a buffer descriptor (no 64-bit address
+// arithmetic per access; loads past the slice read 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, off, 0, 0);
+}
+
 // ------------------------------------------------------------------ channel-split tiles
 // The kernels above give one block a [W][C] window (all channels: 94 x 144 x 2 floats of LDS
 // in the backward), so one block fits a CU and its window loads never overlap arithmetic
@@ -443,6 +456,7 @@ __global__ __launch_bounds__(kThreads) void cm_fwd_tile_kernel(
   __shared__ float gs[NW];
   const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
   const size_t rb = (size_t)b * T;
+  const __amdgpu_buffer_rsrc_t ru = rsrc(u + rb * 2 * C, (size_t)T * 2 * C * 4);
   for (int i0 = 0; i0 < NW; i0 += kLB * kThreads) {
     float va[kLB], vb[kLB];
 #pragma unroll
@@ -451,10 +465,9 @@ __global__ __launch_bounds__(kThreads) void cm_fwd_tile_kernel(
       const int tl = i / CG, c = i - tl * CG;
       const int t = t0 - P + tl;
       const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const float* ur = u + (rb + tc) * (size_t)(2 * C) + c0;
-      const int cc = i < NW ? c : 0;
-      va[q] = ur[cc];
-      vb[q] = ur[C + cc];
+      const int off = 4 * (tc * 2 * C + c0 + (i < NW ? c : 0));
+      va[q] = bload(ru, off);
+      vb[q] = bload(ru, off + 4 * C);
     }
 #pragma unroll
     for (int q = 0; q < kLB; ++q) {
@@ -497,6 +510,11 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
   __shared__ float gs[NW];   // g over the same window
   const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
   const size_t rb = (size_t)b * T;
+  const int pass = (int)(rb / rows_pp);  // every frame of utterance b is in its pass
+  const size_t sl = (size_t)T * C * 4;
+  const __amdgpu_buffer_rsrc_t rdv = rsrc(dv + rb * C, sl), rz = rsrc(z + rb * C, sl),
+                               rg = rsrc(g + rb * C, sl);
+  const __amdgpu_buffer_rsrc_t ru = rsrc(u + rb * 2 * C, 2 * sl), rdu = rsrc(du + rb * 2 * C, 2 * sl);
   // window: dz = BatchNorm + swish backward (per-pass statistics, cm_dz_kernel's formula)
   for (int i0 = 0; i0 < NW; i0 += kLB * kThreads) {
     float va[kLB], vz[kLB], vg[kLB];
@@ -506,10 +524,10 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
       const int tl = i / CG, c = i - tl * CG;
       const int t = t0 - P + tl;
       const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const size_t e = (rb + tc) * C + c0 + (i < NW ? c : 0);
-      va[q] = dv[e];
-      vz[q] = z[e];
-      vg[q] = g[e];
+      const int e = 4 * (tc * C + c0 + (i < NW ? c : 0));
+      va[q] = bload(rdv, e);
+      vz[q] = bload(rz, e);
+      vg[q] = bload(rg, e);
     }
 #pragma unroll
     for (int q = 0; q < kLB; ++q) {
@@ -518,9 +536,8 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
       const int tl = i / CG, c = i - tl * CG;
       const int t = t0 - P + tl;
       const bool in = t >= 0 && t < T;
-      const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
       const int cg = c0 + c;
-      const size_t pc = 2 * ((size_t)((rb + tc) / rows_pp) * C + cg);
+      const int pc = 2 * (pass * C + cg);
       float xh;
       const float dy = bn_dy(va[q], vz[q], stats + pc, gamma[cg], beta[cg], xh);
       const float dzv = gamma[cg] * stats[pc + 1] * (dy - coef[pc] - xh * coef[pc + 1]);
@@ -540,21 +557,18 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
     for (int j = 0; j < KT; ++j) wt[j] = wdw[(c0 + c) * KT + (KT - 1 - j)];
     conv_window<KT, kR>(dzs, CG, c, tl0, wt, out);
     float ua[kR], ub[kR];
+    const int a0 = 4 * ((t0 + tl0) * 2 * C + c0 + c);  // frames past T read 0, never stored
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      const int t = min(t0 + tl0 + r, T - 1);
-      const size_t a = (rb + t) * (size_t)(2 * C) + c0 + c;
-      ua[r] = u[a];
-      ub[r] = u[a + C];
+      ua[r] = bload(ru, a0 + 8 * C * r);
+      ub[r] = bload(ru, a0 + 8 * C * r + 4 * C);
     }
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      const int t = t0 + tl0 + r;
-      if (t < T) {
-        const size_t a = (rb + t) * (size_t)(2 * C) + c0 + c;
+      if (t0 + tl0 + r < T) {
         const float sb = sigm(ub[r]);
-        du[a] = out[r] * sb;
-        du[a + C] = out[r] * ua[r] * sb * (1.0f - sb);
+        bstore(rdu, a0 + 8 * C * r, out[r] * sb);
+        bstore(rdu, a0 + 8 * C * r + 4 * C, out[r] * ua[r] * sb * (1.0f - sb));
       }
     }
   }

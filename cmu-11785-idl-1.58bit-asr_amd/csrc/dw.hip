@@ -424,26 +424,6 @@ __global__ __launch_bounds__(kThreads, 2) void dw_bf16x6_kernel(
 // step. Loader unit = 4 rows x 4 columns of one operand (row quad fastest across lanes:
 // conflict-free ds_write_b64).
 // ---------------------------------------------------------------------------------
-// Profiling switches (tools/variant.sh builds; 0 in the product, results wrong otherwise):
-// drop the MFMAs / the split+store / the global loads of the LDS kernel to price them.
-#ifndef DW_EXP_NOMFMA
-#define DW_EXP_NOMFMA 0
-#endif
-#ifndef DW_EXP_NOSTORE
-#define DW_EXP_NOSTORE 0
-#endif
-#ifndef DW_EXP_NOLOAD
-#define DW_EXP_NOLOAD 0
-#endif
-#ifndef DW_EXP_STEPS1
-#define DW_EXP_STEPS1 0
-#endif
-#ifndef DW_EXP_NOOUT
-#define DW_EXP_NOOUT 0
-#endif
-#ifndef DW_EXP_EXIT
-#define DW_EXP_EXIT 0
-#endif
 constexpr int kLdsPitch = 224;  // bytes per column slot: 3 planes x 32 bf16 rows + 32 B pad
 constexpr int kStepRows = 32;
 
@@ -494,9 +474,8 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   const int64_t m_lim = (pass + 1) * M;
   const int64_t m_begin = pass * M + (chunk - pass * cpp) * rows_per_chunk;
   const int64_t m_end = m_begin + rows_per_chunk < m_lim ? m_begin + rows_per_chunk : m_lim;
-  const int steps = DW_EXP_STEPS1 ? 1 : (int)((m_end - m_begin + kStepRows - 1) / kStepRows);
+  const int steps = (int)((m_end - m_begin + kStepRows - 1) / kStepRows);
   const bool do_db = (part_db != nullptr) && (tk == 0);
-  if (DW_EXP_EXIT && steps < 1000000) return;
 
   // Loader units: 2 rows x 4 columns of one operand, row pair fastest across lanes
   // (conflict-free ds_write_b32: the two columns a 32-lane group writes sit 32 banks
@@ -531,7 +510,6 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
     f32x4 x[UX][2];
   };
   auto load = [&](Raw& raw, int step) {
-    if (DW_EXP_NOLOAD) step = 0;
     const int soy = step * kStepRows * N * 4, sox = step * kStepRows * K * 4;
 #pragma unroll
     for (int j = 0; j < UY; ++j)
@@ -566,7 +544,6 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
     }
   };
   auto store = [&](const Raw& raw, int buf) {
-    if (DW_EXP_NOSTORE) return;
     unsigned char* base = lds + buf * C::kBuf;
 #pragma unroll
     for (int j = 0; j < UY; ++j) {
@@ -607,11 +584,7 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
       for (int p = 0; p < 6; ++p)
 #pragma unroll
         for (int u = 0; u < 3; ++u)
-          if (!DW_EXP_NOMFMA) acc[t][u] = mfma_bf16(a[kProdA[p]], b[u][kProdB[p]], acc[t][u]);
-      if (DW_EXP_NOMFMA) {
-#pragma unroll
-        for (int u = 0; u < 3; ++u) acc[t][u][0] += (float)a[0][0] * (float)b[u][0][0];
-      }
+          acc[t][u] = mfma_bf16(a[kProdA[p]], b[u][kProdB[p]], acc[t][u]);
     }
   };
 
@@ -668,7 +641,7 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
           const int64_t e = (int64_t)n * K + k0 + 48 * wk + 16 * u + r;
-          if (!DW_EXP_NOOUT || acc[t][u][reg] == 12345.0f) out[e] = acc[t][u][reg];
+          out[e] = acc[t][u][reg];
           if constexpr (decltype(with_al)::value)
             prod += acc[t][u][reg] * alpha_term(al.W[e] / a, bits);
         }

@@ -36,23 +36,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// Phase-pricing experiments (tools/variant.sh builds; all 0 in the product)
-#ifndef SS_EXP_NOMFMA
-#define SS_EXP_NOMFMA 0
-#endif
-#ifndef SS_EXP_NOA
-#define SS_EXP_NOA 0
-#endif
-#ifndef SS_EXP_NOB
-#define SS_EXP_NOB 0
-#endif
-#ifndef SS_EXP_CLASS
-#define SS_EXP_CLASS -1
-#endif
-#ifndef SS_EXP_NOSTORE
-#define SS_EXP_NOSTORE 0
-#endif
-
 constexpr int kThr = 256;
 constexpr int kSlot = 224;  // LDS / image bytes per (row or column): 3 planes x 32 bf16 + pad
 constexpr int kBM = 64;     // GEMM rows per row fragment of the 4 waves
@@ -277,7 +260,6 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
   const int F1c = DGRAD ? (pf ? d.F1 / 2 : (d.F1 + 1) / 2) : 1;
   const int nblk = DGRAD ? ga.nblk[cl] : (int)gridDim.x;
   if ((int)blockIdx.x >= nblk) return;
-  if (DGRAD && SS_EXP_CLASS >= 0 && cl != SS_EXP_CLASS) return;
   const int L = DGRAD ? (int)blockIdx.x : xcd_logical((int)blockIdx.x, nblk);
   const int64_t t_begin = tiles * L / nblk, t_end = tiles * (L + 1) / nblk;
 
@@ -354,7 +336,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
           src = ga.src +
                 (((int64_t)ab[u] * d.T1 + 2 * ap1[u] + i) * d.F1 + 2 * ap2[u] + j) * C + cc;
         }
-        ok = ok && aok[u] && kok && !SS_EXP_NOA;
+        ok = ok && aok[u] && kok;
         aval |= (ok ? 1u : 0u) << u;
         ax[u][0] = *reinterpret_cast<const f32x4*>(src);
         ax[u][1] = *reinterpret_cast<const f32x4*>(src + 4);
@@ -366,7 +348,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
       for (int j = 0; j < kBSlotsPT; ++j) {
         const int e = threadIdx.x + j * kThr;
         const int ec = e < BN * kSlot / 16 ? e : BN * kSlot / 16 - 1;  // clamped, unguarded
-        bv[j] = SS_EXP_NOB ? f32x4{1.f, 1.f, 1.f, 1.f} : s4[ec];
+        bv[j] = s4[ec];
       }
     };
     f32x4 ax[MR][2], bv[kBSlotsPT];
@@ -381,7 +363,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
     for (int st = 0; st < ks; ++st) {
       __syncthreads();  // the previous step's fragment reads are done
 #pragma unroll
-      for (int u = 0; u < (SS_EXP_NOSTORE ? 0 : MR); ++u) {
+      for (int u = 0; u < MR; ++u) {
         // A: split 8 values (k = 8 aq .. +7 of row ar) into the row's slot
         unsigned char* s = la + ((threadIdx.x >> 2) + 64 * u) * kSlot + 16 * aq;
         const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
@@ -401,8 +383,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
 #pragma unroll
         for (int j = 0; j < kBSlotsPT; ++j) {
           const int e = threadIdx.x + j * kThr;
-          if (e < BN * kSlot / 16 && !SS_EXP_NOSTORE) d4[e] = bv[j];
-          if (SS_EXP_NOSTORE) acc[0][0][0] += bv[j][0] + ax[0][0][j & 3];
+          if (e < BN * kSlot / 16) d4[e] = bv[j];
         }
       }
       __syncthreads();
@@ -427,10 +408,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
         for (int p = 0; p < 6; ++p)
 #pragma unroll
           for (int u = 0; u < MR; ++u) {
-            if (SS_EXP_NOMFMA)
-              acc[u][t][p & 3] += (float)a[u][kProdA[p]][p] * (float)bq[kProdB[p]][u];
-            else
-              acc[u][t] = mfma_bf16(a[u][kProdA[p]], bq[kProdB[p]], acc[u][t]);
+            acc[u][t] = mfma_bf16(a[u][kProdA[p]], bq[kProdB[p]], acc[u][t]);
           }
       }
     }

@@ -30,20 +30,6 @@
 #include "ob_launch.h"
 #include "ob_quant.h"
 
-// Phase-pricing experiments (tools/variant.sh builds; all 0 in the product)
-#ifndef TG_EXP_NOSTORE
-#define TG_EXP_NOSTORE 0
-#endif
-#ifndef TG_EXP_NOMFMA
-#define TG_EXP_NOMFMA 0
-#endif
-#ifndef TG_EXP_NOA
-#define TG_EXP_NOA 0
-#endif
-#ifndef TG_EXP_PLAINEPI
-#define TG_EXP_PLAINEPI 0
-#endif
-
 namespace ob {
 
 namespace {
@@ -114,25 +100,19 @@ __device__ __forceinline__ float silu_bwd_f(float dy, float z) {
 // Store y = a*acc + b through the fused epilogue. `c` is this element's output address,
 // grow its pass-inclusive row. Non-contracting ops (ob_fp.h) keep hipcc from contracting the unfused
 // reference sequence (y, then *scale, then +R) into an fma.
-#ifndef TG_EXP_NODROP
-#define TG_EXP_NODROP 0
-#endif
-#ifndef TG_EXP_NOLENS
-#define TG_EXP_NOLENS 0
-#endif
 template <int MODE>
 __device__ __forceinline__ void epi_store(const EpiArgs& ep, uint32_t dkey, float* c,
                                           int64_t grow, int col, int N, float y, float rv) {
   const int64_t i = grow * N + col;
   const float keep =
-      (ep.dc.on && !TG_EXP_NODROP) ? (drop_keep(dkey, (uint64_t)i, ep.dc.thresh) ? ep.dc.scale : 0.0f) : 1.0f;
+      ep.dc.on ? (drop_keep(dkey, (uint64_t)i, ep.dc.thresh) ? ep.dc.scale : 0.0f) : 1.0f;
   if constexpr (MODE == kEpiSwishDrop) {
     ep.C2[i] = y;
     const float sv = silu_f(y);
     *c = ep.dc.on ? nc_mul(sv, keep) : sv;
   } else if constexpr (MODE == kEpiResidual) {
     bool valid = true;
-    if (ep.lens && !TG_EXP_NOLENS) {
+    if (ep.lens) {
       const int64_t b = grow / ep.T;
       valid = (grow - b * ep.T) < ep.lens[b];
     }
@@ -160,11 +140,6 @@ __device__ __forceinline__ void load8(const float* __restrict__ arow, int k, int
                                       f32x4& b) {
   const int ka = k < K - 4 ? k : K - 4;
   const int kb = k + 4 < K - 4 ? k + 4 : K - 4;
-  if (TG_EXP_NOA) {
-    a = f32x4{0.5f, 0.25f, 0.125f, 1.0f} * (float)ka;
-    b = f32x4{0.5f, 0.25f, 0.125f, 1.0f} * (float)kb;
-    return;
-  }
   a = *reinterpret_cast<const f32x4*>(arow + ka);
   b = *reinterpret_cast<const f32x4*>(arow + kb);
 }
@@ -199,7 +174,7 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
                                            const f32x4& rv) {
   const int64_t i = grow * N + col;
   float keep[4] = {1.f, 1.f, 1.f, 1.f};
-  if (ep.dc.on && !TG_EXP_NODROP) drop_scale4(dkey, (uint64_t)i, ep.dc, keep);  // i % 4 == 0
+  if (ep.dc.on) drop_scale4(dkey, (uint64_t)i, ep.dc, keep);  // i % 4 == 0
   f32x4 out;
   if constexpr (MODE == kEpiNone) {
     out = y;
@@ -347,12 +322,6 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       split3(x0, x1, hi, mid, lo);
       // part-major: consecutive MFMAs update different accumulators (no back-to-back
       // dependence on the MFMA just issued)
-      if (TG_EXP_NOMFMA) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acc[t][t & 3] += (float)lo[t & 7] * (float)bq[t][1] + (float)mid[1] * (float)hi[2];
-        return;
-      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(lo, bq[t], acc[t]);
 #pragma unroll
@@ -408,7 +377,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     // keep the epilogue's loads (residual / pre-activation) from being hoisted into the
     // main loop, where they would hold NT*4 VGPRs across it
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (VEC_EPI && !TG_EXP_NOSTORE) {
+    if constexpr (VEC_EPI) {
       // Row-coalesced epilogue: each chunk of <= 4 column tiles goes through the wave's LDS
       // staging tile, then every lane handles 4 consecutive columns of one row (dwordx4 R
       // loads and C / C2 stores; 16 lanes = 256 contiguous bytes). The wave's LDS ops run
@@ -422,7 +391,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
         // addresses before the LDS staging: its latency runs under the staging instead of
         // one load-to-use wait per guarded store below
         f32x4 rpre[kEpiCW];
-        if constexpr (kHasR && !TG_EXP_PLAINEPI) {
+        if constexpr (kHasR) {
 #pragma unroll
           for (int it = 0; it < kEpiCW; ++it) {
             const int idx = it * 64 + lane, row = idx / kQ, c4 = idx - row * kQ;
@@ -448,13 +417,13 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
           const f32x4 y = *reinterpret_cast<const f32x4*>(stg + row * kEpiLd + 4 * c4);
           // (the last chunk of an NT that is not a multiple of 4 holds fewer columns)
           if (orow < M && col < N && 4 * c4 < 16 * (NT - c0)) {
-            if constexpr (EPI == kEpiNone || TG_EXP_PLAINEPI) {
+            if constexpr (EPI == kEpiNone) {
               *reinterpret_cast<f32x4*>(C + orow * N + col) = y;
               if (EPI == kEpiSwishDrop)
                 *reinterpret_cast<f32x4*>(ep.C2 + (rowbase + orow) * N + col) = y;
             } else {
               bool valid = true;
-              if (EPI == kEpiResidual && ep.lens && !TG_EXP_NOLENS) {
+              if (EPI == kEpiResidual && ep.lens) {
                 const int64_t grow = rowbase + orow;
                 const int64_t bb = grow / ep.T;
                 valid = (grow - bb * ep.T) < ep.lens[bb];
@@ -469,7 +438,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       }
       continue;
     }
-    if constexpr (!VEC_EPI || TG_EXP_NOSTORE) {
+    if constexpr (!VEC_EPI) {
 
     // epilogue operand: all NT*4 loads issued before any is used (one latency, not 4*NT)
     // epilogue operand (residual / pre-activation): rolling prefetch kPre tiles ahead, so at
@@ -502,9 +471,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
         const int64_t orow = m0 + 4 * g + reg;
         if (orow >= M) continue;
         const float y = fmaf(a_eff, acc[t][reg], bcol[t]);
-        if (TG_EXP_NOSTORE) {
-          if (y == 1234.5f) C[orow * N + col] = y;
-        } else if constexpr (EPI == kEpiNone || TG_EXP_PLAINEPI) {
+        if constexpr (EPI == kEpiNone) {
           C[orow * N + col] = y;
           if (EPI == kEpiSwishDrop) ep.C2[(rowbase + orow) * N + col] = y;
         } else {
