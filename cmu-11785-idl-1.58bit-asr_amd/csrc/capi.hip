@@ -619,6 +619,32 @@ int ob_bitlinear_fwd_i8_epi(const float* X, int64_t P, int64_t M, int64_t K,
   return launched();
 }
 
+int ob_bitlinear_fwd_i8q(const int8_t* Xq, int64_t P, int64_t M, int64_t K,
+                         const uint32_t* codes, const uint32_t* codes1, const int32_t* pass_bits,
+                         const float* alpha, int alpha_raw, const float* amax, const float* bias,
+                         int64_t N, int mode, const float* R, float rscale, const int32_t* lens,
+                         int64_t T, float* amax_out, void* Y, void* stream) {
+  if (M < 0 || K < 0 || N < 0 || P < 1 || P > 65535 || (mode != 0 && mode != 2 && mode != 3) ||
+      N % 4)
+    return OB_ERR_SHAPE;
+  if (P > 1 && !pass_bits) return OB_ERR_NULL;
+  if (!alpha || !amax || (M * N > 0 && !Y) || (M * K > 0 && !Xq) || (N * K > 0 && !codes) ||
+      (pass_bits && N * K > 0 && !codes1) || (mode == 3 && !amax_out) ||
+      (mode == 2 && M * N > 0 && !R) || (lens && T < 1))
+    return OB_ERR_NULL;
+  if (M * N > 0 && !ternary_gemm_i8_supported(K, N)) return OB_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(Xq) & 15) || (reinterpret_cast<uintptr_t>(Y) & 15) ||
+      (reinterpret_cast<uintptr_t>(R) & 15) || !aligned4(bias) || !aligned4(amax) ||
+      !aligned4(pass_bits) || !aligned4(amax_out) || !aligned4(lens))
+    return OB_ERR_ALIGN;
+  if (!launch_ternary_gemm_i8q(Xq, (int)P, M, K, codes, pass_bits ? codes1 : codes,
+                               reinterpret_cast<const int*>(pass_bits), N, alpha, alpha_raw, amax,
+                               bias, Y, mode, R, rscale, reinterpret_cast<const int*>(lens), T,
+                               amax_out, as_stream(stream)))
+    return OB_ERR_SHAPE;
+  return launched();
+}
+
 int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
                                const uint32_t* codes2_t, const uint32_t* codes1_t,
                                const int32_t* pass_bits, const float* alpha, int alpha_raw,
@@ -905,6 +931,19 @@ int ob_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
     return OB_ERR_ALIGN;
   launch_layernorm_fwd_amax(x, gamma, beta, rows, d, eps, y, mean, rstd, (int)P, amax, ws,
                             as_stream(stream));
+  return launched();
+}
+
+int ob_layernorm_fwd_i8(const float* x, const float* gamma, const float* beta, int64_t rows,
+                        int64_t d, float eps, int64_t P, float* amax, int8_t* yq, void* ws,
+                        size_t ws_bytes, void* stream) {
+  if (rows < 0 || !layernorm_supported(d) || !(eps >= 0.0f) || P < 1 || P > 8 || rows % P)
+    return OB_ERR_SHAPE;
+  if ((rows > 0 && (!x || !yq)) || !amax || !ws) return OB_ERR_NULL;
+  if (ws_bytes < layernorm_fwd_amax_workspace(P)) return OB_ERR_WORKSPACE;
+  if (!aligned4(x) || !aligned4(yq) || !aligned4(gamma) || !aligned4(beta) || !aligned4(amax))
+    return OB_ERR_ALIGN;
+  launch_layernorm_fwd_i8(x, gamma, beta, rows, d, eps, (int)P, amax, yq, ws, as_stream(stream));
   return launched();
 }
 

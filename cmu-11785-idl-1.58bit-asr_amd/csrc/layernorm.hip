@@ -60,13 +60,15 @@ __device__ __forceinline__ void store_cols(float* __restrict__ p, int c0, const 
 }
 
 // One row (16 lanes): y = LN(x) and the row's (mean, rstd); returns this lane's max|y|.
+// y == nullptr: no fp32 store; yq != nullptr: also the int8 image of y at scale sx.
 template <int NPL, int VW = 1>
 __device__ __forceinline__ float ln_row(const float* __restrict__ x,
                                         const float* __restrict__ gamma,
                                         const float* __restrict__ beta, int64_t row, int d,
                                         float eps, float* __restrict__ y,
                                         float* __restrict__ mean_out,
-                                        float* __restrict__ rstd_out) {
+                                        float* __restrict__ rstd_out,
+                                        int8_t* __restrict__ yq = nullptr, float sx = 0.0f) {
   const int j = threadIdx.x & (kLanesPerRow - 1);
   const float* xr = x + row * d;
   float v[NPL][VW];
@@ -90,7 +92,6 @@ __device__ __forceinline__ float ln_row(const float* __restrict__ x,
     }
   const float var = row_sum16(q) * inv_d;
   const float rstd = 1.0f / sqrtf(var + eps);
-  float* yr = y + row * d;
   float amx = 0.0f;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
@@ -104,7 +105,18 @@ __device__ __forceinline__ float ln_row(const float* __restrict__ x,
         o[e] = fmaf((v[i][e] - mean) * rstd, gamma ? g[e] : 1.0f, beta ? b[e] : 0.0f);
         amx = fmaxf(amx, fabsf(o[e]));
       }
-      store_cols<VW>(yr, c0, o);
+      if (y) store_cols<VW>(y + row * d, c0, o);  // (nullptr: the absmax pass of the int8 LN)
+      if (yq) {  // int8 consumer: xq = clamp(rint(y * sx), -127, 127) (tgemm_i8.hip's q4)
+        uint32_t pk = 0;
+#pragma unroll
+        for (int e = 0; e < VW; ++e) {
+          float q = rintf(o[e] * sx);
+          q = fminf(fmaxf(q, -127.0f), 127.0f);
+          pk |= ((uint32_t)(int)q & 0xFFu) << (8 * e);
+        }
+        if constexpr (VW == 4) *reinterpret_cast<uint32_t*>(yq + row * d + c0) = pk;
+        else yq[row * d + c0] = (int8_t)pk;
+      }
     }
   }
   if (j == 0) {
@@ -176,6 +188,21 @@ __global__ __launch_bounds__(kThreads) void ln_amax_final_kernel(
 }
 
 constexpr int kAmaxBlocks = 2048;
+
+// The int8 image of LN(x) for an int8 consumer: the rows are normalised again (the same
+// ln_row arithmetic as the absmax pass, so the same y) and quantised at the pass's scale
+// sx = 127 / max(amax[p], 1e-5) -- exactly the quantisation tgemm_i8 applies in registers
+// to an fp32 operand, so the int8-operand GEMM is bit-identical to that path.
+template <int NPL, int VW>
+__global__ __launch_bounds__(kThreads) void ln_fwd_q8_kernel(
+    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int64_t rows, int d, float eps, int64_t rows_per_pass, const float* __restrict__ amax,
+    int8_t* __restrict__ yq) {
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
+  if (row >= rows) return;
+  const float sx = 127.0f / fmaxf(amax[(int)(row / rows_per_pass)], 1e-5f);
+  (void)ln_row<NPL, VW>(x, gamma, beta, row, d, eps, nullptr, nullptr, nullptr, yq, sx);
+}
 
 // The backward of a residual junction's "R + rscale * rowvalid * drop(y)" applied to this
 // LN's dx (the junction's output gradient): dy2 = rscale * rowvalid * keep * scale * dx,
@@ -431,6 +458,35 @@ void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* 
 #undef OB_LNFA4
   hipLaunchKernelGGL(ln_amax_final_kernel, dim3((unsigned)P), dim3(kThreads), 0, s,
                      (const uint32_t*)part, (int)nb, reinterpret_cast<uint32_t*>(amax));
+}
+
+void launch_layernorm_fwd_i8(const float* x, const float* gamma, const float* beta, int64_t rows,
+                             int64_t d, float eps, int P, float* amax, int8_t* yq, void* ws,
+                             hipStream_t s) {
+  // pass 1: per-pass max|LN(x)| (no y store); pass 2: LN(x) again, quantised
+  launch_layernorm_fwd_amax(x, gamma, beta, rows, d, eps, nullptr, nullptr, nullptr, P, amax, ws,
+                            s);
+  if (rows == 0) return;
+  const int npl = (int)ceil_div(d, kLanesPerRow);
+  const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
+  const int64_t rpp = rows / P;
+  const dim3 grid((unsigned)ceil_div(rows, kRowsPerBlock));
+  // the same column slots (hence the same summation order) as the absmax pass, whose y is
+  // nullptr; yq is 4-byte aligned (checked by the C ABI), so a 4-column slot is one dword
+  const bool vec = d % 4 == 0 && al16(x) && al16(gamma) && al16(beta);
+#define OB_LNQ(N)                                                                                \
+  hipLaunchKernelGGL((ln_fwd_q8_kernel<N, 1>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
+                     (int)d, eps, rpp, (const float*)amax, yq);
+#define OB_LNQ4(N)                                                                               \
+  hipLaunchKernelGGL((ln_fwd_q8_kernel<N, 4>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
+                     (int)d, eps, rpp, (const float*)amax, yq);
+  if (vec) {
+    OB_LN_NPL4(OB_LNQ4)
+  } else {
+    OB_LN_NPL(OB_LNQ)
+  }
+#undef OB_LNQ
+#undef OB_LNQ4
 }
 
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,

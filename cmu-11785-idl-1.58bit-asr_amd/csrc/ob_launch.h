@@ -201,6 +201,14 @@ bool launch_ternary_gemm_i8_epi(const float* A, int P, int64_t M, int64_t K,
                                 int alpha_raw, const float* amax, const float* bias, float* C,
                                 int mode, const float* R, float rscale, const int* lens, int64_t T,
                                 float* amax_out, hipStream_t s);
+// int8 operand Aq [P*M][K] (quantised by its producer at amax's scale); mode 0 plain / 2
+// residual (C fp32), mode 3: silu(y) quantised to int8 at its own per-pass absmax (C int8,
+// amax_out = that absmax; two launches)
+bool launch_ternary_gemm_i8q(const int8_t* Aq, int P, int64_t M, int64_t K,
+                             const uint32_t* codes, const uint32_t* codes1, const int* pass_bits,
+                             int64_t N, const float* alpha, int alpha_raw, const float* amax,
+                             const float* bias, void* C, int mode, const float* R, float rscale,
+                             const int* lens, int64_t T, float* amax_out, hipStream_t s);
 
 // layernorm.hip (LayerNorm over the last dim, d <= 512; deterministic dgamma/dbeta)
 bool layernorm_supported(int64_t d);
@@ -212,6 +220,11 @@ size_t layernorm_fwd_amax_workspace(int64_t P);
 void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,
                                int64_t rows, int64_t d, float eps, float* y, float* mean,
                                float* rstd, int P, float* amax, void* ws, hipStream_t s);
+// the int8 image of LN(x) at its per-pass absmax scale (absmax pass, then LN again + quantise;
+// ws as launch_layernorm_fwd_amax; yq 4-byte aligned)
+void launch_layernorm_fwd_i8(const float* x, const float* gamma, const float* beta, int64_t rows,
+                             int64_t d, float eps, int P, float* amax, int8_t* yq, void* ws,
+                             hipStream_t s);
 // Optional second output of the backward: dy2 = rscale * rowvalid * drop(dx) (the residual
 // dropout backward of the module whose output this LN normalises; lens/T as TgemmEpi).
 struct LnGradScale {

@@ -162,7 +162,12 @@ __global__ __launch_bounds__(kThreads) void act_dequant_kernel(const float* __re
 //                next BitLinear, ff.lin2: conformer.py:36-45 at dropout 0);
 //   I8_RESIDUAL  C = R + rscale * (row valid ? y : 0*y)  (ff.lin2 / mhsa.out_proj + x).
 // Stores go row-coalesced through a per-wave LDS staging tile, as in tgemm.hip.
-constexpr int kI8Plain = 0, kI8Swish = 1, kI8Residual = 2;
+//   I8_SWISH_AMAX  only the per-pass max|silu(y)| (no store): the first of the two
+//                launches that give ff.lin2 an int8 operand in HBM;
+//   I8_SWISH_Q     the second: C8 = clamp(rint(silu(y) * 127 / max(amax_out[p], 1e-5)))
+//                as int8 -- the same values and scale the in-register quantisation of
+//                an fp32 silu(y) operand would produce, so ff.lin2 is bit-identical.
+constexpr int kI8Plain = 0, kI8Swish = 1, kI8Residual = 2, kI8SwishAmax = 3, kI8SwishQ = 4;
 struct I8Epi {
   const float* R;
   float rscale;
@@ -184,19 +189,28 @@ __host__ __device__ inline size_t i8_stage_bytes(int nt) {
   return (size_t)4 * 16 * (16 * cw + 4) * sizeof(float);
 }
 
-template <int NT, int NCH, int EPI>
+// AI8: A is the int8 image of the activation ([M][K] bytes, quantised by its producer at
+// the pass's scale 127 / max(amax[p], 1e-5)); else fp32, quantised here in registers.
+// C is fp32 [M][N], or int8 for I8_SWISH_Q (C8).
+template <int NT, int NCH, int EPI, bool AI8>
 __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
-    const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
+    const void* __restrict__ Av, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
-    const float* __restrict__ amax, const float* __restrict__ bias, float* __restrict__ C,
+    const float* __restrict__ amax, const float* __restrict__ bias, void* __restrict__ Cv,
     const uint32_t* __restrict__ codes1, const int* __restrict__ pass_bits, I8Epi ep) {
   const int64_t rowbase = pass_bits ? (int64_t)blockIdx.y * M : 0;
+  const float* A = static_cast<const float*>(Av);
+  const int8_t* A8 = static_cast<const int8_t*>(Av);
+  float* C = static_cast<float*>(Cv);
+  int8_t* C8 = static_cast<int8_t*>(Cv);
   int p = 0;
   if (pass_bits) {
     p = blockIdx.y;
     if (pass_bits[p] == 1) codes = codes1;
     A += (int64_t)p * M * K;
+    A8 += (int64_t)p * M * K;
     C += (int64_t)p * M * N;
+    C8 += (int64_t)p * M * N;
   }
   (void)rowbase;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -226,6 +240,9 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
   const float gam = act_gamma(amax, p);
   const float sx = 127.0f / gam;
   const float osc = __fmul_rn(effective_alpha(alpha, alpha_raw), gam / 127.0f);
+  // I8_SWISH_Q: the output's int8 scale (amax_out holds the max of the I8_SWISH_AMAX launch)
+  const float sx_out =
+      EPI == kI8SwishQ ? 127.0f / fmaxf(__uint_as_float(ep.amax_out[p]), 1e-5f) : 0.0f;
   float bcol[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -238,6 +255,7 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
     const int64_t m0 = (int64_t)rt * kRows + wave * 16;
     const int64_t row = m0 + r < M ? m0 + r : M - 1;
     const float* arow = A + row * (int64_t)K;
+    const int8_t* arow8 = A8 + row * (int64_t)K;
     i32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = i32x4{0, 0, 0, 0};
@@ -250,24 +268,46 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = src[e];
     };
-    constexpr int kWin = NCH < 3 ? NCH : 3;
-    f32x4 buf[NCH][4];
+    if constexpr (AI8) {
+      // the chunk's 16 int8 of the row: one dwordx4 (all chunks of the row in flight)
+      i32x4 qa[NCH];
 #pragma unroll
-    for (int c = 0; c < kWin; ++c) load16(c, buf[c]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if (c + kWin < NCH) load16(c + kWin, buf[c + kWin]);
+      for (int c = 0; c < NCH; ++c) {
+        int k = 64 * c + 16 * g;
+        k = k < K ? k : K - 16;
+        qa[c] = *reinterpret_cast<const i32x4*>(arow8 + k);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      i32x4 bq[NT];
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        bq[t] = *reinterpret_cast<const i32x4*>(brow + t * 16 * stride + 64 * c);
-      i32x4 a;
+      for (int c = 0; c < NCH; ++c) {
+        i32x4 bq[NT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = (int)q4(buf[c][e], sx);
+        for (int t = 0; t < NT; ++t)
+          bq[t] = *reinterpret_cast<const i32x4*>(brow + t * 16 * stride + 64 * c);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[t], acc[t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(qa[c], bq[t], acc[t], 0, 0, 0);
+      }
+    } else {
+      constexpr int kWin = NCH < 3 ? NCH : 3;
+      f32x4 buf[NCH][4];
+#pragma unroll
+      for (int c = 0; c < kWin; ++c) load16(c, buf[c]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + kWin < NCH) load16(c + kWin, buf[c + kWin]);
+        __builtin_amdgcn_sched_barrier(0);
+        i32x4 bq[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          bq[t] = *reinterpret_cast<const i32x4*>(brow + t * 16 * stride + 64 * c);
+        i32x4 a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = (int)q4(buf[c][e], sx);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[t], acc[t], 0, 0, 0);
+      }
     }
 
     if constexpr (EPI == kI8Plain) {
@@ -304,12 +344,18 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
           const f32x4 y = *reinterpret_cast<const f32x4*>(stg + row * kLd + 4 * c4);
           if (orow < M && col < N && 4 * c4 < 16 * (NT - c0)) {
             f32x4 out;
-            if constexpr (EPI == kI8Swish) {
+            if constexpr (EPI == kI8Swish || EPI == kI8SwishAmax) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 out[e] = silu_ref(y[e]);
                 amx = fmaxf(amx, fabsf(out[e]));
               }
+              if constexpr (EPI == kI8SwishAmax) continue;  // max only
+            } else if constexpr (EPI == kI8SwishQ) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) out[e] = silu_ref(y[e]);
+              *reinterpret_cast<uint32_t*>(C8 + orow * N + col) = q4(out, sx_out);
+              continue;
             } else {
               bool valid = true;
               if (ep.lens) {
@@ -333,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
       }
     }
   }
-  if constexpr (EPI == kI8Swish) {
+  if constexpr (EPI == kI8Swish || EPI == kI8SwishAmax) {
     // the block's max|C| -> one atomicMax per block (order-independent: deterministic)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o));
@@ -368,9 +414,9 @@ int pick_nt_i8(int64_t N, int64_t K, bool epi = false) {
 }
 
 template <int NT>
-bool launch_i8_nt(const float* A, int P, int64_t M, int64_t K, const uint32_t* codes,
+bool launch_i8_nt(const void* A, bool ai8, int P, int64_t M, int64_t K, const uint32_t* codes,
                   const uint32_t* codes1, const int* pass_bits, int64_t N, const float* alpha,
-                  int alpha_raw, const float* amax, const float* bias, float* C, hipStream_t s,
+                  int alpha_raw, const float* amax, const float* bias, void* C, hipStream_t s,
                   int mode = kI8Plain, const I8Epi& ep = I8Epi{}) {
   const int n_ct = (int)ceil_div(N, 16 * NT);
   const int n_rt = (int)ceil_div(M, kRows);
@@ -379,15 +425,26 @@ bool launch_i8_nt(const float* A, int P, int64_t M, int64_t K, const uint32_t* c
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
   const int KW = (int)ceil_div(K, 16);
-#define OB_I8E(NCH, E)                                                                        \
-  hipLaunchKernelGGL((tgemm_i8_kernel<NT, NCH, E>), grid, dim3(kThreads),                     \
+#define OB_I8E(NCH, E, Q)                                                                     \
+  hipLaunchKernelGGL((tgemm_i8_kernel<NT, NCH, E, Q>), grid, dim3(kThreads),                  \
                      i8_stage_off(NT, NCH) + (E == kI8Plain ? 0 : i8_stage_bytes(NT)), s, A, M, \
                      (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, amax,     \
                      bias, C, codes1, pass_bits, ep);
-#define OB_I8(NCH)                                                   \
-  if (mode == kI8Swish) { OB_I8E(NCH, kI8Swish) }                    \
-  else if (mode == kI8Residual) { OB_I8E(NCH, kI8Residual) }         \
-  else { OB_I8E(NCH, kI8Plain) }                                     \
+  // int8 operands: the plain / residual consumers and the two swish producer launches;
+  // fp32 operands: plain / swish (+ absmax) / residual
+#define OB_I8(NCH)                                                         \
+  if (ai8) {                                                               \
+    if (mode == kI8Residual) { OB_I8E(NCH, kI8Residual, true) }            \
+    else if (mode == kI8SwishAmax) { OB_I8E(NCH, kI8SwishAmax, true) }     \
+    else if (mode == kI8SwishQ) { OB_I8E(NCH, kI8SwishQ, true) }           \
+    else if (mode == kI8Plain) { OB_I8E(NCH, kI8Plain, true) }             \
+    else return false;                                                     \
+  } else {                                                                 \
+    if (mode == kI8Swish) { OB_I8E(NCH, kI8Swish, false) }                 \
+    else if (mode == kI8Residual) { OB_I8E(NCH, kI8Residual, false) }      \
+    else if (mode == kI8Plain) { OB_I8E(NCH, kI8Plain, false) }            \
+    else return false;                                                     \
+  }                                                                        \
   return true;
   switch (ceil_div(K, 64)) {
     case 1: OB_I8(1)
@@ -403,6 +460,27 @@ bool launch_i8_nt(const float* A, int P, int64_t M, int64_t K, const uint32_t* c
   }
 #undef OB_I8
 #undef OB_I8E
+}
+
+bool launch_i8_any(const void* A, bool ai8, int P, int64_t M, int64_t K, const uint32_t* codes,
+                   const uint32_t* codes1, const int* pass_bits, int64_t N, const float* alpha,
+                   int alpha_raw, const float* amax, const float* bias, void* C, hipStream_t s,
+                   int mode, const I8Epi& ep) {
+#define OB_I8NT(V)                                                                              \
+  case V:                                                                                       \
+    return launch_i8_nt<V>(A, ai8, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, \
+                           bias, C, s, mode, ep);
+  switch (pick_nt_i8(N, K, mode != kI8Plain)) {
+    OB_I8NT(12)
+    OB_I8NT(9)
+    OB_I8NT(6)
+    OB_I8NT(4)
+    OB_I8NT(3)
+    OB_I8NT(2)
+    OB_I8NT(1)
+    default: return false;
+  }
+#undef OB_I8NT
 }
 
 }  // namespace
@@ -436,16 +514,8 @@ bool launch_ternary_gemm_i8(const float* A, int P, int64_t M, int64_t K, const u
                             const float* alpha, int alpha_raw, const float* amax,
                             const float* bias, float* C, hipStream_t s) {
   if (M == 0 || N == 0 || P == 0) return true;
-  switch (pick_nt_i8(N, K)) {
-    case 12: return launch_i8_nt<12>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    case 9: return launch_i8_nt<9>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    case 6: return launch_i8_nt<6>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    case 4: return launch_i8_nt<4>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    case 3: return launch_i8_nt<3>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    case 2: return launch_i8_nt<2>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    case 1: return launch_i8_nt<1>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, C, s);
-    default: return false;
-  }
+  return launch_i8_any(A, false, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax,
+                       bias, C, s, kI8Plain, I8Epi{});
 }
 
 bool launch_ternary_gemm_i8_epi(const float* A, int P, int64_t M, int64_t K,
@@ -457,21 +527,31 @@ bool launch_ternary_gemm_i8_epi(const float* A, int P, int64_t M, int64_t K,
   I8Epi ep{R, rscale, lens, (int)(T > 0 ? T : 1), reinterpret_cast<uint32_t*>(amax_out)};
   if (mode == kI8Swish) launch_zero_words(amax_out, P, s);
   if (M == 0 || N == 0 || P == 0) return true;
-#define OB_I8NT(V)                                                                             \
-  case V:                                                                                      \
-    return launch_i8_nt<V>(A, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax, bias, \
-                           C, s, mode, ep);
-  switch (pick_nt_i8(N, K, true)) {
-    OB_I8NT(12)
-    OB_I8NT(9)
-    OB_I8NT(6)
-    OB_I8NT(4)
-    OB_I8NT(3)
-    OB_I8NT(2)
-    OB_I8NT(1)
-    default: return false;
+  return launch_i8_any(A, false, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax,
+                       bias, C, s, mode, ep);
+}
+
+// int8 operand Aq (its producer's scale from amax). mode 0 plain / 2 residual: C fp32;
+// mode 3 (swish -> int8): two launches over the same tiles -- the first only reduces the
+// per-pass max|silu(y)| into amax_out, the second recomputes silu(y) and stores it as int8
+// at that scale (C int8 [P*M][N]). Recomputing the K-wide product is cheaper than a round
+// trip of the fp32 activation through HBM (4 bytes written + read per element).
+bool launch_ternary_gemm_i8q(const int8_t* Aq, int P, int64_t M, int64_t K,
+                             const uint32_t* codes, const uint32_t* codes1, const int* pass_bits,
+                             int64_t N, const float* alpha, int alpha_raw, const float* amax,
+                             const float* bias, void* C, int mode, const float* R, float rscale,
+                             const int* lens, int64_t T, float* amax_out, hipStream_t s) {
+  I8Epi ep{R, rscale, lens, (int)(T > 0 ? T : 1), reinterpret_cast<uint32_t*>(amax_out)};
+  if (mode == 3) launch_zero_words(amax_out, P, s);
+  if (M == 0 || N == 0 || P == 0) return true;
+  if (mode == 3) {
+    return launch_i8_any(Aq, true, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax,
+                         bias, nullptr, s, kI8SwishAmax, ep) &&
+           launch_i8_any(Aq, true, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax,
+                         bias, C, s, kI8SwishQ, ep);
   }
-#undef OB_I8NT
+  return launch_i8_any(Aq, true, P, M, K, codes, codes1, pass_bits, N, alpha, alpha_raw, amax,
+                       bias, C, s, mode == 2 ? kI8Residual : kI8Plain, ep);
 }
 
 }  // namespace ob

@@ -119,6 +119,8 @@ SIGNATURES = {
     "ob_layernorm_fwd_amax_workspace": (_sz, [_i64]),
     "ob_layernorm_fwd_amax": (_int, [_c_f, _c_f, _c_f, _i64, _i64, _f32, _c_f, _c_f, _c_f, _i64,
                                      _c_f, _c_f, _sz, _c_f]),
+    "ob_layernorm_fwd_i8": (_int, [_c_f, _c_f, _c_f, _i64, _i64, _f32, _i64, _c_f, _c_f, _c_f,
+                                   _sz, _c_f]),
     "ob_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
     "ob_layernorm_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
@@ -133,6 +135,9 @@ SIGNATURES = {
     "ob_bitlinear_fwd_i8": (
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _c_f, _i64, _c_f, _c_f]),
     "ob_bitlinear_fwd_i8_epi": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _c_f, _i64, _int, _c_f,
+               _f32, _c_f, _i64, _c_f, _c_f, _c_f]),
+    "ob_bitlinear_fwd_i8q": (
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _c_f, _i64, _int, _c_f,
                _f32, _c_f, _i64, _c_f, _c_f, _c_f]),
     "ob_bitlinear_bwd_dx_passes": (

@@ -34,8 +34,9 @@ from .conv import (conv2d_bias_relu, conv_module_fused, conv_module_supported, d
                    subsample_convs, subsample_supported)
 from .embedding import embedding
 from .fused import (ffn_residual, ffn_residual_i8, fused_supported, i8_fused_supported,
-                    linear_residual, linear_residual_i8, qkv_projections)
-from .layernorm import fused_layernorm_supported, layer_norm, layer_norm_amax, layer_norm_fork
+                    i8_linear, linear_residual, linear_residual_i8, qkv_projections)
+from .layernorm import (Int8Act, fused_layernorm_supported, layer_norm, layer_norm_amax,
+                        layer_norm_fork, layer_norm_i8)
 from .linear import linear
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
@@ -68,6 +69,10 @@ class LayerNorm(nn.Module):
             return layer_norm_amax(x, self.ln.weight, self.ln.bias, self.ln.eps)
         return layer_norm(x, self.ln.weight, self.ln.bias, self.ln.eps)
 
+    def forward_i8(self, x):
+        """Inference, int8 consumers: LN(x) as its int8 image + absmax (layernorm.Int8Act)."""
+        return layer_norm_i8(x, self.ln.weight, self.ln.bias, self.ln.eps)
+
     def fork(self, x):
         """(LN(x), x) with the residual branch's gradient added in the LN backward."""
         return layer_norm_fork(x, self.ln.weight, self.ln.bias, self.ln.eps)
@@ -98,7 +103,9 @@ class FeedForwardModule(nn.Module):
                                                p_drop=self.dropout.p if self.training else 0.0):
             # inference, int8 activations: LN (+absmax) -> lin1 i8 + swish (+absmax of its
             # output) -> lin2 i8 + 0.5 * residual, no separate absmax / elementwise passes
-            return ffn_residual_i8(self.ln(x), x, self.lin1, self.lin2, bitwidth)
+            h = (self.ln.forward_i8(x) if self.ln.emit_amax and fused_layernorm_supported(x, x.shape[-1])
+                 else self.ln(x))
+            return ffn_residual_i8(h, x, self.lin1, self.lin2, bitwidth)
         if mask is None and fused_supported(x, self.lin1, self.lin2, bitwidth=bitwidth):
             # same computation, elementwise ops in the GEMM epilogues (onebit_asr/fused.py)
             p = self.dropout.p if self.training else 0.0
@@ -181,7 +188,9 @@ class MHSA(nn.Module):
         """The same computation with the attention core in one HIP kernel per direction
         (onebit_asr/attention.py); used on a ROCm device for supported shapes."""
         bsz, tlen, width = x.shape
-        if fused_supported(h, self.q_proj, self.k_proj, self.v_proj, bitwidth=bitwidth):
+        if isinstance(h, Int8Act):  # inference, int8 activations: LN(x) read as int8
+            qp, kp, vp = (i8_linear(h, m, bitwidth) for m in (self.q_proj, self.k_proj, self.v_proj))
+        elif fused_supported(h, self.q_proj, self.k_proj, self.v_proj, bitwidth=bitwidth):
             # one autograd node: dX of k / v accumulated in the GEMM epilogue (no adds)
             qp, kp, vp = qkv_projections(h, self.q_proj, self.k_proj, self.v_proj, bitwidth)
         else:
@@ -225,6 +234,11 @@ class MHSA(nn.Module):
                                                                          bitwidth=bitwidth):
             h, xr = self.ln.fork(x)
             return self._fused(xr, h, mask, bitwidth, pos_emb)
+        if (fused_attention_supported(x, self.d_head) and self.ln.emit_amax
+                and fused_layernorm_supported(x, width)
+                and i8_fused_supported(x, self.q_proj, self.k_proj, self.v_proj,
+                                       bitwidth=bitwidth, p_drop=self.dropout.p if self.training else 0.0)):
+            return self._fused(x, self.ln.forward_i8(x), mask, bitwidth, pos_emb)
         h = self.ln(x)
         if fused_attention_supported(h, self.d_head):
             return self._fused(x, h, mask, bitwidth, pos_emb)

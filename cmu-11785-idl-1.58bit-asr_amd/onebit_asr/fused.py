@@ -30,11 +30,12 @@ from typing import Dict, Optional
 import torch
 
 from . import _lib
-from .layernorm import GradScale, attach_grad_scale
+from .layernorm import GradScale, Int8Act, attach_grad_scale
 from .quant import PassBits, QuantizedLinear
 
 __all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
-           "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8", "qkv_projections"]
+           "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8", "qkv_projections",
+           "i8_linear"]
 
 _DW_GROUP = os.environ.get("OB_DW_GROUP", "1") != "0"  # 0: q/k/v dW finishes one by one
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
@@ -431,15 +432,45 @@ def _amax_of(t: torch.Tensor) -> torch.Tensor:
     return amax if amax is not None and amax.numel() == 1 else act_absmax(t.contiguous(), 1)
 
 
+def _i8q(aq: torch.Tensor, amax: torch.Tensor, lin: QuantizedLinear, bits: int, mode: int,
+         R: Optional[torch.Tensor] = None, rscale: float = 1.0):
+    """ob_bitlinear_fwd_i8q: lin on an int8 operand aq [rows, K] (quantised at amax).
+    mode 0 / 2: fp32 output (plain / + rscale * y onto R); mode 3: (int8 silu(y), its amax)."""
+    rows, k = aq.shape
+    n = lin.out_features
+    codes, _ = lin._codes(bits)
+    dt = torch.int8 if mode == 3 else torch.float32
+    y = torch.empty((rows, n), dtype=dt, device=aq.device)
+    amax_out = torch.empty((1,), dtype=torch.float32, device=aq.device) if mode == 3 else None
+    lib = _lib.load()
+    _lib.check(lib.ob_bitlinear_fwd_i8q(
+        aq.data_ptr(), 1, rows, k, codes.data_ptr(), None, None, lin.alpha.data_ptr(), 1,
+        amax.data_ptr(), _lib.ptr(lin.bias), n, mode, _lib.ptr(R), float(rscale), None, 0,
+        _lib.ptr(amax_out), y.data_ptr(), _lib.stream_of(aq)), "ob_bitlinear_fwd_i8q")
+    return y, amax_out
+
+
+def i8_linear(h: Int8Act, lin: QuantizedLinear, bitwidth) -> torch.Tensor:
+    """lin(h) (fp32 out) for an activation held as its int8 image (q/k/v on LN(x))."""
+    y, _ = _i8q(h.q, h.amax, lin, int(bitwidth), 0)
+    return y.view(*h.shape[:-1], lin.out_features)
+
+
 @torch.no_grad()
-def ffn_residual_i8(h: torch.Tensor, x: torch.Tensor, lin1: QuantizedLinear,
+def ffn_residual_i8(h, x: torch.Tensor, lin1: QuantizedLinear,
                     lin2: QuantizedLinear, bitwidth) -> torch.Tensor:
     """x + 0.5 * lin2(swish(lin1(h))) (conformer.py:36-45, eval) with int8 activations; h =
-    LN(x), ideally carrying its absmax (LayerNorm.emit_amax)."""
+    LN(x) as an Int8Act (layer_norm_i8: every activation is int8 in HBM -- lin1 writes the
+    int8 image of swish(lin1(h)) at its own absmax, lin2 reads it), or as fp32, ideally
+    carrying its absmax (LayerNorm.emit_amax; the operands are quantised in registers)."""
     bits = int(bitwidth)
+    x2 = _flat(x, lin2.out_features).contiguous()
+    if isinstance(h, Int8Act):
+        a, amax_a = _i8q(h.q, h.amax, lin1, bits, 3)
+        out, _ = _i8q(a, amax_a, lin2, bits, 2, R=x2, rscale=0.5)
+        return out.view(x.shape)
     amax_h = _amax_of(h)
     h2 = _flat(h, lin1.in_features).contiguous()
-    x2 = _flat(x, lin2.out_features).contiguous()
     a, amax_a = _i8_epi(h2, amax_h, lin1, bits, 1)
     out, _ = _i8_epi(a, amax_a, lin2, bits, 2, R=x2, rscale=0.5)
     return out.view(x.shape)

@@ -8,14 +8,15 @@ square root); the backward's dgamma / dbeta are summed in a fixed order.
 from __future__ import annotations
 
 import os
+from typing import NamedTuple
 
 import torch
 import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "fused_layernorm_supported",
-           "GradScale", "attach_grad_scale"]
+__all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "layer_norm_i8", "Int8Act",
+           "fused_layernorm_supported", "GradScale", "attach_grad_scale"]
 
 _GSCALE = os.environ.get("OB_LN_GSCALE", "1") != "0"  # 0: consumers run ob_drop_scale_bwd
 
@@ -140,6 +141,34 @@ def layer_norm_amax(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.T
     y = y.view(x.shape)
     y._ob_amax = amax
     return y
+
+
+class Int8Act(NamedTuple):
+    """An activation held as its int8 image in HBM: q [rows, d] int8 at the scale
+    127 / max(amax, 1e-5), amax device fp32 [1], shape = the fp32 tensor's shape."""
+    q: torch.Tensor
+    amax: torch.Tensor
+    shape: torch.Size
+
+
+@torch.no_grad()
+def layer_norm_i8(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> Int8Act:
+    """Inference: LN(x) as an int8 operand (ob_layernorm_fwd_i8): the absmax pass and a
+    second LN pass that writes the int8 image only -- the fp32 LN(x) never reaches HBM, and
+    the int8 BitLinears that consume it read d bytes per row instead of 4d."""
+    d = x.shape[-1]
+    x2 = x.contiguous().view(-1, d)
+    rows = x2.shape[0]
+    yq = torch.empty((rows, d), dtype=torch.int8, device=x.device)
+    amax = torch.empty((1,), dtype=torch.float32, device=x.device)
+    lib = _lib.load()
+    wsb = lib.ob_layernorm_fwd_amax_workspace(1)
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=x.device)
+    _lib.check(lib.ob_layernorm_fwd_i8(x2.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), rows, d,
+                                       float(eps), 1, amax.data_ptr(), yq.data_ptr(),
+                                       ws.data_ptr(), wsb, _lib.stream_of(x2)),
+               "ob_layernorm_fwd_i8")
+    return Int8Act(yq, amax, x.shape)
 
 
 class _LayerNormForkFn(torch.autograd.Function):

@@ -298,6 +298,23 @@ OB_API int ob_bitlinear_fwd_i8_epi(const float* X, int64_t P, int64_t M, int64_t
                                    const float* R, float rscale, const int32_t* lens, int64_t T,
                                    float* amax_out, float* Y, void* stream);
 
+/* ob_bitlinear_fwd_i8 on an int8 operand Xq [P*M][K] already quantised by its producer at
+ * the scale of amax (ob_layernorm_fwd_i8, or mode 3 below): the A tiles are read as int8
+ * (K bytes per row instead of 4K). N % 4 == 0; Xq / Y / R 16-byte aligned.
+ *   mode 0  Y fp32 = y                              (as ob_bitlinear_fwd_i8)
+ *   mode 2  Y fp32 = R + rscale * (valid ? y : 0*y)  (as ob_bitlinear_fwd_i8_epi mode 2)
+ *   mode 3  Y int8 = the int8 image of silu(y) at amax_out[p] = max|silu(y)| over pass p
+ *           (ff.lin1 -> ff.lin2, conformer.py:36-39 at dropout 0): the product is
+ *           computed twice (absmax, then quantise + store), so silu(y) never reaches HBM
+ *           in fp32; ff.lin2 on Y (mode 2) equals ob_bitlinear_fwd_i8_epi mode 1 -> mode 2
+ *           bit for bit. */
+OB_API int ob_bitlinear_fwd_i8q(const int8_t* Xq, int64_t P, int64_t M, int64_t K,
+                                const uint32_t* codes, const uint32_t* codes1,
+                                const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                const float* amax, const float* bias, int64_t N, int mode,
+                                const float* R, float rscale, const int32_t* lens, int64_t T,
+                                float* amax_out, void* Y, void* stream);
+
 OB_API int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
                                       const uint32_t* codes2_t, const uint32_t* codes1_t,
                                       const int32_t* pass_bits, const float* alpha,
@@ -428,6 +445,16 @@ OB_API int ob_layernorm_fwd_amax(const float* x, const float* gamma, const float
                                  int64_t rows, int64_t d, float eps, float* y, float* mean,
                                  float* rstd, int64_t P, float* amax, void* ws,
                                  size_t ws_bytes, void* stream);
+/* The int8 image of LN(x) for an int8 BitLinear consumer (north_star "int8 activation tiles"
+ * in HBM): amax[p] = max|LN(x)| over pass p, then yq = clamp(rint(LN(x) * 127 /
+ * max(amax[p], 1e-5)), -127, 127) int8 [rows][d] -- the quantisation ob_bitlinear_fwd_i8
+ * applies in registers to an fp32 operand, so ob_bitlinear_fwd_i8q on yq is bit-identical to
+ * ob_bitlinear_fwd_i8 on LN(x). Two row passes (LN is recomputed; no fp32 y in HBM);
+ * ws: ob_layernorm_fwd_amax_workspace(P) bytes; yq 4-byte aligned. Replaces the pair
+ * LayerNorm (conformer.py:19-24) -> activation quantisation of the consumer. */
+OB_API int ob_layernorm_fwd_i8(const float* x, const float* gamma, const float* beta,
+                               int64_t rows, int64_t d, float eps, int64_t P, float* amax,
+                               int8_t* yq, void* ws, size_t ws_bytes, void* stream);
 OB_API size_t ob_layernorm_bwd_workspace(int64_t rows, int64_t d);
 OB_API int ob_layernorm_bwd(const float* dy, const float* x, const float* gamma,
                             const float* mean, const float* rstd, int64_t rows, int64_t d,
