@@ -326,9 +326,14 @@ PEAK_I8_MFMA_TOPS = 5000.0  # 2x the dense bf16 rate (MI355X_MICROARCH.md, Matri
 
 
 def roofline_i8(batch, frames, dev, act_quant, reps=20):
-    """The inference step's BitLinear kernels at their B=256 shapes (one pass, 2-bit):
-    int8 path = absmax + i8-MFMA GEMM, fp32 path = bf16x3 GEMM; HIP events around a
-    graph of `reps` launches on the launch stream."""
+    """The inference step's BitLinear kernels at their B=256 shapes (one pass, 2-bit), as the
+    step launches them. int8 path: ff.lin1 on the int8 LN image writing the int8 swish image
+    at its own absmax (two launches: absmax, quantise + store), ff.lin2 reading that int8
+    image with the 0.5-scaled residual, q/k/v on the int8 LN image, out_proj on the fp32
+    attention context (absmax pass + in-register quantisation, residual), pos_proj; fp32
+    path: the bf16x3 GEMM. Algorithmic bytes: each operand read once, each output written
+    once (int8 = 1 byte, fp32 = 4). HIP events around a graph of `reps` launches on the
+    launch stream."""
     from onebit_asr import _lib
     from onebit_asr.conformer import subsampled_length
     from onebit_asr.quant import pack_codes
@@ -336,35 +341,54 @@ def roofline_i8(batch, frames, dev, act_quant, reps=20):
     lib = _lib.load()
     t = subsampled_length(frames)
     m = batch * t
-    shapes = [("lin1", m, 144, 576, 32), ("lin2", m, 576, 144, 32), ("qkvo", m, 144, 144, 64),
-              ("pos", t, 144, 144, 16)]
+    # (name, M, K, N, launches per step, kind)
+    if act_quant:
+        shapes = [("lin1", m, 144, 576, 32, "swish_q8"), ("lin2", m, 576, 144, 32, "resid_q8"),
+                  ("qkv", m, 144, 144, 48, "plain_q8"), ("out", m, 144, 144, 16, "resid_f32"),
+                  ("pos", t, 144, 144, 16, "plain_f32")]
+    else:
+        shapes = [("lin1", m, 144, 576, 32, "plain"), ("lin2", m, 576, 144, 32, "plain"),
+                  ("qkvo", m, 144, 144, 64, "plain"), ("pos", t, 144, 144, 16, "plain")]
     side = torch.cuda.Stream(dev)
     tot_t = tot_b = tot_f = 0.0
     n_launch = 0
     detail = []
-    for name, M, K, N, count in shapes:
+    for name, M, K, N, count, kind in shapes:
         g = torch.Generator(device=dev).manual_seed(M + K + N)
         X = torch.randn(M, K, device=dev, generator=g)
+        Xq = torch.randint(-127, 128, (M, K), device=dev, generator=g, dtype=torch.int32).to(torch.int8)
+        R = torch.randn(M, N, device=dev, generator=g)
         W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
         alpha = W.abs().mean()
         b = torch.zeros(N, device=dev)
         c2, _ = pack_codes(W, alpha, 2)
         Y = torch.empty(M, N, device=dev)
-        amax = torch.empty(1, device=dev)
-
-        def gemm(s):
-            if act_quant:
-                return lib.ob_bitlinear_fwd_i8(X.data_ptr(), 1, M, K, c2.data_ptr(), None, None,
-                                               alpha.data_ptr(), 1, amax.data_ptr(), b.data_ptr(),
-                                               N, Y.data_ptr(), s)
-            return lib.ob_bitlinear_fwd(X.data_ptr(), M, K, c2.data_ptr(), alpha.data_ptr(), 1,
-                                        b.data_ptr(), N, Y.data_ptr(), s)
-
+        amax = torch.full((1,), 4.0, device=dev)
+        amax_out = torch.empty(1, device=dev)
         wsb = lib.ob_act_absmax_workspace(1)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
-        def absmax(s):
-            return lib.ob_act_absmax(X.data_ptr(), 1, M * K, amax.data_ptr(), ws.data_ptr(), wsb, s)
+        def gemm(s):
+            if kind == "plain":
+                return lib.ob_bitlinear_fwd(X.data_ptr(), M, K, c2.data_ptr(), alpha.data_ptr(), 1,
+                                            b.data_ptr(), N, Y.data_ptr(), s)
+            if kind.endswith("q8"):
+                mode = {"swish_q8": 3, "resid_q8": 2, "plain_q8": 0}[kind]
+                return lib.ob_bitlinear_fwd_i8q(Xq.data_ptr(), 1, M, K, c2.data_ptr(), None, None,
+                                                alpha.data_ptr(), 1, amax.data_ptr(), b.data_ptr(),
+                                                N, mode, R.data_ptr(), 0.5, None, 0,
+                                                amax_out.data_ptr(), Y.data_ptr(), s)
+            st = lib.ob_act_absmax(X.data_ptr(), 1, M * K, amax.data_ptr(), ws.data_ptr(), wsb, s)
+            if st:
+                return st
+            if kind == "resid_f32":
+                return lib.ob_bitlinear_fwd_i8_epi(X.data_ptr(), 1, M, K, c2.data_ptr(), None, None,
+                                                   alpha.data_ptr(), 1, amax.data_ptr(),
+                                                   b.data_ptr(), N, 2, R.data_ptr(), 1.0, None, 0,
+                                                   None, Y.data_ptr(), s)
+            return lib.ob_bitlinear_fwd_i8(X.data_ptr(), 1, M, K, c2.data_ptr(), None, None,
+                                           alpha.data_ptr(), 1, amax.data_ptr(), b.data_ptr(), N,
+                                           Y.data_ptr(), s)
 
         def timed(fn):
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -383,28 +407,26 @@ def roofline_i8(batch, frames, dev, act_quant, reps=20):
             e1.synchronize()
             return e0.elapsed_time(e1) * 1e3 / reps
 
-        if act_quant:
-            _lib.check(absmax(side.cuda_stream), "absmax")
-            torch.cuda.synchronize()
         tg = timed(gemm)
-        ta = timed(absmax) if act_quant else 0.0
-        by = 4 * (M * K + M * N + N) + 4 * N * ((K + 15) // 16)
+        a_bytes = (1 if kind.endswith("q8") else 4) * M * K
+        out_bytes = {"swish_q8": 1, "resid_q8": 8, "resid_f32": 8}.get(kind, 4) * M * N
+        by = a_bytes + out_bytes + 4 * N + 4 * N * ((K + 15) // 16)
         fl = 2.0 * M * K * N
         tot_t += count * tg
         tot_b += count * by
         tot_f += count * fl
         n_launch += count
-        detail.append({"layer": name, "M": M, "K": K, "N": N, "launches_per_step": count,
-                       "gemm_us": round(tg, 2), "absmax_us": round(ta, 2),
-                       "gemm_GBs": round(by / (tg * 1e-6) / 1e9, 1),
-                       "gemm_TOPs": round(fl / (tg * 1e-6) / 1e12, 2)})
+        detail.append({"layer": name, "kind": kind, "M": M, "K": K, "N": N,
+                       "launches_per_step": count, "us": round(tg, 2),
+                       "alg_bytes": int(by), "GBs": round(by / (tg * 1e-6) / 1e9, 1),
+                       "TOPs": round(fl / (tg * 1e-6) / 1e12, 2)})
     avg = tot_t / n_launch
     gbs = (tot_b / n_launch) / (avg * 1e-6) / 1e9
     tops = (tot_f / n_launch) / (avg * 1e-6) / 1e12
     peak_c = PEAK_I8_MFMA_TOPS if act_quant else 2500.0
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(gbs / PEAK_HBM_GBS, 4),
-            "kernel": "tgemm_i8 (i8 MFMA)" if act_quant else "tgemm_bf16x3",
+            "kernel": "tgemm_i8 (i8 MFMA, int8 operands in HBM)" if act_quant else "tgemm_bf16x3",
             "avg_launch_us": round(avg, 3), "bytes_per_launch": int(tot_b / n_launch),
             "flops_per_launch": int(tot_f / n_launch), "achieved_TOPs": round(tops, 2),
             "mfma_peak_TOPs": peak_c, "mfma_frac": round(tops / peak_c, 4),

@@ -176,10 +176,14 @@ struct I8Epi {
   uint32_t* amax_out;
 };
 
-// torch's silu formula (x / (1 + exp(-x)), accurate expf and IEEE division): the fused
-// int8 FFN equals the unfused module path bit for bit (same values -> same absmax -> same
-// int8 quantization of ff.lin2's input).
-__device__ __forceinline__ float silu_ref(float z) { return z / (1.0f + expf(-z)); }
+// silu(z) = z / (1 + exp(-z)) through v_exp_f32 and a fast reciprocal (tgemm.hip's silu_f):
+// the accurate expf + IEEE division cost ~40 VALU ops per element, which made the swish
+// launches VALU-bound (ff.lin1's two int8-output launches 47 + 51 us at B = 256). Every
+// int8 swish epilogue uses this one formula, so the fp32-operand and int8-operand paths
+// agree bit for bit; against torch's silu it differs by a few ulp (the module path's
+// int8 image of the FFN hidden can differ by one step where a value sits on a rounding
+// boundary -- tests/test_i8_fused_gpu.py bounds that).
+__device__ __forceinline__ float silu_fast(float z) { return __fdividef(z, 1.0f + __expf(-z)); }
 
 __host__ __device__ inline size_t i8_stage_off(int nt, int nch) {
   return (((size_t)(16 * nt) * (size_t)(64 * nch + 16)) + 15) & ~(size_t)15;
@@ -347,13 +351,13 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
             if constexpr (EPI == kI8Swish || EPI == kI8SwishAmax) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                out[e] = silu_ref(y[e]);
+                out[e] = silu_fast(y[e]);
                 amx = fmaxf(amx, fabsf(out[e]));
               }
               if constexpr (EPI == kI8SwishAmax) continue;  // max only
             } else if constexpr (EPI == kI8SwishQ) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) out[e] = silu_ref(y[e]);
+              for (int e = 0; e < 4; ++e) out[e] = silu_fast(y[e]);
               *reinterpret_cast<uint32_t*>(C8 + orow * N + col) = q4(out, sx_out);
               continue;
             } else {

@@ -42,7 +42,15 @@ def test_ffn_i8_fused_equals_unfused(gpu, bits, monkeypatch):
         monkeypatch.setenv("OB_FUSED", "0")
         m.ln.emit_amax = False
         y0 = m(x, bits)
-    assert torch.equal(y1, y0), (y1 - y0).abs().max().item()
+        # the fused swish is silu through v_exp / a fast reciprocal (tgemm_i8.hip), torch's
+        # is expf + IEEE division: a few ulp apart, so an element of lin2's int8 operand can
+        # round one step differently; each such step moves an output by 0.5 * osc (lin2's
+        # output scale, a * g / 127) at most
+        hid = torch.nn.functional.silu(m.lin1(m.ln(x), bits))
+        osc = (m.lin2.alpha.abs() + 1e-8).item() * hid.abs().max().item() / 127.0
+    diff = (y1 - y0).abs()
+    assert diff.max().item() <= 4 * 0.5 * osc * (1 + 1e-3), (diff.max().item(), osc)
+    assert (diff > 0).float().mean().item() < 0.05
 
 
 def test_mhsa_i8_out_proj_residual(gpu, monkeypatch):
