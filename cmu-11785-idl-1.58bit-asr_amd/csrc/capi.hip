@@ -625,7 +625,7 @@ int ob_bitlinear_fwd_i8q(const int8_t* Xq, int64_t P, int64_t M, int64_t K,
                          int64_t N, int mode, const float* R, float rscale, const int32_t* lens,
                          int64_t T, float* amax_out, void* Y, void* stream) {
   if (M < 0 || K < 0 || N < 0 || P < 1 || P > 65535 || (mode != 0 && mode != 2 && mode != 3) ||
-      N % 4)
+      N % 4 || (mode == 3 && N % 16))
     return OB_ERR_SHAPE;
   if (P > 1 && !pass_bits) return OB_ERR_NULL;
   if (!alpha || !amax || (M * N > 0 && !Y) || (M * K > 0 && !Xq) || (N * K > 0 && !codes) ||

@@ -20,6 +20,7 @@
 
 #include <cstdlib>
 
+#include "ob_fp.h"
 #include "ob_launch.h"
 
 namespace ob {
@@ -32,7 +33,7 @@ constexpr size_t kMaxLds = 160 * 1024;
 // sigmoid through v_exp_f32 and v_rcp_f32 (a few ulp from torch's expf-based sigmoid, far
 // inside the fused-vs-unfused bars of tests/test_convmod_gpu.py; the accurate expf and IEEE
 // division were ~35 VALU ops per element, most of the depthwise tiles' arithmetic)
-__device__ __forceinline__ float sigm(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigm(float x) { return fast_sigmoid(x); }  // ob_fp.h
 // swish y * sigmoid(y)
 __device__ __forceinline__ float swish(float y) { return y * sigm(y); }
 

@@ -82,18 +82,13 @@ struct EpiArgs {
 
 // torch's silu and silu backward formulas: x / (1 + exp(-x)) and
 // (dy * s) * (1 + x * (1 - s)), s = 1 / (1 + exp(-x)), evaluated in that order.
-// TG_FASTMATH (default 1): exp through v_exp_f32 and a fast reciprocal / division -- a few
+// Fast math (ob_fp.h): exp through v_exp_f32 and the reciprocal through v_rcp_f32 -- a few
 // ulp from torch's expf-based formula, well inside the fused-vs-unfused bar of
-// tests/test_fused_gpu.py (1e-6 of max|ref|); 5 us per Conformer-S FFN launch.
-#ifndef TG_FASTMATH
-#define TG_FASTMATH 1
-#endif
-__device__ __forceinline__ float silu_f(float z) {
-  if (TG_FASTMATH) return __fdividef(z, 1.0f + __expf(-z));
-  return z / (1.0f + expf(-z));
-}
+// tests/test_fused_gpu.py (1e-6 of max|ref|). (HIP's __fdividef / __frcp_rn are full IEEE
+// divisions: ~10 VALU ops per element in these epilogues.)
+__device__ __forceinline__ float silu_f(float z) { return fast_silu(z); }
 __device__ __forceinline__ float silu_bwd_f(float dy, float z) {
-  const float s = TG_FASTMATH ? __frcp_rn(1.0f + __expf(-z)) : 1.0f / (1.0f + expf(-z));
+  const float s = fast_sigmoid(z);
   return nc_mul(nc_mul(dy, s), 1.0f + z * (1.0f - s));
 }
 

@@ -22,6 +22,7 @@
 // 16-byte fragment and issues one i8 MFMA per 16-column tile. A and B fragments take
 // element j of lane (r, g) from k = 64c + 16g + j; any k permutation the hardware applies
 // is the same for both operands, so the sum over k is unaffected.
+#include "ob_fp.h"
 #include "ob_launch.h"
 #include "ob_quant.h"
 
@@ -176,14 +177,14 @@ struct I8Epi {
   uint32_t* amax_out;
 };
 
-// silu(z) = z / (1 + exp(-z)) through v_exp_f32 and a fast reciprocal (tgemm.hip's silu_f):
-// the accurate expf + IEEE division cost ~40 VALU ops per element, which made the swish
-// launches VALU-bound (ff.lin1's two int8-output launches 47 + 51 us at B = 256). Every
-// int8 swish epilogue uses this one formula, so the fp32-operand and int8-operand paths
-// agree bit for bit; against torch's silu it differs by a few ulp (the module path's
-// int8 image of the FFN hidden can differ by one step where a value sits on a rounding
-// boundary -- tests/test_i8_fused_gpu.py bounds that).
-__device__ __forceinline__ float silu_fast(float z) { return __fdividef(z, 1.0f + __expf(-z)); }
+// silu(z) = z / (1 + exp(-z)) through v_exp_f32 and v_rcp_f32 (ob_fp.h fast_silu): the
+// accurate expf + IEEE division cost ~40 VALU ops per element, which made the swish launches
+// VALU-bound (ff.lin1's two int8-output launches 47 + 51 us at B = 256). Every int8 swish
+// epilogue uses this one formula, so the fp32-operand and int8-operand paths agree bit for
+// bit; against torch's silu it differs by a few ulp (the module path's int8 image of the FFN
+// hidden can differ by one step where a value sits on a rounding boundary --
+// tests/test_i8_fused_gpu.py bounds that).
+__device__ __forceinline__ float silu_fast(float z) { return fast_silu(z); }
 
 __host__ __device__ inline size_t i8_stage_off(int nt, int nch) {
   return (((size_t)(16 * nt) * (size_t)(64 * nch + 16)) + 15) & ~(size_t)15;
@@ -325,6 +326,48 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
           if (orow < M) C[orow * N + col] = epilogue(acc[t][reg], osc, bcol[t]);
         }
       }
+    } else if constexpr (EPI == kI8SwishAmax) {
+      // max only: straight from the accumulators (the element order does not matter)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = n0 + 16 * t + r;
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int64_t orow = m0 + 4 * g + reg;
+          const float v = fabsf(silu_fast(epilogue(acc[t][reg], osc, bcol[t])));
+          amx = (orow < M && col < N) ? fmaxf(amx, v) : amx;
+        }
+      }
+    } else if constexpr (EPI == kI8SwishQ) {
+      // int8 image through a per-wave byte tile [16 rows][16 NT + 16] in LDS: lane (r, g)
+      // quantises rows 4g .. 4g+3 of column 16t + r in registers; the tile's rows then
+      // leave as 16-byte segments (host-checked: N % 16 == 0, C8 16-B aligned)
+      constexpr int kBP = 16 * NT + 16;
+      uint8_t* bt = reinterpret_cast<uint8_t*>(smem + i8_stage_off(NT, NCH)) + wave * 16 * kBP;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          float q = rintf(silu_fast(epilogue(acc[t][reg], osc, bcol[t])) * sx_out);
+          q = fminf(fmaxf(q, -127.0f), 127.0f);
+          bt[(4 * g + reg) * kBP + 16 * t + r] = (uint8_t)(int)q;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int kSeg = 16 * NT;  // 16 rows x NT segments
+#pragma unroll
+      for (int it = 0; it < (kSeg + 63) / 64; ++it) {
+        const int idx = it * 64 + lane;
+        const int row = idx / NT, seg = idx - row * NT;
+        const int64_t orow = m0 + row;
+        const int col = n0 + 16 * seg;
+        if (idx < kSeg && orow < M && col < N)
+          *reinterpret_cast<u32x4*>(C8 + orow * N + col) =
+              *reinterpret_cast<const u32x4*>(bt + row * kBP + 16 * seg);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
     } else {
       // row-coalesced (host-checked: N % 4 == 0, C / R 16-B aligned)
       constexpr int kCW = NT < 4 ? NT : 4, kCC = 16 * kCW, kLd = kCC + 4, kQ = kCC / 4;
@@ -348,18 +391,12 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
           const f32x4 y = *reinterpret_cast<const f32x4*>(stg + row * kLd + 4 * c4);
           if (orow < M && col < N && 4 * c4 < 16 * (NT - c0)) {
             f32x4 out;
-            if constexpr (EPI == kI8Swish || EPI == kI8SwishAmax) {
+            if constexpr (EPI == kI8Swish) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 out[e] = silu_fast(y[e]);
                 amx = fmaxf(amx, fabsf(out[e]));
               }
-              if constexpr (EPI == kI8SwishAmax) continue;  // max only
-            } else if constexpr (EPI == kI8SwishQ) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) out[e] = silu_fast(y[e]);
-              *reinterpret_cast<uint32_t*>(C8 + orow * N + col) = q4(out, sx_out);
-              continue;
             } else {
               bool valid = true;
               if (ep.lens) {

@@ -304,6 +304,7 @@ OB_API int ob_bitlinear_fwd_i8_epi(const float* X, int64_t P, int64_t M, int64_t
  *   mode 0  Y fp32 = y                              (as ob_bitlinear_fwd_i8)
  *   mode 2  Y fp32 = R + rscale * (valid ? y : 0*y)  (as ob_bitlinear_fwd_i8_epi mode 2)
  *   mode 3  Y int8 = the int8 image of silu(y) at amax_out[p] = max|silu(y)| over pass p
+ *           (N % 16 == 0)
  *           (ff.lin1 -> ff.lin2, conformer.py:36-39 at dropout 0): the product is
  *           computed twice (absmax, then quantise + store), so silu(y) never reaches HBM
  *           in fp32; ff.lin2 on Y (mode 2) equals ob_bitlinear_fwd_i8_epi mode 1 -> mode 2
