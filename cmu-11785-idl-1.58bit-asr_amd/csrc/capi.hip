@@ -29,8 +29,9 @@ struct DwWorkspace {
   size_t part, part_db, apart, total;
 };
 
-DwWorkspace dw_layout(int64_t P, int64_t M, int64_t N, int64_t K) {
-  const DwPlan p = plan_dw_passes(P, M, N, K);
+// G > 1: one layer's share of a grouped launch (plan of the G layers' N_total = G * N)
+DwWorkspace dw_layout(int64_t P, int64_t M, int64_t N, int64_t K, int64_t G = 1) {
+  const DwPlan p = plan_dw_passes(P, M, G * N, K);
   DwWorkspace w;
   w.part = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N * (size_t)K);
   w.part_db = align_up(sizeof(float) * (size_t)p.chunks * (size_t)N);
@@ -161,7 +162,9 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N
                 const float* W, const float* alpha, int alpha_raw, int bits,
                 const int32_t* bits_dev, const int32_t* pass_bits, float* dW, float* dalpha,
                 float* db, void* ws, size_t ws_bytes, void* stream,
-                DwFinish* defer = nullptr) {
+                DwFinish* defer = nullptr, DwFinishEntry* table = nullptr, int slot = 0,
+                int64_t start = 0, int64_t* n_blocks = nullptr) {
+  if (n_blocks) *n_blocks = 0;
   if (M < 0 || N < 0 || K < 0 || P < 1 || P > kMaxPasses) return OB_ERR_SHAPE;
   if (!alpha || !dalpha || !ws || (N * K > 0 && (!W || !dW)) || (M > 0 && (!dY || (K > 0 && !X))))
     return OB_ERR_NULL;
@@ -191,9 +194,16 @@ int bwd_dw_impl(const float* dY, const float* X, int64_t P, int64_t M, int64_t N
   } else if (p.variant >= 9) {  // LDS path: alpha partials in the GEMM, no ticket
     const DwAlpha al{W, alpha, alpha_raw, bits, reinterpret_cast<const int*>(bits_dev),
                      reinterpret_cast<const int*>(pass_bits), apart};
-    launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s, &al);
     const DwFinish fin{part, chunks, N * K, part_db, db ? N : 0, W, alpha, alpha_raw, apart,
                        (int)(p.tiles_n * p.tiles_k * p.chunks), dW, db, dalpha};
+    if (table) {  // finish deferred to ob_dw_finish_table (entry written by the partial launch)
+      const DwFinishEntry ent{fin, start};
+      launch_dw_partial_group_defer(&dY, 1, X, P * M, N, K, p, &part, &part_db, &al, table, slot,
+                                    &ent, s);
+      if (n_blocks) *n_blocks = dw_finish_blocks(fin);
+      return launched();
+    }
+    launch_dw_partial(dY, X, P * M, N, K, p, part, part_db, ticket, s, &al);
     if (defer) {  // the caller launches it (grouped with other layers' finishes)
       *defer = fin;
       return launched();
@@ -678,8 +688,18 @@ size_t ob_bitlinear_bwd_dw_passes_group_workspace(int64_t G, int64_t P, int64_t 
                                                   int64_t K) {
   if (G < 1 || G > kMaxDwGroup) return 0;
   const size_t one = ob_bitlinear_bwd_dw_passes_workspace(P, M, N, K);
-  return one ? (size_t)G * align_up(one) : 0;
+  if (!one) return 0;
+  return (size_t)G * std::max(align_up(one), dw_layout(P, M, N, K, G).total);
 }
+
+namespace {
+int dw_group_impl(int64_t G, const float* const* dY, const float* X, int64_t P, int64_t M,
+                  int64_t N, int64_t K, const float* const* W, const float* const* alpha,
+                  int alpha_raw, const int32_t* pass_bits, float* const* dW,
+                  float* const* dalpha, float* const* db, void* ws, size_t ws_bytes,
+                  void* stream, DwFinishEntry* table, int slot, int64_t start,
+                  int64_t* n_blocks);
+}  // namespace
 
 int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, const float* X,
                                      int64_t P, int64_t M, int64_t N, int64_t K,
@@ -687,12 +707,79 @@ int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, const fl
                                      int alpha_raw, const int32_t* pass_bits, float* const* dW,
                                      float* const* dalpha, float* const* db, void* ws,
                                      size_t ws_bytes, void* stream) {
+  return dw_group_impl(G, dY, X, P, M, N, K, W, alpha, alpha_raw, pass_bits, dW, dalpha, db, ws,
+                       ws_bytes, stream, nullptr, 0, 0, nullptr);
+}
+
+int ob_bitlinear_bwd_dw_passes_group_defer(int64_t G, const float* const* dY, const float* X,
+                                           int64_t P, int64_t M, int64_t N, int64_t K,
+                                           const float* const* W, const float* const* alpha,
+                                           int alpha_raw, const int32_t* pass_bits,
+                                           float* const* dW, float* const* dalpha,
+                                           float* const* db, void* ws, size_t ws_bytes,
+                                           void* table, int64_t slot, int64_t start,
+                                           int64_t* n_blocks, void* stream) {
+  if (!table || !n_blocks || slot < 0 || start < 0) return OB_ERR_NULL;
+  return dw_group_impl(G, dY, X, P, M, N, K, W, alpha, alpha_raw, pass_bits, dW, dalpha, db, ws,
+                       ws_bytes, stream, static_cast<DwFinishEntry*>(table), (int)slot, start,
+                       n_blocks);
+}
+
+namespace {
+int dw_group_impl(int64_t G, const float* const* dY, const float* X, int64_t P, int64_t M,
+                  int64_t N, int64_t K, const float* const* W, const float* const* alpha,
+                  int alpha_raw, const int32_t* pass_bits, float* const* dW,
+                  float* const* dalpha, float* const* db, void* ws, size_t ws_bytes,
+                  void* stream, DwFinishEntry* table, int slot, int64_t start,
+                  int64_t* n_blocks) {
+  if (n_blocks) *n_blocks = 0;
   if (G < 1 || G > kMaxDwGroup) return OB_ERR_SHAPE;
   if (!dY || !W || !alpha || !dW || !dalpha || !db || !pass_bits || !ws) return OB_ERR_NULL;
   const size_t need = ob_bitlinear_bwd_dw_passes_group_workspace(G, P, M, N, K);
   if (need == 0) return OB_ERR_SHAPE;
   if (ws_bytes < need) return OB_ERR_WORKSPACE;
   const size_t one = need / (size_t)G;
+  const DwPlan pg = plan_dw_passes(P, M, G * N, K);
+  if (pg.variant >= 9 && M > 0 && N > 0 && K > 0 && P <= kMaxPasses) {
+    // one partial launch for the G layers (they share X), then one grouped finish
+    for (int64_t i = 0; i < G; ++i)
+      if (!dY[i] || !W[i] || !alpha[i] || !dW[i] || !dalpha[i]) return OB_ERR_NULL;
+    if (!X) return OB_ERR_NULL;
+    if (!aligned4(X) || !aligned4(pass_bits)) return OB_ERR_ALIGN;
+    const DwWorkspace Lg = dw_layout(P, M, N, K, G);
+    float* part[kMaxDwGroup];
+    float* part_db[kMaxDwGroup];
+    DwAlpha al[kMaxDwGroup];
+    DwFinish fin[kMaxDwGroup];
+    for (int64_t i = 0; i < G; ++i) {
+      if (!aligned4(dY[i]) || !aligned4(dW[i]) || !aligned4(db[i])) return OB_ERR_ALIGN;
+      char* base = static_cast<char*>(ws) + i * one;
+      part[i] = reinterpret_cast<float*>(base);
+      part_db[i] = db[i] ? reinterpret_cast<float*>(base + Lg.part) : nullptr;
+      float* apart = reinterpret_cast<float*>(base + Lg.part + Lg.part_db + 16);
+      al[i] = DwAlpha{W[i], alpha[i], alpha_raw, 2, nullptr,
+                      reinterpret_cast<const int*>(pass_bits), apart};
+      fin[i] = DwFinish{part[i], (int)pg.chunks, N * K, part_db[i], db[i] ? N : 0, W[i],
+                        alpha[i], alpha_raw, apart, (int)(pg.tiles_n / G * pg.tiles_k * pg.chunks),
+                        dW[i], db[i], dalpha[i]};
+    }
+    hipStream_t s = as_stream(stream);
+    if (table) {  // finishes deferred to ob_dw_finish_table
+      DwFinishEntry ent[kMaxDwGroup];
+      int64_t at = start;
+      for (int64_t i = 0; i < G; ++i) {
+        ent[i] = DwFinishEntry{fin[i], at};
+        at += dw_finish_blocks(fin[i]);
+      }
+      launch_dw_partial_group_defer(dY, (int)G, X, P * M, N, K, pg, part, part_db, al, table,
+                                    slot, ent, s);
+      *n_blocks = at - start;
+      return launched();
+    }
+    launch_dw_partial_group(dY, (int)G, X, P * M, N, K, pg, part, part_db, al, s);
+    launch_dw_finish_group(fin, (int)G, s);
+    return launched();
+  }
   DwFinish fin[kMaxDwGroup];
   bool deferred[kMaxDwGroup] = {false, false, false};
   for (int64_t i = 0; i < G; ++i) {
@@ -709,6 +796,29 @@ int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, const fl
   for (int64_t i = 0; i < G; ++i)
     if (deferred[i]) grp[nd++] = fin[i];
   if (nd) launch_dw_finish_group(grp, nd, as_stream(stream));
+  return launched();
+}
+}  // namespace
+
+int ob_bitlinear_bwd_dw_passes_defer(const float* dY, const float* X, int64_t P, int64_t M,
+                                     int64_t N, int64_t K, const float* W, const float* alpha,
+                                     int alpha_raw, const int32_t* pass_bits, float* dW,
+                                     float* dalpha, float* db, void* ws, size_t ws_bytes,
+                                     void* table, int64_t slot, int64_t start, int64_t* n_blocks,
+                                     void* stream) {
+  if (!pass_bits || !table || !n_blocks || slot < 0 || start < 0) return OB_ERR_NULL;
+  return bwd_dw_impl(dY, X, P, M, N, K, W, alpha, alpha_raw, 2, nullptr, pass_bits, dW, dalpha,
+                     db, ws, ws_bytes, stream, nullptr, static_cast<DwFinishEntry*>(table),
+                     (int)slot, start, n_blocks);
+}
+
+size_t ob_dw_finish_entry_bytes(void) { return sizeof(DwFinishEntry); }
+
+int ob_dw_finish_table(const void* table, int64_t n, int64_t total_blocks, void* stream) {
+  if (n < 0 || total_blocks < 0 || total_blocks > 0x7fffffff) return OB_ERR_SHAPE;
+  if (n > 0 && !table) return OB_ERR_NULL;
+  launch_dw_finish_table(static_cast<const DwFinishEntry*>(table), (int)n, total_blocks,
+                         as_stream(stream));
   return launched();
 }
 
@@ -983,6 +1093,28 @@ int ob_layernorm_bwd_ex(const float* dy, const float* x, const float* gamma, con
                         float* dgamma, float* dbeta, void* ws, size_t ws_bytes, float* dy2,
                         float rscale, float p_drop, const uint64_t* rng, int64_t rng_offset,
                         const int32_t* lens, int64_t T, void* stream) {
+  return ob_layernorm_bwd_defer(dy, x, gamma, mean, rstd, rows, d, dres, dx, dgamma, dbeta, ws,
+                                ws_bytes, dy2, rscale, p_drop, rng, rng_offset, lens, T, nullptr,
+                                0, stream);
+}
+
+size_t ob_ln_param_entry_bytes(void) { return sizeof(LnParamEntry); }
+
+int ob_ln_param_table(const void* table, int64_t n, int64_t dmax, void* stream) {
+  if (n < 0 || dmax < 0 || dmax > 512) return OB_ERR_SHAPE;
+  if (n > 0 && !table) return OB_ERR_NULL;
+  launch_ln_param_table(static_cast<const LnParamEntry*>(table), (int)n, (int)dmax,
+                        as_stream(stream));
+  return launched();
+}
+
+int ob_layernorm_bwd_defer(const float* dy, const float* x, const float* gamma, const float* mean,
+                           const float* rstd, int64_t rows, int64_t d, const float* dres,
+                           float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+                           float* dy2, float rscale, float p_drop, const uint64_t* rng,
+                           int64_t rng_offset, const int32_t* lens, int64_t T, void* table,
+                           int64_t slot, void* stream) {
+  if (table && slot < 0) return OB_ERR_SHAPE;
   if (rows < 0 || !layernorm_supported(d)) return OB_ERR_SHAPE;
   if (rows > 0 && (!dy || !x || !mean || !rstd || !dx)) return OB_ERR_NULL;
   if ((dgamma || dbeta) && !ws) return OB_ERR_NULL;
@@ -997,8 +1129,9 @@ int ob_layernorm_bwd_ex(const float* dy, const float* x, const float* gamma, con
   }
   LnGradScale gs{dy2, rscale, p_drop, rng, (uint64_t)rng_offset,
                  reinterpret_cast<const int*>(lens), (int)T};
+  const LnDefer df{static_cast<LnParamEntry*>(table), (int)slot};
   launch_layernorm_bwd(dy, x, gamma, mean, rstd, rows, d, dres, dx, dgamma, dbeta, ws,
-                       as_stream(stream), &gs);
+                       as_stream(stream), &gs, &df);
   return launched();
 }
 

@@ -453,21 +453,42 @@ __device__ __forceinline__ uint32_t cvt2(float a, float b, float& ra, float& rb)
 constexpr int kProdA[6] = {1, 2, 0, 1, 0, 0};  // plane of A per product: mm lh hl mh hm hh
 constexpr int kProdB[6] = {1, 0, 2, 0, 1, 0};
 
+// Layers sharing X (q / k / v of one LN output: dW_i = dY_i^T X) in one launch: the n-tiles
+// of layer i follow those of layer i-1, and a block reads dY / writes the partials of its
+// tile's layer. Every per-layer quantity (partial slab, db partials, alpha partial at
+// (chunk, layer-local tile)) has the single-layer layout, so the finish is unchanged.
+struct DwLdsGroup {
+  const float* dY[kMaxDwGroup];
+  float* part[kMaxDwGroup];
+  float* part_db[kMaxDwGroup];
+  DwAlpha al[kMaxDwGroup];
+  int layers;
+  // deferred finish: block 0 writes ent[0 .. layers) to table[slot ..] (table == nullptr: off)
+  DwFinishEntry* table;
+  int slot;
+  DwFinishEntry ent[kMaxDwGroup];
+};
+
 template <int WN, int WK>
 __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
-    const float* __restrict__ dY, const float* __restrict__ X, int64_t M, int N, int K,
-    int tiles_k, int64_t rows_per_chunk, int64_t cpp, float* __restrict__ part,
-    float* __restrict__ part_db, DwAlpha al) {
+    const float* __restrict__ X, int64_t M, int N, int K, int tiles_k, int64_t rows_per_chunk,
+    int64_t cpp, DwLdsGroup grp) {
   using C = DwLdsCfg<WN, WK>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave / WK, wk = wave - wn * WK;
   const int r = lane & 15, g = lane >> 4;
-  const int tiles = (N / C::BN) * tiles_k;
+  const int tiles_nl = N / C::BN;  // n-tiles of one layer
+  const int tiles = grp.layers * tiles_nl * tiles_k;
   const int L = xcd_logical((int)blockIdx.x, (int)gridDim.x);
   const int tile = L % tiles;
-  const int tn = tile / tiles_k, tk = tile - tn * tiles_k;
+  const int tng = tile / tiles_k, tk = tile - tng * tiles_k;
+  const int layer = tng / tiles_nl, tn = tng - layer * tiles_nl;
+  const float* __restrict__ dY = grp.dY[layer];
+  float* __restrict__ part = grp.part[layer];
+  float* __restrict__ part_db = grp.part_db[layer];
+  const DwAlpha& al = grp.al[layer];
   const int n0 = tn * C::BN, k0 = tk * C::BK;
   const int64_t chunk = L / tiles;
   const int64_t pass = chunk / cpp;
@@ -475,6 +496,8 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   const int64_t m_begin = pass * M + (chunk - pass * cpp) * rows_per_chunk;
   const int64_t m_end = m_begin + rows_per_chunk < m_lim ? m_begin + rows_per_chunk : m_lim;
   const int steps = (int)((m_end - m_begin + kStepRows - 1) / kStepRows);
+  if (grp.table && blockIdx.x == 0 && (int)threadIdx.x < grp.layers)
+    grp.table[grp.slot + threadIdx.x] = grp.ent[threadIdx.x];
   const bool do_db = (part_db != nullptr) && (tk == 0);
 
   // Loader units: 2 rows x 4 columns of one operand, row pair fastest across lanes
@@ -659,7 +682,8 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
     if (threadIdx.x == 0) {
       float t = 0.0f;
       for (int w = 0; w < WN * WK; ++w) t += wred[w];
-      al.apart[L] = t;  // logical block id: the finish kernel sums these in order
+      // (chunk, layer-local tile): the finish kernel sums these in order
+      al.apart[chunk * (tiles_nl * tiles_k) + tn * tiles_k + tk] = t;
     }
   }
   if (do_db) {
@@ -744,6 +768,24 @@ __device__ __forceinline__ void dw_finish_body(const DwFinish& a, int bid, int n
 }
 
 int64_t finish_blocks(const DwFinish& a) { return ceil_div(a.nk + a.n_db, kFinElems) + 1; }
+
+// Every deferred finish of a backward in one launch: block b runs the finish of the table
+// entry whose [start, next start) holds b (binary search over the starts; the entries are in
+// slot order with increasing starts).
+__global__ __launch_bounds__(kThreads) void dw_finish_table_kernel(
+    const DwFinishEntry* __restrict__ tab, int n, int64_t total) {
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last entry with start <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].start <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t st = tab[lo].start;
+  const int64_t end = lo + 1 < n ? tab[lo + 1].start : total;
+  const DwFinish f = tab[lo].f;
+  dw_finish_body(f, (int)(b - st), (int)(end - st));
+}
 
 __global__ __launch_bounds__(kThreads) void dw_finish_kernel(DwFinish a) {
   dw_finish_body(a, blockIdx.x, gridDim.x);
@@ -850,16 +892,7 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
                      dim3(kThreads), 0, s, dY, X, M, (int)N, (int)K, (int)p.tiles_n,            \
                      (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db, ticket)
   if (p.variant >= 9) {  // requires al (the finish is launch_dw_finish, not ste_reduce)
-    const unsigned nb = (unsigned)(p.tiles_n * p.tiles_k * p.chunks);
-#define OB_DWL(WN, WK)                                                                        \
-  hipLaunchKernelGGL((dw_lds_kernel<WN, WK>), dim3(nb), dim3(64 * WN * WK),                   \
-                     (size_t)(2 * DwLdsCfg<WN, WK>::kBuf), s, dY, X, M, (int)N, (int)K,       \
-                     (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, part, part_db, *al)
-    if (p.variant == 9) OB_DWL(3, 3);
-    else if (p.variant == 31) OB_DWL(3, 1);
-    else if (p.variant == 13) OB_DWL(1, 3);
-    else OB_DWL(1, 1);
-#undef OB_DWL
+    launch_dw_partial_group(&dY, 1, X, M * p.passes, N, K, p, &part, &part_db, al, s);
     return;
   }
   if (p.variant != 0) {
@@ -884,6 +917,44 @@ void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, in
 #undef OB_DW
 }
 
+void launch_dw_partial_group(const float* const* dY, int G, const float* X, int64_t M,
+                             int64_t N, int64_t K, const DwPlan& p, float* const* part,
+                             float* const* part_db, const DwAlpha* al, hipStream_t s) {
+  launch_dw_partial_group_defer(dY, G, X, M, N, K, p, part, part_db, al, nullptr, 0, nullptr, s);
+}
+
+void launch_dw_partial_group_defer(const float* const* dY, int G, const float* X, int64_t M,
+                                   int64_t N, int64_t K, const DwPlan& p, float* const* part,
+                                   float* const* part_db, const DwAlpha* al,
+                                   DwFinishEntry* table, int slot, const DwFinishEntry* ent,
+                                   hipStream_t s) {
+  if (p.rows_per_pass == 0 || N == 0) return;
+  M = p.rows_per_pass;
+  DwLdsGroup grp{};
+  grp.layers = G;
+  grp.table = table;
+  grp.slot = slot;
+  if (table)
+    for (int i = 0; i < G; ++i) grp.ent[i] = ent[i];
+  for (int i = 0; i < G; ++i) {
+    grp.dY[i] = dY[i];
+    grp.part[i] = part[i];
+    grp.part_db[i] = part_db[i];
+    grp.al[i] = al[i];
+  }
+  // p.tiles_n counts the n-tiles of all G layers (plan of N_total = G * N)
+  const unsigned nb = (unsigned)(p.tiles_n * p.tiles_k * p.chunks);
+#define OB_DWL(WN, WK)                                                                        \
+  hipLaunchKernelGGL((dw_lds_kernel<WN, WK>), dim3(nb), dim3(64 * WN * WK),                   \
+                     (size_t)(2 * DwLdsCfg<WN, WK>::kBuf), s, X, M, (int)N, (int)K,           \
+                     (int)p.tiles_k, p.rows_per_chunk, p.chunks_per_pass, grp)
+  if (p.variant == 9) OB_DWL(3, 3);
+  else if (p.variant == 31) OB_DWL(3, 1);
+  else if (p.variant == 13) OB_DWL(1, 3);
+  else OB_DWL(1, 1);
+#undef OB_DWL
+}
+
 void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* part_db,
                       int64_t n_db, const float* W, const float* alpha, int alpha_raw,
                       const float* apart, int n_apart, float* dW, float* db, float* dalpha,
@@ -892,6 +963,15 @@ void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* pa
                    dW, db, dalpha};
   const int64_t nb = finish_blocks(a);  // + the alpha block
   hipLaunchKernelGGL(dw_finish_kernel, dim3((unsigned)nb), dim3(kThreads), 0, s, a);
+}
+
+int64_t dw_finish_blocks(const DwFinish& a) { return finish_blocks(a); }
+
+void launch_dw_finish_table(const DwFinishEntry* table, int n, int64_t total_blocks,
+                            hipStream_t s) {
+  if (n <= 0 || total_blocks <= 0) return;
+  hipLaunchKernelGGL(dw_finish_table_kernel, dim3((unsigned)total_blocks), dim3(kThreads), 0, s,
+                     table, n, total_blocks);
 }
 
 void launch_dw_finish_group(const DwFinish* a, int n, hipStream_t s) {

@@ -223,9 +223,11 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows, int d,
     int rows_per_block, const float* __restrict__ dres, float* __restrict__ dx,
-    float* __restrict__ part_g, float* __restrict__ part_b, GScale gs) {
+    float* __restrict__ part_g, float* __restrict__ part_b, GScale gs, LnDefer df,
+    LnParamEntry ent) {
   __shared__ float red_g[kRowsPerBlock][kLanesPerRow * NPL * VW];
   __shared__ float red_b[kRowsPerBlock][kLanesPerRow * NPL * VW];
+  if (df.table && blockIdx.x == 0 && threadIdx.x == 0) df.table[df.slot] = ent;
   const int j = threadIdx.x & (kLanesPerRow - 1);
   const int sub = threadIdx.x / kLanesPerRow;
   const float inv_d = 1.0f / (float)d;
@@ -369,6 +371,49 @@ __global__ __launch_bounds__(kThreads) void ln_param_reduce_kernel(
   }
 }
 
+// Every deferred LN parameter reduction of a backward in one launch: grid (column groups of
+// 4, entries); the same fixed-order arithmetic as ln_param_reduce_kernel per entry.
+__global__ __launch_bounds__(kThreads) void ln_param_table_kernel(
+    const LnParamEntry* __restrict__ tab) {
+  const LnParamEntry e = tab[blockIdx.y];
+  if ((int)blockIdx.x * kRedCols >= e.d) return;
+  __shared__ float sg[kRedSlices][kRedCols], sb[kRedSlices][kRedCols];
+  const int cl = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int c = blockIdx.x * kRedCols + cl;
+  const int d = e.d, nblk = e.nblk;
+  float ag = 0.0f, ab = 0.0f;
+  if (c < d) {
+    float g4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = sl;
+    for (; b + 3 * kRedSlices < nblk; b += 4 * kRedSlices) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g4[u] += e.part_g[(int64_t)(b + u * kRedSlices) * d + c];
+        b4[u] += e.part_b[(int64_t)(b + u * kRedSlices) * d + c];
+      }
+    }
+    for (int u = 0; b < nblk; b += kRedSlices, ++u) {
+      g4[u & 3] += e.part_g[(int64_t)b * d + c];
+      b4[u & 3] += e.part_b[(int64_t)b * d + c];
+    }
+    ag = (g4[0] + g4[1]) + (g4[2] + g4[3]);
+    ab = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+  }
+  sg[sl][cl] = ag;
+  sb[sl][cl] = ab;
+  __syncthreads();
+  if (sl == 0 && c < d) {
+    float tg = 0.0f, tb = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kRedSlices; ++q) {
+      tg += sg[q][cl];
+      tb += sb[q][cl];
+    }
+    if (e.dgamma) e.dgamma[c] = tg;
+    if (e.dbeta) e.dbeta[c] = tb;
+  }
+}
+
 constexpr int kMaxBwdBlocks = 512;
 
 int bwd_blocks(int64_t rows, int* rows_per_block) {
@@ -489,10 +534,16 @@ void launch_layernorm_fwd_i8(const float* x, const float* gamma, const float* be
 #undef OB_LNQ4
 }
 
+void launch_ln_param_table(const LnParamEntry* table, int n, int dmax, hipStream_t s) {
+  if (n <= 0 || dmax <= 0) return;
+  hipLaunchKernelGGL(ln_param_table_kernel, dim3((unsigned)ceil_div(dmax, kRedCols), (unsigned)n),
+                     dim3(kThreads), 0, s, table);
+}
+
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                           const float* rstd, int64_t rows, int64_t d, const float* dres,
                           float* dx, float* dgamma, float* dbeta, void* ws, hipStream_t s,
-                          const LnGradScale* gsc) {
+                          const LnGradScale* gsc, const LnDefer* defer) {
   GScale gs{};
   if (gsc && gsc->dy2) {
     gs.dy2 = gsc->dy2;
@@ -509,6 +560,9 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
   const int nb = rows > 0 ? bwd_blocks(rows, &rpb) : 0;
   float* part_b = part_g + (size_t)nb * d;
   const bool params = dgamma || dbeta;
+  LnDefer df{nullptr, 0};
+  if (defer && defer->table && params && rows > 0) df = *defer;
+  const LnParamEntry ent{part_g, part_b, dgamma, dbeta, nb, (int)d};
   const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
   const bool vec = d % 4 == 0 && al16(dy) && al16(x) && al16(gamma) && al16(dres) && al16(dx) &&
                    al16(gs.dy2);
@@ -516,11 +570,11 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
 #define OB_LNB(N)                                                                              \
   hipLaunchKernelGGL((ln_bwd_kernel<N, 1>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
                      gamma, mean, rstd, rows, (int)d, rpb, dres, dx,                           \
-                     params ? part_g : nullptr, part_b, gs);
+                     params ? part_g : nullptr, part_b, gs, df, ent);
 #define OB_LNB4(N)                                                                             \
   hipLaunchKernelGGL((ln_bwd_kernel<N, 4>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy, x, \
                      gamma, mean, rstd, rows, (int)d, rpb, dres, dx,                           \
-                     params ? part_g : nullptr, part_b, gs);
+                     params ? part_g : nullptr, part_b, gs, df, ent);
     if (vec) {
       OB_LN_NPL4(OB_LNB4)
     } else {
@@ -529,7 +583,7 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
 #undef OB_LNB
 #undef OB_LNB4
   }
-  if (params)
+  if (params && !df.table)
     hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, kRedCols)), dim3(kThreads), 0,
                        s, part_g, part_b, nb, (int)d, dgamma, dbeta);
 }

@@ -147,6 +147,12 @@ struct DwAlpha {
 void launch_dw_partial(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        const DwPlan& p, float* part, float* part_db, uint32_t* ticket,
                        hipStream_t s, const DwAlpha* al = nullptr);
+// G layers sharing X (G <= kMaxDwGroup), LDS path only: p = plan_dw_passes(P, M, G * N, K)
+// (its tiles_n counts all G layers' n-tiles); per layer i the single-layer outputs
+// part[i] / part_db[i] / al[i].apart (alpha partial index chunk * tiles_of_one_layer + tile).
+void launch_dw_partial_group(const float* const* dY, int G, const float* X, int64_t M,
+                             int64_t N, int64_t K, const DwPlan& p, float* const* part,
+                             float* const* part_db, const DwAlpha* al, hipStream_t s);
 void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* part_db,
                       int64_t n_db, const float* W, const float* alpha, int alpha_raw,
                       const float* apart, int n_apart, float* dW, float* db, float* dalpha,
@@ -171,6 +177,23 @@ struct DwFinish {
 };
 constexpr int kMaxDwGroup = 3;
 void launch_dw_finish_group(const DwFinish* a, int n, hipStream_t s);
+
+// Deferred finishes (one launch for every layer of a backward): the dW partial launch writes
+// its layers' finish descriptors into a device table (block 0, from its arguments); the table
+// kernel later runs every entry's finish -- entry i owns finish blocks [start, next start).
+struct DwFinishEntry {
+  DwFinish f;
+  int64_t start;
+};
+int64_t dw_finish_blocks(const DwFinish& a);
+void launch_dw_finish_table(const DwFinishEntry* table, int n, int64_t total_blocks, hipStream_t s);
+// launch_dw_partial_group with the finish deferred: ent[i] (start filled in) is written to
+// table[slot + i] by the partial launch itself
+void launch_dw_partial_group_defer(const float* const* dY, int G, const float* X, int64_t M,
+                                   int64_t N, int64_t K, const DwPlan& p, float* const* part,
+                                   float* const* part_db, const DwAlpha* al,
+                                   DwFinishEntry* table, int slot, const DwFinishEntry* ent,
+                                   hipStream_t s);
 
 // dgemm.hip (dense exact-fp32 GEMM of the pointwise convs): false = shape not taken
 bool dense_gemm_supported(int64_t K, int64_t N);
@@ -236,9 +259,25 @@ struct LnGradScale {
   const int* lens;
   int T;
 };
+// Deferred LN parameter reduction: ln_bwd (block 0) writes its partials' descriptor into
+// table[slot]; launch_ln_param_table reduces every entry in one launch (dmax = max d).
+struct LnParamEntry {
+  const float* part_g;
+  const float* part_b;
+  float* dgamma;
+  float* dbeta;
+  int nblk;
+  int d;
+};
+struct LnDefer {
+  LnParamEntry* table;  // nullptr: reduce now
+  int slot;
+};
+void launch_ln_param_table(const LnParamEntry* table, int n, int dmax, hipStream_t s);
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                           const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx, float* dgamma,
-                          float* dbeta, void* ws, hipStream_t s, const LnGradScale* gsc = nullptr);
+                          float* dbeta, void* ws, hipStream_t s, const LnGradScale* gsc = nullptr,
+                          const LnDefer* defer = nullptr);
 
 // dwconv.hip (depthwise Conv1d of the conv module, odd kernel width, 'same' padding)
 bool dwconv_supported(int KT);

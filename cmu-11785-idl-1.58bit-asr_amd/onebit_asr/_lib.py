@@ -121,6 +121,19 @@ SIGNATURES = {
                                      _c_f, _c_f, _sz, _c_f]),
     "ob_layernorm_fwd_i8": (_int, [_c_f, _c_f, _c_f, _i64, _i64, _f32, _i64, _c_f, _c_f, _c_f,
                                    _sz, _c_f]),
+    "ob_layernorm_bwd_defer": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f,
+               _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f, _i64, _c_f]),
+    "ob_ln_param_entry_bytes": (_sz, []),
+    "ob_ln_param_table": (_int, [_c_f, _i64, _i64, _c_f]),
+    "ob_dw_finish_entry_bytes": (_sz, []),
+    "ob_bitlinear_bwd_dw_passes_defer": (
+        _int, [_c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f, _c_f,
+               _sz, _c_f, _i64, _i64, _c_f, _c_f]),
+    "ob_bitlinear_bwd_dw_passes_group_defer": (
+        _int, [_i64, _c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f,
+               _c_f, _sz, _c_f, _i64, _i64, _c_f, _c_f]),
+    "ob_dw_finish_table": (_int, [_c_f, _i64, _i64, _c_f]),
     "ob_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
     "ob_layernorm_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),

@@ -1,0 +1,164 @@
+"""Deferred gradient finishes: every BitLinear weight-gradient finish and every LayerNorm
+dgamma / dbeta reduction of a backward runs in ONE launch each, at the end of the backward.
+
+In the reference step (train.py:104-111: loss.backward(), clip_grad_norm_, AdamW) a parameter
+gradient is read only after the backward ends. On the HIP library each BitLinear dW is a
+split-M partial GEMM plus a small finish launch (chunk sum, STE mask, db, dalpha;
+csrc/dw.hip) and each LayerNorm backward is a row kernel plus a small parameter-reduce launch
+(csrc/layernorm.hip); at Conformer-S that is ~230 launches of 5-7 us each, mostly launch
+floor. Inside a ``scope()`` (the training step's forward + backward) the backward entries
+instead write their finish descriptors into device tables (``*_defer`` entry points: the
+producing launch writes its own entry) and one table launch per kind runs them all, from an
+autograd final callback on the backward's stream -- captured into the HIP graph like the
+rest of the backward.
+
+A gradient is deferred only when nothing can read it before the flush:
+* the parameter's ``.grad`` is None (AccumulateGrad then installs the returned tensor
+  without a kernel; an existing ``.grad`` -- gradient accumulation, the N > 1 flat buffer --
+  would be added to on the spot), and
+* the parameter was used by exactly one deferrable op in this scope's forward (several uses
+  -- the literal three-pass step -- make autograd add the contributions as they arrive).
+The workspaces holding the partials are kept referenced until the flush. ``OB_DEFER=0``
+finishes everything immediately (A/B, debugging).
+"""
+from __future__ import annotations
+
+import os
+from contextlib import contextmanager
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _lib
+
+__all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "keep", "active"]
+
+_ON = os.environ.get("OB_DEFER", "1") != "0"
+_CAP = 512  # table entries per kind
+
+
+class _State:
+    def __init__(self):
+        self.active = False
+        self.uses: Dict[int, int] = {}
+        self.tables: Dict[int, tuple] = {}  # device index -> (dw table, ln table)
+        self.reset()
+
+    def reset(self):
+        self.dw_n = 0
+        self.dw_blocks = 0
+        self.ln_n = 0
+        self.ln_dmax = 0
+        self.refs: List[torch.Tensor] = []
+        self.stream: Optional[int] = None
+        self.dev: Optional[int] = None
+        self.queued = False
+
+
+_S = _State()
+
+
+def active() -> bool:
+    return _ON and _S.active
+
+
+@contextmanager
+def scope():
+    """Forward + backward of one training step: deferrable gradients are finished by one
+    launch per kind at the end of the backward."""
+    prev = _S.active
+    _S.active = True
+    _S.uses = {}
+    try:
+        yield
+    finally:
+        _flush()  # (a no-op when the backward's final callback already ran)
+        _S.active = prev
+        _S.uses = {}
+
+
+def note(*params) -> None:
+    """A deferrable op's forward uses these parameters (counted per scope)."""
+    if not _S.active:
+        return
+    for p in params:
+        if p is not None:
+            _S.uses[id(p)] = _S.uses.get(id(p), 0) + 1
+
+
+def can_defer(*params) -> bool:
+    if not (_ON and _S.active):
+        return False
+    for p in params:
+        if p is None:
+            continue
+        if not p.is_cuda or p.grad is not None or _S.uses.get(id(p), 0) != 1:
+            return False
+    return True
+
+
+def _tables(dev: torch.device):
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    t = _S.tables.get(idx)
+    if t is None:
+        lib = _lib.load()
+        dw = torch.zeros((_CAP * lib.ob_dw_finish_entry_bytes(),), dtype=torch.uint8, device=dev)
+        ln = torch.zeros((_CAP * lib.ob_ln_param_entry_bytes(),), dtype=torch.uint8, device=dev)
+        t = (dw, ln)
+        _S.tables[idx] = t
+    return idx, t
+
+
+def _begin(dev: torch.device, stream: int) -> None:
+    if _S.stream is None:
+        _S.stream = stream
+        _S.dev = dev.index if dev.index is not None else torch.cuda.current_device()
+    if not _S.queued:
+        torch.autograd.Variable._execution_engine.queue_callback(_flush)
+        _S.queued = True
+
+
+def dw_slot(dev: torch.device, stream: int, n: int = 1):
+    """(table pointer, first slot, start block) for n dW finish entries, or None when the
+    table is full (finish immediately)."""
+    if _S.dw_n + n > _CAP:
+        return None
+    _begin(dev, stream)
+    _, (dw, _) = _tables(dev)
+    return dw.data_ptr(), _S.dw_n, _S.dw_blocks
+
+
+def dw_done(n: int, blocks: int) -> None:
+    if blocks > 0:
+        _S.dw_n += n
+        _S.dw_blocks += blocks
+
+
+def ln_slot(dev: torch.device, stream: int, d: int):
+    if _S.ln_n + 1 > _CAP:
+        return None
+    _begin(dev, stream)
+    _, (_, ln) = _tables(dev)
+    slot = _S.ln_n
+    _S.ln_n += 1
+    _S.ln_dmax = max(_S.ln_dmax, d)
+    return ln.data_ptr(), slot
+
+
+def keep(*tensors) -> None:
+    _S.refs.extend(t for t in tensors if t is not None)
+
+
+def _flush() -> None:
+    if _S.stream is None:
+        _S.reset()
+        return
+    lib = _lib.load()
+    dw, ln = _S.tables[_S.dev]
+    if _S.dw_n:
+        _lib.check(lib.ob_dw_finish_table(dw.data_ptr(), _S.dw_n, _S.dw_blocks, _S.stream),
+                   "ob_dw_finish_table")
+    if _S.ln_n:
+        _lib.check(lib.ob_ln_param_table(ln.data_ptr(), _S.ln_n, _S.ln_dmax, _S.stream),
+                   "ob_ln_param_table")
+    _S.reset()

@@ -29,7 +29,7 @@ from typing import Dict, Optional
 
 import torch
 
-from . import _lib
+from . import _lib, deferred
 from .layernorm import GradScale, Int8Act, attach_grad_scale
 from .quant import PassBits, QuantizedLinear
 
@@ -127,10 +127,26 @@ def _dx(lib, dy, P, m, n, codes, pb, alpha, k, stream):
     return dx
 
 
-def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream):
+def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream, bias=None):
+    """dW / dalpha / db of one BitLinear; the finish deferred to the end of the backward
+    (deferred.py) when nothing can read these gradients before it."""
     gw = torch.empty_like(weight)
     ga = torch.empty((), dtype=torch.float32, device=dy.device)
     gb = torch.empty((n,), dtype=torch.float32, device=dy.device) if has_bias else None
+    slot = (deferred.dw_slot(dy.device, stream)
+            if pb is not None and deferred.can_defer(weight, alpha, bias) else None)
+    if slot is not None:
+        wsb = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
+        ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dy.device)
+        nb = ctypes.c_int64(0)
+        _lib.check(lib.ob_bitlinear_bwd_dw_passes_defer(
+            dy.data_ptr(), x.data_ptr(), P, m, n, k, weight.data_ptr(), alpha.data_ptr(), 1,
+            pb.data_ptr(), gw.data_ptr(), ga.data_ptr(), _lib.ptr(gb), ws.data_ptr(), wsb,
+            slot[0], slot[1], slot[2], ctypes.addressof(nb), stream),
+            "ob_bitlinear_bwd_dw_passes_defer")
+        deferred.dw_done(1, nb.value)
+        deferred.keep(ws)
+        return gw, ga, gb
     if pb is not None:
         wsb = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dy.device)
@@ -172,6 +188,8 @@ class _FFNFn(torch.autograd.Function):
             out.data_ptr(), stream), "ob_bitlinear_fwd_residual")
         ctx.meta = meta
         ctx.has_bias = (b1 is not None, b2 is not None)
+        ctx.biases = (b1, b2)
+        deferred.note(w1, a1, b1, w2, a2, b2)
         ctx.save_for_backward(h, pre, act, w1, a1, w2, a2)
         return out
 
@@ -196,9 +214,11 @@ class _FFNFn(torch.autograd.Function):
             dy2.data_ptr(), P, m, n2, codes2[2].data_ptr(), codes2[3].data_ptr(), _lib.ptr(pb),
             a2.data_ptr(), 1, n1, pre.data_ptr(), p, _lib.ptr(rng), off1, dpre.data_ptr(), stream),
             "ob_bitlinear_bwd_dx_swish_drop")
-        gw2, ga2, gb2 = _dw(lib, dy2, act, P, m, n2, n1, w2, a2, ctx.has_bias[1], pb, bits, stream)
+        gw2, ga2, gb2 = _dw(lib, dy2, act, P, m, n2, n1, w2, a2, ctx.has_bias[1], pb, bits, stream,
+                            ctx.biases[1])
         gh = _dx(lib, dpre, P, m, n1, codes1, pb, a1, k, stream) if ctx.needs_input_grad[0] else None
-        gw1, ga1, gb1 = _dw(lib, dpre, h, P, m, n1, k, w1, a1, ctx.has_bias[0], pb, bits, stream)
+        gw1, ga1, gb1 = _dw(lib, dpre, h, P, m, n1, k, w1, a1, ctx.has_bias[0], pb, bits, stream,
+                            ctx.biases[0])
         return gh, gout, gw1, ga1, gb1, gw2, ga2, gb2, None
 
 
@@ -219,6 +239,8 @@ class _LinearResidualFn(torch.autograd.Function):
             _lib.ptr(lens), T, out.data_ptr(), _lib.stream_of(x)), "ob_bitlinear_fwd_residual")
         ctx.meta = meta
         ctx.has_bias = b is not None
+        ctx.bias = b
+        deferred.note(w, a, b)
         ctx.save_for_backward(x, w, a)
         return out
 
@@ -239,7 +261,7 @@ class _LinearResidualFn(torch.autograd.Function):
                                              off, _lib.ptr(lens), T, dy.data_ptr(), stream),
                        "ob_drop_scale_bwd")
         gx = _dx(lib, dy, P, m, n, codes, pb, a, k, stream) if ctx.needs_input_grad[0] else None
-        gw, ga, gb = _dw(lib, dy, x, P, m, n, k, w, a, ctx.has_bias, pb, bits, stream)
+        gw, ga, gb = _dw(lib, dy, x, P, m, n, k, w, a, ctx.has_bias, pb, bits, stream, ctx.bias)
         return gx, gout, gw, ga, gb, None
 
 
@@ -270,6 +292,8 @@ class _QKVFn(torch.autograd.Function):
             outs.append(y)
         ctx.meta = meta
         ctx.has_bias = (bq is not None, bk is not None, bv is not None)
+        ctx.biases = (bq, bk, bv)
+        deferred.note(wq, aq, bq, wk, ak, bk, wv, av, bv)
         ctx.save_for_backward(h, wq, aq, wk, ak, wv, av)
         return tuple(outs)
 
@@ -315,14 +339,26 @@ class _QKVFn(torch.autograd.Function):
                     [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs],
                     [_lib.ptr(o[2]) for o in outs])]
                 ad = [ctypes.addressof(x) for x in arrs]
-                _lib.check(lib.ob_bitlinear_bwd_dw_passes_group(
-                    3, ad[0], h.data_ptr(), P, m, n, k, ad[1], ad[2], 1, pb.data_ptr(), ad[3],
-                    ad[4], ad[5], ws.data_ptr(), wsb, stream), "ob_bitlinear_bwd_dw_passes_group")
+                slot = (deferred.dw_slot(h.device, stream, 3)
+                        if deferred.can_defer(wq, aq, wk, ak, wv, av, *ctx.biases) else None)
+                if slot is not None:
+                    nb = ctypes.c_int64(0)
+                    _lib.check(lib.ob_bitlinear_bwd_dw_passes_group_defer(
+                        3, ad[0], h.data_ptr(), P, m, n, k, ad[1], ad[2], 1, pb.data_ptr(), ad[3],
+                        ad[4], ad[5], ws.data_ptr(), wsb, slot[0], slot[1], slot[2],
+                        ctypes.addressof(nb), stream), "ob_bitlinear_bwd_dw_passes_group_defer")
+                    deferred.dw_done(3, nb.value)
+                    deferred.keep(ws)
+                else:
+                    _lib.check(lib.ob_bitlinear_bwd_dw_passes_group(
+                        3, ad[0], h.data_ptr(), P, m, n, k, ad[1], ad[2], 1, pb.data_ptr(), ad[3],
+                        ad[4], ad[5], ws.data_ptr(), wsb, stream), "ob_bitlinear_bwd_dw_passes_group")
                 for (_, w, _, _, _), o in zip(layers, outs):
                     grads[id(w)] = o
         for i, (g, w, a, c, hb) in zip(range(3), layers):
             if id(w) not in grads:
-                grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream)
+                b = ctx.biases[[id(t) for t in (wq, wk, wv)].index(id(w))]
+                grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream, b)
         out = [gh]
         for w in (wq, wk, wv):
             out.extend(grads.get(id(w), (None, None, None)))

@@ -41,6 +41,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from . import deferred
 from .optim import FusedAdamW
 from .quant import DeviceBits, QuantizedLinear
 from .train_step import WarmupCosine
@@ -93,8 +94,9 @@ class GraphedTrainStep:
         """One forward+backward (no update) to find the parameters the step differentiates."""
         for p in self.step_module.parameters():
             p.grad = None
-        loss, _ = self.step_module(self.batch, self.bits)
-        loss.backward()
+        with deferred.scope():
+            loss, _ = self.step_module(self.batch, self.bits)
+            loss.backward()
         self.params = [p for p in self.step_module.parameters() if p.grad is not None]
         for p in self.step_module.parameters():
             p.grad = None
@@ -134,8 +136,9 @@ class GraphedTrainStep:
         else:  # N == 1: autograd hands its gradient buffers over (no accumulate kernels)
             for p in self.params:
                 p.grad = None
-        loss, parts = self.step_module(self.batch, self.bits)
-        loss.backward()
+        with deferred.scope():  # one finish launch per kind at the end of the backward
+            loss, parts = self.step_module(self.batch, self.bits)
+            loss.backward()
         return loss.detach(), parts
 
     def _update(self):

@@ -13,7 +13,7 @@ from typing import NamedTuple
 import torch
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, deferred
 
 __all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "layer_norm_i8", "Int8Act",
            "fused_layernorm_supported", "GradScale", "attach_grad_scale"]
@@ -51,7 +51,26 @@ def attach_grad_scale(out: torch.Tensor, spec: GradScale) -> torch.Tensor:
     return out
 
 
-def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, wsb, spec, stream):
+def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, wsb, spec, stream,
+              params=()):
+    slot = None
+    if (dw is not None or db is not None) and deferred.can_defer(*params):
+        # dgamma / dbeta reduced at the end of the backward with every other LN's (deferred.py)
+        slot = deferred.ln_slot(x2.device, stream, d)
+    if slot is not None:
+        deferred.keep(ws)
+        dy2 = torch.empty_like(dx) if spec is not None else None
+        st = lib.ob_layernorm_bwd_defer(
+            g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight), mean.data_ptr(), rstd.data_ptr(),
+            rows, d, _lib.ptr(dres), dx.data_ptr(), _lib.ptr(dw), _lib.ptr(db), ws.data_ptr(), wsb,
+            _lib.ptr(dy2), spec.rscale if spec is not None else 1.0,
+            spec.p if spec is not None else 0.0, _lib.ptr(spec.rng) if spec is not None else None,
+            spec.off if spec is not None else 0,
+            _lib.ptr(spec.lens) if spec is not None else None, spec.T if spec is not None else 0,
+            slot[0], slot[1], stream)
+        if spec is not None:
+            spec.dx_ptr, spec.dy2 = dx.data_ptr(), dy2
+        return st
     if spec is None:
         if dres is None:
             return lib.ob_layernorm_bwd(g2.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
@@ -95,6 +114,8 @@ class _LayerNormFn(torch.autograd.Function):
         if need:
             ctx.save_for_backward(x2, weight, mean, rstd)
             ctx.has = (weight is not None, bias is not None)
+            ctx.params = (weight, bias)
+            deferred.note(weight, bias)
         return y.view(x.shape)
 
     @staticmethod
@@ -110,7 +131,7 @@ class _LayerNormFn(torch.autograd.Function):
         wsb = lib.ob_layernorm_bwd_workspace(rows, d)
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
         _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, None, dx, dw, db, ws, wsb,
-                             ctx.spec, _lib.stream_of(g2)), "ob_layernorm_bwd")
+                             ctx.spec, _lib.stream_of(g2), ctx.params), "ob_layernorm_bwd")
         return dx.view(gy.shape), dw, db, None, None
 
 
@@ -199,7 +220,7 @@ class _LayerNormForkFn(torch.autograd.Function):
         wsb = lib.ob_layernorm_bwd_workspace(rows, d)
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
         _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, r2, dx, dw, db, ws, wsb,
-                             ctx.spec, _lib.stream_of(g2)), "ob_layernorm_bwd_res")
+                             ctx.spec, _lib.stream_of(g2), ctx.params), "ob_layernorm_bwd_res")
         return dx.view(gy.shape), dw, db, None, None
 
 

@@ -24,6 +24,7 @@ There is no CPU path for bitwidth 1/2: the oracle under ``oracle/`` is the check
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Optional
 
@@ -32,7 +33,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, deferred
 from .linear import linear
 
 __all__ = ["QuantizedLinear", "BitLinear", "quantize_weight", "pack_codes", "set_quant_off", "DeviceBits",
@@ -275,6 +276,8 @@ class _BitLinearPassesFn(torch.autograd.Function):
         )
         ctx.P = P
         ctx.has_bias = bias is not None
+        ctx.bias = bias
+        deferred.note(weight, alpha, bias)
         ctx.save_for_backward(x2d, weight, alpha, pass_bits, codes2_t, codes1_t)
         return y
 
@@ -303,14 +306,26 @@ class _BitLinearPassesFn(torch.autograd.Function):
             gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
             ws_bytes = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
             ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
-            _lib.check(
-                lib.ob_bitlinear_bwd_dw_passes(gy.data_ptr(), x2d.data_ptr(), P, m, n, k,
-                                               weight.data_ptr(), alpha.data_ptr(), 1,
-                                               pass_bits.data_ptr(), gw.data_ptr(),
-                                               galpha.data_ptr(), _lib.ptr(gb), ws.data_ptr(),
-                                               ws_bytes, stream),
-                "ob_bitlinear_bwd_dw_passes",
-            )
+            slot = (deferred.dw_slot(gy.device, stream)
+                    if deferred.can_defer(weight, alpha, ctx.bias) else None)
+            if slot is not None:  # finish at the end of the backward (deferred.py)
+                nb = ctypes.c_int64(0)
+                _lib.check(lib.ob_bitlinear_bwd_dw_passes_defer(
+                    gy.data_ptr(), x2d.data_ptr(), P, m, n, k, weight.data_ptr(),
+                    alpha.data_ptr(), 1, pass_bits.data_ptr(), gw.data_ptr(), galpha.data_ptr(),
+                    _lib.ptr(gb), ws.data_ptr(), ws_bytes, slot[0], slot[1], slot[2],
+                    ctypes.addressof(nb), stream), "ob_bitlinear_bwd_dw_passes_defer")
+                deferred.dw_done(1, nb.value)
+                deferred.keep(ws)
+            else:
+                _lib.check(
+                    lib.ob_bitlinear_bwd_dw_passes(gy.data_ptr(), x2d.data_ptr(), P, m, n, k,
+                                                   weight.data_ptr(), alpha.data_ptr(), 1,
+                                                   pass_bits.data_ptr(), gw.data_ptr(),
+                                                   galpha.data_ptr(), _lib.ptr(gb), ws.data_ptr(),
+                                                   ws_bytes, stream),
+                    "ob_bitlinear_bwd_dw_passes",
+                )
         return gx, gw, galpha, gb, None, None, None, None, None, None
 
 

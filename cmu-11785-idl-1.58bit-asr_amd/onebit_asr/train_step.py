@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import deferred
 from .losses import att_ce_loss, ctc_loss_from_logits, kl_logits, make_att_targets
 from .seqloss import att_kl_losses, att_kl_supported
 
@@ -233,9 +234,10 @@ def train_step(step_module: nn.Module, optimizer: torch.optim.Optimizer,
                sp_mask: List[int], max_norm: float = 5.0):
     """train.py:114-120: zero_grad, backward, clip_grad_norm_(5.0), step, sched.step().
     Returns the (device) loss and loss parts; nothing here synchronises with the host."""
-    loss, parts = step_module(batch, sp_mask)
     optimizer.zero_grad(set_to_none=True)
-    loss.backward()
+    with deferred.scope():  # gradient finishes batched at the end of the backward
+        loss, parts = step_module(batch, sp_mask)
+        loss.backward()
     params = [p for p in step_module.parameters() if p.grad is not None]
     torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm)
     optimizer.step()

@@ -340,6 +340,32 @@ OB_API int ob_bitlinear_bwd_dw_passes_group(int64_t G, const float* const* dY, c
                                             float* const* db, void* ws, size_t ws_bytes,
                                             void* stream);
 
+/* Deferred weight-gradient finishes (reference train.py:104-111: the parameter gradients
+ * are read only by clip_grad_norm_ / AdamW after loss.backward() ends). The *_defer entries
+ * launch only the split-M partial GEMM; the partial launch itself writes the layer's finish
+ * descriptor (chunk sum + STE mask + db + dalpha, as ob_bitlinear_bwd_dw_passes) into slot
+ * `slot` of a caller-owned device table of ob_dw_finish_entry_bytes() entries, at finish
+ * block offset `start`, and returns the layer's finish block count in *n_blocks (0: the shape
+ * took a path that finished immediately -- no entry written). ob_dw_finish_table then runs
+ * every entry's finish in ONE launch (total_blocks = the sum of the counts, entries in slot
+ * order). Until it has run, dW / dalpha / db are undefined; the workspace must stay
+ * allocated. The group form writes G consecutive entries (G <= 3). */
+OB_API size_t ob_dw_finish_entry_bytes(void);
+OB_API int ob_bitlinear_bwd_dw_passes_defer(const float* dY, const float* X, int64_t P,
+                                            int64_t M, int64_t N, int64_t K, const float* W,
+                                            const float* alpha, int alpha_raw,
+                                            const int32_t* pass_bits, float* dW, float* dalpha,
+                                            float* db, void* ws, size_t ws_bytes, void* table,
+                                            int64_t slot, int64_t start, int64_t* n_blocks,
+                                            void* stream);
+OB_API int ob_bitlinear_bwd_dw_passes_group_defer(
+    int64_t G, const float* const* dY, const float* X, int64_t P, int64_t M, int64_t N,
+    int64_t K, const float* const* W, const float* const* alpha, int alpha_raw,
+    const int32_t* pass_bits, float* const* dW, float* const* dalpha, float* const* db,
+    void* ws, size_t ws_bytes, void* table, int64_t slot, int64_t start, int64_t* n_blocks,
+    void* stream);
+OB_API int ob_dw_finish_table(const void* table, int64_t n, int64_t total_blocks, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * Relative-position attention core of MHSA.forward (onebit_asr/conformer.py:115-127),
  * fused: ac = (q+u) k^T, bd = rel_shift((q+v) pos^T) (:97-103), S = (ac + bd) / sqrt(d),
@@ -480,6 +506,20 @@ OB_API int ob_layernorm_bwd_ex(const float* dy, const float* x, const float* gam
                                void* ws, size_t ws_bytes, float* dy2, float rscale,
                                float p_drop, const uint64_t* rng, int64_t rng_offset,
                                const int32_t* lens, int64_t T, void* stream);
+/* ob_layernorm_bwd_ex with the dgamma / dbeta reduction deferred (table != NULL): the
+ * backward launch writes its partials' descriptor into slot `slot` of a caller-owned device
+ * table of ob_ln_param_entry_bytes() entries; ob_ln_param_table reduces entries 0 .. n-1 in
+ * one launch (dmax = the largest d) with the same fixed-order arithmetic. ws stays allocated
+ * until then. dres / dy2 may be NULL. */
+OB_API int ob_layernorm_bwd_defer(const float* dy, const float* x, const float* gamma,
+                                  const float* mean, const float* rstd, int64_t rows, int64_t d,
+                                  const float* dres, float* dx, float* dgamma, float* dbeta,
+                                  void* ws, size_t ws_bytes, float* dy2, float rscale,
+                                  float p_drop, const uint64_t* rng, int64_t rng_offset,
+                                  const int32_t* lens, int64_t T, void* table, int64_t slot,
+                                  void* stream);
+OB_API size_t ob_ln_param_entry_bytes(void);
+OB_API int ob_ln_param_table(const void* table, int64_t n, int64_t dmax, void* stream);
 
 /*
  * Batched greedy CTC decode (inference path). Replaces onebit_asr/metrics.py:51-60

@@ -270,7 +270,9 @@ def test_qkv_projections_match_separate_layers(gpu, stacked):
     assert (dh0 - dh1).abs().max().item() <= 1e-6 * dh0.abs().max().item()
     for a, b in zip(g0, g1):
         assert (a - b).abs().max().item() <= 1e-6 * max(a.abs().max().item(), 1e-30), (a, b)
-    # stacked: the three dW finishes run as one grouped launch; the same bits as one by one
+    # stacked: the three dW GEMMs run as one grouped launch (144x144 tiles, one per layer)
+    # and one grouped finish: dW / db the same bits as one by one (same chunks, same per-element
+    # product order); dalpha sums the same terms in other per-block groupings (rounding only)
     from onebit_asr import fused
 
     prev, fused._DW_GROUP = fused._DW_GROUP, False
@@ -279,7 +281,10 @@ def test_qkv_projections_match_separate_layers(gpu, stacked):
     finally:
         fused._DW_GROUP = prev
     for a, b in zip(g1, g2):
-        assert torch.equal(a, b)
+        if a.dim() == 0:
+            assert abs(a.item() - b.item()) <= 1e-6 * abs(b.item()) + 1e-12, (a, b)
+        else:
+            assert torch.equal(a, b)
 
 
 def test_decoder_residual_dropout(gpu):

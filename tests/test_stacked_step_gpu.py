@@ -66,3 +66,41 @@ def test_stacked_graph_step_runs(gpu):
     losses = [gs.step(batch, mk)[0].item() for mk in ([1, 0], [0, 1], [1, 1], [0, 0])]
     assert gs.graph_a is not None
     assert all(torch.isfinite(torch.tensor(losses)))
+
+
+def test_deferred_finishes_equal_immediate(gpu, monkeypatch):
+    """Inside deferred.scope() every BitLinear dW finish and LayerNorm parameter reduction of
+    the stacked step runs as one table launch per kind at the end of the backward: every
+    gradient is bit-identical to finishing each layer on the spot (OB_DEFER=0), and the
+    tables were actually used (the launch count drops)."""
+    from onebit_asr import deferred
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CFG1, synthetic_batch
+    from onebit_asr.train_step import OneBitStep
+
+    batch = synthetic_batch([734, 349], [27, 12], seed=0, device=gpu)
+    res = {}
+    used = {}
+    for on in (False, True):
+        monkeypatch.setattr(deferred, "_ON", on)
+        torch.manual_seed(0)
+        m = ConformerASR(80, 5004, **CFG1).to(gpu)
+        step = OneBitStep(m, n_layers=2, stacked=True)
+        counts = []
+
+        def spy(orig=deferred._flush, counts=counts):
+            counts.append((deferred._S.dw_n, deferred._S.ln_n))
+            orig()
+
+        monkeypatch.setattr(deferred, "_flush", spy)
+        with deferred.scope():
+            loss, _ = step(batch, [1, 0])
+            loss.backward()
+        torch.cuda.synchronize()
+        used[on] = max((c for c in counts), default=(0, 0))
+        res[on] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    assert used[False] == (0, 0)
+    assert used[True][0] >= 2 * 9 and used[True][1] >= 2 * 5, used[True]
+    assert res[False].keys() == res[True].keys()
+    for k in res[False]:
+        assert torch.equal(res[False][k], res[True][k]), k
