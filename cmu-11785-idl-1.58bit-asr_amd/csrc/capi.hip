@@ -431,6 +431,14 @@ size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K) {
 
 int ob_dense_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K, float* dW,
                 float* db, void* ws, size_t ws_bytes, void* stream) {
+  return ob_dense_dw_defer(dY, X, M, N, K, dW, db, ws, ws_bytes, nullptr, 0, 0, nullptr, stream);
+}
+
+int ob_dense_dw_defer(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                      float* dW, float* db, void* ws, size_t ws_bytes, void* table, int64_t slot,
+                      int64_t start, int64_t* n_blocks, void* stream) {
+  if (n_blocks) *n_blocks = 0;
+  if (table && (!n_blocks || slot < 0 || start < 0)) return OB_ERR_NULL;
   const size_t need = ob_dense_dw_workspace(M, N, K);
   if (need == 0) return OB_ERR_SHAPE;
   if (!dW || !ws || (M > 0 && (!dY || !X))) return OB_ERR_NULL;
@@ -448,6 +456,15 @@ int ob_dense_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K
   float* part = reinterpret_cast<float*>(base);
   float* part_db = db ? reinterpret_cast<float*>(base + L.part) : nullptr;
   const DwAlpha al{nullptr, nullptr, 0, 2, nullptr, nullptr, nullptr};  // no alpha: dense
+  if (table) {  // finish deferred to ob_dw_finish_table
+    const DwFinish fin{part, (int)p.chunks, N * K, part_db, db ? N : 0, nullptr, nullptr, 0,
+                       nullptr, 0, dW, db, nullptr};
+    const DwFinishEntry ent{fin, start};
+    launch_dw_partial_group_defer(&dY, 1, X, M, N, K, p, &part, &part_db, &al,
+                                  static_cast<DwFinishEntry*>(table), (int)slot, &ent, s);
+    *n_blocks = dw_finish_blocks(fin);
+    return launched();
+  }
   launch_dw_partial(dY, X, M, N, K, p, part, part_db, nullptr, s, &al);
   launch_dw_finish(part, (int)p.chunks, N * K, part_db, db ? N : 0, nullptr, nullptr, 0, nullptr,
                    0, dW, db, nullptr, s);

@@ -134,6 +134,8 @@ SIGNATURES = {
         _int, [_i64, _c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f,
                _c_f, _sz, _c_f, _i64, _i64, _c_f, _c_f]),
     "ob_dw_finish_table": (_int, [_c_f, _i64, _i64, _c_f]),
+    "ob_dense_dw_defer": (_int, [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _sz, _c_f, _i64,
+                                 _i64, _c_f, _c_f]),
     "ob_layernorm_bwd_workspace": (_sz, [_i64, _i64]),
     "ob_layernorm_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, deferred
 from .layernorm import GradScale, attach_grad_scale
 from .linear import colsum
 
@@ -221,6 +221,9 @@ class _PointwiseFn(torch.autograd.Function):
                 y = torch.addmm(b, x2d, w.t()) if b is not None else x2d @ w.t()
         ctx.save_for_backward(x2d, w)
         ctx.has_b = b is not None
+        ctx.bias = b
+        if ctx.hip:
+            deferred.note(w, b)
         return y
 
     @staticmethod
@@ -243,8 +246,7 @@ class _PointwiseFn(torch.autograd.Function):
                       if ctx.has_b and ctx.needs_input_grad[2] else None)
                 wsb = lib.ob_dense_dw_workspace(m, n, k)
                 ws = torch.empty((wsb,), dtype=torch.uint8, device=g.device)
-                _lib.check(lib.ob_dense_dw(g.data_ptr(), x2d.data_ptr(), m, n, k, gw.data_ptr(),
-                                           _lib.ptr(gb), ws.data_ptr(), wsb, st), "ob_dense_dw")
+                deferred.dense_dw(g, x2d, m, n, k, gw, gb, ws, wsb, st, w, ctx.bias)
                 if not ctx.needs_input_grad[1]:
                     gw = None
             return gx, gw, gb

@@ -17,7 +17,8 @@ A gradient is deferred only when nothing can read it before the flush:
   without a kernel; an existing ``.grad`` -- gradient accumulation, the N > 1 flat buffer --
   would be added to on the spot), and
 * the parameter was used by exactly one deferrable op in this scope's forward (several uses
-  -- the literal three-pass step -- make autograd add the contributions as they arrive).
+  -- the literal three-pass step -- make autograd add the contributions as they arrive;
+  the model ties no weights, so every use of these parameters goes through a counted op).
 The workspaces holding the partials are kept referenced until the flush. ``OB_DEFER=0``
 finishes everything immediately (A/B, debugging).
 """
@@ -143,6 +144,26 @@ def ln_slot(dev: torch.device, stream: int, d: int):
     _S.ln_n += 1
     _S.ln_dmax = max(_S.ln_dmax, d)
     return ln.data_ptr(), slot
+
+
+def dense_dw(g2, x2d, m, n, k, gw, gb, ws, wsb, stream, weight, bias) -> None:
+    """ob_dense_dw (full-precision weight gradient on the dW kernels), its finish deferred
+    when the parameters qualify."""
+    import ctypes
+
+    lib = _lib.load()
+    slot = dw_slot(g2.device, stream) if can_defer(weight, bias) else None
+    if slot is not None:
+        nb = ctypes.c_int64(0)
+        _lib.check(lib.ob_dense_dw_defer(g2.data_ptr(), x2d.data_ptr(), m, n, k, gw.data_ptr(),
+                                         _lib.ptr(gb), ws.data_ptr(), wsb, slot[0], slot[1],
+                                         slot[2], ctypes.addressof(nb), stream),
+                   "ob_dense_dw_defer")
+        dw_done(1, nb.value)
+        keep(ws)
+        return
+    _lib.check(lib.ob_dense_dw(g2.data_ptr(), x2d.data_ptr(), m, n, k, gw.data_ptr(),
+                               _lib.ptr(gb), ws.data_ptr(), wsb, stream), "ob_dense_dw")
 
 
 def keep(*tensors) -> None:

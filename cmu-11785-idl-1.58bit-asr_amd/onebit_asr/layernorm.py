@@ -54,7 +54,7 @@ def attach_grad_scale(out: torch.Tensor, spec: GradScale) -> torch.Tensor:
 def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, wsb, spec, stream,
               params=()):
     slot = None
-    if (dw is not None or db is not None) and deferred.can_defer(*params):
+    if rows > 0 and (dw is not None or db is not None) and deferred.can_defer(*params):
         # dgamma / dbeta reduced at the end of the backward with every other LN's (deferred.py)
         slot = deferred.ln_slot(x2.device, stream, d)
     if slot is not None:

@@ -32,7 +32,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, deferred
 
 __all__ = ["linear", "colsum"]
 
@@ -96,6 +96,9 @@ class _LinearFn(torch.autograd.Function):
             y = yd.to(torch.float32)
         ctx.save_for_backward(x2d, weight)
         ctx.meta = (bias is not None, dtype, x.shape)
+        ctx.bias = bias
+        if dtype is None:
+            deferred.note(weight, bias)
         return y.view(*x.shape[:-1], weight.shape[0])
 
     @staticmethod
@@ -120,9 +123,8 @@ class _LinearFn(torch.autograd.Function):
                 if has_b and ctx.needs_input_grad[2]:
                     gb = torch.empty((n,), dtype=torch.float32, device=g2.device)
                 ws = torch.empty((wsb,), dtype=torch.uint8, device=g2.device)
-                _lib.check(_lib.load().ob_dense_dw(g2.data_ptr(), x2d.data_ptr(), m, n, k,
-                                                   gw.data_ptr(), _lib.ptr(gb), ws.data_ptr(),
-                                                   wsb, _lib.stream_of(g2)), "ob_dense_dw")
+                deferred.dense_dw(g2, x2d, m, n, k, gw, gb, ws, wsb, _lib.stream_of(g2), weight,
+                                  ctx.bias)
                 return gx, gw, gb, None
             if ctx.needs_input_grad[1]:
                 gw = g2.t() @ x2d

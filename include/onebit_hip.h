@@ -618,6 +618,11 @@ OB_API int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, i
 OB_API size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K);
 OB_API int ob_dense_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        float* dW, float* db, void* ws, size_t ws_bytes, void* stream);
+/* ob_dense_dw with the finish deferred to ob_dw_finish_table (same table and contract as
+ * ob_bitlinear_bwd_dw_passes_defer; dense weights carry no STE mask / alpha). */
+OB_API int ob_dense_dw_defer(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
+                             float* dW, float* db, void* ws, size_t ws_bytes, void* table,
+                             int64_t slot, int64_t start, int64_t* n_blocks, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Conv module core (ConvModule, conformer.py:139-167; full precision), channels-last.

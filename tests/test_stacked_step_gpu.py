@@ -78,13 +78,16 @@ def test_deferred_finishes_equal_immediate(gpu, monkeypatch):
     from onebit_asr.data import CFG1, synthetic_batch
     from onebit_asr.train_step import OneBitStep
 
-    batch = synthetic_batch([734, 349], [27, 12], seed=0, device=gpu)
+    # d_model 144 / d_ff 576 (Conformer-S widths: the dW shapes that take the LDS path),
+    # two blocks, short utterances
+    cfg = dict(CFG1, enc_d_model=144, enc_d_ff=576)
+    batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
     res = {}
     used = {}
     for on in (False, True):
         monkeypatch.setattr(deferred, "_ON", on)
         torch.manual_seed(0)
-        m = ConformerASR(80, 5004, **CFG1).to(gpu)
+        m = ConformerASR(80, 5004, **cfg).to(gpu)
         step = OneBitStep(m, n_layers=2, stacked=True)
         counts = []
 
