@@ -207,7 +207,11 @@ class _PointwiseFn(torch.autograd.Function):
     dX = dY W, and dW / db through the dW kernel family); others on rocBLAS fp32."""
 
     @staticmethod
-    def forward(ctx, x2d, w, b):
+    def forward(ctx, x2d, wp, b):
+        # wp: the Conv1d weight parameter itself ([out, in, 1]; a leaf, so its gradient may be
+        # finished at the end of the backward, deferred.py); w: its [out, in] view
+        w = wp.view(wp.shape[0], -1)
+        ctx.wshape = wp.shape
         ctx.hip = _dense_ok(x2d, w)
         if ctx.hip:
             m, k = x2d.shape
@@ -222,8 +226,9 @@ class _PointwiseFn(torch.autograd.Function):
         ctx.save_for_backward(x2d, w)
         ctx.has_b = b is not None
         ctx.bias = b
+        ctx.wparam = wp
         if ctx.hip:
-            deferred.note(w, b)
+            deferred.note(wp, b)
         return y
 
     @staticmethod
@@ -241,12 +246,12 @@ class _PointwiseFn(torch.autograd.Function):
                 _lib.check(lib.ob_dense_gemm(g.data_ptr(), m, n, w.data_ptr(), 1, None, k,
                                              gx.data_ptr(), st), "ob_dense_gemm")
             if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
-                gw = torch.empty_like(w)
+                gw = torch.empty(ctx.wshape, dtype=torch.float32, device=g.device)  # [out, in, 1]
                 gb = (torch.empty((n,), dtype=torch.float32, device=g.device)
                       if ctx.has_b and ctx.needs_input_grad[2] else None)
                 wsb = lib.ob_dense_dw_workspace(m, n, k)
                 ws = torch.empty((wsb,), dtype=torch.uint8, device=g.device)
-                deferred.dense_dw(g, x2d, m, n, k, gw, gb, ws, wsb, st, w, ctx.bias)
+                deferred.dense_dw(g, x2d, m, n, k, gw, gb, ws, wsb, st, ctx.wparam, ctx.bias)
                 if not ctx.needs_input_grad[1]:
                     gw = None
             return gx, gw, gb
@@ -254,7 +259,7 @@ class _PointwiseFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 gx = g @ w
             if ctx.needs_input_grad[1]:
-                gw = g.t() @ x2d
+                gw = (g.t() @ x2d).view(ctx.wshape)
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = colsum(g)
         return gx, gw, gb
@@ -373,8 +378,7 @@ def subsample_convs(x: torch.Tensor, conv0: nn.Conv2d, conv2: nn.Conv2d) -> torc
 
 def _pointwise(x: torch.Tensor, conv: nn.Conv1d) -> torch.Tensor:
     c_in = x.shape[-1]
-    y = _PointwiseFn.apply(x.reshape(-1, c_in), conv.weight.view(conv.out_channels, c_in),
-                           conv.bias)
+    y = _PointwiseFn.apply(x.reshape(-1, c_in), conv.weight, conv.bias)
     return y.view(*x.shape[:-1], conv.out_channels)
 
 

@@ -13,7 +13,8 @@ autograd final callback on the backward's stream -- captured into the HIP graph 
 rest of the backward.
 
 A gradient is deferred only when nothing can read it before the flush:
-* the parameter's ``.grad`` is None (AccumulateGrad then installs the returned tensor
+* the tensor is a leaf (a parameter, not a view or copy of one) whose ``.grad`` is None
+  (AccumulateGrad then installs the returned tensor
   without a kernel; an existing ``.grad`` -- gradient accumulation, the N > 1 flat buffer --
   would be added to on the spot), and
 * the parameter was used by exactly one deferrable op in this scope's forward (several uses
@@ -93,7 +94,10 @@ def can_defer(*params) -> bool:
     for p in params:
         if p is None:
             continue
-        if not p.is_cuda or p.grad is not None or _S.uses.get(id(p), 0) != 1:
+        # a leaf: a derived tensor (a permuted view of a weight, e.g. the subsampling output
+        # layer's) passes its gradient on through autograd ops that would read it at once
+        if (not p.is_leaf or not p.is_cuda or p.grad is not None
+                or _S.uses.get(id(p), 0) != 1):
             return False
     return True
 
