@@ -62,10 +62,12 @@ def parse():
     ap.add_argument("--roofline-only", action="store_true", help="skip the step timing")
     ap.add_argument("--progress", action="store_true", help="progress lines on stderr")
     ap.add_argument("--mode", default="train",
-                    choices=["train", "quant-off", "infer", "infer-fp32act"],
+                    choices=["train", "quant-off", "quant-off-lib", "infer", "infer-fp32act"],
                     help="train: configs[1]/[2] (default); quant-off: configs[3] (BitLinear -> "
-                         "bf16 nn.Linear); infer / infer-fp32act: configs[4] (B=256, 2-bit, "
-                         "int8 / fp32 activations, greedy CTC decode)")
+                         "bf16 weights on the same fused kernels, set_quant_off 'bf16w'); "
+                         "quant-off-lib: the same with bf16 library GEMMs (hipBLASLt); "
+                         "infer / infer-fp32act: configs[4] (B=256, 2-bit, int8 / fp32 "
+                         "activations, greedy CTC decode)")
     ap.add_argument("--conv-pw-ternary", action="store_true",
                     help="opt-in ternary conv-module pw1/pw2 (north_star; not reference math)")
     ap.add_argument("--conv-find", action="store_true",
@@ -558,11 +560,13 @@ def main():
     torch.manual_seed(1234)  # identical init on every rank (DDP / the graph path broadcast)
     model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S,
                          quantize_conv_pointwise=args.conv_pw_ternary).to(dev)
-    quant_off = args.mode == "quant-off"
-    if quant_off:  # configs[3]: every BitLinear -> bf16 F.linear (hipBLASLt), same step body
+    quant_off = args.mode.startswith("quant-off")
+    if quant_off:  # configs[3]: every BitLinear -> bf16 weights, same step body
         from onebit_asr.quant import set_quant_off
 
-        set_quant_off(model, torch.bfloat16)
+        # quant-off: the ternary path's fused kernels with B = bf16(W) (only the weight format
+        # differs); quant-off-lib: bf16 F.linear on hipBLASLt
+        set_quant_off(model, "bf16w" if args.mode == "quant-off" else torch.bfloat16)
     n_layers = CONFORMER_S["enc_layers"]
     step_mod = OneBitStep(model, n_layers=n_layers)
     batch = synthetic_batch([args.frames] * args.batch, [args.tokens] * args.batch,
@@ -628,6 +632,9 @@ def main():
     out = {
         "metric": ("mel-frames/sec (Conformer-S quant-off train step, BitLinear -> bf16 nn.Linear)"
                    if quant_off else "mel-frames/sec (Conformer-S 1.58-bit train step)"),
+        "quant_off": (None if not quant_off else
+                      "bf16 weights on the fused ternary-GEMM kernels (exact fp32 activations)"
+                      if args.mode == "quant-off" else "bf16 F.linear on hipBLASLt"),
         "value": round(value, 1),
         "unit": "mel-frames/s",
         "n_gpus": world,
@@ -637,7 +644,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16 linears (hipBLASLt), fp32 elsewhere" if quant_off else "fp32",
+        "dtype": ("bf16 weights x fp32 activations (fused kernels), fp32 elsewhere"
+                  if args.mode == "quant-off" else
+                  "bf16 linears (hipBLASLt), fp32 elsewhere" if quant_off else "fp32"),
         "data": "synthetic (N(0,1) 80-mel x 1000-frame padded batches, random-init weights)",
         "config": {"workload": ("conformer-s-quant-off-bf16-train-step" if quant_off
                                 else "conformer-s-1.58bit-train-step"), "global_batch": args.batch * world,

@@ -12,7 +12,10 @@ namespace ob {
 
 // quant.py:124 — QuantizedLinear passes |alpha| + 1e-8 into the quantizer.
 // 1e-8f is the fp32 rounding of the Python float 1e-8 that torch applies.
+// alpha_raw: 0 = alpha as given, 1 = |alpha| + 1e-8 (quant.py:124); >= 2 = the GEMM's B
+// operand is the fp32 weight itself rounded to bf16 (quant-off, tgemm.hip): no alpha scale.
 __device__ __forceinline__ float effective_alpha(const float* alpha, int alpha_raw) {
+  if (alpha_raw >= 2) return 1.0f;
   const float a = *alpha;
   return alpha_raw ? (fabsf(a) + 1e-8f) : a;
 }

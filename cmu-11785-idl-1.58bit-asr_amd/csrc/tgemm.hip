@@ -20,6 +20,12 @@
 // Fragment map of v_mfma_f32_16x16x32_bf16 (lane l, r = l&15, g = l>>4):
 //   A[i=r][kk=8g+j] (j<8), B[kk=8g+j][col=r], D[row=4g+reg][col=r].
 //
+// Quant-off ceiling (BASELINE configs[3], quant.py:121-122 with bf16 weights): alpha_raw 2 / 3
+// makes the "codes" argument the fp32 weight W [N][K] itself (3: read transposed, for dX);
+// the block then builds its LDS image from bf16(W) (round to nearest even) instead of
+// decoding codes, and the scale is 1 -- the same kernel, tiles and fused epilogues, only the
+// weight format differs.
+//
 // OB_GEMM=f32 in the environment selects an fp32-MFMA kernel (v_mfma_f32_16x16x4_f32,
 // exact fp32 fma chain) for A/B checks; it is also the path for shapes the bf16x3 kernel
 // does not take (K % 4 != 0, misaligned A, B image over 64 KB).
@@ -268,19 +274,51 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   constexpr bool kCross = NT <= 9;
   constexpr int kWin = NCH > 0 ? (NCH < kWmax ? NCH : kWmax) : 1;
   f32x4 buf[NCH > 0 ? NCH : 1][2];
-  if constexpr (NCH > 0) {
-    constexpr int kWpt = (16 * NT * 2 * NCH + kThreads - 1) / kThreads;
-    uint32_t wv[kWpt];
+  // quant-off: the image from bf16(W); W [N][K] (alpha_raw 2) or, for dX, W [K][N] read
+  // transposed (alpha_raw 3). Unit = 8 consecutive k of one image row (one 16-byte store).
+  auto weight_image = [&]() {
+    const float* Wf = reinterpret_cast<const float*>(codes);
+    const int upr = kpad >> 3;
+    for (int u = threadIdx.x; u < 16 * NT * upr; u += kThreads) {
+      const int nl = u / upr, k0 = 8 * (u - nl * upr);
+      const int n = n0 + nl;
+      bf16x8 v;
 #pragma unroll
-    for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThreads);
-    if constexpr (kCross) {
-      const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
-#pragma unroll
-      for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + j;
+        const float w = (n < N && k < K)
+                            ? (alpha_raw == 3 ? Wf[(int64_t)k * N + n] : Wf[(int64_t)n * K + k])
+                            : 0.0f;
+        v[j] = (__bf16)w;
+      }
+      *reinterpret_cast<bf16x8*>(bimg + nl * stride + k0) = v;
     }
-    __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (NCH > 0) {
+    if (alpha_raw >= 2) {
+      if constexpr (kCross) {
+        const float* a0 = arow_of(rg);
 #pragma unroll
-    for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThreads, wv[i]);
+        for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      weight_image();
+    } else {
+      constexpr int kWpt = (16 * NT * 2 * NCH + kThreads - 1) / kThreads;
+      uint32_t wv[kWpt];
+#pragma unroll
+      for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThreads);
+      if constexpr (kCross) {
+        const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
+#pragma unroll
+        for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThreads, wv[i]);
+    }
+  } else if (alpha_raw >= 2) {
+    weight_image();
   } else {
     for (int idx = threadIdx.x; idx < nwords; idx += kThreads) decode_store(idx, word_at(idx));
   }
@@ -521,6 +559,16 @@ __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
 #pragma unroll
     for (int t = 0; t < kF32NT; ++t) {
       const int64_t n = n0 + 16 * t + r;
+      if (alpha_raw >= 2) {  // quant-off: B = bf16(W)
+        const float* Wf = reinterpret_cast<const float*>(codes);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t k = kc + 4 * g + e;
+          const float w = (n < N && k < K) ? (alpha_raw == 3 ? Wf[k * N + n] : Wf[n * K + k]) : 0.0f;
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], (float)(__bf16)w, acc[t], 0, 0, 0);
+        }
+        continue;
+      }
       const uint32_t word = codes[(n < N ? n : N - 1) * KW + (kc >> 4)];
       const uint32_t byte = (n < N) ? (word >> (8 * g)) : 0u;
 #pragma unroll

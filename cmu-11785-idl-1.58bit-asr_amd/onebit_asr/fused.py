@@ -94,7 +94,7 @@ def fused_supported(x: torch.Tensor, *layers: QuantizedLinear, bitwidth=None) ->
         if m._packed is not None:
             m._check_packed_use(bitwidth)
     return x.is_cuda and x.dtype == torch.float32 and all(
-        m.act_quant is None and m.quant_off is None for m in layers)
+        m.act_quant is None and m.quant_off in (None, "bf16w") for m in layers)
 
 
 def _bits_args(bitwidth):
@@ -104,35 +104,60 @@ def _bits_args(bitwidth):
     return 1, None, int(bitwidth)
 
 
+class Codes(tuple):
+    """(codes2, codes1, codes2_t, codes1_t) of one layer, with the C ABI's alpha_raw for its
+    forward and dX GEMMs: 1 / 1 for ternary codes; 2 / 3 for the quant-off ceiling
+    (quant_off="bf16w": every slot is the fp32 weight itself, B = bf16(W), no alpha), whose
+    weight gradient is a plain dense dW (dense=True)."""
+    fwd_raw = 1
+    dx_raw = 1
+    dense = False
+
+
 def _codes(layer: QuantizedLinear, P: int, bits: Optional[int]):
     """(codes2, codes1, codes2_t, codes1_t); single-pass: both slots hold the layer's bits."""
+    if layer.quant_off == "bf16w":
+        c = Codes((layer.weight,) * 4)
+        c.fwd_raw, c.dx_raw, c.dense = 2, 3, True
+        return c
     if P == 1 and bits is not None and bits != 2:
         c, ct = layer._codes(bits)
-        return c, c, ct, ct
+        return Codes((c, c, ct, ct))
     c2, c2t = layer._codes(2)
     if P == 1:
-        return c2, c2, c2t, c2t
+        return Codes((c2, c2, c2t, c2t))
     c1, c1t = layer._codes(1)
-    return c2, c1, c2t, c1t
+    return Codes((c2, c1, c2t, c1t))
 
 
 def _dx(lib, dy, P, m, n, codes, pb, alpha, k, stream):
     dx = torch.empty((P * m, k), dtype=torch.float32, device=dy.device)
     _lib.check(lib.ob_bitlinear_bwd_dx_passes(dy.data_ptr(), P, m, n, codes[2].data_ptr(),
                                               codes[3].data_ptr(), pb.data_ptr(), alpha.data_ptr(),
-                                              1, k, dx.data_ptr(), stream)
+                                              codes.dx_raw, k, dx.data_ptr(), stream)
                if pb is not None else
                lib.ob_bitlinear_bwd_dx(dy.data_ptr(), m, n, codes[2].data_ptr(), alpha.data_ptr(),
-                                       1, k, dx.data_ptr(), stream), "ob_bitlinear_bwd_dx")
+                                       codes.dx_raw, k, dx.data_ptr(), stream), "ob_bitlinear_bwd_dx")
     return dx
 
 
-def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream, bias=None):
+def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream, bias=None,
+        dense=False):
     """dW / dalpha / db of one BitLinear; the finish deferred to the end of the backward
-    (deferred.py) when nothing can read these gradients before it."""
+    (deferred.py) when nothing can read these gradients before it. dense (quant-off): the
+    plain dW = dY^T X and db on the same kernels, no STE mask, no alpha gradient."""
     gw = torch.empty_like(weight)
-    ga = torch.empty((), dtype=torch.float32, device=dy.device)
     gb = torch.empty((n,), dtype=torch.float32, device=dy.device) if has_bias else None
+    if dense:
+        wsb = lib.ob_dense_dw_workspace(P * m, n, k)
+        if not wsb:  # shapes off the dW kernels: library fp32
+            from .linear import colsum
+
+            return dy.t() @ x, None, colsum(dy) if has_bias else None
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=dy.device)
+        deferred.dense_dw(dy, x, P * m, n, k, gw, gb, ws, wsb, stream, weight, bias)
+        return gw, None, gb
+    ga = torch.empty((), dtype=torch.float32, device=dy.device)
     slot = (deferred.dw_slot(dy.device, stream)
             if pb is not None and deferred.can_defer(weight, alpha, bias) else None)
     if slot is not None:
@@ -179,12 +204,13 @@ class _FFNFn(torch.autograd.Function):
         act = torch.empty((rows, n1), dtype=torch.float32, device=h.device)
         _lib.check(lib.ob_bitlinear_fwd_swish_drop(
             h.data_ptr(), P, m, k, codes1[0].data_ptr(), codes1[1].data_ptr(), _lib.ptr(pb),
-            a1.data_ptr(), 1, _lib.ptr(b1), n1, p, _lib.ptr(rng), off1, pre.data_ptr(),
+            a1.data_ptr(), codes1.fwd_raw, _lib.ptr(b1), n1, p, _lib.ptr(rng), off1, pre.data_ptr(),
             act.data_ptr(), stream), "ob_bitlinear_fwd_swish_drop")
         out = torch.empty((rows, n2), dtype=torch.float32, device=h.device)
         _lib.check(lib.ob_bitlinear_fwd_residual(
             act.data_ptr(), P, m, n1, codes2[0].data_ptr(), codes2[1].data_ptr(), _lib.ptr(pb),
-            a2.data_ptr(), 1, _lib.ptr(b2), n2, x.data_ptr(), 0.5, p, _lib.ptr(rng), off2, None, 0,
+            a2.data_ptr(), codes2.fwd_raw, _lib.ptr(b2), n2, x.data_ptr(), 0.5, p, _lib.ptr(rng),
+            off2, None, 0,
             out.data_ptr(), stream), "ob_bitlinear_fwd_residual")
         ctx.meta = meta
         ctx.has_bias = (b1 is not None, b2 is not None)
@@ -212,13 +238,14 @@ class _FFNFn(torch.autograd.Function):
         dpre = torch.empty((rows, n1), dtype=torch.float32, device=gout.device)
         _lib.check(lib.ob_bitlinear_bwd_dx_swish_drop(
             dy2.data_ptr(), P, m, n2, codes2[2].data_ptr(), codes2[3].data_ptr(), _lib.ptr(pb),
-            a2.data_ptr(), 1, n1, pre.data_ptr(), p, _lib.ptr(rng), off1, dpre.data_ptr(), stream),
+            a2.data_ptr(), codes2.dx_raw, n1, pre.data_ptr(), p, _lib.ptr(rng), off1,
+            dpre.data_ptr(), stream),
             "ob_bitlinear_bwd_dx_swish_drop")
         gw2, ga2, gb2 = _dw(lib, dy2, act, P, m, n2, n1, w2, a2, ctx.has_bias[1], pb, bits, stream,
-                            ctx.biases[1])
+                            ctx.biases[1], codes2.dense)
         gh = _dx(lib, dpre, P, m, n1, codes1, pb, a1, k, stream) if ctx.needs_input_grad[0] else None
         gw1, ga1, gb1 = _dw(lib, dpre, h, P, m, n1, k, w1, a1, ctx.has_bias[0], pb, bits, stream,
-                            ctx.biases[0])
+                            ctx.biases[0], codes1.dense)
         return gh, gout, gw1, ga1, gb1, gw2, ga2, gb2, None
 
 
@@ -235,7 +262,7 @@ class _LinearResidualFn(torch.autograd.Function):
         out = torch.empty((rows, n), dtype=torch.float32, device=x.device)
         _lib.check(lib.ob_bitlinear_fwd_residual(
             x.data_ptr(), P, m, k, codes[0].data_ptr(), codes[1].data_ptr(), _lib.ptr(pb),
-            a.data_ptr(), 1, _lib.ptr(b), n, resid.data_ptr(), rscale, p, _lib.ptr(rng), off,
+            a.data_ptr(), codes.fwd_raw, _lib.ptr(b), n, resid.data_ptr(), rscale, p, _lib.ptr(rng), off,
             _lib.ptr(lens), T, out.data_ptr(), _lib.stream_of(x)), "ob_bitlinear_fwd_residual")
         ctx.meta = meta
         ctx.has_bias = b is not None
@@ -261,7 +288,8 @@ class _LinearResidualFn(torch.autograd.Function):
                                              off, _lib.ptr(lens), T, dy.data_ptr(), stream),
                        "ob_drop_scale_bwd")
         gx = _dx(lib, dy, P, m, n, codes, pb, a, k, stream) if ctx.needs_input_grad[0] else None
-        gw, ga, gb = _dw(lib, dy, x, P, m, n, k, w, a, ctx.has_bias, pb, bits, stream, ctx.bias)
+        gw, ga, gb = _dw(lib, dy, x, P, m, n, k, w, a, ctx.has_bias, pb, bits, stream, ctx.bias,
+                         codes.dense)
         return gx, gout, gw, ga, gb, None
 
 
@@ -283,11 +311,11 @@ class _QKVFn(torch.autograd.Function):
             n = w.shape[0]
             y = torch.empty((rows, n), dtype=torch.float32, device=h.device)
             st = (lib.ob_bitlinear_fwd_passes(h.data_ptr(), P, m, k, c[0].data_ptr(),
-                                              c[1].data_ptr(), pb.data_ptr(), a.data_ptr(), 1,
-                                              _lib.ptr(b), n, y.data_ptr(), stream)
+                                              c[1].data_ptr(), pb.data_ptr(), a.data_ptr(),
+                                              c.fwd_raw, _lib.ptr(b), n, y.data_ptr(), stream)
                   if pb is not None else
-                  lib.ob_bitlinear_fwd(h.data_ptr(), m, k, c[0].data_ptr(), a.data_ptr(), 1,
-                                       _lib.ptr(b), n, y.data_ptr(), stream))
+                  lib.ob_bitlinear_fwd(h.data_ptr(), m, k, c[0].data_ptr(), a.data_ptr(),
+                                       c.fwd_raw, _lib.ptr(b), n, y.data_ptr(), stream))
             _lib.check(st, "ob_bitlinear_fwd")
             outs.append(y)
         ctx.meta = meta
@@ -319,10 +347,10 @@ class _QKVFn(torch.autograd.Function):
                 # by one lane)
                 _lib.check(lib.ob_bitlinear_fwd_residual(
                     g.data_ptr(), P, m, n, c[2].data_ptr(), c[3].data_ptr(), _lib.ptr(pb),
-                    a.data_ptr(), 1, None, k, gh.data_ptr(), 1.0, 0.0, None, 0, None, 0,
+                    a.data_ptr(), c.dx_raw, None, k, gh.data_ptr(), 1.0, 0.0, None, 0, None, 0,
                     gh.data_ptr(), stream), "ob_bitlinear_fwd_residual (dX accumulate)")
         grads = {}
-        if _DW_GROUP and pb is not None and len(layers) == 3 and \
+        if _DW_GROUP and pb is not None and len(layers) == 3 and not codes[0].dense and \
                 len({w.shape for _, w, _, _, _ in layers}) == 1:
             # the three dW GEMMs share X = h: their finishes in one launch
             n = layers[0][1].shape[0]
@@ -358,7 +386,8 @@ class _QKVFn(torch.autograd.Function):
         for i, (g, w, a, c, hb) in zip(range(3), layers):
             if id(w) not in grads:
                 b = ctx.biases[[id(t) for t in (wq, wk, wv)].index(id(w))]
-                grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream, b)
+                grads[id(w)] = _dw(lib, g, h, P, m, w.shape[0], k, w, a, hb, pb, bits, stream, b,
+                                   c.dense)
         out = [gh]
         for w in (wq, wk, wv):
             out.extend(grads.get(id(w), (None, None, None)))

@@ -155,16 +155,26 @@ def set_act_quant(module: nn.Module, mode: Optional[str]) -> nn.Module:
     return module
 
 
-def set_quant_off(module: nn.Module, dtype: Optional[torch.dtype] = torch.bfloat16) -> nn.Module:
-    """BASELINE configs[3]: every QuantizedLinear under ``module`` becomes a plain
-    ``F.linear`` computed in ``dtype`` (bf16 -> hipBLASLt bf16 MFMA), whatever the bitwidth;
-    ``alpha`` then receives no gradient. ``None`` restores the BitLinear path. The reference
-    has no such mode (its bitwidth 32 is fp32 F.linear, quant.py:121-122); this is the
-    measurement ceiling for the ternary kernels, not a parity path."""
+def set_quant_off(module: nn.Module, dtype=torch.bfloat16) -> nn.Module:
+    """BASELINE configs[3]: every QuantizedLinear under ``module`` becomes a plain linear
+    layer whatever the bitwidth; ``alpha`` then receives no gradient. ``None`` restores the
+    BitLinear path. The reference has no such mode (its bitwidth 32 is fp32 F.linear,
+    quant.py:121-122); this is the measurement ceiling for the ternary kernels, not a
+    parity path.
+    * a torch dtype (bf16): ``F.linear`` in that dtype on the library GEMMs (hipBLASLt);
+    * ``"bf16w"``: the SAME fused call sites and kernels as the ternary path with the weight
+      operand bf16(W) instead of the 2-bit codes (alpha_raw 2/3 of include/onebit_hip.h;
+      activations exact fp32) and a plain dense dW -- only the weight format differs, so
+      the comparison with the 1.58-bit step isolates it."""
+    if dtype is not None and dtype != "bf16w" and not isinstance(dtype, torch.dtype):
+        raise ValueError(f"quant_off must be None, a torch dtype or 'bf16w', got {dtype!r}")
     for m in module.modules():
         if isinstance(m, QuantizedLinear):
             m.quant_off = dtype
     return module
+
+
+_ONE_PASS = {}  # device index -> int32 [1] pass_bits of a one-pass quant-off call
 
 
 def _require_device(*tensors: torch.Tensor) -> None:
@@ -268,10 +278,13 @@ class _BitLinearPassesFn(torch.autograd.Function):
         n = weight.shape[0]
         y = torch.empty((rows, n), dtype=torch.float32, device=x2d.device)
         lib = _lib.load()
+        # fp32 "codes" = the weight itself: the quant-off ceiling (alpha_raw 2 / 3, dense dW)
+        ctx.dense = codes2.dtype == torch.float32
         _lib.check(
             lib.ob_bitlinear_fwd_passes(x2d.data_ptr(), P, m, k, codes2.data_ptr(), codes1.data_ptr(),
-                                        pass_bits.data_ptr(), alpha.data_ptr(), 1, _lib.ptr(bias), n,
-                                        y.data_ptr(), _lib.stream_of(x2d)),
+                                        pass_bits.data_ptr(), alpha.data_ptr(),
+                                        2 if ctx.dense else 1, _lib.ptr(bias), n, y.data_ptr(),
+                                        _lib.stream_of(x2d)),
             "ob_bitlinear_fwd_passes",
         )
         ctx.P = P
@@ -297,9 +310,23 @@ class _BitLinearPassesFn(torch.autograd.Function):
             _lib.check(
                 lib.ob_bitlinear_bwd_dx_passes(gy.data_ptr(), P, m, n, codes2_t.data_ptr(),
                                                codes1_t.data_ptr(), pass_bits.data_ptr(),
-                                               alpha.data_ptr(), 1, k, gx.data_ptr(), stream),
+                                               alpha.data_ptr(), 3 if ctx.dense else 1, k,
+                                               gx.data_ptr(), stream),
                 "ob_bitlinear_bwd_dx_passes",
             )
+        if ctx.dense and (ctx.needs_input_grad[1] or ctx.needs_input_grad[3]):
+            wsb = lib.ob_dense_dw_workspace(rows, n, k)
+            if wsb and gy.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0:
+                gw = torch.empty_like(weight)
+                gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+                ws = torch.empty((wsb,), dtype=torch.uint8, device=gy.device)
+                deferred.dense_dw(gy, x2d, rows, n, k, gw, gb, ws, wsb, stream, weight, ctx.bias)
+            else:  # shapes off the dW kernels (N or K not a multiple of 48): library fp32
+                from .linear import colsum
+
+                gw = gy.t() @ x2d
+                gb = colsum(gy) if ctx.has_bias else None
+            return gx, gw, None, gb, None, None, None, None, None, None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
             gw = torch.empty_like(weight)
             galpha = torch.empty((), dtype=torch.float32, device=gy.device)
@@ -522,6 +549,8 @@ class QuantizedLinear(nn.Module):
         return codes, codes_t
 
     def forward(self, x: torch.Tensor, bitwidth: int) -> torch.Tensor:
+        if self.quant_off == "bf16w":  # configs[3] ceiling on the fused kernels (bf16 W)
+            return self._forward_bf16w(x)
         if self.quant_off is not None:  # configs[3] ceiling: no quantizer, library GEMM
             return linear(x, self.weight, self.bias, dtype=self.quant_off)
         if self._packed is not None:
@@ -551,6 +580,23 @@ class QuantizedLinear(nn.Module):
                                      codes_t, None, None, amax)
             return y.view(*lead, self.out_features)
         y = _BitLinearFn.apply(x2d, self.weight, self.alpha, self.bias, bits, codes, codes_t)
+        return y.view(*lead, self.out_features)
+
+    def _forward_bf16w(self, x: torch.Tensor) -> torch.Tensor:
+        """Quant-off (set_quant_off "bf16w") on the stacked-pass GEMM entries with B =
+        bf16(W): one pass, the weight itself in every codes slot (alpha_raw 2 / 3)."""
+        _require_device(x, self.weight)
+        lead = x.shape[:-1]
+        x2d = x.reshape(-1, self.in_features)
+        if not x2d.is_contiguous():
+            x2d = x2d.contiguous()
+        key = x.device.index
+        one = _ONE_PASS.get(key)
+        if one is None:
+            one = torch.full((1,), 2, dtype=torch.int32, device=x.device)
+            _ONE_PASS[key] = one
+        W = self.weight
+        y = _BitLinearPassesFn.apply(x2d, W, self.alpha, self.bias, one, 1, W, W, W, W)
         return y.view(*lead, self.out_features)
 
     def _forward_passes(self, x: torch.Tensor, pb: PassBits) -> torch.Tensor:

@@ -19,6 +19,12 @@
  *     learnable parameter and the kernels use a = |alpha| + 1e-8f exactly as
  *     QuantizedLinear.forward does (quant.py:124); with alpha_raw = 0 it is used
  *     as given (the quantize_weight(W, alpha, bits) entry, quant.py:95-96).
+ *   - quant-off ceiling (BASELINE configs[3]: BitLinear -> bf16 nn.Linear): on the GEMM
+ *     entries (ob_bitlinear_fwd*, ob_bitlinear_bwd_dx*), alpha_raw = 2 makes each codes
+ *     argument the fp32 weight W [N][K] itself and the GEMM's B operand bf16(W) (round to
+ *     nearest even; activations stay exact fp32, as in every entry), with no alpha scale;
+ *     alpha_raw = 3 is the same for the dX entries' codes_t arguments (W [N][K], read
+ *     transposed). Same kernels, tiles and fused epilogues as the ternary path.
  *   - bits is 1 (binary {-1,+1}, zero -> +1) or 2 (ternary {-1,0,+1}, threshold 0.5)
  *     (quant.py:52-60). bits = 32 is the full-precision passthrough and never
  *     reaches this library (quant.py:121-122); any other value -> OB_ERR_BITWIDTH,
