@@ -86,6 +86,11 @@ int64_t ob_quant_pack_item_blocks(int64_t N, int64_t K) {
   return quant_pack_item_blocks(N, K);
 }
 
+int64_t ob_weight_bf16_item_blocks(int64_t N, int64_t K) {
+  if (N < 0 || K < 0) return OB_ERR_SHAPE;
+  return quant_pack_item_blocks16(N, K);
+}
+
 int ob_quant_pack_group(const ob_pack_item* items, int n_items, int64_t total_blocks,
                         void* stream) {
   if (n_items < 0 || total_blocks < 0 || total_blocks > 0x7fffffff) return OB_ERR_SHAPE;

@@ -19,6 +19,7 @@ void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bi
                        uint32_t* codes_t, hipStream_t s);
 // Grouped pack (ob_pack_item from include/onebit_hip.h; table on device).
 int64_t quant_pack_item_blocks(int64_t N, int64_t K);
+int64_t quant_pack_item_blocks16(int64_t N, int64_t K);  // a bits == 16 (bf16 image) item
 void launch_quant_pack_group(const ob_pack_item* items_dev, int n_items, int64_t total_blocks,
                              hipStream_t s);
 void launch_quant_dequant(const float* W, const float* alpha, int alpha_raw, int bits, int64_t n,

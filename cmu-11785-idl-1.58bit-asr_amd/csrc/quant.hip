@@ -73,6 +73,22 @@ __global__ __launch_bounds__(kThreads) void quant_pack_group_kernel(
     if (items[mid].block0 <= blk) lo = mid; else hi = mid - 1;
   }
   const ob_pack_item it = items[lo];
+  if (it.bits == 16) {  // bf16 weight images (quant-off): codes <- bf16(W), codes_t <- bf16(W^T)
+    const int64_t nk = it.N * it.K;
+    uint16_t* img = reinterpret_cast<uint16_t*>(it.codes);
+    uint16_t* imgt = reinterpret_cast<uint16_t*>(it.codes_t);
+#pragma unroll 4
+    for (int i = 0; i < kPackIters; ++i) {
+      const int64_t e = ((blk - it.block0) * kPackIters + i) * kThreads + threadIdx.x;
+      if (e < nk) {
+        img[e] = __builtin_bit_cast(uint16_t, (__bf16)it.W[e]);
+      } else if (e < 2 * nk) {
+        const int64_t e2 = e - nk, k = e2 / it.N, n = e2 - k * it.N;
+        imgt[e2] = __builtin_bit_cast(uint16_t, (__bf16)it.W[n * it.K + k]);
+      }
+    }
+    return;
+  }
   const float a = effective_alpha(it.alpha, it.alpha_raw);
   const int64_t N = it.N, K = it.K, KW = (K + 15) >> 4, NW = (N + 15) >> 4;
   const int j = threadIdx.x & 15;
@@ -250,6 +266,10 @@ void launch_quant_pack(const float* W, const float* alpha, int alpha_raw, int bi
   const int64_t blocks = ceil_div(total, kThreads);
   hipLaunchKernelGGL(quant_pack_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, W, alpha,
                      alpha_raw, bits, bits_dev, N, K, KW, NW, codes, codes_t);
+}
+
+int64_t quant_pack_item_blocks16(int64_t N, int64_t K) {
+  return ceil_div(2 * N * K, (int64_t)kPackIters * kThreads);
 }
 
 int64_t quant_pack_item_blocks(int64_t N, int64_t K) {

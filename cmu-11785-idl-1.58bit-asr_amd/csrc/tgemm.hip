@@ -20,11 +20,11 @@
 // Fragment map of v_mfma_f32_16x16x32_bf16 (lane l, r = l&15, g = l>>4):
 //   A[i=r][kk=8g+j] (j<8), B[kk=8g+j][col=r], D[row=4g+reg][col=r].
 //
-// Quant-off ceiling (BASELINE configs[3], quant.py:121-122 with bf16 weights): alpha_raw 2 / 3
-// makes the "codes" argument the fp32 weight W [N][K] itself (3: read transposed, for dX);
-// the block then builds its LDS image from bf16(W) (round to nearest even) instead of
-// decoding codes, and the scale is 1 -- the same kernel, tiles and fused epilogues, only the
-// weight format differs.
+// Quant-off ceiling (BASELINE configs[3], quant.py:121-122 with bf16 weights): alpha_raw 2
+// makes the "codes" argument a bf16 weight image [N][K] (uint16; for dX the transposed
+// image, both packed once per step like the codes: ob_quant_pack_group items with bits 16);
+// the block copies its rows into the LDS image instead of decoding codes, and the scale is
+// 1 -- the same kernel, tiles and fused epilogues, only the weight format differs.
 //
 // OB_GEMM=f32 in the environment selects an fp32-MFMA kernel (v_mfma_f32_16x16x4_f32,
 // exact fp32 fma chain) for A/B checks; it is also the path for shapes the bf16x3 kernel
@@ -274,24 +274,25 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   constexpr bool kCross = NT <= 9;
   constexpr int kWin = NCH > 0 ? (NCH < kWmax ? NCH : kWmax) : 1;
   f32x4 buf[NCH > 0 ? NCH : 1][2];
-  // quant-off: the image from bf16(W); W [N][K] (alpha_raw 2) or, for dX, W [K][N] read
-  // transposed (alpha_raw 3). Unit = 8 consecutive k of one image row (one 16-byte store).
+  // quant-off (alpha_raw 2): the LDS image is a copy of the block's rows of the bf16 weight
+  // image [N][K]. Unit = 8 consecutive k of one row (one 16-byte load and store).
   auto weight_image = [&]() {
-    const float* Wf = reinterpret_cast<const float*>(codes);
+    const uint16_t* Wb = reinterpret_cast<const uint16_t*>(codes);
     const int upr = kpad >> 3;
     for (int u = threadIdx.x; u < 16 * NT * upr; u += kThreads) {
       const int nl = u / upr, k0 = 8 * (u - nl * upr);
       const int n = n0 + nl;
-      bf16x8 v;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (n < N && (K & 7) == 0 && k0 + 8 <= K) {
+        v = *reinterpret_cast<const u32x4*>(Wb + (int64_t)n * K + k0);
+      } else if (n < N) {
+        uint16_t h[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = k0 + j;
-        const float w = (n < N && k < K)
-                            ? (alpha_raw == 3 ? Wf[(int64_t)k * N + n] : Wf[(int64_t)n * K + k])
-                            : 0.0f;
-        v[j] = (__bf16)w;
+        for (int j = 0; j < 8; ++j) h[j] = k0 + j < K ? Wb[(int64_t)n * K + k0 + j] : (uint16_t)0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (uint32_t)h[2 * q] | ((uint32_t)h[2 * q + 1] << 16);
       }
-      *reinterpret_cast<bf16x8*>(bimg + nl * stride + k0) = v;
+      *reinterpret_cast<u32x4*>(bimg + nl * stride + k0) = v;
     }
   };
   if constexpr (NCH > 0) {
@@ -559,13 +560,13 @@ __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
 #pragma unroll
     for (int t = 0; t < kF32NT; ++t) {
       const int64_t n = n0 + 16 * t + r;
-      if (alpha_raw >= 2) {  // quant-off: B = bf16(W)
-        const float* Wf = reinterpret_cast<const float*>(codes);
+      if (alpha_raw >= 2) {  // quant-off: B from the bf16 weight image [N][K]
+        const uint16_t* Wb = reinterpret_cast<const uint16_t*>(codes);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int64_t k = kc + 4 * g + e;
-          const float w = (n < N && k < K) ? (alpha_raw == 3 ? Wf[k * N + n] : Wf[n * K + k]) : 0.0f;
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], (float)(__bf16)w, acc[t], 0, 0, 0);
+          const float w = (n < N && k < K) ? __uint_as_float((uint32_t)Wb[n * K + k] << 16) : 0.0f;
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], w, acc[t], 0, 0, 0);
         }
         continue;
       }

@@ -37,6 +37,7 @@ SIGNATURES = {
     "ob_quant_pack": (_int, [_c_f, _c_f, _int, _int, _i64, _i64, _c_f, _c_f, _c_f]),
     "ob_quant_pack_item_blocks": (_i64, [_i64, _i64]),
     "ob_quant_pack_group": (_int, [_c_f, _int, _i64, _c_f]),
+    "ob_weight_bf16_item_blocks": (_i64, [_i64, _i64]),
     "ob_bitlinear_fwd_swish_drop": (
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _f32, _c_f, _i64,
                _c_f, _c_f, _c_f]),

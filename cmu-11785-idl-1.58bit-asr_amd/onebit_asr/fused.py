@@ -106,9 +106,9 @@ def _bits_args(bitwidth):
 
 class Codes(tuple):
     """(codes2, codes1, codes2_t, codes1_t) of one layer, with the C ABI's alpha_raw for its
-    forward and dX GEMMs: 1 / 1 for ternary codes; 2 / 3 for the quant-off ceiling
-    (quant_off="bf16w": every slot is the fp32 weight itself, B = bf16(W), no alpha), whose
-    weight gradient is a plain dense dW (dense=True)."""
+    forward and dX GEMMs: 1 / 1 for ternary codes; 2 / 2 for the quant-off ceiling
+    (quant_off="bf16w": the slots hold the bf16 weight images W [N][K] / W^T [K][N], no
+    alpha), whose weight gradient is a plain dense dW (dense=True)."""
     fwd_raw = 1
     dx_raw = 1
     dense = False
@@ -117,8 +117,9 @@ class Codes(tuple):
 def _codes(layer: QuantizedLinear, P: int, bits: Optional[int]):
     """(codes2, codes1, codes2_t, codes1_t); single-pass: both slots hold the layer's bits."""
     if layer.quant_off == "bf16w":
-        c = Codes((layer.weight,) * 4)
-        c.fwd_raw, c.dx_raw, c.dense = 2, 3, True
+        img, img_t = layer._bf16_images()
+        c = Codes((img, img, img_t, img_t))
+        c.fwd_raw, c.dx_raw, c.dense = 2, 2, True
         return c
     if P == 1 and bits is not None and bits != 2:
         c, ct = layer._codes(bits)

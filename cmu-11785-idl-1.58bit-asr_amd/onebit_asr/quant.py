@@ -278,8 +278,8 @@ class _BitLinearPassesFn(torch.autograd.Function):
         n = weight.shape[0]
         y = torch.empty((rows, n), dtype=torch.float32, device=x2d.device)
         lib = _lib.load()
-        # fp32 "codes" = the weight itself: the quant-off ceiling (alpha_raw 2 / 3, dense dW)
-        ctx.dense = codes2.dtype == torch.float32
+        # int16 "codes" = bf16 weight images: the quant-off ceiling (alpha_raw 2, dense dW)
+        ctx.dense = codes2.dtype == torch.int16
         _lib.check(
             lib.ob_bitlinear_fwd_passes(x2d.data_ptr(), P, m, k, codes2.data_ptr(), codes1.data_ptr(),
                                         pass_bits.data_ptr(), alpha.data_ptr(),
@@ -310,7 +310,7 @@ class _BitLinearPassesFn(torch.autograd.Function):
             _lib.check(
                 lib.ob_bitlinear_bwd_dx_passes(gy.data_ptr(), P, m, n, codes2_t.data_ptr(),
                                                codes1_t.data_ptr(), pass_bits.data_ptr(),
-                                               alpha.data_ptr(), 3 if ctx.dense else 1, k,
+                                               alpha.data_ptr(), 2 if ctx.dense else 1, k,
                                                gx.data_ptr(), stream),
                 "ob_bitlinear_bwd_dx_passes",
             )
@@ -595,9 +595,30 @@ class QuantizedLinear(nn.Module):
         if one is None:
             one = torch.full((1,), 2, dtype=torch.int32, device=x.device)
             _ONE_PASS[key] = one
-        W = self.weight
-        y = _BitLinearPassesFn.apply(x2d, W, self.alpha, self.bias, one, 1, W, W, W, W)
+        img, img_t = self._bf16_images()
+        y = _BitLinearPassesFn.apply(x2d, self.weight, self.alpha, self.bias, one, 1, img, img_t,
+                                     img, img_t)
         return y.view(*lead, self.out_features)
+
+    def _bf16_images(self):
+        """(bf16(W) [N][K], bf16(W^T) [K][N]) as int16 tensors, the quant-off GEMM operand;
+        packed once per step for every layer by PackGroup, else here (one-item group)."""
+        key = (self.weight.data_ptr(), self.weight._version)
+        hit = self._codes_cache.get(16)
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        n, k = self.weight.shape
+        img = torch.empty((n, k), dtype=torch.int16, device=self.weight.device)
+        img_t = torch.empty((k, n), dtype=torch.int16, device=self.weight.device)
+        lib = _lib.load()
+        items = np.zeros(1, dtype=PackGroup.ITEM)
+        items[0] = (self.weight.data_ptr(), self.alpha.data_ptr(), img.data_ptr(),
+                    img_t.data_ptr(), n, k, 0, 16, 1)
+        table = torch.from_numpy(items.view(np.uint8).copy()).to(self.weight.device)
+        _lib.check(lib.ob_quant_pack_group(table.data_ptr(), 1, lib.ob_weight_bf16_item_blocks(n, k),
+                                           _lib.stream_of(self.weight)), "ob_quant_pack_group")
+        self._codes_cache[16] = (key, img, img_t)
+        return img, img_t
 
     def _forward_passes(self, x: torch.Tensor, pb: PassBits) -> torch.Tensor:
         """x: the P passes stacked on the leading dim ([P*B, ..., K] or [P*M, K])."""
@@ -682,7 +703,7 @@ class PackGroup:
 
     def __init__(self, module: nn.Module, bits=(2, 1)):
         self.layers = [m for m in module.modules()
-                       if isinstance(m, QuantizedLinear) and m.quant_off is None
+                       if isinstance(m, QuantizedLinear) and m.quant_off in (None, "bf16w")
                        and m._packed is None]  # packed layers keep their loaded codes
         self.bits = tuple(bits)
         self._ptrs = None
@@ -691,7 +712,8 @@ class PackGroup:
 
     def _build(self):
         lib = _lib.load()
-        items = np.zeros(len(self.layers) * len(self.bits), dtype=self.ITEM)
+        items = np.zeros(sum(1 if m.quant_off == "bf16w" else len(self.bits) for m in self.layers),
+                         dtype=self.ITEM)
         self.codes = []
         block0 = 0
         i = 0
@@ -699,6 +721,16 @@ class PackGroup:
             _require_device(m.weight, m.alpha)
             n, k = m.weight.shape
             per = {}
+            if m.quant_off == "bf16w":  # quant-off ceiling: bf16 weight images (bits 16)
+                c = torch.empty((n, k), dtype=torch.int16, device=m.weight.device)
+                ct = torch.empty((k, n), dtype=torch.int16, device=m.weight.device)
+                items[i] = (m.weight.data_ptr(), m.alpha.data_ptr(), c.data_ptr(), ct.data_ptr(),
+                            n, k, block0, 16, 1)
+                block0 += int(lib.ob_weight_bf16_item_blocks(n, k))
+                per[16] = (c, ct)
+                i += 1
+                self.codes.append(per)
+                continue
             for b in self.bits:
                 c = torch.empty((n, (k + 15) // 16), dtype=torch.int32, device=m.weight.device)
                 ct = torch.empty((k, (n + 15) // 16), dtype=torch.int32, device=m.weight.device)
@@ -709,6 +741,7 @@ class PackGroup:
                 i += 1
             self.codes.append(per)
         self.total_blocks = block0
+        self.n_items = i
         dev = self.layers[0].weight.device
         self.table = torch.from_numpy(items.view(np.uint8).copy()).to(dev)
         self._ptrs = [m.weight.data_ptr() for m in self.layers]
@@ -720,13 +753,14 @@ class PackGroup:
             self._build()
         lib = _lib.load()
         w0 = self.layers[0].weight
-        _lib.check(lib.ob_quant_pack_group(self.table.data_ptr(), len(self.codes) * len(self.bits),
+        _lib.check(lib.ob_quant_pack_group(self.table.data_ptr(), self.n_items,
                                            self.total_blocks, _lib.stream_of(w0)),
                    "ob_quant_pack_group")
         for m, per in zip(self.layers, self.codes):
             key = (m.weight.data_ptr(), m.weight._version, m.alpha.data_ptr(), m.alpha._version)
             for b, (c, ct) in per.items():
-                m._codes_cache[b] = (key, c, ct)
+                m._codes_cache[b] = ((m.weight.data_ptr(), m.weight._version) if b == 16 else key,
+                                     c, ct)
 
 
 # north_star's name for the same layer.

@@ -21,10 +21,10 @@
  *     as given (the quantize_weight(W, alpha, bits) entry, quant.py:95-96).
  *   - quant-off ceiling (BASELINE configs[3]: BitLinear -> bf16 nn.Linear): on the GEMM
  *     entries (ob_bitlinear_fwd*, ob_bitlinear_bwd_dx*), alpha_raw = 2 makes each codes
- *     argument the fp32 weight W [N][K] itself and the GEMM's B operand bf16(W) (round to
- *     nearest even; activations stay exact fp32, as in every entry), with no alpha scale;
- *     alpha_raw = 3 is the same for the dX entries' codes_t arguments (W [N][K], read
- *     transposed). Same kernels, tiles and fused epilogues as the ternary path.
+ *     argument a bf16 weight image (uint16 [N][K] = bf16(W) for the forward entries, [K][N]
+ *     = bf16(W^T) for the dX entries' codes_t; ob_pack_item bits = 16 packs both) and the
+ *     GEMM's B operand that image, with no alpha scale (activations stay exact fp32, as in
+ *     every entry). Same kernels, tiles and fused epilogues as the ternary path.
  *   - bits is 1 (binary {-1,+1}, zero -> +1) or 2 (ternary {-1,0,+1}, threshold 0.5)
  *     (quant.py:52-60). bits = 32 is the full-precision passthrough and never
  *     reaches this library (quant.py:121-122); any other value -> OB_ERR_BITWIDTH,
@@ -89,11 +89,14 @@ typedef struct ob_pack_item {
   uint32_t* codes_t;   /* [K][ceil(N/16)] */
   int64_t N, K;
   int64_t block0;      /* first block of this item */
-  int32_t bits;        /* 1 or 2 */
+  int32_t bits;        /* 1 or 2; 16: bf16 weight images (quant-off), codes <- uint16 [N][K]
+                          bf16(W), codes_t <- uint16 [K][N] bf16(W^T), block count from
+                          ob_weight_bf16_item_blocks */
   int32_t alpha_raw;
 } ob_pack_item;
 
 OB_API int64_t ob_quant_pack_item_blocks(int64_t N, int64_t K);
+OB_API int64_t ob_weight_bf16_item_blocks(int64_t N, int64_t K);
 OB_API int ob_quant_pack_group(const ob_pack_item* items, int n_items, int64_t total_blocks,
                                void* stream);
 

@@ -124,6 +124,10 @@ def test_quant_off_bf16w_fused_equals_module_gpu(gpu, monkeypatch):
     assert (y1 - y0).abs().max().item() <= 1e-5 * y0.abs().max().item()
     assert (gx1 - gx0).abs().max().item() <= 1e-5 * gx0.abs().max().item()
     assert g1.keys() == g0.keys()
+    scale = max(g.abs().max().item() for g in g0.values())
     for k in g0:
         err = (g1[k] - g0[k]).abs().max().item()
+        if "k_proj.bias" in k or "dw.bias" in k:  # exact gradient 0 (softmax shift / BatchNorm)
+            assert err <= 1e-6 * scale, (k, err)
+            continue
         assert err <= 1e-4 * g0[k].abs().max().item() + 1e-7, (k, err)
