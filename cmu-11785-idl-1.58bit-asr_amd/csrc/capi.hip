@@ -429,8 +429,9 @@ int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_tr
 }
 
 size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K) {
-  if (M < 0 || N <= 0 || K <= 0 || N % 48 != 0 || K % 48 != 0) return 0;
-  if (plan_dw(M, N, K).variant < 9) return 0;  // the LDS bf16x6 tiles only
+  if (M < 0 || N <= 0 || K <= 0 || N % 4 != 0 || K % 4 != 0) return 0;
+  const int v = plan_dw(M, N, K).variant;
+  if (v != 4 && v < 9) return 0;  // the bf16x6 tiles (LDS: widths % 48; register: % 4)
   return dw_layout(1, M, N, K).total;
 }
 
@@ -461,6 +462,22 @@ int ob_dense_dw_defer(const float* dY, const float* X, int64_t M, int64_t N, int
   float* part = reinterpret_cast<float*>(base);
   float* part_db = db ? reinterpret_cast<float*>(base + L.part) : nullptr;
   const DwAlpha al{nullptr, nullptr, 0, 2, nullptr, nullptr, nullptr};  // no alpha: dense
+  if (p.variant < 9) {  // register bf16x6 tiles (64-wide): the same chunk partials + finish
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(base + L.part + L.part_db);
+    launch_dw_partial(dY, X, M, N, K, p, part, part_db, ticket, s);
+    const DwFinish fin{part, (int)p.chunks, N * K, part_db, db ? N : 0, nullptr, nullptr, 0,
+                       nullptr, 0, dW, db, nullptr};
+    if (table) {
+      // (no entry written by the register kernel: a 1-block launch writes it)
+      const DwFinishEntry ent{fin, start};
+      launch_dw_table_entry(static_cast<DwFinishEntry*>(table), (int)slot, ent, s);
+      *n_blocks = dw_finish_blocks(fin);
+      return launched();
+    }
+    launch_dw_finish(part, (int)p.chunks, N * K, part_db, db ? N : 0, nullptr, nullptr, 0,
+                     nullptr, 0, dW, db, nullptr, s);
+    return launched();
+  }
   if (table) {  // finish deferred to ob_dw_finish_table
     const DwFinish fin{part, (int)p.chunks, N * K, part_db, db ? N : 0, nullptr, nullptr, 0,
                        nullptr, 0, dW, db, nullptr};

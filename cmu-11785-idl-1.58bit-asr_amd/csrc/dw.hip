@@ -967,6 +967,15 @@ void launch_dw_finish(const float* part, int chunks, int64_t nk, const float* pa
 
 int64_t dw_finish_blocks(const DwFinish& a) { return finish_blocks(a); }
 
+__global__ void dw_table_entry_kernel(DwFinishEntry* table, int slot, DwFinishEntry ent) {
+  table[slot] = ent;
+}
+
+void launch_dw_table_entry(DwFinishEntry* table, int slot, const DwFinishEntry& ent,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(dw_table_entry_kernel, dim3(1), dim3(1), 0, s, table, slot, ent);
+}
+
 void launch_dw_finish_table(const DwFinishEntry* table, int n, int64_t total_blocks,
                             hipStream_t s) {
   if (n <= 0 || total_blocks <= 0) return;

@@ -187,6 +187,7 @@ struct DwFinishEntry {
   int64_t start;
 };
 int64_t dw_finish_blocks(const DwFinish& a);
+void launch_dw_table_entry(DwFinishEntry* table, int slot, const DwFinishEntry& ent, hipStream_t s);
 void launch_dw_finish_table(const DwFinishEntry* table, int n, int64_t total_blocks, hipStream_t s);
 // launch_dw_partial_group with the finish deferred: ent[i] (start filled in) is written to
 // table[slot + i] by the partial launch itself

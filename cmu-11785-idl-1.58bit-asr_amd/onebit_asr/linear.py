@@ -38,6 +38,9 @@ __all__ = ["linear", "colsum"]
 
 _DENSE = os.environ.get("OB_DENSE_LINEAR", "1") != "0"
 _DENSE_DW = _DENSE and os.environ.get("OB_DENSE_LINEAR_DW", "1") != "0"
+# widths that are not multiples of 48 (the V = 5004 CTC head / decoder output layer) on the
+# register bf16x6 dW tiles; 0 keeps them on the library
+_DENSE_DW_WIDE = os.environ.get("OB_DENSE_DW_WIDE", "1") != "0"
 
 
 def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
@@ -49,11 +52,14 @@ def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
 
 def _dense_dw_ws(g2: torch.Tensor, x2d: torch.Tensor, w: torch.Tensor) -> int:
     """Workspace bytes of ob_dense_dw for this linear's weight gradient, 0 if not taken
-    (N, K multiples of 48; 16-byte aligned operands)."""
+    (N, K multiples of 4; 16-byte aligned operands)."""
     if not (_DENSE_DW and g2.is_cuda and x2d.is_contiguous() and w.is_contiguous()
             and g2.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0):
         return 0
-    return int(_lib.load().ob_dense_dw_workspace(g2.shape[0], w.shape[0], w.shape[1]))
+    n, k = w.shape
+    if not _DENSE_DW_WIDE and (n % 48 or k % 48):
+        return 0
+    return int(_lib.load().ob_dense_dw_workspace(g2.shape[0], n, k))
 
 
 def _dense(x2d: torch.Tensor, w: torch.Tensor, trans: int, bias, n: int) -> torch.Tensor:

@@ -90,7 +90,9 @@ def _dw(dy, x, with_db=True):
 
 
 @pytest.mark.parametrize("m,n,k", [(23904, 288, 144), (23904, 144, 144), (777, 144, 288),
-                                   (33, 48, 96), (1, 144, 144)])
+                                   (33, 48, 96), (1, 144, 144),
+                                   # V = 5004 widths on the register tiles (CTC head, decoder out)
+                                   (23904, 5004, 144), (3936, 5004, 144), (100, 52, 20)])
 def test_dense_dw_matches_fp64(gpu, m, n, k):
     g = torch.Generator(device=gpu).manual_seed(m * 3 + n)
     dy = torch.randn(m, n, device=gpu, generator=g)
@@ -117,7 +119,8 @@ def test_dense_abi_errors(gpu):
     lib = L.load()
     assert lib.ob_dense_supported(142, 144) == 0  # K % 4
     assert lib.ob_dense_supported(144, 30) == 0   # N % 4
-    assert lib.ob_dense_dw_workspace(10, 144, 100) == 0  # K % 48
+    assert lib.ob_dense_dw_workspace(10, 144, 102) == 0  # K % 4
+    assert lib.ob_dense_dw_workspace(10, 5004, 144) > 0  # register bf16x6 tiles (N % 4)
     x = torch.randn(8, 144, device=gpu)
     w = torch.randn(144, 144, device=gpu)
     y = torch.empty(8, 144, device=gpu)
