@@ -236,6 +236,104 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
     return roof
 
 
+def roofline_fused(batch, frames, dev, reps=20, log=lambda m: None):
+    """The ternary GEMM launches as the step issues them (stacked P = 3 passes, dropout 0.1):
+    fused swish / residual / swish-backward epilogues, the k/v dX accumulations and the plain
+    q / out launches, each timed like roofline() and priced at its algorithmic bytes (every
+    operand read once, every output written once, fp32)."""
+    from onebit_asr import _lib
+    from onebit_asr.conformer import subsampled_length
+    from onebit_asr.quant import pack_codes
+
+    lib = _lib.load()
+    P = PASSES
+    m = batch * subsampled_length(frames)
+    rows = P * m
+    d, f = 144, 576
+    bits_t = torch.tensor(PASS_BITS, dtype=torch.int32, device=dev)
+    rng = torch.tensor([1234, 1], dtype=torch.int64, device=dev)
+    side = torch.cuda.Stream(dev)
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def codes(N, K):
+        W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
+        a = W.abs().mean()
+        c2, c2t = pack_codes(W, a, 2)
+        c1, c1t = pack_codes(W, a, 1)
+        return c2, c1, c2t, c1t, a
+
+    T = lambda *shape: torch.randn(*shape, device=dev, generator=g)  # noqa: E731
+    x144, x576, y144, y576 = T(rows, d), T(rows, f), T(rows, d), T(rows, f)
+    pre, o576, o144, gh = T(rows, f), T(rows, f), T(rows, d), T(rows, d)
+    b144, b576 = torch.zeros(d, device=dev), torch.zeros(f, device=dev)
+    c1 = codes(f, d)  # lin1 [576, 144]
+    c2 = codes(d, f)  # lin2 [144, 576]
+    cq = codes(d, d)
+    bp = bits_t.data_ptr()
+    variants = [  # (name, launches per step, algorithmic bytes, fn(stream))
+        ("lin1 fwd + swish + dropout (stores pre and act)", 32, 4 * rows * (d + 2 * f),
+         lambda s: lib.ob_bitlinear_fwd_swish_drop(
+             x144.data_ptr(), P, m, d, c1[0].data_ptr(), c1[1].data_ptr(), bp, c1[4].data_ptr(), 1,
+             b576.data_ptr(), f, 0.1, rng.data_ptr(), 0, pre.data_ptr(), o576.data_ptr(), s)),
+        ("lin2 fwd + dropout + 0.5 residual", 32, 4 * rows * (f + 2 * d),
+         lambda s: lib.ob_bitlinear_fwd_residual(
+             x576.data_ptr(), P, m, f, c2[0].data_ptr(), c2[1].data_ptr(), bp, c2[4].data_ptr(), 1,
+             b144.data_ptr(), d, y144.data_ptr(), 0.5, 0.1, rng.data_ptr(), 0, None, 0,
+             o144.data_ptr(), s)),
+        ("lin2 dX + dropout / swish backward", 32, 4 * rows * (d + 2 * f),
+         lambda s: lib.ob_bitlinear_bwd_dx_swish_drop(
+             y144.data_ptr(), P, m, d, c2[2].data_ptr(), c2[3].data_ptr(), bp, c2[4].data_ptr(), 1,
+             f, pre.data_ptr(), 0.1, rng.data_ptr(), 0, o576.data_ptr(), s)),
+        ("lin1 dX", 32, 4 * rows * (f + d),
+         lambda s: lib.ob_bitlinear_bwd_dx_passes(
+             y576.data_ptr(), P, m, f, c1[2].data_ptr(), c1[3].data_ptr(), bp, c1[4].data_ptr(), 1,
+             d, o144.data_ptr(), s)),
+        ("q / k / v fwd", 48, 4 * rows * 2 * d,
+         lambda s: lib.ob_bitlinear_fwd_passes(
+             x144.data_ptr(), P, m, d, cq[0].data_ptr(), cq[1].data_ptr(), bp, cq[4].data_ptr(), 1,
+             b144.data_ptr(), d, o144.data_ptr(), s)),
+        ("k / v dX accumulated into q's (residual epilogue)", 32, 4 * rows * 3 * d,
+         lambda s: lib.ob_bitlinear_fwd_residual(
+             y144.data_ptr(), P, m, d, cq[2].data_ptr(), cq[3].data_ptr(), bp, cq[4].data_ptr(), 1,
+             None, d, gh.data_ptr(), 1.0, 0.0, None, 0, None, 0, gh.data_ptr(), s)),
+        ("q / out_proj dX", 32, 4 * rows * 2 * d,
+         lambda s: lib.ob_bitlinear_bwd_dx_passes(
+             y144.data_ptr(), P, m, d, cq[2].data_ptr(), cq[3].data_ptr(), bp, cq[4].data_ptr(), 1,
+             d, o144.data_ptr(), s)),
+        ("out_proj fwd + dropout + residual", 16, 4 * rows * 3 * d,
+         lambda s: lib.ob_bitlinear_fwd_residual(
+             x144.data_ptr(), P, m, d, cq[0].data_ptr(), cq[1].data_ptr(), bp, cq[4].data_ptr(), 1,
+             b144.data_ptr(), d, y144.data_ptr(), 1.0, 0.1, rng.data_ptr(), 0, None, 0,
+             o144.data_ptr(), s)),
+    ]
+    out = []
+    tot_t = tot_b = 0.0
+    for name, count, by, fn in variants:
+        log(f"roofline in-step: {name}")
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                _lib.check(fn(side.cuda_stream), name)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=side):
+                for _ in range(reps):
+                    fn(torch.cuda.current_stream(dev).cuda_stream)
+            graph.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(side)
+            graph.replay()
+            e1.record(side)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        tot_t += count * us
+        tot_b += count * by
+        out.append({"launch": name, "per_step": count, "us": round(us, 2), "alg_bytes": int(by),
+                    "GBs": round(by / (us * 1e-6) / 1e9, 1)})
+    gbs = tot_b / (tot_t * 1e-6) / 1e9
+    return {"ms_per_step": round(tot_t / 1e3, 3), "achieved_GBs": round(gbs, 1),
+            "frac_of_hbm": round(gbs / PEAK_HBM_GBS, 4), "launches": out}
+
+
 def traffic_from(path, kernel):
     """PMC HBM bytes per launch from profiles/pmc_traffic.json, only when it was measured
     on the kernel sources of this tree (its csrc_sha256 == the current source digest);
@@ -600,6 +698,8 @@ def main():
 
     if args.roofline_only:
         roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
+        roof["in_step_fused"] = roofline_fused(args.batch, args.frames, dev,
+                                               log=lambda m: log(args, m))
         print(json.dumps({"roofline": roof}), flush=True)
         return
     log(args, "model built; first step (graph mode: warm-up steps + capture)")
@@ -670,6 +770,9 @@ def main():
     elif rank == 0 and world == 1 and not args.no_roofline:
         roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
         roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
+        # the same family as the step launches it (fused epilogues, dX accumulations)
+        roof["in_step_fused"] = roofline_fused(args.batch, args.frames, dev,
+                                               log=lambda m: log(args, m))
         out["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not quant_off:
         # (progress always on stderr: the CPU leg runs minutes without other output)

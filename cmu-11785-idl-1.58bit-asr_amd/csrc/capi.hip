@@ -262,6 +262,27 @@ int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t K,
   return launched();
 }
 
+int ob_bitlinear_fwd_passes_group(int64_t G, const float* X, int64_t P, int64_t M, int64_t K,
+                                  const uint32_t* const* codes2, const uint32_t* const* codes1,
+                                  const int32_t* pass_bits, const float* const* alpha,
+                                  int alpha_raw, const float* const* bias, int64_t N,
+                                  float* const* Y, void* stream) {
+  if (G < 1 || G > 3 || M < 0 || K < 0 || N < 0 || P < 1 || P > 65535) return OB_ERR_SHAPE;
+  if (!codes2 || !codes1 || !alpha || !bias || !Y || !pass_bits || (M * K > 0 && !X))
+    return OB_ERR_NULL;
+  for (int64_t i = 0; i < G; ++i) {
+    if (!alpha[i] || (M * N > 0 && !Y[i]) || (N * K > 0 && (!codes2[i] || !codes1[i])))
+      return OB_ERR_NULL;
+    if (!aligned4(Y[i]) || !aligned4(bias[i])) return OB_ERR_ALIGN;
+  }
+  if (!aligned4(X) || !aligned4(pass_bits)) return OB_ERR_ALIGN;
+  if (!launch_ternary_gemm_passes_group(X, (int)P, M, K, (int)G, codes2, codes1,
+                                        reinterpret_cast<const int*>(pass_bits), N, alpha,
+                                        alpha_raw, bias, Y, as_stream(stream)))
+    return OB_ERR_SHAPE;
+  return launched();
+}
+
 namespace {
 
 // Shared argument checks of the fused-epilogue GEMM entries.

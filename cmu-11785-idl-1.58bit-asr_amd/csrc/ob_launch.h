@@ -59,6 +59,13 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
                                 const int* pass_bits, int64_t N, const float* alpha,
                                 int alpha_raw, const float* bias, float* C, hipStream_t s,
                                 const TgemmEpi* ep = nullptr);
+// G <= 3 layers sharing A (same K, N) in one launch (each layer's codes / alpha / bias / C);
+// false: shape refused
+bool launch_ternary_gemm_passes_group(const float* A, int P, int64_t M, int64_t K, int G,
+                                      const uint32_t* const* codes,
+                                      const uint32_t* const* codes1, const int* pass_bits,
+                                      int64_t N, const float* const* alpha, int alpha_raw,
+                                      const float* const* bias, float* const* C, hipStream_t s);
 
 // Fused epilogues of the ternary GEMM, y = a * acc + bias; element (row, col) of the
 // P*M x N output has dropout index row * N + col (ob_drop.h):

@@ -75,6 +75,14 @@ __device__ __forceinline__ f32x4 mfma_bf16(const bf16x8& a, const bf16x8& b, f32
 
 // Kernel-side form of TgemmEpi (ob_launch.h): the dropout config resolved on the host.
 struct EpiArgs {
+  // layers sharing A (q / k / v of one LN output) in one launch: the column tiles of layer i
+  // follow those of layer i-1; glayers == 1: one layer (the kernel's own pointers)
+  int glayers;
+  const uint32_t* gcodes[3];
+  const uint32_t* gcodes1[3];
+  const float* galpha[3];
+  const float* gbias[3];
+  float* gC[3];
   int mode;
   const float* R;
   float* C2;
@@ -209,6 +217,16 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
     const int* __restrict__ pass_bits, EpiArgs ep) {
+  const int L = xcd_logical(blockIdx.x, gridDim.x);
+  const int n_ct_l = n_ct / ep.glayers;  // column tiles of one layer
+  if (ep.glayers > 1) {
+    const int layer = (L % n_ct) / n_ct_l;
+    codes = ep.gcodes[layer];
+    codes1 = ep.gcodes1[layer];
+    alpha = ep.galpha[layer];
+    bias = ep.gbias[layer];
+    C = ep.gC[layer];
+  }
   select_pass(A, C, codes, codes1, pass_bits, M, K, N);
   const int64_t rowbase = pass_bits ? (int64_t)blockIdx.y * M : 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -220,8 +238,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   constexpr int kEpiCW = NT < 4 ? NT : 4, kEpiCC = 16 * kEpiCW, kEpiLd = kEpiCC + 4;
   // VEC_EPI (host-checked: N % 4 == 0, C / C2 / R 16-B aligned): the row-coalesced epilogue
 
-  const int L = xcd_logical(blockIdx.x, gridDim.x);
-  const int ct = L % n_ct;
+  const int ct = (L % n_ct) % n_ct_l;
   const int rg = L / n_ct;
   const int n0 = ct * (16 * NT);
 
@@ -656,7 +673,7 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
                    const float* alpha, int alpha_raw, const float* bias, float* C,
                    const uint32_t* codes1, const int* pass_bits, int P, const EpiArgs& ep,
                    hipStream_t s) {
-  const int n_ct = (int)ceil_div(N, 16 * NT);
+  const int n_ct = ep.glayers * (int)ceil_div(N, 16 * NT);  // all layers' column tiles
   const int n_rt = (int)ceil_div(M, kRows);
   static const int target = [] {  // OB_TGEMM_BLOCKS: tuning experiments
     const char* e = getenv("OB_TGEMM_BLOCKS");
@@ -707,6 +724,7 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
                                 const TgemmEpi* epi) {
   if (M == 0 || N == 0 || P == 0) return;
   EpiArgs ep{};
+  ep.glayers = 1;
   ep.mode = kEpiNone;
   if (epi && epi->mode != kEpiNone) {
     ep.mode = epi->mode;
@@ -740,6 +758,51 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
   const dim3 grid((unsigned)ceil_div(M, kRows), (unsigned)ceil_div(N, 16 * kF32NT), (unsigned)P);
   hipLaunchKernelGGL(tgemm_f32_kernel, grid, dim3(kThreads), 0, s, A, M, K, codes,
                      ceil_div(K, 16), N, alpha, alpha_raw, bias, C, codes1, pass_bits, ep);
+}
+
+bool launch_ternary_gemm_passes_group(const float* A, int P, int64_t M, int64_t K, int G,
+                                      const uint32_t* const* codes,
+                                      const uint32_t* const* codes1, const int* pass_bits,
+                                      int64_t N, const float* const* alpha, int alpha_raw,
+                                      const float* const* bias, float* const* C, hipStream_t s) {
+  if (G < 1 || G > 3) return false;
+  const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+  const int nt = vec && !use_f32_gemm() ? pick_nt(N, K, kEpiNone) : 0;
+  if (M == 0 || N == 0 || P == 0) return true;
+  bool al = (N % 4 == 0);
+  for (int i = 0; i < G; ++i) al = al && aligned16(C[i]);
+  if (nt == 0 || N % (16 * nt) != 0 || !al) {  // one launch per layer
+    for (int i = 0; i < G; ++i)
+      launch_ternary_gemm_passes(A, P, M, K, codes[i], codes1[i], pass_bits, N, alpha[i],
+                                 alpha_raw, bias[i], C[i], s);
+    return true;
+  }
+  EpiArgs ep{};
+  ep.glayers = G;
+  ep.mode = kEpiNone;
+  for (int i = 0; i < G; ++i) {
+    ep.gcodes[i] = codes[i];
+    ep.gcodes1[i] = codes1[i];
+    ep.galpha[i] = alpha[i];
+    ep.gbias[i] = bias[i];
+    ep.gC[i] = C[i];
+  }
+#define OB_NTG(V)                                                                                \
+  case V:                                                                                        \
+    launch_bf16x3<V>(A, M, K, codes[0], N, alpha[0], alpha_raw, bias[0], C[0], codes1[0],       \
+                     pass_bits, P, ep, s);                                                       \
+    return true;
+  switch (nt) {
+    OB_NTG(12)
+    OB_NTG(9)
+    OB_NTG(6)
+    OB_NTG(4)
+    OB_NTG(3)
+    OB_NTG(2)
+    OB_NTG(1)
+    default: return false;
+  }
+#undef OB_NTG
 }
 
 void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,

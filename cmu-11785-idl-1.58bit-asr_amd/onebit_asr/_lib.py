@@ -153,6 +153,8 @@ SIGNATURES = {
     "ob_bitlinear_fwd_i8_epi": (
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _c_f, _i64, _int, _c_f,
                _f32, _c_f, _i64, _c_f, _c_f, _c_f]),
+    "ob_bitlinear_fwd_passes_group": (
+        _int, [_i64, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
     "ob_bitlinear_fwd_i8q": (
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _c_f, _i64, _int, _c_f,
                _f32, _c_f, _i64, _c_f, _c_f, _c_f]),

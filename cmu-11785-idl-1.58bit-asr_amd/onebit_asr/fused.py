@@ -37,7 +37,8 @@ __all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
            "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8", "qkv_projections",
            "i8_linear"]
 
-_DW_GROUP = os.environ.get("OB_DW_GROUP", "1") != "0"  # 0: q/k/v dW finishes one by one
+_DW_GROUP = os.environ.get("OB_DW_GROUP", "1") != "0"  # 0: q/k/v dW one by one
+_QKV_FWD_GROUP = os.environ.get("OB_QKV_FWD_GROUP", "1") != "0"  # 0: q / k / v fwd one by one
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
 
@@ -308,7 +309,21 @@ class _QKVFn(torch.autograd.Function):
         lib = _lib.load()
         stream = _lib.stream_of(h)
         outs = []
-        for w, a, b, c in ((wq, aq, bq, codes[0]), (wk, ak, bk, codes[1]), (wv, av, bv, codes[2])):
+        if pb is not None and _QKV_FWD_GROUP and wq.shape == wk.shape == wv.shape and \
+                codes[0].fwd_raw == codes[1].fwd_raw == codes[2].fwd_raw:
+            # the three projections in one launch (their column tiles side by side)
+            n = wq.shape[0]
+            outs = [torch.empty((rows, n), dtype=torch.float32, device=h.device) for _ in range(3)]
+            arrs = [_lib.ptr_array(v) for v in (
+                [c[0].data_ptr() for c in codes], [c[1].data_ptr() for c in codes],
+                [aq.data_ptr(), ak.data_ptr(), av.data_ptr()],
+                [_lib.ptr(bq), _lib.ptr(bk), _lib.ptr(bv)], [y.data_ptr() for y in outs])]
+            ad = [ctypes.addressof(x) for x in arrs]
+            _lib.check(lib.ob_bitlinear_fwd_passes_group(
+                3, h.data_ptr(), P, m, k, ad[0], ad[1], pb.data_ptr(), ad[2], codes[0].fwd_raw,
+                ad[3], n, ad[4], stream), "ob_bitlinear_fwd_passes_group")
+        for w, a, b, c in (((wq, aq, bq, codes[0]), (wk, ak, bk, codes[1]), (wv, av, bv, codes[2]))
+                           if not outs else ()):
             n = w.shape[0]
             y = torch.empty((rows, n), dtype=torch.float32, device=h.device)
             st = (lib.ob_bitlinear_fwd_passes(h.data_ptr(), P, m, k, c[0].data_ptr(),

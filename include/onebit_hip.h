@@ -266,6 +266,16 @@ OB_API int ob_bitlinear_fwd_passes(const float* X, int64_t P, int64_t M, int64_t
                                    const uint32_t* codes2, const uint32_t* codes1,
                                    const int32_t* pass_bits, const float* alpha, int alpha_raw,
                                    const float* bias, int64_t N, float* Y, void* stream);
+/* G <= 3 layers of one input (the q / k / v projections of one LayerNorm output,
+ * conformer.py:111-113) as ONE launch: Y[i] = ob_bitlinear_fwd_passes(X, codes2[i],
+ * codes1[i], alpha[i], bias[i]) for each i (same K, N; the arrays are HOST arrays of device
+ * pointers, bias[i] may be NULL). Same arithmetic as G separate calls (bit-identical). */
+OB_API int ob_bitlinear_fwd_passes_group(int64_t G, const float* X, int64_t P, int64_t M,
+                                         int64_t K, const uint32_t* const* codes2,
+                                         const uint32_t* const* codes1, const int32_t* pass_bits,
+                                         const float* const* alpha, int alpha_raw,
+                                         const float* const* bias, int64_t N, float* const* Y,
+                                         void* stream);
 /*
  * Opt-in int8 activation mode (north_star "per-tensor absmax int8 activations"; NOT the
  * reference's arithmetic, which keeps activations fp32 at quant.py:126 -- SURVEY.md §0

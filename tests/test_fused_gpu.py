@@ -320,3 +320,26 @@ def test_decoder_residual_dropout(gpu):
     d2 = gy != 0
     assert torch.equal(torch.where(d2, gx * scale, torch.zeros_like(gx)), gy)
     assert torch.equal(_residual_dropout(x, y, p, False), x + y)
+
+
+def test_qkv_forward_group_equals_separate(gpu, monkeypatch):
+    """The q/k/v projections as one grouped launch (ob_bitlinear_fwd_passes_group) == three
+    separate launches, bit for bit (stacked passes, both bitwidths)."""
+    from onebit_asr import fused
+    from onebit_asr.quant import QuantizedLinear, StackedBits
+
+    torch.manual_seed(7)
+    layers = [QuantizedLinear(144, 144).to(gpu) for _ in range(3)]
+    for l in layers:
+        with torch.no_grad():
+            l.bias.uniform_(-0.1, 0.1)
+    bits = StackedBits(1, gpu)
+    bits.set([1])  # passes at 2, 1, 1 bits
+    h = torch.randn(3 * 500, 144, device=gpu)
+    outs = {}
+    for grp in (True, False):
+        monkeypatch.setattr(fused, "_QKV_FWD_GROUP", grp)
+        with torch.no_grad():
+            outs[grp] = fused.qkv_projections(h, *layers, bits[0])
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
