@@ -21,6 +21,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -270,6 +271,10 @@ def roofline_fused(batch, frames, dev, reps=20, log=lambda m: None):
     c2 = codes(d, f)  # lin2 [144, 576]
     cq = codes(d, d)
     bp = bits_t.data_ptr()
+    qkv_out = [T(rows, d) for _ in range(3)]
+    qkv = [_lib.ptr_array(v) for v in ([cq[0].data_ptr()] * 3, [cq[1].data_ptr()] * 3,
+                                        [cq[4].data_ptr()] * 3, [b144.data_ptr()] * 3,
+                                        [y.data_ptr() for y in qkv_out])]
     variants = [  # (name, launches per step, algorithmic bytes, fn(stream))
         ("lin1 fwd + swish + dropout (stores pre and act)", 32, 4 * rows * (d + 2 * f),
          lambda s: lib.ob_bitlinear_fwd_swish_drop(
@@ -288,10 +293,11 @@ def roofline_fused(batch, frames, dev, reps=20, log=lambda m: None):
          lambda s: lib.ob_bitlinear_bwd_dx_passes(
              y576.data_ptr(), P, m, f, c1[2].data_ptr(), c1[3].data_ptr(), bp, c1[4].data_ptr(), 1,
              d, o144.data_ptr(), s)),
-        ("q / k / v fwd", 48, 4 * rows * 2 * d,
-         lambda s: lib.ob_bitlinear_fwd_passes(
-             x144.data_ptr(), P, m, d, cq[0].data_ptr(), cq[1].data_ptr(), bp, cq[4].data_ptr(), 1,
-             b144.data_ptr(), d, o144.data_ptr(), s)),
+        ("q / k / v fwd (one grouped launch)", 16, 4 * rows * 4 * d,
+         lambda s: lib.ob_bitlinear_fwd_passes_group(
+             3, x144.data_ptr(), P, m, d, ctypes.addressof(qkv[0]), ctypes.addressof(qkv[1]), bp,
+             ctypes.addressof(qkv[2]), 1, ctypes.addressof(qkv[3]), d, ctypes.addressof(qkv[4]),
+             s)),
         ("k / v dX accumulated into q's (residual epilogue)", 32, 4 * rows * 3 * d,
          lambda s: lib.ob_bitlinear_fwd_residual(
              y144.data_ptr(), P, m, d, cq[2].data_ptr(), cq[3].data_ptr(), bp, cq[4].data_ptr(), 1,
