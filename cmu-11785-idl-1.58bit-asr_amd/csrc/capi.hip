@@ -617,6 +617,38 @@ int ob_convmod_bwd(const float* dv, const float* u, const float* z, const float*
   return launched();
 }
 
+int ob_convmod_bwd_defer(const float* dv, const float* u, const float* z, const float* g,
+                         const float* stats, const float* w_dw, const float* gamma,
+                         const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
+                         float* du, float* dw_dw, float* db_dw, float* dgamma, float* dbeta,
+                         void* ws, size_t ws_bytes, void* table, int64_t slot, int64_t* deferred,
+                         void* stream) {
+  if (int st = convmod_check(P, Bt, T, C, K)) return st;
+  if (!dw_dw || !dgamma || !dbeta || !w_dw || !gamma || !beta) return OB_ERR_NULL;
+  if (Bt * T > 0 && (!dv || !u || !z || !g || !stats || !du || !ws)) return OB_ERR_NULL;
+  if (ws_bytes < convmod_workspace(P, Bt, T, C, K)) return OB_ERR_WORKSPACE;
+  if (((uintptr_t)ws & 7u) || !aligned4(dv) || !aligned4(u) || !aligned4(z) || !aligned4(g) ||
+      !aligned4(du))
+    return OB_ERR_ALIGN;
+  if (slot < 0) return OB_ERR_SHAPE;
+  const bool dfr = table && Bt * T > 0 && convmod_bwd_deferrable(C, K);
+  const CmDefer df{dfr ? static_cast<CmWgradEntry*>(table) : nullptr, (int)slot};
+  launch_convmod_bwd(dv, u, z, g, stats, w_dw, gamma, beta, P, Bt, T, C, K, du, dw_dw, db_dw,
+                     dgamma, dbeta, ws, as_stream(stream), &df);
+  if (deferred) *deferred = dfr ? 1 : 0;
+  return launched();
+}
+
+size_t ob_cm_wgrad_entry_bytes(void) { return sizeof(CmWgradEntry); }
+
+int ob_cm_wgrad_table(const void* table, int64_t n, int64_t nmax, void* stream) {
+  if (n < 0 || nmax < 0 || nmax > (1 << 24)) return OB_ERR_SHAPE;
+  if (n > 0 && !table) return OB_ERR_NULL;
+  launch_cm_wgrad_table(static_cast<const CmWgradEntry*>(table), (int)n, (int)nmax,
+                        as_stream(stream));
+  return launched();
+}
+
 size_t ob_act_absmax_workspace(int64_t P) {
   return (P < 1 || P > 65535) ? 0 : act_absmax_workspace((int)P);
 }

@@ -505,8 +505,9 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
     const float* __restrict__ u, const float* __restrict__ stats, const float* __restrict__ coef,
     const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ wdw, int64_t rows_pp, int T, int C, float* __restrict__ du,
-    float* __restrict__ wpart) {
+    float* __restrict__ wpart, CmWgradEntry* __restrict__ tslot, CmWgradEntry ent) {
   constexpr int P = KT / 2, W = kTT + KT - 1, NW = W * CG;
+  if (tslot && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) *tslot = ent;
   __shared__ float dzs[NW];  // dz over frames [t0-P, t0+kTT+P), the group's channels
   __shared__ float gs[NW];   // g over the same window
   const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
@@ -729,13 +730,13 @@ int tile_cg(int64_t C, int64_t K) {
 // consecutive outputs of one partial: coalesced (one wave per output walked the partials
 // 18 KB apart: a cache line per 4-byte value, 16 us per launch).
 constexpr int kWfSlices = 16;
-__global__ __launch_bounds__(64 * kWfSlices) void cm_wgrad_final_kernel(
-    const float* __restrict__ wpart, int nblk, int C, int K, float* __restrict__ dw,
+__device__ __forceinline__ void cm_wgrad_final_block(
+    int bid, const float* __restrict__ wpart, int nblk, int C, int K, float* __restrict__ dw,
     float* __restrict__ db) {
   __shared__ double red[kWfSlices][64];
   const int n = C * (K + 1);
   const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;  // c * (K + 1) + j
+  const int i = bid * 64 + lane;  // c * (K + 1) + j
   const int ic = i < n ? i : n - 1;
   double acc = 0.0;
   for (int k0 = sl; k0 < nblk; k0 += 8 * kWfSlices) {
@@ -758,6 +759,20 @@ __global__ __launch_bounds__(64 * kWfSlices) void cm_wgrad_final_kernel(
   const int c = i / (K + 1), j = i - c * (K + 1);
   if (j < K) dw[(size_t)c * K + j] = (float)t;
   else if (db) db[c] = (float)t;
+}
+
+__global__ __launch_bounds__(64 * kWfSlices) void cm_wgrad_final_kernel(
+    const float* __restrict__ wpart, int nblk, int C, int K, float* __restrict__ dw,
+    float* __restrict__ db) {
+  cm_wgrad_final_block((int)blockIdx.x, wpart, nblk, C, K, dw, db);
+}
+
+// every deferred finish of a backward: grid (output groups of 64, entries)
+__global__ __launch_bounds__(64 * kWfSlices) void cm_wgrad_table_kernel(
+    const CmWgradEntry* __restrict__ tab) {
+  const CmWgradEntry e = tab[blockIdx.y];
+  if ((int)blockIdx.x * 64 >= e.C * (e.K + 1)) return;
+  cm_wgrad_final_block((int)blockIdx.x, e.wpart, e.nblk, e.C, e.K, e.dw, e.db);
 }
 
 // Row chunks per pass of the BatchNorm statistics / backward sums: ~16 rows per block at
@@ -873,7 +888,7 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
                         const float* stats, const float* wdw, const float* gamma,
                         const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
                         float* du, float* dwdw, float* dbdw, float* dgamma, float* dbeta, void* ws,
-                        hipStream_t s) {
+                        hipStream_t s, const CmDefer* defer) {
   const int64_t rows_pp = Bt / P * T;
   const int S = stats_chunks(rows_pp);
   const int TT = pick_tt(C, K);
@@ -899,16 +914,21 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
   const int cg = TT == kTT ? tile_cg(C, K) : 0;
   if (cg) {  // dz, dg and the GLU backward inside the channel-split tiles
     const dim3 gt((unsigned)ntt, (unsigned)Bt, (unsigned)(C / cg));
+    const bool dfr = defer && defer->table && Bt * ntt > 0;
+    CmWgradEntry* tslot = dfr ? defer->table + defer->slot : nullptr;
+    const CmWgradEntry ent{wpart, dwdw, dbdw, (int)(Bt * ntt), (int)C, (int)K};
 #define OB_CM_BWD_TILE(CG)                                                                      \
   hipLaunchKernelGGL((cm_bwd_tile_kernel<31, CG>), gt, dim3(kThreads), 0, s, dv, z, g, u, stats, \
-                     (const float*)coef, gamma, beta, wdw, rows_pp, (int)T, (int)C, du, wpart)
+                     (const float*)coef, gamma, beta, wdw, rows_pp, (int)T, (int)C, du, wpart,   \
+                     tslot, ent)
     if (cg == 48) OB_CM_BWD_TILE(48);
     else if (cg == 32) OB_CM_BWD_TILE(32);
     else OB_CM_BWD_TILE(16);
 #undef OB_CM_BWD_TILE
-    hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)ceil_div(C * (K + 1), 64)),
-                       dim3(64 * kWfSlices), 0, s,
-                       (const float*)wpart, (int)(Bt * ntt), (int)C, (int)K, dwdw, dbdw);
+    if (!dfr)
+      hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)ceil_div(C * (K + 1), 64)),
+                         dim3(64 * kWfSlices), 0, s,
+                         (const float*)wpart, (int)(Bt * ntt), (int)C, (int)K, dwdw, dbdw);
     return;
   }
   hipLaunchKernelGGL(cm_dz_kernel, dim3((unsigned)eblocks), dim3(kThreads), 0, s, dv, z, stats,
@@ -925,6 +945,17 @@ void launch_convmod_bwd(const float* dv, const float* u, const float* z, const f
   hipLaunchKernelGGL(cm_wgrad_final_kernel, dim3((unsigned)ceil_div(C * (K + 1), 64)),
                      dim3(64 * kWfSlices), 0, s,
                      (const float*)wpart, (int)(Bt * ntt), (int)C, (int)K, dwdw, dbdw);
+}
+
+bool convmod_bwd_deferrable(int64_t C, int64_t K) {
+  const int TT = pick_tt(C, K);
+  return TT == kTT && tile_cg(C, K) != 0;
+}
+
+void launch_cm_wgrad_table(const CmWgradEntry* table, int n, int nmax, hipStream_t s) {
+  if (n <= 0 || nmax <= 0) return;
+  hipLaunchKernelGGL(cm_wgrad_table_kernel, dim3((unsigned)ceil_div(nmax, 64), (unsigned)n),
+                     dim3(64 * kWfSlices), 0, s, table);
 }
 
 }  // namespace ob

@@ -16,6 +16,8 @@
 //             residual-dropout backward of the module feeding this LN needs no pass
 //             of its own.
 // Numerics: var = mean((x - mean)^2) (biased, as torch), rstd = 1/sqrt(var + eps).
+#include <cstdlib>
+
 #include "ob_drop.h"
 #include "ob_fp.h"
 #include "ob_launch.h"
@@ -61,24 +63,31 @@ __device__ __forceinline__ void store_cols(float* __restrict__ p, int c0, const 
 
 // One row (16 lanes): y = LN(x) and the row's (mean, rstd); returns this lane's max|y|.
 // y == nullptr: no fp32 store; yq != nullptr: also the int8 image of y at scale sx.
-template <int NPL, int VW = 1>
-__device__ __forceinline__ float ln_row(const float* __restrict__ x,
-                                        const float* __restrict__ gamma,
-                                        const float* __restrict__ beta, int64_t row, int d,
-                                        float eps, float* __restrict__ y,
-                                        float* __restrict__ mean_out,
-                                        float* __restrict__ rstd_out,
-                                        int8_t* __restrict__ yq = nullptr, float sx = 0.0f) {
+// this lane's columns of one row (the loads of ln_row, separable so that a thread can have
+// several rows in flight before it reduces the first)
+template <int NPL, int VW>
+__device__ __forceinline__ void ln_load(const float* __restrict__ x, int64_t row, int d,
+                                        float (&v)[NPL][VW]) {
   const int j = threadIdx.x & (kLanesPerRow - 1);
   const float* xr = x + row * d;
-  float v[NPL][VW];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) load_cols<VW>(xr, VW * (j + kLanesPerRow * i), d, v[i]);
+}
+
+template <int NPL, int VW = 1>
+__device__ __forceinline__ float ln_row_v(const float (&v)[NPL][VW],
+                                          const float* __restrict__ gamma,
+                                          const float* __restrict__ beta, int64_t row, int d,
+                                          float eps, float* __restrict__ y,
+                                          float* __restrict__ mean_out,
+                                          float* __restrict__ rstd_out,
+                                          int8_t* __restrict__ yq = nullptr, float sx = 0.0f) {
+  const int j = threadIdx.x & (kLanesPerRow - 1);
   float s = 0.0f;
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    load_cols<VW>(xr, VW * (j + kLanesPerRow * i), d, v[i]);
+  for (int i = 0; i < NPL; ++i)
 #pragma unroll
     for (int e = 0; e < VW; ++e) s += v[i][e];
-  }
   const float inv_d = 1.0f / (float)d;
   const float mean = row_sum16(s) * inv_d;
   float q = 0.0f;
@@ -126,14 +135,44 @@ __device__ __forceinline__ float ln_row(const float* __restrict__ x,
   return amx;
 }
 
-template <int NPL, int VW>  // columns per lane: d <= 16 * NPL * VW
+template <int NPL, int VW = 1>
+__device__ __forceinline__ float ln_row(const float* __restrict__ x,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ beta, int64_t row, int d,
+                                        float eps, float* __restrict__ y,
+                                        float* __restrict__ mean_out,
+                                        float* __restrict__ rstd_out,
+                                        int8_t* __restrict__ yq = nullptr, float sx = 0.0f) {
+  float v[NPL][VW];
+  ln_load<NPL, VW>(x, row, d, v);
+  return ln_row_v<NPL, VW>(v, gamma, beta, row, d, eps, y, mean_out, rstd_out, yq, sx);
+}
+
+// RPT rows per 16-lane group (rows sub, sub + 16, ... of the block's 16 * RPT): every row's
+// loads are issued before the first row is reduced (RPT x the bytes in flight per wave).
+// Measured at d = 144 (tools/ln_bench.py): RPT 2 / 4 are slower (7.1 / 9.5 us vs 6.3 us), so
+// the default stays 1; OB_LN_RPT keeps the others for other widths.
+template <int NPL, int VW, int RPT>  // columns per lane: d <= 16 * NPL * VW
 __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
     int64_t rows, int d, float eps, float* __restrict__ y, float* __restrict__ mean_out,
     float* __restrict__ rstd_out) {
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
-  if (row >= rows) return;
-  (void)ln_row<NPL, VW>(x, gamma, beta, row, d, eps, y, mean_out, rstd_out);
+  const int64_t row0 = (int64_t)blockIdx.x * (kRowsPerBlock * RPT) + (threadIdx.x / kLanesPerRow);
+  if constexpr (RPT == 1) {
+    if (row0 < rows) (void)ln_row<NPL, VW>(x, gamma, beta, row0, d, eps, y, mean_out, rstd_out);
+    return;
+  }
+  float v[RPT][NPL][VW];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int64_t row = row0 + kRowsPerBlock * q;
+    ln_load<NPL, VW>(x, row < rows ? row : rows - 1, d, v[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int64_t row = row0 + kRowsPerBlock * q;
+    if (row < rows) (void)ln_row_v<NPL, VW>(v[q], gamma, beta, row, d, eps, y, mean_out, rstd_out);
+  }
 }
 
 // The same rows plus the per-pass max|y| (the int8 activation scale of the BitLinear that
@@ -246,23 +285,39 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(rows, r0 + rows_per_block);
   const uint32_t dkey = (gs.dy2 && gs.dc.on) ? drop_key(gs.rng[0], gs.rng[1] + gs.rng_off) : 0u;
-  for (int64_t row = r0 + sub; row < r1; row += kRowsPerBlock) {
-    const float mu = mean_in[row], rs = rstd_in[row];
-    const float* xr = x + row * d;
-    const float* gr = dy + row * d;
-    float xh[NPL][VW], g[NPL][VW], res[NPL][VW];
-    float s1 = 0.0f, s2 = 0.0f;
-    const float* rr = dres ? dres + row * d : nullptr;
-    if (rr) {  // issued with x / dy, not after the row reductions (one latency, not two)
+  // The next row's operands (mean, rstd, x, dy, dres) are loaded before this row is
+  // reduced: two rows in flight per 16-lane group (the kernel is latency-bound otherwise).
+  struct RowIn {
+    float mu, rs;
+    float xv[NPL][VW], dv[NPL][VW], res[NPL][VW];
+  };
+  auto fetch = [&](int64_t row, RowIn& in) {
+    in.mu = mean_in[row];
+    in.rs = rstd_in[row];
+    if (dres) {
 #pragma unroll
-      for (int i = 0; i < NPL; ++i) load_cols<VW>(rr, VW * (j + kLanesPerRow * i), d, res[i]);
+      for (int i = 0; i < NPL; ++i) load_cols<VW>(dres + row * d, VW * (j + kLanesPerRow * i), d, in.res[i]);
     }
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
       const int c0 = VW * (j + kLanesPerRow * i);
-      float xv[VW], dv[VW];
-      load_cols<VW>(xr, c0, d, xv);
-      load_cols<VW>(gr, c0, d, dv);
+      load_cols<VW>(x + row * d, c0, d, in.xv[i]);
+      load_cols<VW>(dy + row * d, c0, d, in.dv[i]);
+    }
+  };
+  RowIn cur, nxt;
+  if (r0 + sub < r1) fetch(r0 + sub, cur);
+  for (int64_t row = r0 + sub; row < r1; row += kRowsPerBlock) {
+    if (row + kRowsPerBlock < r1) fetch(row + kRowsPerBlock, nxt);
+    const float mu = cur.mu, rs = cur.rs;
+    float xh[NPL][VW], g[NPL][VW];
+    const float (&res)[NPL][VW] = cur.res;
+    float s1 = 0.0f, s2 = 0.0f;
+    const bool rr = dres != nullptr;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const float (&xv)[VW] = cur.xv[i];
+      const float (&dv)[VW] = cur.dv[i];
 #pragma unroll
       for (int e = 0; e < VW; ++e) {
         xh[i][e] = (xv[e] - mu) * rs;
@@ -304,6 +359,7 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
         if (gs.dy2) store_cols<VW>(gs.dy2 + row * d, c0, w2);
       }
     }
+    cur = nxt;
   }
   if (!part_g) return;
 #pragma unroll
@@ -414,11 +470,27 @@ __global__ __launch_bounds__(kThreads) void ln_param_table_kernel(
   }
 }
 
-constexpr int kMaxBwdBlocks = 512;
+// OB_LN_BWD_BLOCKS / OB_LN_RPT: tuning experiments (same arithmetic per row and column)
+int max_bwd_blocks() {
+  static const int v = [] {
+    const char* e = getenv("OB_LN_BWD_BLOCKS");
+    const int n = e ? atoi(e) : 512;
+    return n > 0 ? n : 512;
+  }();
+  return v;
+}
+int fwd_rows_per_group() {
+  static const int v = [] {
+    const char* e = getenv("OB_LN_RPT");
+    const int n = e ? atoi(e) : 1;
+    return n == 2 || n == 4 ? n : 1;
+  }();
+  return v;
+}
 
 int bwd_blocks(int64_t rows, int* rows_per_block) {
   int64_t nb = ceil_div(rows, kRowsPerBlock);
-  if (nb > kMaxBwdBlocks) nb = kMaxBwdBlocks;
+  if (nb > max_bwd_blocks()) nb = max_bwd_blocks();
   if (nb < 1) nb = 1;
   int64_t rpb = ceil_div(rows, nb);
   rpb = ceil_div(rpb, kRowsPerBlock) * kRowsPerBlock;
@@ -454,12 +526,17 @@ void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta,
   const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
   const dim3 grid((unsigned)ceil_div(rows, kRowsPerBlock));
   const bool vec = d % 4 == 0 && al16(x) && al16(y) && al16(gamma) && al16(beta);
-#define OB_LNF(N)                                                                             \
-  hipLaunchKernelGGL((ln_fwd_kernel<N, 1>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
+  const int rpt = fwd_rows_per_group();
+  const dim3 grid_r((unsigned)ceil_div(rows, kRowsPerBlock * rpt));
+#define OB_LNF(N)                                                                                \
+  hipLaunchKernelGGL((ln_fwd_kernel<N, 1, 1>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
                      (int)d, eps, y, mean, rstd);
-#define OB_LNF4(N)                                                                            \
-  hipLaunchKernelGGL((ln_fwd_kernel<N, 4>), grid, dim3(kThreads), 0, s, x, gamma, beta, rows, \
-                     (int)d, eps, y, mean, rstd);
+#define OB_LNF4R(N, R)                                                                           \
+  hipLaunchKernelGGL((ln_fwd_kernel<N, 4, R>), grid_r, dim3(kThreads), 0, s, x, gamma, beta,     \
+                     rows, (int)d, eps, y, mean, rstd);
+#define OB_LNF4(N)                                                   \
+  if (rpt == 4) { OB_LNF4R(N, 4) } else if (rpt == 2) { OB_LNF4R(N, 2) } \
+  else { OB_LNF4R(N, 1) }
   if (vec) {
     OB_LN_NPL4(OB_LNF4)
   } else {
@@ -467,6 +544,7 @@ void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta,
   }
 #undef OB_LNF
 #undef OB_LNF4
+#undef OB_LNF4R
 }
 
 size_t layernorm_fwd_amax_workspace(int64_t P) {

@@ -117,11 +117,29 @@ void launch_convmod_fwd(const float* u, const float* wdw, const float* bdw, cons
                         const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
                         float eps, float* z, float* g, float* stats, float* v, void* ws,
                         hipStream_t s);
+// Deferred depthwise weight-gradient finish: the channel-tile backward (block 0) writes the
+// partials' descriptor into table[slot]; launch_cm_wgrad_table finishes every entry in one
+// launch (nmax = the largest C * (K + 1)).
+struct CmWgradEntry {
+  const float* wpart;
+  float* dw;
+  float* db;
+  int nblk;
+  int C;
+  int K;
+};
+struct CmDefer {
+  CmWgradEntry* table;  // nullptr: finish now
+  int slot;
+};
 void launch_convmod_bwd(const float* dv, const float* u, const float* z, const float* g,
                         const float* stats, const float* wdw, const float* gamma,
                         const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K,
                         float* du, float* dwdw, float* dbdw, float* dgamma, float* dbeta, void* ws,
-                        hipStream_t s);
+                        hipStream_t s, const CmDefer* defer = nullptr);
+// true when launch_convmod_bwd can defer its weight-gradient finish at this shape
+bool convmod_bwd_deferrable(int64_t C, int64_t K);
+void launch_cm_wgrad_table(const CmWgradEntry* table, int n, int nmax, hipStream_t s);
 
 // dY = rscale * rowvalid * drop(dOut) over [rows][N] (the backward of kEpiResidual's
 // dropout / pad / scale, same keep mask).

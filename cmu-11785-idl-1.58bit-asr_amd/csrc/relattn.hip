@@ -11,7 +11,7 @@
 // kernel that keeps a query tile's scores in registers and writes only ctx and the
 // softmax probabilities (kept for the backward). The backward is a query-side kernel (dq,
 // dS' to global) and a key-side kernel (dk, dv, per-row dpos over all queries: no
-// per-query-tile partials), plus two small fixed-order reductions (du/dvb over tiles,
+// per-query-tile partials), plus one launch holding two fixed-order reductions (du/dvb over tiles,
 // dpos over the pass's batch rows).
 //
 // rel_shift as a FLAT re-reading (conformer.py:97-103 pads a zero column on the left of X =
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 
 // ------------------------------------------------------------------------------------
 // Backward, query side: block = (query tile, head, batch row). Writes dq (final), the
-// tile's du / dvb partials (summed by relattn_bias_reduce_kernel) and dS' = dS / sqrt(d)
+// tile's du / dvb partials (summed by relattn_reduce_kernel) and dS' = dS / sqrt(d)
 // to global for the key-side kernel. The softmax backward's row term is
 //   delta_i = sum_j Pd_ij dPd_ij = dO_i . ctx_i
 // (ctx = Pd v), so each score's dS' is formed as soon as its dP tile is: no parking of dP.
@@ -819,12 +819,12 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
 // 24 partials per thread measured 15 us at Conformer-S).
 constexpr int kBiasCols = 4, kBiasSlices = kThreads / kBiasCols;
 
-__global__ __launch_bounds__(kThreads) void relattn_bias_reduce_kernel(
-    const float* __restrict__ du_part, const float* __restrict__ dvb_part, int Bt, int H, int D,
-    int nqt, float* __restrict__ du, float* __restrict__ dvb) {
+__device__ __forceinline__ void relattn_bias_reduce_block(
+    int bid, const float* __restrict__ du_part, const float* __restrict__ dvb_part, int Bt, int H,
+    int D, int nqt, float* __restrict__ du, float* __restrict__ dvb) {
   __shared__ float red[kBiasSlices][kBiasCols];
   const int ncg = (D + kBiasCols - 1) / kBiasCols;
-  const int cg = blockIdx.x % ncg, wh = blockIdx.x / ncg;
+  const int cg = bid % ncg, wh = bid / ncg;
   const int which = wh / H, h = wh - which * H;
   const int cl = threadIdx.x % kBiasCols, sl = threadIdx.x / kBiasCols;
   const int c = cg * kBiasCols + cl;
@@ -851,14 +851,14 @@ __global__ __launch_bounds__(kThreads) void relattn_bias_reduce_kernel(
 // dpos [P][T][H*D]: sum over the pass's Bp batch rows. Block = 64 consecutive output
 // elements x 4 batch slices (slice s: rows s, s+4, ... of the pass); the slices are added
 // in slice order through LDS (fixed order: deterministic).
-__global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
-    const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D,
+__device__ __forceinline__ void relattn_dpos_reduce_block(
+    int bid, const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D,
     float* __restrict__ dpos) {
   __shared__ float red[4][64];
   const int C = H * D;
   const int64_t n_p = (int64_t)P * T * C;
   const int el = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int64_t f = (int64_t)blockIdx.x * 64 + el;
+  const int64_t f = (int64_t)bid * 64 + el;
   const int Bp = Bt / P;
   float s = 0.0f;
   if (f < n_p) {
@@ -874,6 +874,20 @@ __global__ __launch_bounds__(kThreads) void relattn_dpos_reduce_kernel(
   red[sl][el] = s;
   __syncthreads();
   if (sl == 0 && f < n_p) dpos[f] = ((red[0][el] + red[1][el]) + red[2][el]) + red[3][el];
+}
+
+// Both reductions of the backward in one launch (they read different partials and write
+// different outputs): blocks [0, n_dpos) reduce dpos, the rest du / dvb -- one launch per
+// attention layer fewer at the per-launch floor, the same arithmetic per output.
+__global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
+    const float* __restrict__ dp_part, const float* __restrict__ du_part,
+    const float* __restrict__ dvb_part, int Bt, int P, int T, int H, int D, int nqt, int n_dpos,
+    float* __restrict__ dpos, float* __restrict__ du, float* __restrict__ dvb) {
+  const int bid = (int)blockIdx.x;
+  if (bid < n_dpos)
+    relattn_dpos_reduce_block(bid, dp_part, Bt, P, T, H, D, dpos);
+  else
+    relattn_bias_reduce_block(bid - n_dpos, du_part, dvb_part, Bt, H, D, nqt, du, dvb);
 }
 
 // keep mask of n elements in rows of T (element e = row * T + j): the attention kernels'
@@ -968,13 +982,11 @@ void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, con
   OB_RA_DISPATCH(OB_RA_KV);
 #undef OB_RA_KV
   const int64_t C = H * d;
-  hipLaunchKernelGGL(relattn_bias_reduce_kernel,
-                     dim3((unsigned)(2 * H * ((d + kBiasCols - 1) / kBiasCols))), dim3(kThreads),
-                     0, s, (const float*)du_part, (const float*)dvb_part, (int)Bt, (int)H, (int)d,
-                     nqt, du, dvb);
-  hipLaunchKernelGGL(relattn_dpos_reduce_kernel, dim3((unsigned)ceil_div(P * T * C, 64)),
-                     dim3(kThreads), 0, s, (const float*)dp_part, (int)Bt, (int)P, (int)T, (int)H,
-                     (int)d, dpos);
+  const int n_dpos = (int)ceil_div(P * T * C, 64);
+  const int n_bias = (int)(2 * H * ((d + kBiasCols - 1) / kBiasCols));
+  hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)(n_dpos + n_bias)), dim3(kThreads), 0, s,
+                     (const float*)dp_part, (const float*)du_part, (const float*)dvb_part, (int)Bt,
+                     (int)P, (int)T, (int)H, (int)d, nqt, n_dpos, dpos, du, dvb);
 }
 
 void launch_relattn_dropout_mask(int64_t n, int64_t T, float p_drop, const uint64_t* rng,

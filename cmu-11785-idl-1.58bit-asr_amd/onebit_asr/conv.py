@@ -14,6 +14,7 @@ the reference behaviour of this full-precision op (it is not the BitLinear hot p
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -96,6 +97,8 @@ class _ConvCoreFn(torch.autograd.Function):
                                       g.data_ptr(), stats.data_ptr(), v.data_ptr(), ws.data_ptr(), wsb,
                                       _lib.stream_of(u)), "ob_convmod_fwd")
         ctx.meta = (P, T, K, bdw is not None, wdw.shape)
+        ctx.params = (wdw, bdw)
+        deferred.note(wdw, bdw)
         ctx.save_for_backward(u, z, g, stats, w2, gamma, beta)
         return v
 
@@ -115,6 +118,21 @@ class _ConvCoreFn(torch.autograd.Function):
         dbt = torch.empty_like(beta)
         wsb = lib.ob_convmod_workspace(P, Bt, T, C, K)
         ws = torch.empty((wsb,), dtype=torch.uint8, device=u.device)
+        stream = _lib.stream_of(dv)
+        # the depthwise weight-gradient finish joins the end-of-backward table launch when the
+        # weight and bias qualify (deferred.py); the kernel reports whether the shape allowed it
+        slot = deferred.cm_slot(u.device, stream) if deferred.can_defer(*ctx.params) else None
+        if slot is not None:
+            took = ctypes.c_int64(0)
+            _lib.check(lib.ob_convmod_bwd_defer(
+                dv.data_ptr(), u.data_ptr(), z.data_ptr(), g.data_ptr(), stats.data_ptr(),
+                w2.data_ptr(), gamma.data_ptr(), beta.data_ptr(), P, Bt, T, C, K, du.data_ptr(),
+                dw.data_ptr(), _lib.ptr(db), dg.data_ptr(), dbt.data_ptr(), ws.data_ptr(), wsb,
+                slot[0], slot[1], ctypes.addressof(took), stream), "ob_convmod_bwd_defer")
+            if took.value:
+                deferred.cm_done(C * (K + 1))
+                deferred.keep(ws)
+            return du, dw.reshape(wshape), db, dg, dbt, None, None, None
         _lib.check(lib.ob_convmod_bwd(dv.data_ptr(), u.data_ptr(), z.data_ptr(), g.data_ptr(),
                                       stats.data_ptr(),
                                       w2.data_ptr(), gamma.data_ptr(), beta.data_ptr(), P, Bt, T, C,

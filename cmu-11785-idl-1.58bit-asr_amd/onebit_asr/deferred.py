@@ -1,5 +1,6 @@
 """Deferred gradient finishes: every BitLinear weight-gradient finish and every LayerNorm
-dgamma / dbeta reduction of a backward runs in ONE launch each, at the end of the backward.
+dgamma / dbeta reduction (and every depthwise-conv weight-gradient finish) of a backward runs
+in ONE launch per kind, at the end of the backward.
 
 In the reference step (train.py:104-111: loss.backward(), clip_grad_norm_, AdamW) a parameter
 gradient is read only after the backward ends. On the HIP library each BitLinear dW is a
@@ -33,7 +34,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "keep", "active"]
+__all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "cm_slot", "keep", "active"]
 
 _ON = os.environ.get("OB_DEFER", "1") != "0"
 _CAP = 512  # table entries per kind
@@ -43,7 +44,7 @@ class _State:
     def __init__(self):
         self.active = False
         self.uses: Dict[int, int] = {}
-        self.tables: Dict[int, tuple] = {}  # device index -> (dw table, ln table)
+        self.tables: Dict[int, tuple] = {}  # device index -> (dw, ln, cm tables)
         self.reset()
 
     def reset(self):
@@ -51,6 +52,8 @@ class _State:
         self.dw_blocks = 0
         self.ln_n = 0
         self.ln_dmax = 0
+        self.cm_n = 0
+        self.cm_nmax = 0
         self.refs: List[torch.Tensor] = []
         self.stream: Optional[int] = None
         self.dev: Optional[int] = None
@@ -109,7 +112,8 @@ def _tables(dev: torch.device):
         lib = _lib.load()
         dw = torch.zeros((_CAP * lib.ob_dw_finish_entry_bytes(),), dtype=torch.uint8, device=dev)
         ln = torch.zeros((_CAP * lib.ob_ln_param_entry_bytes(),), dtype=torch.uint8, device=dev)
-        t = (dw, ln)
+        cm = torch.zeros((_CAP * lib.ob_cm_wgrad_entry_bytes(),), dtype=torch.uint8, device=dev)
+        t = (dw, ln, cm)
         _S.tables[idx] = t
     return idx, t
 
@@ -129,7 +133,7 @@ def dw_slot(dev: torch.device, stream: int, n: int = 1):
     if _S.dw_n + n > _CAP:
         return None
     _begin(dev, stream)
-    _, (dw, _) = _tables(dev)
+    _, (dw, _, _) = _tables(dev)
     return dw.data_ptr(), _S.dw_n, _S.dw_blocks
 
 
@@ -143,11 +147,27 @@ def ln_slot(dev: torch.device, stream: int, d: int):
     if _S.ln_n + 1 > _CAP:
         return None
     _begin(dev, stream)
-    _, (_, ln) = _tables(dev)
+    _, (_, ln, _) = _tables(dev)
     slot = _S.ln_n
     _S.ln_n += 1
     _S.ln_dmax = max(_S.ln_dmax, d)
     return ln.data_ptr(), slot
+
+
+def cm_slot(dev: torch.device, stream: int):
+    """(table pointer, slot) for one depthwise weight-gradient finish (ob_convmod_bwd_defer),
+    or None when the table is full."""
+    if _S.cm_n + 1 > _CAP:
+        return None
+    _begin(dev, stream)
+    _, (_, _, cm) = _tables(dev)
+    return cm.data_ptr(), _S.cm_n
+
+
+def cm_done(n_out: int) -> None:
+    """The slot handed out by cm_slot was taken (n_out = C * (K + 1) outputs)."""
+    _S.cm_n += 1
+    _S.cm_nmax = max(_S.cm_nmax, n_out)
 
 
 def dense_dw(g2, x2d, m, n, k, gw, gb, ws, wsb, stream, weight, bias) -> None:
@@ -179,11 +199,14 @@ def _flush() -> None:
         _S.reset()
         return
     lib = _lib.load()
-    dw, ln = _S.tables[_S.dev]
+    dw, ln, cm = _S.tables[_S.dev]
     if _S.dw_n:
         _lib.check(lib.ob_dw_finish_table(dw.data_ptr(), _S.dw_n, _S.dw_blocks, _S.stream),
                    "ob_dw_finish_table")
     if _S.ln_n:
         _lib.check(lib.ob_ln_param_table(ln.data_ptr(), _S.ln_n, _S.ln_dmax, _S.stream),
                    "ob_ln_param_table")
+    if _S.cm_n:
+        _lib.check(lib.ob_cm_wgrad_table(cm.data_ptr(), _S.cm_n, _S.cm_nmax, _S.stream),
+                   "ob_cm_wgrad_table")
     _S.reset()

@@ -669,6 +669,20 @@ OB_API int ob_convmod_bwd(const float* dv, const float* u, const float* z, const
                           const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C,
                           int64_t K, float* du, float* dw_dw, float* db_dw, float* dgamma,
                           float* dbeta, void* ws, size_t ws_bytes, void* stream);
+/* ob_convmod_bwd with the depthwise weight-gradient finish (dw_dw, db_dw: the fixed-order
+ * sum of the per-tile partials) deferred when table != NULL and the shape runs on the
+ * channel-split tiles: the backward launch writes the partials' descriptor into slot `slot`
+ * of a caller-owned device table of ob_cm_wgrad_entry_bytes() entries, *deferred = 1, and
+ * ob_cm_wgrad_table finishes entries 0 .. n-1 in one launch (nmax = the largest C * (K + 1))
+ * with the same arithmetic. ws stays allocated until then. *deferred = 0: finished now. */
+OB_API int ob_convmod_bwd_defer(const float* dv, const float* u, const float* z, const float* g,
+                                const float* stats, const float* w_dw, const float* gamma,
+                                const float* beta, int64_t P, int64_t Bt, int64_t T, int64_t C,
+                                int64_t K, float* du, float* dw_dw, float* db_dw, float* dgamma,
+                                float* dbeta, void* ws, size_t ws_bytes, void* table, int64_t slot,
+                                int64_t* deferred, void* stream);
+OB_API size_t ob_cm_wgrad_entry_bytes(void);
+OB_API int ob_cm_wgrad_table(const void* table, int64_t n, int64_t nmax, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Conv2dSubsampling's two convolutions (conformer.py:170-208: Conv2d(1, C, 3, 2) -> ReLU ->
