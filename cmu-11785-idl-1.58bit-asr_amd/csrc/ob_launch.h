@@ -110,6 +110,17 @@ void launch_zero_words(void* p, int64_t n_words, hipStream_t s);
 size_t colsum_workspace(int64_t N);
 void launch_colsum(const float* x, int64_t rows, int64_t N, float* out, void* ws, hipStream_t s);
 
+// decattn.hip (the decoder's attention core; see the file header)
+bool decattn_supported(int64_t Lq, int64_t Lk, int64_t dh);
+void launch_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v,
+                        int64_t sv, const uint8_t* kmask, int causal, int64_t B, int64_t H,
+                        int64_t Lq, int64_t Lk, int64_t dh, float p_drop, const uint64_t* rng,
+                        uint64_t rng_off, float* probs, float* ctx, hipStream_t s);
+void launch_decattn_bwd(const float* dctx, const float* q, int64_t sq, const float* k, int64_t sk,
+                        const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                        int64_t dh, float p_drop, const float* probs, float* dq, int64_t gq,
+                        float* dk, int64_t gk, float* dv, int64_t gv, hipStream_t s);
+
 // convmod.hip (conv module core, channels-last; see the file header)
 bool convmod_supported(int64_t C, int64_t K);
 size_t convmod_workspace(int64_t P, int64_t Bt, int64_t T, int64_t C, int64_t K);

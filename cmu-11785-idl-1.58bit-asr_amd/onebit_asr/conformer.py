@@ -32,6 +32,7 @@ import torch.nn.functional as F
 from .attention import fused_attention_supported, rel_pos_attention
 from .conv import (conv2d_bias_relu, conv_module_fused, conv_module_supported, depthwise_conv1d,
                    subsample_convs, subsample_supported)
+from .decattn import dec_attention, dec_attention_supported
 from .embedding import embedding
 from .fused import (ffn_residual, ffn_residual_i8, fused_supported, i8_fused_supported,
                     i8_linear, linear_residual, linear_residual_i8, qkv_projections)
@@ -496,11 +497,21 @@ class TransformerDecoder(nn.Module):
     def _attention(mha: nn.MultiheadAttention, x, mem, bias, training: bool):
         """torch.nn.functional.multi_head_attention_forward (need_weights=False) for
         batch-first inputs: packed in-projection, softmax(q k^T / sqrt(dh) + bias) with
-        attention dropout, out-projection."""
+        attention dropout, out-projection. ``bias`` is the additive mask, or a
+        (key-padding mask, causal) pair for the HIP core (decattn.py)."""
         e, h = mha.embed_dim, mha.num_heads
         dh = e // h
         w, b = mha.in_proj_weight, mha.in_proj_bias
         bsz, lq, _ = x.shape
+        if isinstance(bias, tuple):  # HIP attention core on the packed projections
+            kmask, causal = bias
+            if mem is None:
+                ctx = dec_attention(linear(x, w, b), None, h, kmask, causal, mha.dropout,
+                                    training)
+            else:
+                ctx = dec_attention(linear(x, w[:e], b[:e]), linear(mem, w[e:], b[e:]), h,
+                                    kmask, causal, mha.dropout, training)
+            return linear(ctx, mha.out_proj.weight, mha.out_proj.bias)
         if mem is None:  # self-attention: one packed projection, chunks q | k | v
             q, k, v = linear(x, w, b).chunk(3, dim=-1)
             lk = lq
@@ -532,9 +543,21 @@ class TransformerDecoder(nn.Module):
 
     def forward(self, tgt_inp, memory, memory_mask, tgt_key_padding_mask):
         tt = tgt_inp.size(1)
+        tok = embedding(tgt_inp, self.emb.weight, self.emb.padding_idx)
+        dh = memory.size(-1) // self.dec.layers[0].self_attn.num_heads
+        if (dec_attention_supported(memory, tt, tt, dh)
+                and dec_attention_supported(memory, tt, memory.size(1), dh)):
+            # the HIP core takes the masks as they are: key padding (+ causal) per batch row
+            self_bias = (tgt_key_padding_mask, True)
+            cross_bias = (memory_mask == 0, False)
+            y = tok
+            for lyr in self.dec.layers:
+                y = self._layer(lyr, y, memory, self_bias, cross_bias)
+            if self.dec.norm is not None:
+                y = layer_norm(y, self.dec.norm.weight, self.dec.norm.bias, self.dec.norm.eps)
+            return linear(self.ln(y), self.out.weight, self.out.bias)
         future = torch.ones(tt, tt, device=tgt_inp.device).triu(diagonal=1).bool()
         causal = torch.zeros(tt, tt, device=tgt_inp.device).masked_fill(future, float("-inf"))
-        tok = embedding(tgt_inp, self.emb.weight, self.emb.padding_idx)
         if not (memory.is_cuda and memory.dtype == torch.float32):
             # tgt_is_causal=True is what torch's _detect_is_causal_mask concludes for this mask
             # in the reference call (the explicit mask is still used).

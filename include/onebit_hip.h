@@ -386,6 +386,30 @@ OB_API int ob_bitlinear_bwd_dw_passes_group_defer(
 OB_API int ob_dw_finish_table(const void* table, int64_t n, int64_t total_blocks, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * The decoder's attention core (onebit_asr/conformer.py:275-299: the stock
+ * nn.TransformerDecoderLayer self- and cross-attention, torch's
+ * multi_head_attention_forward between the in- and out-projections):
+ *   ctx = dropout(softmax((q k^T) * (1/sqrt(dh)) + mask)) v    per head
+ * q [B][Lq][*] with row stride sq floats (head h = columns h*dh .. h*dh+dh-1), k / v
+ * [B][Lk][*] (strides sk / sv): the packed projection outputs are read in place. mask: key j
+ * of batch row b is -inf when kmask[b*Lk + j] != 0 (kmask may be NULL) and, causal != 0,
+ * when j > i. ctx [B][Lq][H*dh]; probs [B][H][Lq][Lk] (the softmax output, a dropped
+ * element stored negated) is kept for the backward. Dropout p_drop: the library's counter
+ * hash on (rng, rng_offset), like every fused dropout. Supported: dh in {16, 32, 36, 64},
+ * Lk <= 256 and the per-(b, h) working set within LDS (ob_decattn_supported).
+ * bwd: dq [B][Lq][*] (row stride gq), dk / dv [B][Lk][*] (gk / gv), every element of the
+ * heads' columns written -- e.g. straight into the packed projection's gradient. */
+OB_API int ob_decattn_supported(int64_t Lq, int64_t Lk, int64_t dh);
+OB_API int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v,
+                          int64_t sv, const uint8_t* kmask, int64_t causal, int64_t B, int64_t H,
+                          int64_t Lq, int64_t Lk, int64_t dh, float p_drop, const int64_t* rng,
+                          int64_t rng_offset, float* probs, float* ctx, void* stream);
+OB_API int ob_decattn_bwd(const float* dctx, const float* q, int64_t sq, const float* k,
+                          int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq,
+                          int64_t Lk, int64_t dh, float p_drop, const float* probs, float* dq,
+                          int64_t gq, float* dk, int64_t gk, float* dv, int64_t gv, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Relative-position attention core of MHSA.forward (onebit_asr/conformer.py:115-127),
  * fused: ac = (q+u) k^T, bd = rel_shift((q+v) pos^T) (:97-103), S = (ac + bd) / sqrt(d),
  * frames i or j >= lens[b] masked to -inf (:121-122), A = nan_to_num(softmax(S))
