@@ -1285,7 +1285,7 @@ static int decattn_check(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t d
   if (B < 0 || H < 1 || !decattn_supported(Lq, Lk, dh) || !(p_drop >= 0.0f && p_drop < 1.0f))
     return OB_ERR_SHAPE;
   if (sq < H * dh || sk < H * dh || sv < H * dh) return OB_ERR_SHAPE;
-  if (B * H > INT32_MAX) return OB_ERR_SHAPE;
+  if (B * H * Lq > INT32_MAX) return OB_ERR_SHAPE;
   return OB_OK;
 }
 
@@ -1295,7 +1295,8 @@ int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const
                    int64_t rng_offset, float* probs, float* ctx, void* stream) {
   if (int st = decattn_check(B, H, Lq, Lk, dh, sq, sk, sv, p_drop)) return st;
   if (B > 0 && (!q || !k || !v || !probs || !ctx || (p_drop > 0.0f && !rng))) return OB_ERR_NULL;
-  if (!aligned4(q) || !aligned4(k) || !aligned4(v) || !aligned4(probs) || !aligned4(ctx))
+  if (!aligned4(q) || !aligned4(k) || !aligned4(v) || !aligned4(probs) ||
+      (reinterpret_cast<uintptr_t>(ctx) & 15))
     return OB_ERR_ALIGN;
   launch_decattn_fwd(q, sq, k, sk, v, sv, kmask, causal ? 1 : 0, B, H, Lq, Lk, dh, p_drop,
                      reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset, probs, ctx,
@@ -1303,17 +1304,17 @@ int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const
   return launched();
 }
 
-int ob_decattn_bwd(const float* dctx, const float* q, int64_t sq, const float* k, int64_t sk,
-                   const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+int ob_decattn_bwd(const float* dctx, const float* ctx, const float* q, int64_t sq, const float* k,
+                   int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
                    int64_t dh, float p_drop, const float* probs, float* dq, int64_t gq, float* dk,
                    int64_t gk, float* dv, int64_t gv, void* stream) {
   if (int st = decattn_check(B, H, Lq, Lk, dh, sq, sk, sv, p_drop)) return st;
   if (gq < H * dh || gk < H * dh || gv < H * dh) return OB_ERR_SHAPE;
-  if (B > 0 && (!dctx || !q || !k || !v || !probs || !dq || !dk || !dv)) return OB_ERR_NULL;
-  if (!aligned4(dctx) || !aligned4(q) || !aligned4(k) || !aligned4(v) || !aligned4(probs) ||
+  if (B > 0 && (!dctx || !ctx || !q || !k || !v || !probs || !dq || !dk || !dv)) return OB_ERR_NULL;
+  if (!aligned4(ctx) || !aligned4(dctx) || !aligned4(q) || !aligned4(k) || !aligned4(v) || !aligned4(probs) ||
       !aligned4(dq) || !aligned4(dk) || !aligned4(dv))
     return OB_ERR_ALIGN;
-  launch_decattn_bwd(dctx, q, sq, k, sk, v, sv, B, H, Lq, Lk, dh, p_drop, probs, dq, gq, dk, gk,
+  launch_decattn_bwd(dctx, ctx, q, sq, k, sk, v, sv, B, H, Lq, Lk, dh, p_drop, probs, dq, gq, dk, gk,
                      dv, gv, as_stream(stream));
   return launched();
 }

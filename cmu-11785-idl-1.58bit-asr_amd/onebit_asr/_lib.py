@@ -63,7 +63,7 @@ SIGNATURES = {
     "ob_decattn_supported": (_int, [_i64, _i64, _i64]),
     "ob_decattn_fwd": (_int, [_c_f, _i64, _c_f, _i64, _c_f, _i64, _c_f, _i64, _i64, _i64, _i64,
                               _i64, _i64, _f32, _c_f, _i64, _c_f, _c_f, _c_f]),
-    "ob_decattn_bwd": (_int, [_c_f, _c_f, _i64, _c_f, _i64, _c_f, _i64, _i64, _i64, _i64, _i64,
+    "ob_decattn_bwd": (_int, [_c_f, _c_f, _c_f, _i64, _c_f, _i64, _c_f, _i64, _i64, _i64, _i64, _i64,
                               _i64, _f32, _c_f, _c_f, _i64, _c_f, _i64, _c_f, _i64, _c_f]),
     "ob_cm_wgrad_entry_bytes": (_sz, []),
     "ob_cm_wgrad_table": (_int, [_c_f, _i64, _i64, _c_f]),

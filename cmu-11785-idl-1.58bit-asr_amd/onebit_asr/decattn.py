@@ -51,13 +51,13 @@ class _DecAttnFn(torch.autograd.Function):
                                       _lib.ptr(rng), int(off), probs.data_ptr(), out.data_ptr(),
                                       _lib.stream_of(xq)), "ob_decattn_fwd")
         ctx.meta = (heads, float(p), xkv is None, e, Lk, sq, skv, koff, voff)
-        ctx.save_for_backward(xq, xkv if xkv is not None else xq, probs)
+        ctx.save_for_backward(xq, xkv if xkv is not None else xq, probs, out)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         heads, p, self_mode, e, Lk, sq, skv, koff, voff = ctx.meta
-        xq, xkv, probs = ctx.saved_tensors
+        xq, xkv, probs, out = ctx.saved_tensors
         dout = dout.contiguous()
         B, Lq, _ = xq.shape
         dh = e // heads
@@ -70,7 +70,7 @@ class _DecAttnFn(torch.autograd.Function):
             dxkv = torch.empty_like(xkv)
             dsrc = dxkv
         base, dbase = src.data_ptr(), dsrc.data_ptr()
-        _lib.check(lib.ob_decattn_bwd(dout.data_ptr(), xq.data_ptr(), sq, base + 4 * koff, skv,
+        _lib.check(lib.ob_decattn_bwd(dout.data_ptr(), out.data_ptr(), xq.data_ptr(), sq, base + 4 * koff, skv,
                                       base + 4 * voff, skv, B, heads, Lq, Lk, dh, p,
                                       probs.data_ptr(), dxq.data_ptr(), sq, dbase + 4 * koff, skv,
                                       dbase + 4 * voff, skv, _lib.stream_of(dout)),

@@ -397,15 +397,16 @@ OB_API int ob_dw_finish_table(const void* table, int64_t n, int64_t total_blocks
  * element stored negated) is kept for the backward. Dropout p_drop: the library's counter
  * hash on (rng, rng_offset), like every fused dropout. Supported: dh in {16, 32, 36, 64},
  * Lk <= 256 and the per-(b, h) working set within LDS (ob_decattn_supported).
- * bwd: dq [B][Lq][*] (row stride gq), dk / dv [B][Lk][*] (gk / gv), every element of the
- * heads' columns written -- e.g. straight into the packed projection's gradient. */
+ * ctx must be 16-byte aligned. bwd (ctx = the forward's output): dq [B][Lq][*] (row stride
+ * gq), dk / dv [B][Lk][*] (gk / gv), every element of the heads' columns written -- e.g.
+ * straight into the packed projection's gradient. */
 OB_API int ob_decattn_supported(int64_t Lq, int64_t Lk, int64_t dh);
 OB_API int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v,
                           int64_t sv, const uint8_t* kmask, int64_t causal, int64_t B, int64_t H,
                           int64_t Lq, int64_t Lk, int64_t dh, float p_drop, const int64_t* rng,
                           int64_t rng_offset, float* probs, float* ctx, void* stream);
-OB_API int ob_decattn_bwd(const float* dctx, const float* q, int64_t sq, const float* k,
-                          int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq,
+OB_API int ob_decattn_bwd(const float* dctx, const float* ctx, const float* q, int64_t sq,
+                          const float* k, int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq,
                           int64_t Lk, int64_t dh, float p_drop, const float* probs, float* dq,
                           int64_t gq, float* dk, int64_t gk, float* dv, int64_t gv, void* stream);
 
