@@ -449,6 +449,19 @@ int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_tr
   return launched();
 }
 
+int ob_dense_gemm_residual_drop(const float* X, int64_t M, int64_t K, const float* W,
+                                const float* bias, int64_t N, const float* R, float p_drop,
+                                const int64_t* rng, int64_t rng_offset, float* Y, void* stream) {
+  if (M < 0 || M > ((int64_t)1 << 40) || !dense_gemm_supported(K, N)) return OB_ERR_SHAPE;
+  if (!(p_drop >= 0.0f && p_drop < 1.0f)) return OB_ERR_SHAPE;
+  if (!W || (M > 0 && (!X || !Y || !R)) || (p_drop > 0.0f && !rng)) return OB_ERR_NULL;
+  if (!aligned16(X) || !aligned16(W) || !aligned16(Y) || !aligned4(bias) || !aligned4(R))
+    return OB_ERR_ALIGN;
+  const DenseEpi epi{R, p_drop, reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset};
+  if (!launch_dense_gemm(X, M, K, W, 0, bias, N, Y, as_stream(stream), &epi)) return OB_ERR_SHAPE;
+  return launched();
+}
+
 size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N <= 0 || K <= 0 || N % 4 != 0 || K % 4 != 0) return 0;
   const int v = plan_dw(M, N, K).variant;

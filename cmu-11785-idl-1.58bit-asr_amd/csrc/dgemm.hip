@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "ob_drop.h"
+#include "ob_fp.h"
 #include "ob_launch.h"
 
 namespace ob {
@@ -92,10 +94,11 @@ __host__ __device__ inline size_t dg_lds_bytes(int nt, int kpad) {
   return (size_t)16 * nt * 3 * (kpad + 8) * sizeof(uint16_t);
 }
 
-template <int NT, int NCH, int WAVES, bool TRANS>
+template <int NT, int NCH, int WAVES, bool TRANS, bool RES = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
     const float* __restrict__ A, int64_t M, int K, const float* __restrict__ W, int N, int n_ct,
-    int n_rt, int rgroups, const float* __restrict__ bias, float* __restrict__ C) {
+    int n_rt, int rgroups, const float* __restrict__ bias, float* __restrict__ C,
+    const float* __restrict__ R, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off) {
   constexpr int kThr = 64 * WAVES, kRowsT = 16 * WAVES, BN = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
   __syncthreads();
 
   const __bf16* brow = bimg + r * cpitch + kg;
+  const uint32_t dkey = (RES && dc.on) ? drop_key(rng[0], rng[1] + rng_off) : 0u;
   float bcol[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -257,15 +261,32 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
     }
 
     __builtin_amdgcn_sched_barrier(0);
-    // D[row = 4g + reg][col = r]: 16 lanes write 64 contiguous bytes of a row per store
+    // D[row = 4g + reg][col = r]: 16 lanes write 64 contiguous bytes of a row per store.
+    // Residual epilogue (RES, its own instantiation: the plain kernels keep their registers):
+    // per column tile, the four R values are loaded before the first store (the whole
+    // tile's R in registers spills at NT 9).
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = n0 + 16 * t + r;
       if (col >= N) continue;
+      float rv[4];
+      if constexpr (RES) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+          rv[reg] = R[min(m0 + 4 * g + reg, M - 1) * N + col];
+      }
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const int64_t orow = m0 + 4 * g + reg;
-        if (orow < M) C[orow * N + col] = acc[t][reg] + bcol[t];
+        if (orow >= M) continue;
+        const int64_t i = orow * N + col;
+        const float y = acc[t][reg] + bcol[t];
+        if constexpr (RES) {  // R + dropout(y), the operation sequence of residual_drop_fwd_kernel
+          const float v = dc.on ? nc_mul(y, drop_keep(dkey, (uint64_t)i, dc.thresh) ? dc.scale : 0.0f) : y;
+          C[i] = nc_add(rv[reg], v);
+        } else {
+          C[i] = y;
+        }
       }
     }
   }
@@ -316,7 +337,8 @@ bool dense_gemm_supported(int64_t K, int64_t N) {
 }
 
 bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int trans,
-                       const float* bias, int64_t N, float* C, hipStream_t s) {
+                       const float* bias, int64_t N, float* C, hipStream_t s,
+                       const DenseEpi* epi) {
   if (!dense_gemm_supported(K, N)) return false;
   if (M == 0) return true;
   const DgCfg cfg = pick_cfg(N, K);
@@ -331,17 +353,41 @@ bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct));
   const int nch = kpad == 160 ? 5 : kpad == 288 ? 9 : 0;
+  const float* R = epi ? epi->R : nullptr;
+  const DropCfg dc = make_drop(R ? epi->p_drop : 0.0f);
+  const uint64_t* rng = R ? epi->rng : nullptr;
+  const uint64_t rng_off = R ? epi->rng_off : 0;
 #define OB_DG(NT, NCH, WV)                                                                       \
   if (cfg.nt == NT && nch == NCH && cfg.waves == WV) {                                           \
     if (trans)                                                                                   \
       hipLaunchKernelGGL((dgemm_kernel<NT, NCH, WV, true>), grid, dim3(64 * WV), lds, s, A, M,    \
-                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C);                        \
+                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C, nullptr, dc,    \
+                         nullptr, 0);                                                            \
     else                                                                                         \
       hipLaunchKernelGGL((dgemm_kernel<NT, NCH, WV, false>), grid, dim3(64 * WV), lds, s, A, M,   \
-                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C);                        \
+                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C, nullptr, dc,    \
+                         nullptr, 0);                                                            \
     return true;                                                                                 \
   }
 #define OB_DG2(NT, NCH) OB_DG(NT, NCH, 4) OB_DG(NT, NCH, 8)
+  if (R && !trans && cfg.nt == 9 && nch == 5) {  // the conv module's pw2 (K, N = 144)
+#define OB_DGR(WV)                                                                               \
+    if (cfg.waves == WV) {                                                                       \
+      hipLaunchKernelGGL((dgemm_kernel<9, 5, WV, false, true>), grid, dim3(64 * WV), lds, s, A,   \
+                         M, (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C, R, dc, rng,         \
+                         rng_off);                                                               \
+      return true;                                                                               \
+    }
+    OB_DGR(4)
+    OB_DGR(8)
+#undef OB_DGR
+  }
+  if (R) {  // other shapes: the plain GEMM, then the residual-dropout pass in place
+    DenseEpi none{nullptr, 0.0f, nullptr, 0};
+    if (!launch_dense_gemm(A, M, K, W, trans, bias, N, C, s, &none)) return false;
+    launch_residual_drop_fwd(R, C, M, N, 1.0f, epi->p_drop, rng, rng_off, nullptr, 0, C, s);
+    return true;
+  }
   OB_DG2(9, 5)
   OB_DG2(6, 5)
   OB_DG2(3, 5)

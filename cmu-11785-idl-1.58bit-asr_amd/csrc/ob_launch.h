@@ -235,8 +235,17 @@ void launch_dw_partial_group_defer(const float* const* dY, int G, const float* X
 
 // dgemm.hip (dense exact-fp32 GEMM of the pointwise convs): false = shape not taken
 bool dense_gemm_supported(int64_t K, int64_t N);
+// Optional residual epilogue: C = R + dropout(A W^T + b) (R [M][N], the flat index
+// row * N + col keying the dropout hash: residual_drop_fwd's arithmetic, element for element)
+struct DenseEpi {
+  const float* R;  // nullptr: plain C = A W^T + b
+  float p_drop;
+  const uint64_t* rng;
+  uint64_t rng_off;
+};
 bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int trans,
-                       const float* bias, int64_t N, float* C, hipStream_t s);
+                       const float* bias, int64_t N, float* C, hipStream_t s,
+                       const DenseEpi* epi = nullptr);
 
 // tgemm_i8.hip (opt-in absmax-int8 activations x ternary codes on the i8 matrix cores)
 bool ternary_gemm_i8_supported(int64_t K, int64_t N);

@@ -202,6 +202,7 @@ _PW_BLAS = os.environ.get("OB_PW_BLAS", "cublas")  # "cublas" selects rocBLAS on
 
 
 _PW = os.environ.get("OB_PW", "hip")  # "blas": the rocBLAS fp32 GEMMs (A/B checks)
+_PW_RESID = os.environ.get("OB_PW_RESID", "1") != "0"  # 0: pw2, then the residual kernel
 
 
 def _aligned(t: torch.Tensor) -> bool:
@@ -251,36 +252,84 @@ class _PointwiseFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        x2d, w = ctx.saved_tensors
-        gx = gw = gb = None
-        g = g.contiguous()
-        if ctx.hip and _aligned(g):
-            lib = _lib.load()
-            m, k = x2d.shape
-            n = w.shape[0]
-            st = _lib.stream_of(g)
-            if ctx.needs_input_grad[0]:
-                gx = torch.empty_like(x2d)
-                _lib.check(lib.ob_dense_gemm(g.data_ptr(), m, n, w.data_ptr(), 1, None, k,
-                                             gx.data_ptr(), st), "ob_dense_gemm")
-            if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
-                gw = torch.empty(ctx.wshape, dtype=torch.float32, device=g.device)  # [out, in, 1]
-                gb = (torch.empty((n,), dtype=torch.float32, device=g.device)
-                      if ctx.has_b and ctx.needs_input_grad[2] else None)
-                wsb = lib.ob_dense_dw_workspace(m, n, k)
-                ws = torch.empty((wsb,), dtype=torch.uint8, device=g.device)
-                deferred.dense_dw(g, x2d, m, n, k, gw, gb, ws, wsb, st, ctx.wparam, ctx.bias)
-                if not ctx.needs_input_grad[1]:
-                    gw = None
-            return gx, gw, gb
-        with _BlasPref(_PW_BLAS):
-            if ctx.needs_input_grad[0]:
-                gx = g @ w
-            if ctx.needs_input_grad[1]:
-                gw = (g.t() @ x2d).view(ctx.wshape)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = colsum(g)
+        return _pointwise_backward(ctx, g, *ctx.needs_input_grad[:3])
+
+
+def _pointwise_backward(ctx, g, need_x, need_w, need_b):
+    """gx, gw, gb of y = x W^T + b from g = dL/dy (ctx: _PointwiseFn's saved state: x2d, w,
+    hip, wshape, has_b, bias, wparam)."""
+    x2d, w = ctx.saved_tensors[:2]
+    gx = gw = gb = None
+    g = g.contiguous()
+    need_b = need_b and ctx.has_b
+    if ctx.hip and _aligned(g):
+        lib = _lib.load()
+        m, k = x2d.shape
+        n = w.shape[0]
+        st = _lib.stream_of(g)
+        if need_x:
+            gx = torch.empty_like(x2d)
+            _lib.check(lib.ob_dense_gemm(g.data_ptr(), m, n, w.data_ptr(), 1, None, k,
+                                         gx.data_ptr(), st), "ob_dense_gemm")
+        if need_w or need_b:
+            gw = torch.empty(ctx.wshape, dtype=torch.float32, device=g.device)  # [out, in, 1]
+            gb = torch.empty((n,), dtype=torch.float32, device=g.device) if need_b else None
+            wsb = lib.ob_dense_dw_workspace(m, n, k)
+            ws = torch.empty((wsb,), dtype=torch.uint8, device=g.device)
+            deferred.dense_dw(g, x2d, m, n, k, gw, gb, ws, wsb, st, ctx.wparam, ctx.bias)
+            if not need_w:
+                gw = None
         return gx, gw, gb
+    with _BlasPref(_PW_BLAS):
+        if need_x:
+            gx = g @ w
+        if need_w:
+            gw = (g.t() @ x2d).view(ctx.wshape)
+    if need_b:
+        gb = colsum(g)
+    return gx, gw, gb
+
+
+class _PointwiseResidualFn(torch.autograd.Function):
+    """R + dropout(x W^T + b): the conv module's pw2 and its residual tail (conformer.py:147,
+    :160-167) in one dgemm launch (ob_dense_gemm_residual_drop; the same arithmetic as
+    ob_dense_gemm + ob_residual_drop_fwd). Backward: dR = g; dy = dropout backward of g
+    (formed by the next LN's backward, layernorm.GradScale); then pw2's backward."""
+
+    @staticmethod
+    def forward(ctx, res, x2d, wp, b, p, rng, off, spec):
+        w = wp.view(wp.shape[0], -1)
+        ctx.wshape = wp.shape
+        ctx.hip = True
+        m, k = x2d.shape
+        n = w.shape[0]
+        out = torch.empty((m, n), dtype=torch.float32, device=x2d.device)
+        _lib.check(_lib.load().ob_dense_gemm_residual_drop(
+            x2d.data_ptr(), m, k, w.data_ptr(), _lib.ptr(b), n, res.data_ptr(), p, _lib.ptr(rng),
+            off, out.data_ptr(), _lib.stream_of(x2d)), "ob_dense_gemm_residual_drop")
+        ctx.save_for_backward(x2d, w)
+        ctx.has_b = b is not None
+        ctx.bias = b
+        ctx.wparam = wp
+        ctx.meta = (p, rng, off, spec)
+        deferred.note(wp, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p, rng, off, spec = ctx.meta
+        g = g.contiguous()
+        n = g.shape[-1]
+        rows = g.numel() // n
+        gy = spec.take(g)
+        if gy is None:
+            gy = torch.empty_like(g)
+            _lib.check(_lib.load().ob_drop_scale_bwd(g.data_ptr(), rows, n, 1.0, p, _lib.ptr(rng),
+                                                     off, None, 0, gy.data_ptr(),
+                                                     _lib.stream_of(g)), "ob_drop_scale_bwd")
+        gx, gw, gb = _pointwise_backward(ctx, gy, ctx.needs_input_grad[1],
+                                         ctx.needs_input_grad[2], ctx.needs_input_grad[3])
+        return g, gx, gw, gb, None, None, None, None
 
 
 class _BiasReluFn(torch.autograd.Function):
@@ -429,8 +478,14 @@ def conv_module_fused(x: torch.Tensor, h: torch.Tensor, module, passes: int, p_d
     u = module.pw1(h, bitwidth) if quant else _pointwise(h, module.pw1)
     v = _ConvCoreFn.apply(u.reshape(bt * t, 2 * c), module.dw.weight, module.dw.bias,
                           module.bn.weight, module.bn.bias, passes, t, float(module.bn.eps))
-    o = module.pw2(v, bitwidth) if quant else _pointwise(v, module.pw2)
     rng, off = _rng(x.device) if p_drop > 0 else (None, 0)
     spec = GradScale(1.0, p_drop, rng, off)
+    if not quant and _PW_RESID and _dense_ok(v, module.pw2.weight.view(c, -1)) and _aligned(x):
+        # pw2 + dropout + residual in one dgemm launch
+        xr = x.contiguous()
+        out = _PointwiseResidualFn.apply(xr.view(bt * t, c), v, module.pw2.weight, module.pw2.bias,
+                                         float(p_drop), rng, off, spec)
+        return attach_grad_scale(out.view(bt, t, c), spec)
+    o = module.pw2(v, bitwidth) if quant else _pointwise(v, module.pw2)
     return attach_grad_scale(_ResidualDropFn.apply(x, o.view(bt, t, c), float(p_drop), rng, off,
                                                    spec), spec)

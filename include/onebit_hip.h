@@ -659,6 +659,14 @@ OB_API int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* 
 OB_API int ob_dense_supported(int64_t K, int64_t N);
 OB_API int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_trans,
                          const float* bias, int64_t N, float* Y, void* stream);
+/* ob_dense_gemm (w_trans 0) with the residual tail of the conv module (conformer.py:160-167,
+ * x + dropout(pw2(.))) in the epilogue: Y = R + dropout(X W^T + bias), R [M][N]; the dropout
+ * is ob_residual_drop_fwd's (hash on the flat index row * N + col with rng / rng_offset, rscale
+ * 1, no row mask), so Y equals ob_dense_gemm followed by ob_residual_drop_fwd bit for bit. */
+OB_API int ob_dense_gemm_residual_drop(const float* X, int64_t M, int64_t K, const float* W,
+                                       const float* bias, int64_t N, const float* R,
+                                       float p_drop, const int64_t* rng, int64_t rng_offset,
+                                       float* Y, void* stream);
 OB_API size_t ob_dense_dw_workspace(int64_t M, int64_t N, int64_t K);
 OB_API int ob_dense_dw(const float* dY, const float* X, int64_t M, int64_t N, int64_t K,
                        float* dW, float* db, void* ws, size_t ws_bytes, void* stream);

@@ -133,3 +133,26 @@ torch.save(out, sys.argv[1])
         if k == "y" or k == "dw.bias":  # dw.bias: a true-zero gradient (rounding residuals)
             continue
         assert _rel(res[0][k], res[1][k]) <= 1e-6, (k, _rel(res[0][k], res[1][k]))
+
+
+def test_pw2_residual_epilogue_bitwise(gpu, monkeypatch):
+    """pw2 + dropout + residual in one dgemm launch (ob_dense_gemm_residual_drop) == pw2, then
+    the residual-dropout kernel: output and every gradient bit for bit (training, p = 0.1)."""
+    from onebit_asr import conv, fused
+
+    m = _module(gpu, 144, p=0.1).train()
+    x = torch.randn(3, 61, 144, device=gpu)
+    monkeypatch.setenv("OB_FUSED", "1")
+    dev = torch.device(gpu)
+    fused._rng(dev)
+    snap = fused.rng_snapshot(dev)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(conv, "_PW_RESID", on)
+        fused.rng_restore(dev, snap)
+        res.append(_run(m, x, 3, True, monkeypatch))
+    (y1, gx1, g1), (y0, gx0, g0) = res
+    assert torch.equal(y1, y0)
+    assert torch.equal(gx1, gx0)
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
