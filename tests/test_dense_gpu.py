@@ -186,3 +186,57 @@ def test_linear_dense_path_matches_float64(gpu, m, k, n):
     assert lib.ob_dense_supported(k, n) == (0 if k == 2736 else 1)
     if n % 48 == 0 and k % 48 == 0:
         assert lib.ob_dense_dw_workspace(m, n, k) > 0  # the weight gradient on the dW kernels
+
+
+@pytest.mark.parametrize("m,k,n,p", [
+    (23904, 144, 144, 0.1),  # the conv module's pw2 + residual (the fused RES instantiation)
+    (777, 144, 144, 0.0),
+    (513, 96, 192, 0.1),     # another tile shape: plain GEMM, then the residual pass in place
+    (1, 144, 144, 0.1),
+])
+def test_dense_gemm_residual_drop_equals_two_launches(gpu, m, k, n, p):
+    """ob_dense_gemm_residual_drop == ob_dense_gemm then ob_residual_drop_fwd, bit for bit."""
+    L = _lib()
+    lib = L.load()
+    g = torch.Generator(device=gpu).manual_seed(m + n)
+    x = torch.randn(m, k, device=gpu, generator=g)
+    w = torch.randn(n, k, device=gpu, generator=g) * 0.1
+    b = torch.randn(n, device=gpu, generator=g)
+    r = torch.randn(m, n, device=gpu, generator=g)
+    rng = torch.tensor([99, 3], dtype=torch.int64, device=gpu)
+    st = L.stream_of(x)
+    out = torch.full((m, n), float("nan"), device=gpu)
+    L.check(lib.ob_dense_gemm_residual_drop(x.data_ptr(), m, k, w.data_ptr(), b.data_ptr(), n,
+                                            r.data_ptr(), p, rng.data_ptr(), 7, out.data_ptr(),
+                                            st), "ob_dense_gemm_residual_drop")
+    y = _gemm(x, w, False, b)
+    ref = torch.empty_like(y)
+    L.check(lib.ob_residual_drop_fwd(r.data_ptr(), y.data_ptr(), m, n, 1.0, p, rng.data_ptr(), 7,
+                                     None, 0, ref.data_ptr(), st), "ob_residual_drop_fwd")
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert lib.ob_dense_gemm_residual_drop(x.data_ptr(), m, k, w.data_ptr(), b.data_ptr(), n,
+                                           None, p, rng.data_ptr(), 7, out.data_ptr(), st) == -1
+
+
+def test_decattn_abi_errors(gpu):
+    L = _lib()
+    lib = L.load()
+    assert lib.ob_decattn_supported(41, 250, 36) == 1
+    assert lib.ob_decattn_supported(41, 257, 36) == 0   # Lk > 256
+    assert lib.ob_decattn_supported(41, 250, 48) == 0   # dh not instantiated
+    assert lib.ob_decattn_supported(600, 250, 64) == 0  # LDS working set too large
+    q = torch.randn(2, 5, 3 * 144, device=gpu)
+    probs = torch.empty(2, 4, 5, 5, device=gpu)
+    ctx = torch.empty(2, 5, 144, device=gpu)
+    st = L.stream_of(q)
+    base = q.data_ptr()
+    ok = lib.ob_decattn_fwd(base, 432, base + 576, 432, base + 1152, 432, None, 1, 2, 4, 5, 5, 36,
+                            0.0, None, 0, probs.data_ptr(), ctx.data_ptr(), st)
+    assert ok == 0
+    assert lib.ob_decattn_fwd(base, 100, base + 576, 432, base + 1152, 432, None, 1, 2, 4, 5, 5,
+                              36, 0.0, None, 0, probs.data_ptr(), ctx.data_ptr(), st) == -2
+    assert lib.ob_decattn_fwd(base, 432, base + 576, 432, base + 1152, 432, None, 1, 2, 4, 5, 5,
+                              36, 0.1, None, 0, probs.data_ptr(), ctx.data_ptr(), st) == -1
+    assert lib.ob_decattn_fwd(base, 432, base + 576, 432, base + 1152, 432, None, 1, 2, 4, 5, 5,
+                              36, 0.0, None, 0, probs.data_ptr(), ctx.data_ptr() + 4, st) == -5
