@@ -1131,6 +1131,21 @@ int ob_layernorm_fwd(const float* x, const float* gamma, const float* beta, int6
   return launched();
 }
 
+int ob_layernorm_fwd_pair(const float* x, const float* g1, const float* b1, const float* g2,
+                          const float* b2, int64_t rows, int64_t d, float eps1, float eps2,
+                          float* y1, float* mean1, float* rstd1, float* y2, float* mean2,
+                          float* rstd2, void* stream) {
+  if (rows < 0 || !layernorm_supported(d) || !(eps1 >= 0.0f) || !(eps2 >= 0.0f))
+    return OB_ERR_SHAPE;
+  if (rows > 0 && (!x || !y1 || !y2)) return OB_ERR_NULL;
+  if (!aligned4(x) || !aligned4(y1) || !aligned4(y2) || !aligned4(g1) || !aligned4(b1) ||
+      !aligned4(g2) || !aligned4(b2))
+    return OB_ERR_ALIGN;
+  launch_layernorm_fwd_pair(x, g1, b1, g2, b2, rows, d, eps1, eps2, y1, mean1, rstd1, y2, mean2,
+                            rstd2, as_stream(stream));
+  return launched();
+}
+
 size_t ob_layernorm_fwd_amax_workspace(int64_t P) {
   return (P < 1 || P > 8) ? 0 : layernorm_fwd_amax_workspace(P);
 }

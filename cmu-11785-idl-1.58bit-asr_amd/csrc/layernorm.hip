@@ -81,7 +81,8 @@ __device__ __forceinline__ float ln_row_v(const float (&v)[NPL][VW],
                                           float eps, float* __restrict__ y,
                                           float* __restrict__ mean_out,
                                           float* __restrict__ rstd_out,
-                                          int8_t* __restrict__ yq = nullptr, float sx = 0.0f) {
+                                          int8_t* __restrict__ yq = nullptr, float sx = 0.0f,
+                                          float (*vout)[NPL][VW] = nullptr) {
   const int j = threadIdx.x & (kLanesPerRow - 1);
   float s = 0.0f;
 #pragma unroll
@@ -113,6 +114,10 @@ __device__ __forceinline__ float ln_row_v(const float (&v)[NPL][VW],
       for (int e = 0; e < VW; ++e) {
         o[e] = fmaf((v[i][e] - mean) * rstd, gamma ? g[e] : 1.0f, beta ? b[e] : 0.0f);
         amx = fmaxf(amx, fabsf(o[e]));
+      }
+      if (vout) {  // the normalised row for a following LN (the stored y values)
+#pragma unroll
+        for (int e = 0; e < VW; ++e) (*vout)[i][e] = o[e];
       }
       if (y) store_cols<VW>(y + row * d, c0, o);  // (nullptr: the absmax pass of the int8 LN)
       if (yq) {  // int8 consumer: xq = clamp(rint(y * sx), -127, 127) (tgemm_i8.hip's q4)
@@ -173,6 +178,24 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(
     const int64_t row = row0 + kRowsPerBlock * q;
     if (row < rows) (void)ln_row_v<NPL, VW>(v[q], gamma, beta, row, d, eps, y, mean_out, rstd_out);
   }
+}
+
+// Two LayerNorms back to back, y1 = LN1(x), y2 = LN2(y1) (a block's final LN and the next
+// module's input LN, conformer.py:228 then :28): one pass over x, y1 never re-read; the
+// per-row arithmetic is ln_row's (y1 is normalised from the registers it is stored from), so
+// y1 / y2 / the statistics equal two ln_fwd launches bit for bit.
+template <int NPL, int VW>
+__global__ __launch_bounds__(kThreads) void ln_fwd_pair_kernel(
+    const float* __restrict__ x, const float* __restrict__ g1, const float* __restrict__ b1,
+    const float* __restrict__ g2, const float* __restrict__ b2, int64_t rows, int d, float eps1,
+    float eps2, float* __restrict__ y1, float* __restrict__ mean1, float* __restrict__ rstd1,
+    float* __restrict__ y2, float* __restrict__ mean2, float* __restrict__ rstd2) {
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x / kLanesPerRow);
+  if (row >= rows) return;
+  float v[NPL][VW];
+  ln_load<NPL, VW>(x, row, d, v);
+  (void)ln_row_v<NPL, VW>(v, g1, b1, row, d, eps1, y1, mean1, rstd1, nullptr, 0.0f, &v);
+  (void)ln_row_v<NPL, VW>(v, g2, b2, row, d, eps2, y2, mean2, rstd2);
 }
 
 // The same rows plus the per-pass max|y| (the int8 activation scale of the BitLinear that
@@ -545,6 +568,31 @@ void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta,
 #undef OB_LNF
 #undef OB_LNF4
 #undef OB_LNF4R
+}
+
+void launch_layernorm_fwd_pair(const float* x, const float* g1, const float* b1, const float* g2,
+                               const float* b2, int64_t rows, int64_t d, float eps1, float eps2,
+                               float* y1, float* mean1, float* rstd1, float* y2, float* mean2,
+                               float* rstd2, hipStream_t s) {
+  if (rows == 0) return;
+  const int npl = (int)ceil_div(d, kLanesPerRow);
+  const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
+  const dim3 grid((unsigned)ceil_div(rows, kRowsPerBlock));
+  const bool vec = d % 4 == 0 && al16(x) && al16(y1) && al16(y2) && al16(g1) && al16(b1) &&
+                   al16(g2) && al16(b2);
+#define OB_LNP(N)                                                                                \
+  hipLaunchKernelGGL((ln_fwd_pair_kernel<N, 1>), grid, dim3(kThreads), 0, s, x, g1, b1, g2, b2,  \
+                     rows, (int)d, eps1, eps2, y1, mean1, rstd1, y2, mean2, rstd2);
+#define OB_LNP4(N)                                                                               \
+  hipLaunchKernelGGL((ln_fwd_pair_kernel<N, 4>), grid, dim3(kThreads), 0, s, x, g1, b1, g2, b2,  \
+                     rows, (int)d, eps1, eps2, y1, mean1, rstd1, y2, mean2, rstd2);
+  if (vec) {
+    OB_LN_NPL4(OB_LNP4)
+  } else {
+    OB_LN_NPL(OB_LNP)
+  }
+#undef OB_LNP
+#undef OB_LNP4
 }
 
 size_t layernorm_fwd_amax_workspace(int64_t P) {

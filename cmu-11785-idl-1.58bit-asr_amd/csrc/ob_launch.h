@@ -285,6 +285,11 @@ bool layernorm_supported(int64_t d);
 size_t layernorm_bwd_workspace(int64_t rows, int64_t d);
 void launch_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                           int64_t d, float eps, float* y, float* mean, float* rstd, hipStream_t s);
+// y1 = LN1(x), y2 = LN2(y1) in one pass (bit-identical to two launch_layernorm_fwd)
+void launch_layernorm_fwd_pair(const float* x, const float* g1, const float* b1, const float* g2,
+                               const float* b2, int64_t rows, int64_t d, float eps1, float eps2,
+                               float* y1, float* mean1, float* rstd1, float* y2, float* mean2,
+                               float* rstd2, hipStream_t s);
 // + per-pass max|y| into amax[P] (rows % P == 0, P <= 8; per-block partials in ws)
 size_t layernorm_fwd_amax_workspace(int64_t P);
 void launch_layernorm_fwd_amax(const float* x, const float* gamma, const float* beta,

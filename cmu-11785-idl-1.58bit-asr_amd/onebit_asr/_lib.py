@@ -129,6 +129,8 @@ SIGNATURES = {
         _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
     "ob_ctc_greedy_decode": (_int, [_c_f, _c_f, _i64, _i64, _i64, _int, _c_f, _c_f, _c_f, _c_f]),
     "ob_layernorm_fwd": (_int, [_c_f, _c_f, _c_f, _i64, _i64, _f32, _c_f, _c_f, _c_f, _c_f]),
+    "ob_layernorm_fwd_pair": (_int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _f32, _f32, _c_f,
+                                     _c_f, _c_f, _c_f, _c_f, _c_f, _c_f]),
     "ob_layernorm_fwd_amax_workspace": (_sz, [_i64]),
     "ob_layernorm_fwd_amax": (_int, [_c_f, _c_f, _c_f, _i64, _i64, _f32, _c_f, _c_f, _c_f, _i64,
                                      _c_f, _c_f, _sz, _c_f]),

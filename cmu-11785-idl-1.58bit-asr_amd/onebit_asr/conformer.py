@@ -37,6 +37,7 @@ from .embedding import embedding
 from .fused import (ffn_residual, ffn_residual_i8, fused_supported, i8_fused_supported,
                     i8_linear, linear_residual, linear_residual_i8, qkv_projections)
 from .layernorm import (Int8Act, fused_layernorm_supported, layer_norm, layer_norm_amax,
+                        layer_norm_pair,
                         layer_norm_fork, layer_norm_i8)
 from .linear import linear
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
@@ -77,6 +78,13 @@ class LayerNorm(nn.Module):
     def fork(self, x):
         """(LN(x), x) with the residual branch's gradient added in the LN backward."""
         return layer_norm_fork(x, self.ln.weight, self.ln.bias, self.ln.eps)
+
+    def pair(self, x, nxt: "LayerNorm"):
+        """LN(x), with nxt's LN of the result formed in the same launch (training)."""
+        if self.emit_amax or nxt.emit_amax:
+            return self(x)
+        return layer_norm_pair(x, self.ln.weight, self.ln.bias, self.ln.eps, nxt.ln.weight,
+                               nxt.ln.bias, nxt.ln.eps)
 
 
 def _pad_rows(y: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
@@ -386,7 +394,11 @@ class ConformerBlock(nn.Module):
         self.ff2 = FeedForwardModule(d_model, d_ff, dropout)
         self.ln = LayerNorm(d_model)
 
-    def forward(self, x, src_mask, bitwidth_linear: int, pos_emb: torch.Tensor):
+    def forward(self, x, src_mask, bitwidth_linear: int, pos_emb: torch.Tensor,
+                next_ln: Optional["LayerNorm"] = None):
+        """next_ln: the LayerNorm that will normalise this block's output next (the following
+        block's ff1.ln or the encoder's ln_out); its forward is formed together with this
+        block's final LN (layernorm.layer_norm_pair)."""
         x = self.ff1(x, bitwidth_linear)
         x = self.mhsa(x, src_mask, bitwidth_linear, pos_emb)
         passes = bitwidth_linear.passes if isinstance(bitwidth_linear, PassBits) else 1
@@ -395,7 +407,7 @@ class ConformerBlock(nn.Module):
         x = self.conv(x, passes=passes,
                       bitwidth=bitwidth_linear if self.conv.quantize_pointwise else None)
         x = self.ff2(x, bitwidth_linear)
-        return self.ln(x)
+        return self.ln(x) if next_ln is None else self.ln.pair(x, next_ln)
 
 
 def block_bitwidths(n_layers: int, precision: int, sp_mask: Optional[Sequence[int]]) -> List[int]:
@@ -445,8 +457,11 @@ class ConformerEncoder(nn.Module):
         attn_mask = key_mask.unsqueeze(2) & key_mask.unsqueeze(1)     # [B, T', T']
         # valid frames per utterance, for the fused attention kernels (prefix masks)
         attn_mask._ob_lens = key_mask.sum(dim=1, dtype=torch.int32)
-        for blk, bw in zip(self.blocks, block_bitwidths(len(self.blocks), precision, sp_mask)):
-            x = blk(x, attn_mask, bw, pos_emb)
+        bws = block_bitwidths(len(self.blocks), precision, sp_mask)
+        n = len(self.blocks)
+        for i, (blk, bw) in enumerate(zip(self.blocks, bws)):
+            nxt = self.blocks[i + 1].ff1.ln if i + 1 < n else self.ln_out
+            x = blk(x, attn_mask, bw, pos_emb, next_ln=nxt)
         return self.ln_out(x), key_mask
 
 

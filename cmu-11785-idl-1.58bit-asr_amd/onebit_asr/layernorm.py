@@ -98,19 +98,40 @@ def fused_layernorm_supported(x: torch.Tensor, d: int) -> bool:
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, spec=None):
+    def forward(ctx, x, weight, bias, eps, spec=None, pre=None, pair=None):
+        """pre: this LN's (y, mean, rstd), already formed by the previous LN's pair launch;
+        pair: (weight2, bias2, eps2, box) -- also form the NEXT LN of y in the same launch
+        (ob_layernorm_fwd_pair) and put its (y2, mean2, rstd2) into box."""
         d = x.shape[-1]
         ctx.spec = spec
         x2 = x.contiguous().view(-1, d)
         rows = x2.shape[0]
-        y = torch.empty_like(x2)
         need = any(ctx.needs_input_grad[:3])
-        mean = torch.empty((rows,), dtype=torch.float32, device=x.device) if need else None
-        rstd = torch.empty((rows,), dtype=torch.float32, device=x.device) if need else None
         lib = _lib.load()
-        _lib.check(lib.ob_layernorm_fwd(x2.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), rows, d,
-                                        float(eps), y.data_ptr(), _lib.ptr(mean), _lib.ptr(rstd),
-                                        _lib.stream_of(x2)), "ob_layernorm_fwd")
+        if pre is not None:
+            y, mean, rstd = pre
+        elif pair is not None:
+            w2, b2, eps2, box = pair
+            y = torch.empty_like(x2)
+            mean = torch.empty((rows,), dtype=torch.float32, device=x.device)
+            rstd = torch.empty((rows,), dtype=torch.float32, device=x.device)
+            y2 = torch.empty_like(x2)
+            mean2 = torch.empty((rows,), dtype=torch.float32, device=x.device)
+            rstd2 = torch.empty((rows,), dtype=torch.float32, device=x.device)
+            _lib.check(lib.ob_layernorm_fwd_pair(
+                x2.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), _lib.ptr(w2), _lib.ptr(b2), rows,
+                d, float(eps), float(eps2), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                y2.data_ptr(), mean2.data_ptr(), rstd2.data_ptr(), _lib.stream_of(x2)),
+                "ob_layernorm_fwd_pair")
+            box.append((w2, b2, float(eps2), y2, mean2, rstd2))
+        else:
+            y = torch.empty_like(x2)
+            mean = torch.empty((rows,), dtype=torch.float32, device=x.device) if need else None
+            rstd = torch.empty((rows,), dtype=torch.float32, device=x.device) if need else None
+            _lib.check(lib.ob_layernorm_fwd(x2.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), rows,
+                                            d, float(eps), y.data_ptr(), _lib.ptr(mean),
+                                            _lib.ptr(rstd), _lib.stream_of(x2)),
+                       "ob_layernorm_fwd")
         if need:
             ctx.save_for_backward(x2, weight, mean, rstd)
             ctx.has = (weight is not None, bias is not None)
@@ -132,14 +153,42 @@ class _LayerNormFn(torch.autograd.Function):
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
         _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, None, dx, dw, db, ws, wsb,
                              ctx.spec, _lib.stream_of(g2), ctx.params), "ob_layernorm_bwd")
-        return dx.view(gy.shape), dw, db, None, None
+        return dx.view(gy.shape), dw, db, None, None, None, None
+
+
+_PAIR = os.environ.get("OB_LN_PAIR", "1") != "0"  # 0: every LN its own launch
+
+
+def _take_pre(x: torch.Tensor, weight, bias, eps):
+    """The (y, mean, rstd) a pair launch already formed for LN(x) with these parameters."""
+    pre = getattr(x, "_ob_ln_pre", None)
+    if pre is None or pre[0] is not weight or pre[1] is not bias or pre[2] != float(eps):
+        return None
+    x._ob_ln_pre = None
+    return pre[3:]
 
 
 def layer_norm(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.Tensor:
     d = x.shape[-1]
     if not fused_layernorm_supported(x, d):
         return F.layer_norm(x, (d,), weight, bias, eps)
-    return _LayerNormFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None))
+    return _LayerNormFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None),
+                              _take_pre(x, weight, bias, eps))
+
+
+def layer_norm_pair(x: torch.Tensor, weight, bias, eps, weight2, bias2, eps2) -> torch.Tensor:
+    """LN(x) whose output's next LN (weight2, bias2, eps2) is formed in the same launch and
+    picked up by that LN's layer_norm / layer_norm_fork call (bit-identical to two launches).
+    Training only (grad enabled): inference consumers may take the int8 LN instead."""
+    d = x.shape[-1]
+    if not (_PAIR and torch.is_grad_enabled() and fused_layernorm_supported(x, d)):
+        return layer_norm(x, weight, bias, eps)
+    box = []
+    y = _LayerNormFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None),
+                           _take_pre(x, weight, bias, eps), (weight2, bias2, eps2, box))
+    if box:
+        y._ob_ln_pre = box[0]
+    return y
 
 
 @torch.no_grad()
@@ -198,18 +247,18 @@ class _LayerNormForkFn(torch.autograd.Function):
     instead of autograd's separate add over the [rows, d] tensor."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, spec=None):
-        y = _LayerNormFn.forward(ctx, x, weight, bias, eps, spec)
+    def forward(ctx, x, weight, bias, eps, spec=None, pre=None):
+        y = _LayerNormFn.forward(ctx, x, weight, bias, eps, spec, pre)
         return y, x.view_as(x)
 
     @staticmethod
     def backward(ctx, gy, gres):
         if gres is None:
-            return _LayerNormFn.backward(ctx, gy)
+            return _LayerNormFn.backward(ctx, gy)[:6]
         x2, weight, mean, rstd = ctx.saved_tensors
         rows, d = x2.shape
         if gy is None:
-            return gres, None, None, None, None
+            return gres, None, None, None, None, None
         g2 = gy.contiguous().view(rows, d)
         r2 = gres.contiguous().view(rows, d)
         dx = torch.empty_like(x2)
@@ -221,7 +270,7 @@ class _LayerNormForkFn(torch.autograd.Function):
         ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
         _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, r2, dx, dw, db, ws, wsb,
                              ctx.spec, _lib.stream_of(g2), ctx.params), "ob_layernorm_bwd_res")
-        return dx.view(gy.shape), dw, db, None, None
+        return dx.view(gy.shape), dw, db, None, None, None
 
 
 def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):
@@ -230,4 +279,5 @@ def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):
     d = x.shape[-1]
     if not fused_layernorm_supported(x, d) or not torch.is_grad_enabled() or not x.requires_grad:
         return layer_norm(x, weight, bias, eps), x
-    return _LayerNormForkFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None))
+    return _LayerNormForkFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None),
+                                  _take_pre(x, weight, bias, eps))

@@ -508,6 +508,14 @@ OB_API int ob_adamw_clip_step(const ob_adamw_tensor* table, int64_t n_tensors,
 OB_API int ob_layernorm_fwd(const float* x, const float* gamma, const float* beta, int64_t rows,
                             int64_t d, float eps, float* y, float* mean, float* rstd,
                             void* stream);
+/* Two LayerNorms back to back (a Conformer block's final LN, conformer.py:228, and the next
+ * module's input LN, :28 / the encoder's output LN): y1 = LN1(x) (gamma g1, beta b1), y2 =
+ * LN2(y1), with both rows' mean / rstd (each may be NULL), in one pass over x -- bit-identical
+ * to two ob_layernorm_fwd calls. */
+OB_API int ob_layernorm_fwd_pair(const float* x, const float* g1, const float* b1,
+                                 const float* g2, const float* b2, int64_t rows, int64_t d,
+                                 float eps1, float eps2, float* y1, float* mean1, float* rstd1,
+                                 float* y2, float* mean2, float* rstd2, void* stream);
 /* ob_layernorm_fwd plus amax[p] = max|y| over pass p (rows split into P equal passes,
  * P <= 8): the producer-side per-tensor scale of the int8 BitLinear that consumes y.
  * ws: ob_layernorm_fwd_amax_workspace(P) bytes (per-block partial maxima). */

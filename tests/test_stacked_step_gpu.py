@@ -107,3 +107,42 @@ def test_deferred_finishes_equal_immediate(gpu, monkeypatch):
     assert res[False].keys() == res[True].keys()
     for k in res[False]:
         assert torch.equal(res[False][k], res[True][k]), k
+
+
+def test_layernorm_pairs_equal_single_launches(gpu, monkeypatch):
+    """A block's final LN and the next LN (next block's ff1.ln, the encoder's ln_out) formed
+    in one launch (ob_layernorm_fwd_pair) == every LN its own launch: loss and every gradient
+    of the stacked step bit for bit, and the pair path was taken."""
+    from onebit_asr import layernorm
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CFG1, synthetic_batch
+    from onebit_asr.train_step import OneBitStep
+
+    cfg = dict(CFG1, enc_d_model=144, enc_d_ff=576)
+    batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
+    res, losses, taken = {}, {}, {}
+    for on in (False, True):
+        monkeypatch.setattr(layernorm, "_PAIR", on)
+        calls = []
+        orig = layernorm._take_pre
+
+        def spy(*a, orig=orig, calls=calls):
+            r = orig(*a)
+            calls.append(r is not None)
+            return r
+
+        monkeypatch.setattr(layernorm, "_take_pre", spy)
+        torch.manual_seed(0)
+        m = ConformerASR(80, 5004, **cfg).to(gpu)
+        step = OneBitStep(m, n_layers=2, stacked=True)
+        loss, _ = step(batch, [1, 0])
+        loss.backward()
+        torch.cuda.synchronize()
+        losses[on] = loss.detach().clone()
+        taken[on] = sum(calls)
+        res[on] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    assert taken[False] == 0 and taken[True] >= 2, taken
+    assert torch.equal(losses[False], losses[True])
+    assert res[False].keys() == res[True].keys()
+    for k in res[False]:
+        assert torch.equal(res[False][k], res[True][k]), k
