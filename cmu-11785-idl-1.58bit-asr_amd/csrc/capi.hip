@@ -1228,6 +1228,36 @@ int ob_ln_param_table(const void* table, int64_t n, int64_t dmax, void* stream) 
   return launched();
 }
 
+size_t ob_layernorm_bwd_pair_workspace(int64_t rows, int64_t d) {
+  if (rows < 0 || !layernorm_supported(d)) return 0;
+  return 2 * layernorm_bwd_workspace(rows, d);
+}
+
+int ob_layernorm_bwd_pair(const float* dy, const float* y1, const float* g2, const float* mean2,
+                          const float* rstd2, const float* gres, const float* x, const float* g1,
+                          const float* mean1, const float* rstd1, int64_t rows, int64_t d,
+                          float* dx, float* dg2, float* db2, float* dg1, float* db1, void* ws,
+                          size_t ws_bytes, float* dy2, float rscale, float p_drop,
+                          const uint64_t* rng, int64_t rng_offset, const int32_t* lens, int64_t T,
+                          void* table, int64_t slot2, int64_t slot1, void* stream) {
+  if (rows < 0 || !layernorm_supported(d) || !(p_drop >= 0.0f && p_drop < 1.0f))
+    return OB_ERR_SHAPE;
+  if (rows > 0 && (!dy || !y1 || !mean2 || !rstd2 || !x || !mean1 || !rstd1 || !dx || !ws))
+    return OB_ERR_NULL;
+  if (dy2 && p_drop > 0.0f && !rng) return OB_ERR_NULL;
+  if (ws_bytes < 2 * layernorm_bwd_workspace(rows, d)) return OB_ERR_WORKSPACE;
+  if (!aligned4(dy) || !aligned4(y1) || !aligned4(gres) || !aligned4(x) || !aligned4(dx) ||
+      !aligned4(dy2) || !aligned4(g1) || !aligned4(g2) || ((uintptr_t)ws & 15))
+    return OB_ERR_ALIGN;
+  LnGradScale gsc{dy2, rscale, p_drop, rng, (uint64_t)rng_offset, lens, (int)T};
+  LnParamEntry* tab = static_cast<LnParamEntry*>(table);
+  const LnDefer f2{tab && slot2 >= 0 ? tab : nullptr, (int)slot2};
+  const LnDefer f1{tab && slot1 >= 0 ? tab : nullptr, (int)slot1};
+  launch_layernorm_bwd_pair(dy, y1, g2, mean2, rstd2, gres, x, g1, mean1, rstd1, rows, d, dx, dg2,
+                            db2, dg1, db1, ws, as_stream(stream), dy2 ? &gsc : nullptr, &f2, &f1);
+  return launched();
+}
+
 int ob_layernorm_bwd_defer(const float* dy, const float* x, const float* gamma, const float* mean,
                            const float* rstd, int64_t rows, int64_t d, const float* dres,
                            float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,

@@ -405,6 +405,159 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(
   }
 }
 
+// One LayerNorm backward row stage (ln_bwd_kernel's arithmetic): dx = rstd * (g - mean(g) -
+// xhat * mean(g * xhat)) (+ res), g = dy * gamma, and the dgamma / dbeta accumulators;
+// columns >= d give 0.
+template <int NPL, int VW>
+__device__ __forceinline__ void ln_bwd_stage(const float (&xv)[NPL][VW], const float (&dv)[NPL][VW],
+                                             const float (*res)[NPL][VW], float mu, float rs,
+                                             const float (&gam)[NPL][VW], float inv_d, int d,
+                                             float (&acc_g)[NPL][VW], float (&acc_b)[NPL][VW],
+                                             float (&o)[NPL][VW]) {
+  const int j = threadIdx.x & (kLanesPerRow - 1);
+  float xh[NPL][VW], g[NPL][VW];
+  float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i)
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      xh[i][e] = (xv[i][e] - mu) * rs;
+      acc_g[i][e] = fmaf(dv[i][e], xh[i][e], acc_g[i][e]);
+      acc_b[i][e] += dv[i][e];
+      g[i][e] = dv[i][e] * gam[i][e];
+      s1 += g[i][e];
+      s2 = fmaf(g[i][e], xh[i][e], s2);
+    }
+  const float m1 = row_sum16(s1) * inv_d;
+  const float m2 = row_sum16(s2) * inv_d;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i)
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      const float v = nc_mul(rs, nc_sub(nc_sub(g[i][e], m1), nc_mul(xh[i][e], m2)));
+      const bool live = VW * (j + kLanesPerRow * i) + e < d;
+      o[i][e] = live ? (res ? nc_add(v, (*res)[i][e]) : v) : 0.0f;
+    }
+}
+
+// The backward of a LayerNorm pair (y1 = LN1(x), y2 = LN2(y1), y1 also taken by a residual
+// branch whose gradient is gres): g = LN2_backward(dy) + gres and dx = LN1_backward(g) (with
+// the dy2 of the residual tail feeding x, as ln_bwd_kernel), in one pass per row -- g never
+// goes to memory; both layers' dgamma / dbeta partials (part_*2 for LN2, part_*1 for LN1,
+// the same row blocks as ln_bwd_kernel).
+template <int NPL, int VW>
+__global__ __launch_bounds__(kThreads) void ln_bwd_pair_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y1, const float* __restrict__ g2,
+    const float* __restrict__ mean2, const float* __restrict__ rstd2,
+    const float* __restrict__ gres, const float* __restrict__ x, const float* __restrict__ g1,
+    const float* __restrict__ mean1, const float* __restrict__ rstd1, int64_t rows, int d,
+    int rows_per_block, float* __restrict__ dx, float* __restrict__ pg2, float* __restrict__ pb2,
+    float* __restrict__ pg1, float* __restrict__ pb1, GScale gs, LnDefer df2, LnParamEntry ent2,
+    LnDefer df1, LnParamEntry ent1) {
+  __shared__ float red[2][kRowsPerBlock][kLanesPerRow * NPL * VW];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (df2.table) df2.table[df2.slot] = ent2;
+    if (df1.table) df1.table[df1.slot] = ent1;
+  }
+  const int j = threadIdx.x & (kLanesPerRow - 1);
+  const int sub = threadIdx.x / kLanesPerRow;
+  const float inv_d = 1.0f / (float)d;
+  float gm2[NPL][VW], gm1[NPL][VW], ag2[NPL][VW], ab2[NPL][VW], ag1[NPL][VW], ab1[NPL][VW];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    const int c0 = VW * (j + kLanesPerRow * i);
+    if (g2) load_cols<VW>(g2, c0, d, gm2[i]);
+    if (g1) load_cols<VW>(g1, c0, d, gm1[i]);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      if (!g2) gm2[i][e] = c0 + e < d ? 1.0f : 0.0f;
+      if (!g1) gm1[i][e] = c0 + e < d ? 1.0f : 0.0f;
+      ag2[i][e] = ab2[i][e] = ag1[i][e] = ab1[i][e] = 0.0f;
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  const uint32_t dkey = (gs.dy2 && gs.dc.on) ? drop_key(gs.rng[0], gs.rng[1] + gs.rng_off) : 0u;
+  // the next row's operands load while this row is reduced (as ln_bwd_kernel)
+  struct RowIn {
+    float mu2, rs2, mu1, rs1;
+    float yv[NPL][VW], dv[NPL][VW], rv[NPL][VW], xv[NPL][VW];
+  };
+  auto fetch = [&](int64_t row, RowIn& in) {
+    in.mu2 = mean2[row];
+    in.rs2 = rstd2[row];
+    in.mu1 = mean1[row];
+    in.rs1 = rstd1[row];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c0 = VW * (j + kLanesPerRow * i);
+      load_cols<VW>(y1 + row * d, c0, d, in.yv[i]);
+      load_cols<VW>(dy + row * d, c0, d, in.dv[i]);
+      if (gres) load_cols<VW>(gres + row * d, c0, d, in.rv[i]);
+      load_cols<VW>(x + row * d, c0, d, in.xv[i]);
+    }
+  };
+  RowIn cur, nxt;
+  if (r0 + sub < r1) fetch(r0 + sub, cur);
+  for (int64_t row = r0 + sub; row < r1; row += kRowsPerBlock) {
+    if (row + kRowsPerBlock < r1) fetch(row + kRowsPerBlock, nxt);
+    float gv[NPL][VW], o[NPL][VW];
+    ln_bwd_stage<NPL, VW>(cur.yv, cur.dv, gres ? &cur.rv : nullptr, cur.mu2, cur.rs2, gm2, inv_d,
+                          d, ag2, ab2, gv);
+    ln_bwd_stage<NPL, VW>(cur.xv, gv, nullptr, cur.mu1, cur.rs1, gm1, inv_d, d, ag1, ab1, o);
+    bool rvalid = true;
+    if (gs.dy2 && gs.lens) {
+      const int64_t b = row / gs.T;
+      rvalid = row - b * gs.T < gs.lens[b];
+    }
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c0 = VW * (j + kLanesPerRow * i);
+      if (c0 < d) {
+        float w2[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) {
+          float w = o[i][e];
+          if (gs.dc.on)
+            w = nc_mul(w, drop_keep(dkey, (uint64_t)(row * d + c0 + e), gs.dc.thresh) ? gs.dc.scale : 0.0f);
+          if (!rvalid) w = nc_mul(w, 0.0f);
+          w2[e] = gs.rscale == 1.0f ? w : nc_mul(gs.rscale, w);
+        }
+        store_cols<VW>(dx + row * d, c0, o[i]);
+        if (gs.dy2) store_cols<VW>(gs.dy2 + row * d, c0, w2);
+      }
+    }
+    cur = nxt;
+  }
+  // the two layers' partials in turn through one [2][16][cols] LDS buffer
+#pragma unroll
+  for (int layer = 0; layer < 2; ++layer) {
+    float* og = layer == 0 ? pg2 : pg1;
+    float* ob = layer == 0 ? pb2 : pb1;
+    if (layer == 1) __syncthreads();  // layer 0's reads are done
+#pragma unroll
+    for (int i = 0; i < NPL; ++i)
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        const int c = VW * (j + kLanesPerRow * i) + e;
+        red[0][sub][c] = layer == 0 ? ag2[i][e] : ag1[i][e];
+        red[1][sub][c] = layer == 0 ? ab2[i][e] : ab1[i][e];
+      }
+    __syncthreads();
+    if (og)
+      for (int c = threadIdx.x; c < d; c += kThreads) {
+        float sg = 0.0f, sb = 0.0f;
+#pragma unroll
+        for (int r = 0; r < kRowsPerBlock; ++r) {
+          sg += red[0][r][c];
+          sb += red[1][r][c];
+        }
+        og[(int64_t)blockIdx.x * d + c] = sg;
+        ob[(int64_t)blockIdx.x * d + c] = sb;
+      }
+  }
+}
+
 // dgamma[c] = sum over blocks of part_g[blk][c], same for dbeta. Block = 4 columns x 64
 // block-slices; slice s sums blocks s, s+64, ... (4 independent accumulators in flight),
 // then the 64 slices are added in slice order through LDS (fixed order: deterministic).
@@ -664,6 +817,64 @@ void launch_ln_param_table(const LnParamEntry* table, int n, int dmax, hipStream
   if (n <= 0 || dmax <= 0) return;
   hipLaunchKernelGGL(ln_param_table_kernel, dim3((unsigned)ceil_div(dmax, kRedCols), (unsigned)n),
                      dim3(kThreads), 0, s, table);
+}
+
+void launch_layernorm_bwd_pair(const float* dy, const float* y1, const float* g2,
+                               const float* mean2, const float* rstd2, const float* gres,
+                               const float* x, const float* g1, const float* mean1,
+                               const float* rstd1, int64_t rows, int64_t d, float* dx,
+                               float* dg2, float* db2, float* dg1, float* db1, void* ws,
+                               hipStream_t s, const LnGradScale* gsc, const LnDefer* defer2,
+                               const LnDefer* defer1) {
+  GScale gs{};
+  if (gsc && gsc->dy2) {
+    gs.dy2 = gsc->dy2;
+    gs.rscale = gsc->rscale;
+    gs.dc = make_drop(gsc->p_drop);
+    gs.rng = gsc->rng;
+    gs.rng_off = gsc->rng_off;
+    gs.lens = gsc->lens;
+    gs.T = gsc->T > 0 ? gsc->T : 1;
+  }
+  int rpb = kRowsPerBlock;
+  const int nb = rows > 0 ? bwd_blocks(rows, &rpb) : 0;
+  // ws: LN2's partials then LN1's, each layernorm_bwd_workspace's layout
+  float* pg2 = static_cast<float*>(ws);
+  float* pb2 = pg2 + (size_t)nb * d;
+  float* pg1 = reinterpret_cast<float*>(static_cast<char*>(ws) + layernorm_bwd_workspace(rows, d));
+  float* pb1 = pg1 + (size_t)nb * d;
+  const bool p2 = dg2 || db2, p1 = dg1 || db1;
+  LnDefer f2{nullptr, 0}, f1{nullptr, 0};
+  if (defer2 && defer2->table && p2 && rows > 0) f2 = *defer2;
+  if (defer1 && defer1->table && p1 && rows > 0) f1 = *defer1;
+  const LnParamEntry e2{pg2, pb2, dg2, db2, nb, (int)d}, e1{pg1, pb1, dg1, db1, nb, (int)d};
+  const int npl = (int)ceil_div(d, kLanesPerRow);
+  const int npl4 = (int)ceil_div(d, 4 * kLanesPerRow);
+  const bool vec = d % 4 == 0 && al16(dy) && al16(y1) && al16(g2) && al16(gres) && al16(x) &&
+                   al16(g1) && al16(dx) && al16(gs.dy2);
+  if (rows > 0) {
+#define OB_LNBP(N, V)                                                                            \
+  hipLaunchKernelGGL((ln_bwd_pair_kernel<N, V>), dim3((unsigned)nb), dim3(kThreads), 0, s, dy,   \
+                     y1, g2, mean2, rstd2, gres, x, g1, mean1, rstd1, rows, (int)d, rpb, dx,     \
+                     p2 ? pg2 : nullptr, p2 ? pb2 : nullptr, p1 ? pg1 : nullptr,                 \
+                     p1 ? pb1 : nullptr, gs, f2, e2, f1, e1);
+#define OB_LNBP1(N) OB_LNBP(N, 1)
+#define OB_LNBP4(N) OB_LNBP(N, 4)
+    if (vec) {
+      OB_LN_NPL4(OB_LNBP4)
+    } else {
+      OB_LN_NPL(OB_LNBP1)
+    }
+#undef OB_LNBP1
+#undef OB_LNBP4
+#undef OB_LNBP
+  }
+  if (p2 && !f2.table)
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, kRedCols)), dim3(kThreads), 0,
+                       s, pg2, pb2, nb, (int)d, dg2, db2);
+  if (p1 && !f1.table)
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)ceil_div(d, kRedCols)), dim3(kThreads), 0,
+                       s, pg1, pb1, nb, (int)d, dg1, db1);
 }
 
 void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,

@@ -330,6 +330,16 @@ void launch_layernorm_bwd(const float* dy, const float* x, const float* gamma, c
                           const float* rstd, int64_t rows, int64_t d, const float* dres, float* dx, float* dgamma,
                           float* dbeta, void* ws, hipStream_t s, const LnGradScale* gsc = nullptr,
                           const LnDefer* defer = nullptr);
+// backward of y1 = LN1(x), y2 = LN2(y1) with y1's residual-branch gradient gres (may be null):
+// dx = LN1_bwd(LN2_bwd(dy) + gres); ws = 2 * layernorm_bwd_workspace(rows, d) bytes (LN2's
+// partials, then LN1's); gsc: the dy2 of the tail feeding x; defer2 / defer1 per layer.
+void launch_layernorm_bwd_pair(const float* dy, const float* y1, const float* g2,
+                               const float* mean2, const float* rstd2, const float* gres,
+                               const float* x, const float* g1, const float* mean1,
+                               const float* rstd1, int64_t rows, int64_t d, float* dx,
+                               float* dg2, float* db2, float* dg1, float* db1, void* ws,
+                               hipStream_t s, const LnGradScale* gsc, const LnDefer* defer2,
+                               const LnDefer* defer1);
 
 // dwconv.hip (depthwise Conv1d of the conv module, odd kernel width, 'same' padding)
 bool dwconv_supported(int KT);

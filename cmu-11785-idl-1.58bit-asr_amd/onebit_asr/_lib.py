@@ -139,6 +139,11 @@ SIGNATURES = {
     "ob_layernorm_bwd_defer": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f,
                _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f, _i64, _c_f]),
+    "ob_layernorm_bwd_pair_workspace": (_sz, [_i64, _i64]),
+    "ob_layernorm_bwd_pair": (
+        _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _c_f, _c_f,
+               _c_f, _c_f, _c_f, _c_f, _sz, _c_f, _f32, _f32, _c_f, _i64, _c_f, _i64, _c_f, _i64,
+               _i64, _c_f]),
     "ob_ln_param_entry_bytes": (_sz, []),
     "ob_ln_param_table": (_int, [_c_f, _i64, _i64, _c_f]),
     "ob_dw_finish_entry_bytes": (_sz, []),

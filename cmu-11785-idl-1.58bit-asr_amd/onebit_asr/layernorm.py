@@ -108,8 +108,10 @@ class _LayerNormFn(torch.autograd.Function):
         rows = x2.shape[0]
         need = any(ctx.needs_input_grad[:3])
         lib = _lib.load()
+        ctx.link = None
         if pre is not None:
-            y, mean, rstd = pre
+            y, mean, rstd = pre[:3]
+            ctx.pre_link = pre[3] if len(pre) > 3 else None
         elif pair is not None:
             w2, b2, eps2, box = pair
             y = torch.empty_like(x2)
@@ -123,7 +125,11 @@ class _LayerNormFn(torch.autograd.Function):
                 d, float(eps), float(eps2), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                 y2.data_ptr(), mean2.data_ptr(), rstd2.data_ptr(), _lib.stream_of(x2)),
                 "ob_layernorm_fwd_pair")
-            box.append((w2, b2, float(eps2), y2, mean2, rstd2))
+            # the consumer's backward may run both LN backwards in one launch: it finds this
+            # LN's saved state here and leaves the result for this node's backward
+            link = _PairLink(x2, weight, bias, mean, rstd, spec, ctx.needs_input_grad[:3])
+            ctx.link = link
+            box.append((w2, b2, float(eps2), y2, mean2, rstd2, link))
         else:
             y = torch.empty_like(x2)
             mean = torch.empty((rows,), dtype=torch.float32, device=x.device) if need else None
@@ -141,6 +147,15 @@ class _LayerNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        link = getattr(ctx, "link", None)
+        if link is not None and link.result is not None:
+            du, dw, db = link.result
+            link.result = None
+            if gy.data_ptr() != du.data_ptr():
+                # the output had a consumer besides the next LN: the pair backward is invalid
+                raise RuntimeError("LayerNorm pair backward: the first LN's output has another "
+                                   "consumer; run with OB_LN_PAIR_BWD=0")
+            return du.view(gy.shape), dw, db, None, None, None, None
         x2, weight, mean, rstd = ctx.saved_tensors
         rows, d = x2.shape
         g2 = gy.contiguous().view(rows, d)
@@ -157,6 +172,19 @@ class _LayerNormFn(torch.autograd.Function):
 
 
 _PAIR = os.environ.get("OB_LN_PAIR", "1") != "0"  # 0: every LN its own launch
+_PAIR_BWD = os.environ.get("OB_LN_PAIR_BWD", "1") != "0"  # 0: the pair's backwards one by one
+
+
+class _PairLink:
+    """The first LN of a pair (its saved input / statistics / parameters), shared with the
+    second LN's fork node, whose backward can then run both LN backwards in one launch
+    (ob_layernorm_bwd_pair) and leave (dx, dgamma, dbeta) here for the first LN's node."""
+
+    __slots__ = ("x2", "weight", "bias", "mean", "rstd", "spec", "need", "result")
+
+    def __init__(self, x2, weight, bias, mean, rstd, spec, need):
+        self.x2, self.weight, self.bias, self.mean, self.rstd = x2, weight, bias, mean, rstd
+        self.spec, self.need, self.result = spec, tuple(need), None
 
 
 def _take_pre(x: torch.Tensor, weight, bias, eps):
@@ -253,6 +281,10 @@ class _LayerNormForkFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, gres):
+        link = getattr(ctx, "pre_link", None)
+        if (_PAIR_BWD and link is not None and gy is not None and ctx.spec is None
+                and any(link.need)):
+            return _pair_backward(ctx, link, gy, gres)
         if gres is None:
             return _LayerNormFn.backward(ctx, gy)[:6]
         x2, weight, mean, rstd = ctx.saved_tensors
@@ -271,6 +303,53 @@ class _LayerNormForkFn(torch.autograd.Function):
         _lib.check(_bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, r2, dx, dw, db, ws, wsb,
                              ctx.spec, _lib.stream_of(g2), ctx.params), "ob_layernorm_bwd_res")
         return dx.view(gy.shape), dw, db, None, None, None
+
+
+def _pair_backward(ctx, link, gy, gres):
+    """Both LN backwards of a pair in one launch: this (second) LN's dx + gres feeds the first
+    LN's backward in registers; the first LN's (dx, dgamma, dbeta) are left on the link."""
+    y1, w2, mean2, rstd2 = ctx.saved_tensors
+    rows, d = y1.shape
+    g2 = gy.contiguous().view(rows, d)
+    r2 = gres.contiguous().view(rows, d) if gres is not None else None
+    u = link.x2
+    du = torch.empty_like(u)
+    has_w2, has_b2 = ctx.has
+    dw2 = torch.empty((d,), dtype=torch.float32, device=u.device) if has_w2 and ctx.needs_input_grad[1] else None
+    db2 = torch.empty((d,), dtype=torch.float32, device=u.device) if has_b2 and ctx.needs_input_grad[2] else None
+    w1, b1 = link.weight, link.bias
+    dw1 = torch.empty((d,), dtype=torch.float32, device=u.device) if w1 is not None and link.need[1] else None
+    db1 = torch.empty((d,), dtype=torch.float32, device=u.device) if b1 is not None and link.need[2] else None
+    lib = _lib.load()
+    stream = _lib.stream_of(g2)
+    wsb = lib.ob_layernorm_bwd_pair_workspace(rows, d)
+    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=u.device)
+    table, s2, s1 = None, -1, -1
+    if rows > 0 and (dw2 is not None or db2 is not None) and deferred.can_defer(*ctx.params):
+        t = deferred.ln_slot(u.device, stream, d)
+        if t is not None:
+            table, s2 = t
+    if rows > 0 and (dw1 is not None or db1 is not None) and deferred.can_defer(w1, b1):
+        t = deferred.ln_slot(u.device, stream, d)
+        if t is not None:
+            table, s1 = t
+    if s2 >= 0 or s1 >= 0:
+        deferred.keep(ws)
+    spec = link.spec
+    dy2 = torch.empty_like(du) if spec is not None else None
+    _lib.check(lib.ob_layernorm_bwd_pair(
+        g2.data_ptr(), y1.data_ptr(), _lib.ptr(w2), mean2.data_ptr(), rstd2.data_ptr(),
+        _lib.ptr(r2), u.data_ptr(), _lib.ptr(w1), link.mean.data_ptr(), link.rstd.data_ptr(),
+        rows, d, du.data_ptr(), _lib.ptr(dw2), _lib.ptr(db2), _lib.ptr(dw1), _lib.ptr(db1),
+        ws.data_ptr(), wsb, _lib.ptr(dy2), spec.rscale if spec is not None else 1.0,
+        spec.p if spec is not None else 0.0, _lib.ptr(spec.rng) if spec is not None else None,
+        spec.off if spec is not None else 0, _lib.ptr(spec.lens) if spec is not None else None,
+        spec.T if spec is not None else 0, table, s2, s1, stream), "ob_layernorm_bwd_pair")
+    if spec is not None:
+        spec.dx_ptr, spec.dy2 = du.data_ptr(), dy2
+    link.result = (du, dw1, db1)
+    # du goes to the first LN's node as this node's input gradient; that node returns it
+    return du.view(gy.shape), dw2, db2, None, None, None
 
 
 def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):

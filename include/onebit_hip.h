@@ -570,6 +570,22 @@ OB_API int ob_layernorm_bwd_defer(const float* dy, const float* x, const float* 
                                   float p_drop, const uint64_t* rng, int64_t rng_offset,
                                   const int32_t* lens, int64_t T, void* table, int64_t slot,
                                   void* stream);
+/* The backward of two LayerNorms back to back (ob_layernorm_fwd_pair: y1 = LN1(x), y2 =
+ * LN2(y1); gres = the gradient of y1's other (residual) use, may be NULL): dx =
+ * LN1_backward(LN2_backward(dy) + gres), the sum never written to memory; dy2 (may be NULL):
+ * the residual-tail gradient of ob_layernorm_bwd_ex for x; dgamma / dbeta of both layers,
+ * deferred into `table` at slot2 / slot1 (>= 0) or reduced now (table NULL or slot < 0).
+ * ws: ob_layernorm_bwd_pair_workspace(rows, d) bytes, 16-byte aligned. */
+OB_API size_t ob_layernorm_bwd_pair_workspace(int64_t rows, int64_t d);
+OB_API int ob_layernorm_bwd_pair(const float* dy, const float* y1, const float* g2,
+                                 const float* mean2, const float* rstd2, const float* gres,
+                                 const float* x, const float* g1, const float* mean1,
+                                 const float* rstd1, int64_t rows, int64_t d, float* dx,
+                                 float* dg2, float* db2, float* dg1, float* db1, void* ws,
+                                 size_t ws_bytes, float* dy2, float rscale, float p_drop,
+                                 const uint64_t* rng, int64_t rng_offset, const int32_t* lens,
+                                 int64_t T, void* table, int64_t slot2, int64_t slot1,
+                                 void* stream);
 OB_API size_t ob_ln_param_entry_bytes(void);
 OB_API int ob_ln_param_table(const void* table, int64_t n, int64_t dmax, void* stream);
 

@@ -146,3 +146,45 @@ def test_layernorm_pairs_equal_single_launches(gpu, monkeypatch):
     assert res[False].keys() == res[True].keys()
     for k in res[False]:
         assert torch.equal(res[False][k], res[True][k]), k
+
+
+def test_layernorm_pair_backward_matches_separate(gpu, monkeypatch):
+    """The pair's two LN backwards in one launch (ob_layernorm_bwd_pair) vs one launch each:
+    every gradient of the stacked step within 1e-6 of max (the kernels' row arithmetic is the
+    same; hipcc may contract it differently), loss identical (the forward is unchanged)."""
+    from onebit_asr import layernorm
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CFG1, synthetic_batch
+    from onebit_asr.train_step import OneBitStep
+
+    cfg = dict(CFG1, enc_d_model=144, enc_d_ff=576)
+    batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
+    res, losses, used = {}, {}, {}
+    for on in (False, True):
+        monkeypatch.setattr(layernorm, "_PAIR_BWD", on)
+        calls = []
+        orig = layernorm._pair_backward
+
+        def spy(*a, orig=orig, calls=calls):
+            calls.append(1)
+            return orig(*a)
+
+        monkeypatch.setattr(layernorm, "_pair_backward", spy)
+        torch.manual_seed(0)
+        m = ConformerASR(80, 5004, **cfg).to(gpu)
+        step = OneBitStep(m, n_layers=2, stacked=True)
+        loss, _ = step(batch, [1, 0])
+        loss.backward()
+        torch.cuda.synchronize()
+        losses[on] = loss.detach().clone()
+        used[on] = len(calls)
+        res[on] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    assert used[False] == 0 and used[True] >= 1, used
+    assert torch.equal(losses[False], losses[True])
+    assert res[False].keys() == res[True].keys()
+    exact = 0
+    for k in res[False]:
+        a, b = res[True][k], res[False][k]
+        exact += int(torch.equal(a, b))
+        assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-12, k
+    print(f"bit-identical gradients: {exact} / {len(res[False])}")
