@@ -33,6 +33,7 @@ _f64 = ctypes.c_double
 # name -> (restype, argtypes); mirrors include/onebit_hip.h one-to-one.
 SIGNATURES = {
     "ob_abi_version": (_int, []),
+    "ob_source_digest": (ctypes.c_char_p, []),
     "ob_status_string": (ctypes.c_char_p, [_int]),
     "ob_quant_pack": (_int, [_c_f, _c_f, _int, _int, _i64, _i64, _c_f, _c_f, _c_f]),
     "ob_quant_pack_item_blocks": (_i64, [_i64, _i64]),
@@ -230,8 +231,24 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     if lib.ob_abi_version() != ABI_VERSION:
         raise OneBitHipError(f"ABI mismatch: library {lib.ob_abi_version()} != {ABI_VERSION}")
+    check_digest(lib)
     _lib = lib
     return lib
+
+
+def check_digest(lib, expected: str | None = None) -> None:
+    """Refuse a stale build: the library's compiled-in source digest must equal the digest of
+    the sources next to it. Skipped for an explicitly chosen library (ONEBIT_HIP_LIB, e.g. an
+    A/B baseline built from another tree) unless ``expected`` is given."""
+    if expected is None:
+        if os.environ.get("ONEBIT_HIP_LIB"):
+            return
+        expected = source_digest()
+    got = lib.ob_source_digest().decode()
+    if got != expected:
+        raise OneBitHipError(
+            f"{LIB_PATH.name} was built from other sources (digest {got[:12]} != {expected[:12]} "
+            "of csrc/ and include/): rebuild with `make -C cmu-11785-idl-1.58bit-asr_amd/csrc`")
 
 
 def ptr_array(ptrs):
@@ -255,17 +272,11 @@ def ptr(t: "torch.Tensor | None") -> int | None:
 
 def source_digest() -> str:
     """sha256 over the library's sources (csrc/*.hip, csrc/*.h, include/*.h, file names
-    included): identifies the kernel revision a measurement (e.g. PMC traffic) belongs to."""
-    import hashlib
+    included): identifies the kernel revision a build or a measurement (e.g. PMC traffic)
+    belongs to; the library carries the value it was built from (ob_source_digest)."""
+    from ._digest import source_digest as _sd
 
-    pkg = Path(__file__).resolve().parents[1]
-    files = sorted(list((pkg / "csrc").glob("*.hip")) + list((pkg / "csrc").glob("*.h")) +
-                   list((pkg.parent / "include").glob("*.h")))
-    h = hashlib.sha256()
-    for f in files:
-        h.update(f.name.encode())
-        h.update(f.read_bytes())
-    return h.hexdigest()
+    return _sd()
 
 
 def stream_of(t: torch.Tensor) -> int:

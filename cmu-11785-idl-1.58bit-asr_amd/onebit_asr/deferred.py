@@ -21,8 +21,13 @@ A gradient is deferred only when nothing can read it before the flush:
 * the parameter was used by exactly one deferrable op in this scope's forward (several uses
   -- the literal three-pass step -- make autograd add the contributions as they arrive;
   the model ties no weights, so every use of these parameters goes through a counted op).
-The workspaces holding the partials are kept referenced until the flush. ``OB_DEFER=0``
-finishes everything immediately (A/B, debugging).
+* no hook can observe the gradient as it is produced: ``scope(enabled=False)`` for a step
+  module wrapped in DistributedDataParallel (its reducer copies each gradient into a bucket
+  and starts the all-reduce from a hook right after AccumulateGrad, before the flush), and
+  no deferral for a parameter carrying a post-accumulate-grad hook.
+The workspaces holding the partials are kept referenced until the flush. A slot is counted
+only once its producing launch returned OB_OK; a scope left by an exception drops the
+pending entries instead of launching them. ``OB_DEFER=0`` finishes everything immediately.
 """
 from __future__ import annotations
 
@@ -34,7 +39,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "cm_slot", "keep", "active"]
+__all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "ln_done", "cm_slot", "keep",
+           "add_after_flush", "active"]
 
 _ON = os.environ.get("OB_DEFER", "1") != "0"
 _CAP = 512  # table entries per kind
@@ -55,6 +61,7 @@ class _State:
         self.cm_n = 0
         self.cm_nmax = 0
         self.refs: List[torch.Tensor] = []
+        self.post: List[tuple] = []  # (dst, src): dst += src once the tables have run
         self.stream: Optional[int] = None
         self.dev: Optional[int] = None
         self.queued = False
@@ -68,16 +75,22 @@ def active() -> bool:
 
 
 @contextmanager
-def scope():
+def scope(enabled: bool = True):
     """Forward + backward of one training step: deferrable gradients are finished by one
-    launch per kind at the end of the backward."""
+    launch per kind at the end of the backward. ``enabled=False``: everything finishes on the
+    spot (e.g. under DistributedDataParallel, whose hooks read each gradient as it lands)."""
     prev = _S.active
-    _S.active = True
+    _S.active = bool(enabled)
     _S.uses = {}
+    ok = False
     try:
         yield
+        ok = True
     finally:
-        _flush()  # (a no-op when the backward's final callback already ran)
+        if ok:
+            _flush()  # (a no-op when the backward's final callback already ran)
+        else:
+            _S.reset()  # an entry point failed: its slot may hold a stale descriptor
         _S.active = prev
         _S.uses = {}
 
@@ -101,6 +114,8 @@ def can_defer(*params) -> bool:
         # layer's) passes its gradient on through autograd ops that would read it at once
         if (not p.is_leaf or not p.is_cuda or p.grad is not None
                 or _S.uses.get(id(p), 0) != 1):
+            return False
+        if getattr(p, "_post_accumulate_grad_hooks", None):  # a hook reads it on arrival
             return False
     return True
 
@@ -143,15 +158,19 @@ def dw_done(n: int, blocks: int) -> None:
         _S.dw_blocks += blocks
 
 
-def ln_slot(dev: torch.device, stream: int, d: int):
-    if _S.ln_n + 1 > _CAP:
+def ln_slot(dev: torch.device, stream: int, d: int, n: int = 1):
+    """(table pointer, first slot) for n LayerNorm parameter entries, or None when the table
+    is full; the caller reports the slots with ln_done once the producing launch succeeded."""
+    if _S.ln_n + n > _CAP:
         return None
     _begin(dev, stream)
     _, (_, ln, _) = _tables(dev)
-    slot = _S.ln_n
-    _S.ln_n += 1
+    return ln.data_ptr(), _S.ln_n
+
+
+def ln_done(n: int, d: int) -> None:
+    _S.ln_n += n
     _S.ln_dmax = max(_S.ln_dmax, d)
-    return ln.data_ptr(), slot
 
 
 def cm_slot(dev: torch.device, stream: int):
@@ -194,6 +213,15 @@ def keep(*tensors) -> None:
     _S.refs.extend(t for t in tensors if t is not None)
 
 
+def add_after_flush(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """dst += src on the flush stream right after the table launches (a correction to a
+    gradient the tables are still to write); immediately when nothing is pending."""
+    if _S.stream is None:
+        dst.add_(src)
+    else:
+        _S.post.append((dst, src))
+
+
 def _flush() -> None:
     if _S.stream is None:
         _S.reset()
@@ -209,4 +237,9 @@ def _flush() -> None:
     if _S.cm_n:
         _lib.check(lib.ob_cm_wgrad_table(cm.data_ptr(), _S.cm_n, _S.cm_nmax, _S.stream),
                    "ob_cm_wgrad_table")
+    if _S.post:
+        dev = torch.device("cuda", _S.dev)
+        with torch.cuda.stream(torch.cuda.ExternalStream(_S.stream, device=dev)):
+            for dst, src in _S.post:
+                dst.add_(src)
     _S.reset()

@@ -54,7 +54,8 @@ def attach_grad_scale(out: torch.Tensor, spec: GradScale) -> torch.Tensor:
 def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, wsb, spec, stream,
               params=()):
     slot = None
-    if rows > 0 and (dw is not None or db is not None) and deferred.can_defer(*params):
+    if (rows > 0 and params and (dw is not None or db is not None)
+            and deferred.can_defer(*params)):
         # dgamma / dbeta reduced at the end of the backward with every other LN's (deferred.py)
         slot = deferred.ln_slot(x2.device, stream, d)
     if slot is not None:
@@ -68,6 +69,8 @@ def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, ws
             spec.off if spec is not None else 0,
             _lib.ptr(spec.lens) if spec is not None else None, spec.T if spec is not None else 0,
             slot[0], slot[1], stream)
+        if st == _lib.OB_OK:
+            deferred.ln_done(1, d)
         if spec is not None:
             spec.dx_ptr, spec.dy2 = dx.data_ptr(), dy2
         return st
@@ -152,9 +155,11 @@ class _LayerNormFn(torch.autograd.Function):
             du, dw, db = link.result
             link.result = None
             if gy.data_ptr() != du.data_ptr():
-                # the output had a consumer besides the next LN: the pair backward is invalid
-                raise RuntimeError("LayerNorm pair backward: the first LN's output has another "
-                                   "consumer; run with OB_LN_PAIR_BWD=0")
+                # the output had a consumer besides the next LN: autograd summed that
+                # consumer's gradient into du (gy = du + g_other). The LN backward is linear
+                # in its output gradient, so the pair's result is completed with the LN
+                # backward of g_other (to the rounding of the subtraction).
+                return _pair_correction(ctx, gy, du, dw, db)
             return du.view(gy.shape), dw, db, None, None, None, None
         x2, weight, mean, rstd = ctx.saved_tensors
         rows, d = x2.shape
@@ -325,15 +330,18 @@ def _pair_backward(ctx, link, gy, gres):
     wsb = lib.ob_layernorm_bwd_pair_workspace(rows, d)
     ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=u.device)
     table, s2, s1 = None, -1, -1
-    if rows > 0 and (dw2 is not None or db2 is not None) and deferred.can_defer(*ctx.params):
-        t = deferred.ln_slot(u.device, stream, d)
+    d2 = rows > 0 and (dw2 is not None or db2 is not None) and deferred.can_defer(*ctx.params)
+    d1 = rows > 0 and (dw1 is not None or db1 is not None) and deferred.can_defer(w1, b1)
+    n_def = int(d2) + int(d1)
+    if n_def:
+        t = deferred.ln_slot(u.device, stream, d, n_def)
         if t is not None:
-            table, s2 = t
-    if rows > 0 and (dw1 is not None or db1 is not None) and deferred.can_defer(w1, b1):
-        t = deferred.ln_slot(u.device, stream, d)
-        if t is not None:
-            table, s1 = t
-    if s2 >= 0 or s1 >= 0:
+            table = t[0]
+            s2 = t[1] if d2 else -1
+            s1 = t[1] + int(d2) if d1 else -1
+        else:
+            n_def = 0
+    if n_def:
         deferred.keep(ws)
     spec = link.spec
     dy2 = torch.empty_like(du) if spec is not None else None
@@ -345,11 +353,38 @@ def _pair_backward(ctx, link, gy, gres):
         spec.p if spec is not None else 0.0, _lib.ptr(spec.rng) if spec is not None else None,
         spec.off if spec is not None else 0, _lib.ptr(spec.lens) if spec is not None else None,
         spec.T if spec is not None else 0, table, s2, s1, stream), "ob_layernorm_bwd_pair")
+    if n_def:
+        deferred.ln_done(n_def, d)
     if spec is not None:
         spec.dx_ptr, spec.dy2 = du.data_ptr(), dy2
     link.result = (du, dw1, db1)
     # du goes to the first LN's node as this node's input gradient; that node returns it
     return du.view(gy.shape), dw2, db2, None, None, None
+
+
+def _pair_correction(ctx, gy, du, dw1, db1):
+    """The first LN of a pair whose output had another consumer: du, dw1, db1 are its
+    backward for the pair consumer's gradient only; add the LN backward of the rest
+    (g_other = gy - du) -- dgamma / dbeta after the deferred tables have written theirs."""
+    x2, weight, mean, rstd = ctx.saved_tensors
+    rows, d = x2.shape
+    g_other = (gy.reshape(rows, d) - du.view(rows, d)).contiguous()
+    dx = torch.empty_like(x2)
+    dw = torch.empty((d,), dtype=torch.float32, device=x2.device) if dw1 is not None else None
+    db = torch.empty((d,), dtype=torch.float32, device=x2.device) if db1 is not None else None
+    lib = _lib.load()
+    wsb = lib.ob_layernorm_bwd_workspace(rows, d)
+    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=x2.device)
+    _lib.check(lib.ob_layernorm_bwd_res(g_other.data_ptr(), x2.data_ptr(), _lib.ptr(weight),
+                                        mean.data_ptr(), rstd.data_ptr(), rows, d,
+                                        du.data_ptr(), dx.data_ptr(), _lib.ptr(dw), _lib.ptr(db),
+                                        ws.data_ptr(), wsb, _lib.stream_of(g_other)),
+               "ob_layernorm_bwd_res")
+    if dw is not None:
+        deferred.add_after_flush(dw1, dw)
+    if db is not None:
+        deferred.add_after_flush(db1, db)
+    return dx.view(gy.shape), dw1, db1, None, None, None, None
 
 
 def layer_norm_fork(x: torch.Tensor, weight, bias, eps: float = 1e-5):

@@ -235,7 +235,10 @@ def train_step(step_module: nn.Module, optimizer: torch.optim.Optimizer,
     """train.py:114-120: zero_grad, backward, clip_grad_norm_(5.0), step, sched.step().
     Returns the (device) loss and loss parts; nothing here synchronises with the host."""
     optimizer.zero_grad(set_to_none=True)
-    with deferred.scope():  # gradient finishes batched at the end of the backward
+    # gradient finishes batched at the end of the backward -- except under DDP, whose reducer
+    # hooks copy each gradient into its bucket (and start the all-reduce) as it lands
+    ddp = isinstance(step_module, torch.nn.parallel.DistributedDataParallel)
+    with deferred.scope(enabled=not ddp):
         loss, parts = step_module(batch, sp_mask)
         loss.backward()
     params = [p for p in step_module.parameters() if p.grad is not None]

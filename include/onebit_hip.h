@@ -61,6 +61,10 @@ enum {
 
 /* ABI version (bumped on any signature change). */
 OB_API int ob_abi_version(void);
+/* sha256 (hex) of the sources the library was built from (the .hip / .h files of csrc/ and
+ * the headers of include/; onebit_asr/_digest.py), generated at build time: the host side refuses a
+ * library whose digest differs from the sources beside it. */
+OB_API const char* ob_source_digest(void);
 /* Static string for a status code. */
 OB_API const char* ob_status_string(int status);
 

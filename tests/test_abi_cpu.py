@@ -101,3 +101,26 @@ def test_i8_entry_validation_without_gpu():
     assert lib.ob_act_absmax(fake, 1, 18, fake, fake, 1 << 20, None) == -5
     assert lib.ob_act_absmax(fake, 1, 16, fake, fake, 4, None) == -4
     assert lib.ob_act_dequant_i8(fake, 1, 16, None, fake, None) == -1
+
+
+def test_library_digest_matches_sources_and_stale_build_is_refused(monkeypatch):
+    """The library carries the digest of the sources it was built from (ob_source_digest);
+    load() refuses one that differs from the sources beside it (a stale .so)."""
+    import subprocess
+    import sys
+
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    assert lib.ob_source_digest().decode() == _lib.source_digest()
+    # the Makefile's generator (torch-free script) agrees with the host-side digest
+    script = ROOT / "cmu-11785-idl-1.58bit-asr_amd" / "onebit_asr" / "_digest.py"
+    out = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == _lib.source_digest()
+    monkeypatch.delenv("ONEBIT_HIP_LIB", raising=False)
+    with pytest.raises(_lib.OneBitHipError, match="built from other sources"):
+        _lib.check_digest(lib, expected="0" * 64)
+    monkeypatch.setattr(_lib, "source_digest", lambda: "f" * 64)
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.OneBitHipError, match="rebuild"):
+        _lib.load()

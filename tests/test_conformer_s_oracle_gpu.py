@@ -1,10 +1,15 @@
 """Conformer-S (BASELINE configs[1] architecture) against the CPU oracle, not against itself.
 
 Full model: 16 blocks, d_model 144, 4 heads (d_head 36), d_ff 576, conv kernel 31, the 2-layer
-decoder, V = 5004, dropout 0. Batch: 4 utterances x 1000 frames (T' = 249), 40 tokens each --
-the S kernel paths (ternary GEMM K = 576 tiles, attention at d_head 36 / T' 249, dW at
-144-wide tiles, conv module at C = 144, subsampling at C = 144) that the cfg1 test
-(tests/test_model_gpu.py) never takes.
+decoder, V = 5004, dropout 0. Batches of 4 utterances padded to 1000 frames (T' = 249) -- the S
+kernel paths (ternary GEMM K = 576 tiles, attention at d_head 36 / T' 249, dW at 144-wide
+tiles, conv module at C = 144, subsampling at C = 144) that the cfg1 test
+(tests/test_model_gpu.py) never takes:
+  * ``full``: every utterance 1000 frames, 40 tokens (enc_lens 250 > T' = 249: nothing padded);
+  * ``ragged``: feat_lens [1000, 873, 612, 401] (enc_lens 250, 218, 153, 100), tokens
+    [40, 33, 25, 12]: key-padding masks and fully masked query rows of the attention
+    (conformer.py:121-127), pad-zeroed residual tails (:134-137), BatchNorm statistics over
+    padded frames (:148) and the CTC input lengths (train.py:87) at S tile sizes.
 
 Bars (the cfg1 bars of tests/test_model_gpu.py):
   * forward at precision 2, precision 1 and an SP mask: CTC logits max|err| <= 1e-3, the
@@ -50,11 +55,18 @@ def s_pair(gpu):
     return prod, orc
 
 
-@pytest.fixture(scope="module")
-def s_batch():
+BATCHES = {
+    "full": ([1000] * 4, [40] * 4),
+    "ragged": ([1000, 873, 612, 401], [40, 33, 25, 12]),
+}
+
+
+@pytest.fixture(scope="module", params=sorted(BATCHES))
+def s_batch(request):
     from onebit_asr.data import synthetic_batch
 
-    return synthetic_batch([1000] * 4, [40] * 4, seed=77)
+    feat_lens, token_lens = BATCHES[request.param]
+    return synthetic_batch(feat_lens, token_lens, seed=77)
 
 
 def _to(b, dev):
