@@ -10,7 +10,7 @@ using namespace ob;
 
 namespace {
 
-constexpr int kAbiVersion = 1;
+constexpr int kAbiVersion = 2;
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -1296,14 +1296,20 @@ int relattn_check(int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float 
 int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                    const float* u, const float* vb, const int32_t* lens, int64_t Bt, int64_t P,
                    int64_t T, int64_t H, int64_t d, float p_drop, const int64_t* rng,
-                   int64_t rng_offset, float* probs, float* ctx, void* stream) {
+                   int64_t rng_offset, float* saved, float* probs, float* ctx, void* stream) {
   if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
   if (!q || !k || !v || !pos || !u || !vb || !lens || !ctx || (p_drop > 0.0f && !rng))
     return OB_ERR_NULL;
+  if (((uintptr_t)saved & 15) || ((uintptr_t)probs & 15)) return OB_ERR_ALIGN;
   launch_relattn_fwd(q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop,
-                     reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset, probs, ctx,
-                     as_stream(stream));
+                     reinterpret_cast<const uint64_t*>(rng), (uint64_t)rng_offset, saved, probs,
+                     ctx, as_stream(stream));
   return launched();
+}
+
+int64_t ob_relattn_saved_elems(int64_t Bt, int64_t T, int64_t H, int64_t d) {
+  if (Bt < 1 || H < 1 || !relattn_supported(T, d)) return 0;
+  return relattn_saved_elems(Bt, T, H, d);
 }
 
 size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
@@ -1319,18 +1325,19 @@ int64_t ob_relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
 int ob_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
                    const float* v, const float* pos, const float* u, const float* vb,
                    const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d,
-                   float p_drop, const int64_t* rng, int64_t rng_offset, const float* probs,
+                   float p_drop, const int64_t* rng, int64_t rng_offset, const float* saved,
                    float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
                    size_t ws_bytes, void* stream) {
   if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
-  if (!dctx || !ctx || !q || !k || !v || !pos || !u || !vb || !lens || !probs || !dq || !dk ||
+  if (!dctx || !ctx || !q || !k || !v || !pos || !u || !vb || !lens || !saved || !dq || !dk ||
       !dv || !dpos || !du || !dvb || !ws)
     return OB_ERR_NULL;
-  (void)rng;  // the forward's keep bits ride in probs' sign bits
+  (void)rng;  // the forward's keep decisions are in the saved state
   (void)rng_offset;
+  if ((uintptr_t)saved & 15) return OB_ERR_ALIGN;
   if (ws_bytes < ob_relattn_bwd_workspace(Bt, T, H, d)) return OB_ERR_WORKSPACE;
-  launch_relattn_bwd(dctx, ctx, q, k, v, pos, u, vb, Bt, P, T, H, d, p_drop, probs, dq, dk, dv,
-                     dpos, du, dvb, ws, as_stream(stream));
+  launch_relattn_bwd(dctx, ctx, q, k, v, pos, u, vb, lens, Bt, P, T, H, d, p_drop, saved, dq, dk,
+                     dv, dpos, du, dvb, ws, as_stream(stream));
   return launched();
 }
 

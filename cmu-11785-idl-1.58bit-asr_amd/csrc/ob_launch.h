@@ -405,15 +405,16 @@ void launch_embed_bwd(const int64_t* idx, int64_t N, const float* g, int64_t C, 
 bool relattn_supported(int64_t T, int64_t d);
 size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
 int64_t relattn_probs_elems(int64_t Bt, int64_t T, int64_t H);
+int64_t relattn_saved_elems(int64_t Bt, int64_t T, int64_t H, int64_t d);
 void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                         const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
                         int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
-                        uint64_t rng_off, float* probs, float* ctx, hipStream_t s);
+                        uint64_t rng_off, float* saved, float* probs, float* ctx, hipStream_t s);
 void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
                         const float* v, const float* pos, const float* u, const float* vb,
-                        int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                        const float* probs, float* dq, float* dk, float* dv, float* dpos,
-                        float* du, float* dvb, void* ws, hipStream_t s);
+                        const int* lens, int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d,
+                        float p_drop, const float* saved, float* dq, float* dk, float* dv,
+                        float* dpos, float* du, float* dvb, void* ws, hipStream_t s);
 void launch_relattn_dropout_mask(int64_t n, int64_t T, float p_drop, const uint64_t* rng,
                                  uint64_t rng_off, uint8_t* out, hipStream_t s);
 

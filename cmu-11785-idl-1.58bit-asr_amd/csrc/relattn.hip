@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     const float* __restrict__ pos, const float* __restrict__ u, const float* __restrict__ vbias,
     const int* __restrict__ lens, int Bp, int T, int H, float inv_sqrt_d, DropCfg dc,
     const uint64_t* __restrict__ rng, uint64_t rng_off, float* __restrict__ probs,
-    float* __restrict__ ctx) {
+    float* __restrict__ stats, uint32_t* __restrict__ kbits, float* __restrict__ ctx) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   extern __shared__ float img[];
@@ -244,9 +244,16 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     for (int m = threadIdx.x; m < T; m += kThreads) {
       float pr[D];
       load_run<D>(pb + (size_t)m * C, pr);
+      // the MFMA's k order (step s, then k = g: column g*DQ + s), so this row is bitwise the
+      // one an MFMA tile would produce (the fused backward recomputes it that way)
       float a = 0.0f;
 #pragma unroll
-      for (int c = 0; c < D; ++c) a = fmaf(qe[c] + vbb[c], pr[c], a);
+      for (int s = 0; s < DQ; ++s)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int c = gg * DQ + s;
+          a = fmaf(qe[c] + vbb[c], pr[c], a);
+        }
       img[kTile * ldi + 1 + m] = a;
     }
     if (threadIdx.x == 0) img[kTile * ldi] = 0.0f;
@@ -300,7 +307,15 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
   const float rsum = row_live ? 1.0f / sum : 0.0f;
+  const int Tp = 16 * nt;  // rows / keys of the saved state
+  if (stats && g == 0 && qi < Tp) {
+    stats[2 * ((size_t)bh * Tp + qi)] = mxs;
+    stats[2 * ((size_t)bh * Tp + qi) + 1] = rsum;
+  }
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
+  uint32_t kw[(NTT + 1) / 2];  // keep bits of keys 32wd .. 32wd + 31 (this lane's share)
+#pragma unroll
+  for (int wd = 0; wd < (NTT + 1) / 2; ++wd) kw[wd] = 0u;
   const uint64_t didx = drop_row_base(bh, T, qi) + 4 * g;  // + 16t
   // this wave's row tile of probs (waves past the last row tile -- T not a multiple of
   // 64 -- store nothing)
@@ -311,6 +326,9 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     if (t >= nt) continue;
     bool keep[4] = {true, true, true, true};
     if (dc.on) keep4(dkey, didx + 16 * t, dc, keep);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      kw[t >> 1] |= (keep[j] ? 1u : 0u) << (16 * (t & 1) + 4 * g + j);
     f32x4 st;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -321,6 +339,16 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       sreg[t][j] = dc.on ? (keep[j] ? pr * dc.scale : 0.0f) : pr;
     }
     if (pf) *reinterpret_cast<f32x4*>(pf + 256 * t) = st;
+  }
+  if (kbits && dc.on) {
+    const int W = (nt + 1) >> 1;
+#pragma unroll
+    for (int wd = 0; wd < (NTT + 1) / 2; ++wd) {
+      uint32_t x = kw[wd];
+      x |= __shfl_xor(x, 16);
+      x |= __shfl_xor(x, 32);
+      if (wd < W && g == 0 && qi < Tp) kbits[((size_t)bh * Tp + qi) * W + wd] = x;
+    }
   }
 
   // ctx = A v: A = the lane's probabilities (row r, k = 4g+j of tile t), B = v rows.
@@ -812,6 +840,477 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Backward, flash style (T <= 256): ONE block per (batch row, head) walks the query rows in
+// chunks of 32 and recomputes each chunk's probabilities from the forward's row statistics
+// (max, 1/sum) and keep bits -- no [T][T] tensor is read or written in HBM. Per chunk:
+//   X  = (q+v) pos^T rows (the rel_shift source, LDS image at pitch T+1) and
+//   S  = (q+u) k^T + bd, P = exp(S/sqrt(d) - max) / sum   (bitwise the forward's P: same
+//        MFMA k order, same VALU expressions),
+//   dP = dO v^T, dS' = P (dP keep scale - dO.ctx) / sqrt(d), Pd = P keep scale,
+// in the "key on the lane" orientation D[query][key]: lane (key r, queries 4g+e of two
+// 16-query tiles) holds 8 queries of one key, which is exactly the A fragment (permuted k
+// order) of the key-side products
+//   dK += dS'^T (q+u),  dV += Pd^T dO          (bf16x6 on 16x16x32 MFMA, accumulated over
+//                                              the chunks in registers: exact fp32 products)
+// and dS' goes to an LDS band (pitch T, the previous chunk's last row kept as row 0) for
+//   dpos += dX^T (q+v)  (dX = the rel_shift adjoint, read flat from the band; bf16x6)
+//   dq    = dS' k + dX pos   (fp32 16x16x4 MFMA, one 16x16 tile per job; K = all keys)
+// Wave w owns key tiles / position tiles w*KPW .. w*KPW+KPW-1; the dq tiles are 4*CT jobs
+// dealt round-robin (waves w and w+4 share a SIMD: 3 jobs per SIMD at CT = 3, NW = 8).
+// du / dvb: per-(b, h) column sums of the dq parts (relattn_reduce_kernel, nqt = 1).
+// ------------------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_bf(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// x = hi + mid + lo exactly (each part the bf16 rounding of what is left)
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8_t (&p)[3]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 h, m, l;
+    split3(x[j], h, m, l);
+    p[0][j] = h;
+    p[1][j] = m;
+    p[2][j] = l;
+  }
+}
+
+// the six products of weight >= 2^-16 (smallest first), as dw.hip's bf16x6 GEMM
+__device__ __forceinline__ f32x4 mfma_x6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4 c) {
+  c = mfma_bf(a[1], b[1], c);
+  c = mfma_bf(a[2], b[0], c);
+  c = mfma_bf(a[0], b[2], c);
+  c = mfma_bf(a[1], b[0], c);
+  c = mfma_bf(a[0], b[1], c);
+  return mfma_bf(a[0], b[0], c);
+}
+
+constexpr int kFQ = 32;        // query rows per chunk
+constexpr int kPlanePitch = 40;  // bf16 per column row of a B plane (80 B: 16-B aligned rows)
+
+// acc[ct] += A^T B for one key tile: A = the lane's 8 queries of its key (fp32, split here),
+// B = the chunk's plane (3 parts, [col][query], part stride 16 CT * kPlanePitch) read in the
+// same k order: queries 4g..4g+3, then 16+4g..16+4g+3
+template <int CT>
+__device__ __forceinline__ void key_side(const float (&a8)[8], const __bf16* pl, int g, int r,
+                                         f32x4 (&acc)[CT]) {
+  bf16x8_t a[3];
+  split8(a8, a);
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    bf16x8_t bb[3];
+#pragma unroll
+    for (int pp = 0; pp < 3; ++pp) {
+      const __bf16* pu = pl + (size_t)pp * 16 * CT * kPlanePitch + (16 * ct + r) * kPlanePitch + 4 * g;
+      const bf16x4_t u0 = *(const bf16x4_t*)pu, u1 = *(const bf16x4_t*)(pu + 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bb[pp][j] = u0[j];
+        bb[pp][4 + j] = u1[j];
+      }
+    }
+    acc[ct] = mfma_x6(a, bb, acc[ct]);
+  }
+}
+
+struct FusedLds {  // float offsets into the dynamic LDS of relattn_bwd_fused_kernel
+  int kimg, reg, qu, qv, dO, planes, stats, delta, kb, comb, sums, total;
+  __host__ __device__ FusedLds(int T, int D, int CT, int nch, int W) {
+    const int Tp16 = 16 * ((T + 15) / 16);
+    const int ap = D + 1;                      // A-image pitch (odd: fewer conflicts)
+    kimg = 0;                                  // k rows [Tp][16 CT] (zero pad)
+    reg = kimg + Tp16 * 16 * CT;               // prev row [T] + X image / dS' band
+    qu = reg + T + 33 * (T + 1);               // (q+u) rows [32][ap]
+    qv = qu + kFQ * ap;                        // (q+v) rows [33][ap]
+    dO = qv + (kFQ + 1) * ap;                  // dO rows [32][ap]
+    planes = dO + kFQ * ap;                    // bf16 [3 tensors][3 parts][16 CT][40]
+    planes = (planes + 3) & ~3;                // 16-B aligned
+    stats = planes + (9 * 16 * CT * kPlanePitch) / 2;
+    delta = stats + 2 * kFQ * nch;             // [32]
+    kb = delta + kFQ;                          // keep bits [32][W]
+    comb = kb + kFQ * W;                       // dq parts [2 which][2 a][CT][256]
+    sums = comb + 2 * 2 * CT * 256;            // column sums [2 which][2 a][16 CT]
+    total = sums + 4 * 16 * CT;
+  }
+};
+
+template <int DQ, int NW>
+__global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
+    const float* __restrict__ dctx, const float* __restrict__ ctxo, const float* __restrict__ q,
+    const float* __restrict__ k, const float* __restrict__ v, const float* __restrict__ pos,
+    const float* __restrict__ u, const float* __restrict__ vbias, const int* __restrict__ lens,
+    const float* __restrict__ stats, const uint32_t* __restrict__ kbits, int Bp, int T, int H,
+    float inv_sqrt_d, DropCfg dc, float* __restrict__ dq, float* __restrict__ dk,
+    float* __restrict__ dv, float* __restrict__ dp_part, float* __restrict__ du_part,
+    float* __restrict__ dvb_part) {
+  constexpr int D = 4 * DQ;
+  constexpr int CT = (D + 15) / 16;
+  constexpr int DP = 16 * CT;           // padded columns
+  constexpr int KPW = 16 / NW;          // key / position tiles per wave
+  constexpr int NTH = 64 * NW;
+  constexpr int NJ = 4 * CT;            // dq jobs (which, a, ct)
+  extern __shared__ float lds[];
+  const int nt = (T + 15) >> 4;
+  const int Tp = 16 * nt;
+  const int W = (nt + 1) >> 1;
+  const int nch = (Tp + kFQ - 1) / kFQ;
+  const FusedLds off(T, D, CT, nch, W);
+  float* kimg = lds + off.kimg;
+  float* R = lds + off.reg;
+  float* qu_a = lds + off.qu;
+  float* qv_a = lds + off.qv;
+  float* do_a = lds + off.dO;
+  __bf16* planes = reinterpret_cast<__bf16*>(lds + off.planes);
+  float* st_s = lds + off.stats;
+  float* delta_s = lds + off.delta;
+  uint32_t* kb_s = reinterpret_cast<uint32_t*>(lds + off.kb);
+  float* comb = lds + off.comb;
+  float* sums = lds + off.sums;
+  constexpr int AP = D + 1;
+  // B plane (tensor z: 0 = q+u, 1 = q+v, 2 = dO; part p): [col][query] bf16
+  auto plane = [&](int z, int p) { return planes + (size_t)(3 * z + p) * DP * kPlanePitch; };
+
+  const int L0 = xcd_logical((int)blockIdx.x, (int)gridDim.x);
+  const int h = L0 % H, b = L0 / H;
+  const int bh = b * H + h;
+  const int pass = b / Bp;
+  const int C = H * D;
+  const int L = min(lens[b], T);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const size_t bo = (size_t)b * T * C + h * D;
+  const float* qb = q + bo;
+  const float* kb = k + bo;
+  const float* vb = v + bo;
+  const float* dob = dctx + bo;
+  const float* cob = ctxo + bo;
+  const float* pb = pos + (size_t)pass * T * C + h * D;
+  const float* ub = u + h * D;
+  const float* vbb = vbias + h * D;
+  const __amdgpu_buffer_rsrc_t rs_p = slice_rsrc(pb, T, C, D);
+
+  // ---- block setup: k image, statistics, this wave's k / v / pos rows (B operands)
+  for (int e = threadIdx.x; e < Tp * CT * 4; e += NTH) {
+    const int row = e / (CT * 4), c4 = 4 * (e - row * (CT * 4));
+    f32x4 x4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (row < T && c4 < D) x4 = *(const f32x4u*)(kb + (size_t)row * C + c4);
+    *(f32x4*)(kimg + row * DP + c4) = x4;
+  }
+  for (int e = threadIdx.x; e < kFQ * nch; e += NTH) {
+    const bool in = e < Tp;
+    st_s[2 * e] = in ? stats[2 * ((size_t)bh * Tp + e)] : 0.0f;
+    st_s[2 * e + 1] = in ? stats[2 * ((size_t)bh * Tp + e) + 1] : 0.0f;
+  }
+  for (int e = threadIdx.x; e < T; e += NTH) R[e] = 0.0f;  // band row "query -1"
+  // this wave's v / pos rows (B operands of dP and X): re-read per chunk (L2-resident) so they
+  // are not live across the whole block; k rows come from the k image
+  auto load_rows = [&](const float* base, int i, float (&dst)[DQ]) {
+    const int row = 16 * (w * KPW + i) + r;
+    if (row < T) {
+      load_run<DQ>(base + (size_t)row * C + g * DQ, dst);
+    } else {
+#pragma unroll
+      for (int s = 0; s < DQ; ++s) dst[s] = 0.0f;
+    }
+  };
+  f32x4 acc_k[KPW][CT], acc_v[KPW][CT], acc_p[KPW][CT];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc_k[i][ct] = acc_v[i][ct] = acc_p[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float csum[(NJ + NW - 1) / NW];
+#pragma unroll
+  for (int jj = 0; jj < (NJ + NW - 1) / NW; ++jj) csum[jj] = 0.0f;
+
+  for (int c = 0; c < nch; ++c) {
+    const int i0 = kFQ * c;
+    __syncthreads();  // the previous chunk's band / image / plane reads are done
+    // ---- phase 0a: finish the previous chunk's dq; stage this chunk's rows
+    if (c > 0) {
+      const int ip = i0 - kFQ;
+      for (int e = threadIdx.x; e < kFQ * D; e += NTH) {
+        const int x = e / D, col = e - x * D;
+        const int a = x >> 4, xr = x & 15, ct = col >> 4, cr = col & 15;
+        if (ip + x < T) {
+          const int ci = ((a * CT + ct) * 16 + xr) * 16 + cr;
+          dq[bo + (size_t)(ip + x) * C + col] = comb[ci] + comb[2 * CT * 256 + ci];
+        }
+      }
+    }
+    for (int e = threadIdx.x; e < T; e += NTH) R[e] = c > 0 ? R[32 * T + e] : 0.0f;
+    {
+      constexpr int nq = kFQ * DQ;  // float4s of 32 rows
+      for (int e = threadIdx.x; e < 2 * nq + DQ; e += NTH) {
+        // [0, nq): q rows 0..31 (+u and +v); [nq, 2nq): dO rows; then q row 32 (+v only)
+        const int kind = e < nq ? 0 : (e < 2 * nq ? 1 : 2);
+        const int rem = e - kind * nq;
+        const int x = kind == 2 ? kFQ : rem / DQ;
+        const int c4 = 4 * (kind == 2 ? rem : rem - x * DQ);
+        const int qi = i0 + x;
+        f32x4 v4 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (qi < T) v4 = *(const f32x4u*)((kind == 1 ? dob : qb) + (size_t)qi * C + c4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (kind == 1) {
+            do_a[x * AP + c4 + j] = v4[j];
+          } else {
+            if (kind == 0) qu_a[x * AP + c4 + j] = qi < T ? v4[j] + ub[c4 + j] : 0.0f;
+            qv_a[x * AP + c4 + j] = qi < T ? v4[j] + vbb[c4 + j] : 0.0f;
+          }
+        }
+      }
+    }
+    if (threadIdx.x < kFQ) {  // delta = dO . ctx (the softmax backward's row term)
+      const int qi = i0 + threadIdx.x;
+      float a = 0.0f;
+      if (qi < T) {
+        const float* dr = dob + (size_t)qi * C;
+        const float* cr = cob + (size_t)qi * C;
+#pragma unroll
+        for (int cc = 0; cc < D; ++cc) a = fmaf(dr[cc], cr[cc], a);
+      }
+      delta_s[threadIdx.x] = a;
+    }
+    if (dc.on)
+      for (int e = threadIdx.x; e < kFQ * W; e += NTH) {
+        const int x = e / W;
+        kb_s[e] = i0 + x < Tp ? kbits[((size_t)bh * Tp + i0) * W + e] : 0u;
+      }
+    __syncthreads();
+    // ---- phase 0b: B planes (split once) ; phase 1: X tiles and the row-32 X on the VALU
+    for (int e = threadIdx.x; e < 3 * DP * (kFQ / 4); e += NTH) {
+      const int z = e / (DP * (kFQ / 4));
+      const int rem = e - z * DP * (kFQ / 4);
+      const int col = rem / (kFQ / 4), x0 = 4 * (rem - col * (kFQ / 4));
+      const float* src = z == 0 ? qu_a : (z == 1 ? qv_a : do_a);
+      bf16x4_t hp, mp, lp;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = col < D ? src[(x0 + j) * AP + col] : 0.0f;
+        __bf16 hh, mm, ll;
+        split3(x, hh, mm, ll);
+        hp[j] = hh;
+        mp[j] = mm;
+        lp[j] = ll;
+      }
+      *(bf16x4_t*)(plane(z, 0) + col * kPlanePitch + x0) = hp;
+      *(bf16x4_t*)(plane(z, 1) + col * kPlanePitch + x0) = mp;
+      *(bf16x4_t*)(plane(z, 2) + col * kPlanePitch + x0) = lp;
+    }
+    float* xim = R + T;  // X image: row x (query i0 + x) at pitch T+1, column 0 = 0
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) {
+      const int pt = w * KPW + i;
+      if (pt >= nt) continue;
+      float preg[DQ];
+      load_rows(pb, i, preg);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < DQ; ++s)
+          acc = mfma4(qv_a[(16 * a + r) * AP + g * DQ + s], preg[s], acc);
+        const int m = 16 * pt + r;
+        if (m < T)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xim[(16 * a + 4 * g + e) * (T + 1) + 1 + m] = acc[e];
+      }
+    }
+    for (int m = threadIdx.x; m < T; m += NTH) {  // row 32 (query i0 + 32), MFMA k order
+      float pr[D];
+      load_run<D>(pb + (size_t)m * C, pr);
+      float a = 0.0f;
+#pragma unroll
+      for (int s = 0; s < DQ; ++s)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) a = fmaf(qv_a[kFQ * AP + gg * DQ + s], pr[gg * DQ + s], a);
+      xim[kFQ * (T + 1) + 1 + m] = a;
+    }
+    if (threadIdx.x <= kFQ) xim[threadIdx.x * (T + 1)] = 0.0f;
+    __syncthreads();
+    // ---- phase 2: S, P, dP, dS' for this wave's key tiles; key-side products
+    float dsv[KPW][8];
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) {
+      const int kt = w * KPW + i;
+      float pdv[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) dsv[i][jj] = pdv[jj] = 0.0f;
+      if (kt < nt) {
+        const int key = 16 * kt + r;
+        float vreg[DQ];
+        load_rows(vb, i, vreg);
+        const float* krow = kimg + key * DP + g * DQ;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          f32x4 sa = f32x4{0.f, 0.f, 0.f, 0.f}, sd = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < DQ; ++s) sa = mfma4(qu_a[(16 * a + r) * AP + g * DQ + s], krow[s], sa);
+#pragma unroll
+          for (int s = 0; s < DQ; ++s) sd = mfma4(do_a[(16 * a + r) * AP + g * DQ + s], vreg[s], sd);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int x = 16 * a + 4 * g + e, qi = i0 + x;
+            const int Lq = qi < L ? L : 0;
+            // bd[qi][key] = X.flat[T + qi*T + key] of the padded image (rel_shift, :97-103)
+            const float bd = xim[T + x * T + key - i0];
+            float sc = (sa[e] + bd) * inv_sqrt_d;
+            sc = key < Lq ? sc : -INFINITY;
+            const float p = __expf(sc - st_s[2 * x + 2 * i0]) * st_s[2 * x + 2 * i0 + 1];
+            float ks = 1.0f;
+            if (dc.on) ks = (kb_s[x * W + (key >> 5)] >> (key & 31)) & 1u ? dc.scale : 0.0f;
+            const float dpd = sd[e] * ks;
+            dsv[i][4 * a + e] = (p * (dpd - delta_s[x])) * inv_sqrt_d;
+            pdv[4 * a + e] = dc.on ? p * ks : p;
+          }
+        }
+        // dK += dS'^T (q+u), dV += Pd^T dO: A = this lane's 8 queries of key r (k order
+        // 4g..4g+3, 16+4g..16+4g+3), B = the planes read in the same order
+        key_side<CT>(dsv[i], plane(0, 0), g, r, acc_k[i]);
+        key_side<CT>(pdv, plane(2, 0), g, r, acc_v[i]);
+      }
+    }
+    __syncthreads();  // every X-image read is done: the band may overwrite it
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) {
+      const int key = 16 * (w * KPW + i) + r;
+      if (key < T)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int x = 16 * (jj >> 2) + 4 * g + (jj & 3);
+          R[(x + 1) * T + key] = dsv[i][jj];
+        }
+    }
+    __syncthreads();
+    // ---- phase 3: dpos (bf16x6, own position tiles) and the dq jobs (fp32)
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) {
+      const int pt = w * KPW + i;
+      if (pt >= nt) continue;
+      const int m = 16 * pt + r;
+      float xv[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int x = 8 * g + jj;  // dX[i0 + x][m] = dS'.flat[(i0+x)(T+1) + m + 1 - T]
+        xv[jj] = i0 + x < T ? R[x * (T + 1) + i0 + m + 1] : 0.0f;
+      }
+      bf16x8_t ax[3];
+      split8(xv, ax);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        bf16x8_t bq[3];
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+          bq[pp] = *(const bf16x8_t*)(plane(1, pp) + (16 * ct + r) * kPlanePitch + 8 * g);
+        acc_p[i][ct] = mfma_x6(ax, bq, acc_p[i][ct]);
+      }
+    }
+    const int nk = 4 * nt;  // k steps of 4 keys / positions
+#pragma unroll
+    for (int jj = 0; jj < (NJ + NW - 1) / NW; ++jj) {
+      const int j = w + NW * jj;
+      if (j >= NJ) continue;
+      const int which = j / (2 * CT), a = (j / CT) & 1, ct = j % CT;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int x = 16 * a + r;
+      if (which == 0) {  // dS' k: A = band row x, B = k rows
+        const float* arow = R + (x + 1) * T + g;
+        const float* brow = kimg + g * DP + 16 * ct + r;
+        for (int s = 0; s < nk; ++s) acc = mfma4(arow[4 * s], brow[4 * s * DP], acc);
+      } else {  // dX pos: A = the band read flat, B = pos rows (range check: m >= T reads 0)
+        const bool live = i0 + x < T;
+        const float* arow = R + x * (T + 1) + i0 + 1 + g;
+        const int voff = (g * C + 16 * ct + r) * 4;
+        float bcur[4], bnxt[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          bcur[qq] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_p, voff, 16 * qq * C, 0));
+        for (int s0 = 0; s0 < nk; s0 += 4) {
+          if (s0 + 4 < nk)
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
+              bnxt[qq] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                       rs_p, voff, 16 * (s0 + 4 + qq) * C, 0));
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const float av = live ? arow[4 * (s0 + qq)] : 0.0f;
+            acc = mfma4(av, bcur[qq], acc);
+          }
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) bcur[qq] = bnxt[qq];
+        }
+      }
+      float cs = 0.0f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        comb[(((which * 2 + a) * CT + ct) * 16 + 4 * g + e) * 16 + r] = acc[e];
+        cs += acc[e];
+      }
+      csum[jj] += cs;
+    }
+  }
+  __syncthreads();
+  // ---- the last chunk's dq; dk, dv, the per-row dpos partial; du / dvb column sums
+  {
+    const int ip = kFQ * (nch - 1);
+    for (int e = threadIdx.x; e < kFQ * D; e += NTH) {
+      const int x = e / D, col = e - x * D;
+      const int a = x >> 4, xr = x & 15, ct = col >> 4, cr = col & 15;
+      if (ip + x < T) {
+        const int ci = ((a * CT + ct) * 16 + xr) * 16 + cr;
+        dq[bo + (size_t)(ip + x) * C + col] = comb[ci] + comb[2 * CT * 256 + ci];
+      }
+    }
+  }
+  float* dkb = dk + bo;
+  float* dvbp = dv + bo;
+  float* dpb = dp_part + (size_t)bh * T * D;
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
+    const int t16 = 16 * (w * KPW + i);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int col = 16 * ct + r;
+      if (col >= D) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = t16 + 4 * g + e;
+        if (row >= T) continue;
+        dkb[(size_t)row * C + col] = acc_k[i][ct][e];
+        dvbp[(size_t)row * C + col] = acc_v[i][ct][e];
+        dpb[(size_t)row * D + col] = acc_p[i][ct][e];
+      }
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < (NJ + NW - 1) / NW; ++jj) {
+    const int j = w + NW * jj;
+    float cs = csum[jj];
+    cs += __shfl_xor(cs, 16);
+    cs += __shfl_xor(cs, 32);
+    if (j < NJ && g == 0) {
+      const int which = j / (2 * CT), a = (j / CT) & 1, ct = j % CT;
+      sums[(which * 2 + a) * DP + 16 * ct + r] = cs;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < D) {
+    const int col = threadIdx.x;
+    du_part[(size_t)bh * D + col] = sums[col] + sums[DP + col];
+    dvb_part[(size_t)bh * D + col] = sums[2 * DP + col] + sums[3 * DP + col];
+  }
+}
+
 // du, dvb [H][D]: sum over (batch row, query tile) of the per-tile partials. Block = one
 // (which, head) x 4 columns x 64 slices (slice s: pairs s, s+64, ..., four accumulators),
 // the slices added in order through LDS (fixed order). 2*H*ceil(D/4) blocks: each thread
@@ -916,13 +1415,27 @@ bool relattn_supported(int64_t T, int64_t d) {
   return T >= 1 && T <= 512 && (d == 16 || d == 32 || d == 36 || d == 64);
 }
 
+// the flash-style backward (relattn_bwd_fused_kernel): T <= 256 (16 key tiles), d <= 36
+bool relattn_fused(int64_t T, int64_t d) { return T <= 256 && d <= 36; }
+
+// saved state of the forward for the backward (fp32 elements): row statistics
+// [Bt*H][Tp][2] (max, 1/sum) | keep bits [Bt*H][Tp][W] | (T > 256 or d = 64) probability tiles
+int64_t relattn_saved_elems(int64_t Bt, int64_t T, int64_t H, int64_t d) {
+  const int64_t nt = (T + 15) / 16, Tp = 16 * nt, W = (nt + 1) / 2;
+  int64_t n = Bt * H * Tp * (2 + W);
+  if (!relattn_fused(T, d)) n += relattn_probs_elems(Bt, T, H);
+  return n;
+}
+
 int64_t relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
   const int64_t nt = (T + 15) / 16;
   return Bt * H * nt * nt * 256;
 }
 
-// ws: dS' [Bt][H][T][T] | dpos per batch row [Bt][H][T][d] | du, dvb tile partials.
+// ws: [probability path: dS' [Bt][H][T][T]] | dpos per batch row [Bt][H][T][d] | du, dvb
+// partials per (batch row, head[, query tile]).
 size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
+  if (relattn_fused(T, d)) return sizeof(float) * (size_t)(Bt * H * T * d + 2 * Bt * H * d + 64);
   const int64_t nqt = (T + kTile - 1) / kTile;
   return sizeof(float) * (size_t)(Bt * H * T * T + Bt * H * T * d + 2 * Bt * H * nqt * d + 64);
 }
@@ -944,23 +1457,60 @@ size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
 void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                         const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
                         int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,
-                        uint64_t rng_off, float* probs, float* ctx, hipStream_t s) {
+                        uint64_t rng_off, float* saved, float* probs, float* ctx, hipStream_t s) {
   const dim3 grid((unsigned)(((T + kTile - 1) / kTile) * H * Bt));
   const DropCfg dc = make_drop(p_drop);
   const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
   const size_t lds = fwd_lds_bytes((int)T, (int)d);
+  const int64_t nt = (T + 15) / 16, Tp = 16 * nt;
+  float* stats = saved;
+  uint32_t* kbits = saved ? reinterpret_cast<uint32_t*>(saved + Bt * H * Tp * 2) : nullptr;
+  // the probability path's backward reads the tiles from the saved state
+  if (saved && !relattn_fused(T, d)) probs = saved + Bt * H * Tp * (2 + (nt + 1) / 2);
 #define OB_RA_FWD(DQ, NTT)                                                                 \
   hipLaunchKernelGGL((relattn_fwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, q, k, v, pos, \
-                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, ctx)
+                     u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, \
+                     stats, kbits, ctx)
   OB_RA_DISPATCH(OB_RA_FWD);
 #undef OB_RA_FWD
 }
 
+constexpr int kFusedWaves = 8;
+
 void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
                         const float* v, const float* pos, const float* u, const float* vb,
-                        int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                        const float* probs, float* dq, float* dk, float* dv, float* dpos,
-                        float* du, float* dvb, void* ws, hipStream_t s) {
+                        const int* lens, int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d,
+                        float p_drop, const float* saved, float* dq, float* dk, float* dv,
+                        float* dpos, float* du, float* dvb, void* ws, hipStream_t s) {
+  const int64_t nt = (T + 15) / 16, Tp = 16 * nt, W = (nt + 1) / 2;
+  if (relattn_fused(T, d)) {
+    const DropCfg dc = make_drop(p_drop);
+    const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);
+    float* dp_part = (float*)ws;
+    float* du_part = dp_part + (size_t)Bt * H * T * d;
+    float* dvb_part = du_part + (size_t)Bt * H * d;
+    const float* stats = saved;
+    const uint32_t* kbits = reinterpret_cast<const uint32_t*>(saved + Bt * H * Tp * 2);
+    const int CT = (int)((d + 15) / 16);
+    const size_t lds = sizeof(float) * FusedLds((int)T, (int)d, CT, (int)((Tp + kFQ - 1) / kFQ), (int)W).total;
+#define OB_RA_FUSED(DQ)                                                                           \
+  hipLaunchKernelGGL((relattn_bwd_fused_kernel<DQ, kFusedWaves>), dim3((unsigned)(Bt * H)),        \
+                     dim3(64 * kFusedWaves), lds, s, dctx, ctx, q, k, v, pos, u, vb, lens, stats,   \
+                     kbits, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, dq, dk, dv, dp_part,     \
+                     du_part, dvb_part)
+    if (d == 16) OB_RA_FUSED(4);
+    else if (d == 32) OB_RA_FUSED(8);
+    else OB_RA_FUSED(9);
+#undef OB_RA_FUSED
+    const int64_t C = H * d;
+    const int n_dpos = (int)ceil_div(P * T * C, 64);
+    const int n_bias = (int)(2 * H * ((d + kBiasCols - 1) / kBiasCols));
+    hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)(n_dpos + n_bias)), dim3(kThreads), 0,
+                       s, (const float*)dp_part, (const float*)du_part, (const float*)dvb_part,
+                       (int)Bt, (int)P, (int)T, (int)H, (int)d, 1, n_dpos, dpos, du, dvb);
+    return;
+  }
+  const float* probs = saved + Bt * H * Tp * (2 + W);
   const int nqt = (int)((T + kTile - 1) / kTile);
   const dim3 grid((unsigned)(nqt * H * Bt));
   const DropCfg dc = make_drop(p_drop);

@@ -190,7 +190,8 @@ SIGNATURES = {
                _c_f, _sz, _c_f]),
     "ob_relattn_fwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64, _f32, _c_f,
-               _i64, _c_f, _c_f, _c_f]),
+               _i64, _c_f, _c_f, _c_f, _c_f]),
+    "ob_relattn_saved_elems": (_i64, [_i64, _i64, _i64, _i64]),
     "ob_relattn_probs_elems": (_i64, [_i64, _i64, _i64]),
     "ob_relattn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64]),
     "ob_relattn_bwd": (
@@ -205,7 +206,7 @@ SIGNATURES = {
                _sz, _c_f]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 

@@ -6,6 +6,9 @@ Reference: onebit_asr/conformer.py:115-127 (between MHSA's projections and out_p
 projection outputs in their natural [B, T, H*d] layout and returns the context in the
 layout out_proj consumes, with one forward kernel and one backward kernel (+ a small
 reduction); see csrc/relattn.hip. Gradients flow to q, k, v, pos, pos_bias_u, pos_bias_v.
+The forward saves only per-row softmax statistics and the dropout keep bits; for
+T <= 256 and d_head <= 36 (every Conformer call site) the backward is flash style and
+recomputes the probabilities on chip (no [B, H, T, T] tensor in HBM).
 
 Dropout uses the kernels' counter-based hash of (seed, counter + offset): the device state
 and per-call host offsets are the fused BitLinear call sites' (fused._rng), whose counter
@@ -44,23 +47,23 @@ class _RelAttnFn(torch.autograd.Function):
         out = torch.empty_like(q)
         need = any(ctx.needs_input_grad[:6])
         lib = _lib.load()
-        probs = (torch.empty((lib.ob_relattn_probs_elems(bt, t, n_heads),), dtype=torch.float32,
-                             device=q.device) if need else None)
+        saved = (torch.empty((lib.ob_relattn_saved_elems(bt, t, n_heads, d),),
+                             dtype=torch.float32, device=q.device) if need else None)
         _lib.check(
             lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt, P, t, n_heads, d,
-                               p_drop, _lib.ptr(rng), rng_off, _lib.ptr(probs), out.data_ptr(),
-                               _lib.stream_of(q)),
+                               p_drop, _lib.ptr(rng), rng_off, _lib.ptr(saved), None,
+                               out.data_ptr(), _lib.stream_of(q)),
             "ob_relattn_fwd",
         )
         ctx.meta = (n_heads, p_drop, rng_off)
         if need:
-            ctx.save_for_backward(q, k, v, pos, u, vb, lens, probs, rng, out)
+            ctx.save_for_backward(q, k, v, pos, u, vb, lens, saved, rng, out)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        q, k, v, pos, u, vb, lens, probs, rng, out = ctx.saved_tensors
+        q, k, v, pos, u, vb, lens, saved, rng, out = ctx.saved_tensors
         n_heads, p_drop, rng_off = ctx.meta
         g = g.contiguous()
         bt, t, c = q.shape
@@ -75,7 +78,7 @@ class _RelAttnFn(torch.autograd.Function):
         _lib.check(
             lib.ob_relattn_bwd(g.data_ptr(), out.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt,
-                               P, t, n_heads, d, p_drop, _lib.ptr(rng), rng_off, probs.data_ptr(),
+                               P, t, n_heads, d, p_drop, _lib.ptr(rng), rng_off, saved.data_ptr(),
                                dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(),
                                du.data_ptr(), dvb.data_ptr(), ws.data_ptr(), wsb,
                                _lib.stream_of(g)),

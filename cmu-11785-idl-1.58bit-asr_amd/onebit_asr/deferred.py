@@ -40,7 +40,7 @@ import torch
 from . import _lib
 
 __all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "ln_done", "cm_slot", "keep",
-           "add_after_flush", "active"]
+           "add_grad_after_flush", "active"]
 
 _ON = os.environ.get("OB_DEFER", "1") != "0"
 _CAP = 512  # table entries per kind
@@ -61,7 +61,7 @@ class _State:
         self.cm_n = 0
         self.cm_nmax = 0
         self.refs: List[torch.Tensor] = []
-        self.post: List[tuple] = []  # (dst, src): dst += src once the tables have run
+        self.post: List[tuple] = []  # (param, src): param.grad += src after the tables
         self.stream: Optional[int] = None
         self.dev: Optional[int] = None
         self.queued = False
@@ -213,13 +213,12 @@ def keep(*tensors) -> None:
     _S.refs.extend(t for t in tensors if t is not None)
 
 
-def add_after_flush(dst: torch.Tensor, src: torch.Tensor) -> None:
-    """dst += src on the flush stream right after the table launches (a correction to a
-    gradient the tables are still to write); immediately when nothing is pending."""
-    if _S.stream is None:
-        dst.add_(src)
-    else:
-        _S.post.append((dst, src))
+def add_grad_after_flush(param: torch.Tensor, src: torch.Tensor) -> None:
+    """param.grad += src on the flush stream right after the table launches: a correction to
+    a deferred gradient the tables are still to write. Keyed by the parameter, not the
+    pending gradient tensor: an extra reference to that tensor would make AccumulateGrad
+    copy it (unwritten) instead of adopting it."""
+    _S.post.append((param, src))
 
 
 def _flush() -> None:
@@ -240,6 +239,6 @@ def _flush() -> None:
     if _S.post:
         dev = torch.device("cuda", _S.dev)
         with torch.cuda.stream(torch.cuda.ExternalStream(_S.stream, device=dev)):
-            for dst, src in _S.post:
-                dst.add_(src)
+            for param, src in _S.post:
+                param.grad.add_(src)
     _S.reset()

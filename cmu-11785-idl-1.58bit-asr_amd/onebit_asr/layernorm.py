@@ -152,14 +152,14 @@ class _LayerNormFn(torch.autograd.Function):
     def backward(ctx, gy):
         link = getattr(ctx, "link", None)
         if link is not None and link.result is not None:
-            du, dw, db = link.result
+            du, dw, db, deferred1 = link.result
             link.result = None
             if gy.data_ptr() != du.data_ptr():
                 # the output had a consumer besides the next LN: autograd summed that
                 # consumer's gradient into du (gy = du + g_other). The LN backward is linear
                 # in its output gradient, so the pair's result is completed with the LN
                 # backward of g_other (to the rounding of the subtraction).
-                return _pair_correction(ctx, gy, du, dw, db)
+                return _pair_correction(ctx, gy, du, dw, db, deferred1)
             return du.view(gy.shape), dw, db, None, None, None, None
         x2, weight, mean, rstd = ctx.saved_tensors
         rows, d = x2.shape
@@ -357,12 +357,12 @@ def _pair_backward(ctx, link, gy, gres):
         deferred.ln_done(n_def, d)
     if spec is not None:
         spec.dx_ptr, spec.dy2 = du.data_ptr(), dy2
-    link.result = (du, dw1, db1)
+    link.result = (du, dw1, db1, s1 >= 0)
     # du goes to the first LN's node as this node's input gradient; that node returns it
     return du.view(gy.shape), dw2, db2, None, None, None
 
 
-def _pair_correction(ctx, gy, du, dw1, db1):
+def _pair_correction(ctx, gy, du, dw1, db1, deferred1):
     """The first LN of a pair whose output had another consumer: du, dw1, db1 are its
     backward for the pair consumer's gradient only; add the LN backward of the rest
     (g_other = gy - du) -- dgamma / dbeta after the deferred tables have written theirs."""
@@ -380,10 +380,13 @@ def _pair_correction(ctx, gy, du, dw1, db1):
                                         du.data_ptr(), dx.data_ptr(), _lib.ptr(dw), _lib.ptr(db),
                                         ws.data_ptr(), wsb, _lib.stream_of(g_other)),
                "ob_layernorm_bwd_res")
-    if dw is not None:
-        deferred.add_after_flush(dw1, dw)
-    if db is not None:
-        deferred.add_after_flush(db1, db)
+    for pending, extra, param in ((dw1, dw, weight), (db1, db, ctx.params[1])):
+        if extra is None:
+            continue
+        if deferred1:  # the table writes `pending` at the flush: add to the installed .grad
+            deferred.add_grad_after_flush(param, extra)
+        else:
+            pending.add_(extra)
     return dx.view(gy.shape), dw1, db1, None, None, None, None
 
 

@@ -424,33 +424,41 @@ OB_API int ob_decattn_bwd(const float* dctx, const float* ctx, const float* q, i
  *   pos, dpos : [P][T][H*d]    (pass p = b / (Bt/P) for stacked passes; P = 1 otherwise)
  *   u, vb, du, dvb : [H][d]    (pos_bias_u / pos_bias_v)
  *   lens : DEVICE int32 [Bt]   (valid frames; the encoder's prefix masks)
- *   probs : MFMA-fragment tiles [Bt*H][nt][nt][64][4], nt = ceil(T/16), of the softmax
- *           before dropout (ob_relattn_probs_elems floats): tile (a, t), lane r + 16g,
- *           element e holds P[16a + r][16t + 4g + e] (rows / keys >= T: 0). Written by
- *           fwd when non-NULL, required by bwd. With p_drop > 0 each element's sign bit is
- *           its dropout decision (dropped: -P; |probs| = softmax)
+ *   saved : the forward's state for the backward (ob_relattn_saved_elems fp32 elements,
+ *           16-B aligned; NULL when no backward follows): row statistics [Bt*H][Tp][2]
+ *           (max of the scaled masked scores, 1/sum; Tp = 16*ceil(T/16)), the dropout keep
+ *           bits [Bt*H][Tp][W] (uint32, W = ceil(Tp/32), key j of row i = bit j%32 of word
+ *           j/32), and for T > 256 or d = 64 the probability tiles below. For T <= 256 and
+ *           d <= 36 the backward is flash style: it recomputes the probabilities of 32-query
+ *           chunks from q, k, pos and the statistics (bitwise the forward's) and keeps every
+ *           [T][T] quantity on chip.
+ *   probs : optional (NULL: not written) MFMA-fragment tiles [Bt*H][nt][nt][64][4],
+ *           nt = ceil(T/16), of the softmax before dropout (ob_relattn_probs_elems floats):
+ *           tile (a, t), lane r + 16g, element e holds P[16a + r][16t + 4g + e] (rows / keys
+ *           >= T: 0); with p_drop > 0 a dropped element is stored as -P.
  *   ctx (bwd) : the forward's output (the softmax backward's row term is dO . ctx)
  *   rng : DEVICE int64 [2] (seed, counter), rng_offset a host offset added to the counter
  *         (the fused BitLinear entries' convention: one device state, a distinct offset per
  *         call site, the counter advanced once per step); dropout keeps element (i, j) of
  *         row bh when the 16-bit field (j & 1) of hash(seed, counter + rng_offset,
  *         ((bh*T + i)*Te + j) / 2) >= p_drop * 2^16, Te = T rounded up to even (the bwd
- *         reads the forward's decision from probs; ob_relattn_dropout_mask writes the mask
- *         out). Unused when p_drop == 0.
+ *         reads the forward's decisions from the saved keep bits; ob_relattn_dropout_mask
+ *         writes the mask out). Unused when p_drop == 0.
  * Supported: 1 <= T <= 512, d in {16, 32, 36, 64}.
  * ------------------------------------------------------------------------------------ */
 OB_API int ob_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                           const float* u, const float* vb, const int32_t* lens, int64_t Bt,
                           int64_t P, int64_t T, int64_t H, int64_t d, float p_drop,
-                          const int64_t* rng, int64_t rng_offset, float* probs, float* ctx,
-                          void* stream);
+                          const int64_t* rng, int64_t rng_offset, float* saved, float* probs,
+                          float* ctx, void* stream);
+OB_API int64_t ob_relattn_saved_elems(int64_t Bt, int64_t T, int64_t H, int64_t d);
 OB_API int64_t ob_relattn_probs_elems(int64_t Bt, int64_t T, int64_t H);
 OB_API size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
 OB_API int ob_relattn_bwd(const float* dctx, const float* ctx, const float* q, const float* k,
                           const float* v, const float* pos, const float* u, const float* vb,
                           const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H,
                           int64_t d, float p_drop, const int64_t* rng, int64_t rng_offset,
-                          const float* probs,
+                          const float* saved,
                           float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb,
                           void* ws, size_t ws_bytes, void* stream);
 /* The dropout keep-mask (1 = kept) of n elements laid out in rows of row_len: the attention

@@ -6,7 +6,9 @@ Bars: ctx max|err| <= 1e-5 * max|ref| + 1e-6; probs max|err| <= 1e-6; every grad
 (q, k, v, pos, pos_bias_u, pos_bias_v) max|err| <= 1e-4 * max|ref| + 1e-6. Dropout is
 checked with the kernels' own keep-mask (ob_relattn_dropout_mask) applied in the
 reference. Edge cases: T = 1, an utterance of length 0 (fully masked rows -> 0), lengths
-off by one around the 64-row tiles, stacked passes (P > 1), T > 256 (the long-row path).
+off by one around the 64-row forward tiles and the 32-query backward chunks, stacked passes
+(P > 1), T <= 256 with d <= 36 (the flash-style backward that recomputes the probabilities)
+and T > 256 or d = 64 (the backward that reads stored probabilities).
 """
 import math
 
@@ -23,6 +25,9 @@ CASES = [  # (Bt, P, T, H, d, lens)
     (4, 2, 249, 4, 36, [249, 249, 200, 1]),
     (2, 1, 300, 4, 36, [300, 150]),
     (2, 1, 512, 2, 64, [512, 511]),
+    (3, 3, 33, 4, 16, [33, 32, 1]),        # two 32-query chunks, the second one row long
+    (2, 1, 256, 2, 32, [256, 200]),        # the largest flash-style shape, d 32
+    (4, 2, 240, 4, 36, [240, 0, 97, 239]),  # Tp = 240: the last chunk half outside Tp
 ]
 
 
@@ -105,8 +110,8 @@ def test_relattn_probs_and_determinism(gpu):
         ctx = torch.empty_like(q)
         _lib.check(lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                       u.data_ptr(), vb.data_ptr(), lens.to(gpu).data_ptr(), bt, P,
-                                      t, H, d, 0.0, None, 0, probs.data_ptr(), ctx.data_ptr(),
-                                      _lib.stream_of(q)), "fwd")
+                                      t, H, d, 0.0, None, 0, None, probs.data_ptr(),
+                                      ctx.data_ptr(), _lib.stream_of(q)), "fwd")
         # every padding slot of the fragment tiles is written (zero)
         assert torch.isfinite(probs).all().item()
         outs.append((probs_dense(probs, bt, H, t).clone(), ctx.clone()))

@@ -33,7 +33,7 @@ def main():
     u, vb = torch.randn(H, d, device=dev) * 0.01, torch.randn(H, d, device=dev) * 0.01
     lens = torch.full((Bt,), T, dtype=torch.int32, device=dev)
     rng = torch.tensor([1234, 1], dtype=torch.int64, device=dev)
-    probs = torch.empty(lib.ob_relattn_probs_elems(Bt, T, H), device=dev)
+    saved = torch.empty(lib.ob_relattn_saved_elems(Bt, T, H, d), device=dev)
     ctx = torch.empty_like(q)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     dpos, du, dvb = torch.empty_like(pos), torch.empty_like(u), torch.empty_like(vb)
@@ -43,12 +43,12 @@ def main():
     def fwd(s):
         return lib.ob_relattn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(),
                                   u.data_ptr(), vb.data_ptr(), lens.data_ptr(), Bt, P, T, H, d, a.p,
-                                  rng.data_ptr(), 0, probs.data_ptr(), ctx.data_ptr(), s)
+                                  rng.data_ptr(), 0, saved.data_ptr(), None, ctx.data_ptr(), s)
 
     def bwd(s):
         return lib.ob_relattn_bwd(do.data_ptr(), ctx.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                   pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), Bt,
-                                  P, T, H, d, a.p, rng.data_ptr(), 0, probs.data_ptr(), dq.data_ptr(),
+                                  P, T, H, d, a.p, rng.data_ptr(), 0, saved.data_ptr(), dq.data_ptr(),
                                   dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(), du.data_ptr(),
                                   dvb.data_ptr(), ws.data_ptr(), wsb, s)
 
@@ -56,7 +56,7 @@ def main():
     for name, fn in (("fwd", fwd), ("bwd", bwd)):
         if a.op and a.op != name:
             if name == "fwd":
-                _lib.check(fwd(s), "fwd")  # bwd needs probs
+                _lib.check(fwd(s), "fwd")  # bwd needs the saved state
             continue
         for _ in range(2):
             _lib.check(fn(s), name)
