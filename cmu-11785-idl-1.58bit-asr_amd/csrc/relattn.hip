@@ -165,7 +165,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     const float* __restrict__ pos, const float* __restrict__ u, const float* __restrict__ vbias,
     const int* __restrict__ lens, int Bp, int T, int H, float inv_sqrt_d, DropCfg dc,
     const uint64_t* __restrict__ rng, uint64_t rng_off, float* __restrict__ probs,
-    float* __restrict__ stats, uint32_t* __restrict__ kbits, float* __restrict__ ctx) {
+    float* __restrict__ stats, uint32_t* __restrict__ kbits, float* __restrict__ anchors,
+    float* __restrict__ ctx) {
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   extern __shared__ float img[];
@@ -259,6 +260,18 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     if (threadIdx.x == 0) img[kTile * ldi] = 0.0f;
   }
   __syncthreads();
+  // X rows of the queries 32, 64, 96, ... (< T): the rows just below each 32-query chunk of
+  // the flash-style backward, which reads them instead of recomputing them
+  if (anchors) {
+    const int nchk = (16 * nt + 31) / 32;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = i0 + 32 * half;
+      if (row < 32 || row >= T) continue;
+      float* dst = anchors + ((size_t)bh * nchk + row / 32 - 1) * T;
+      for (int m = threadIdx.x; m < T; m += kThreads) dst[m] = img[32 * half * ldi + 1 + m];
+    }
+  }
 
   // scores for (query qi, keys 16t+4g+j): ac by MFMA (A = k rows, B = q+u); bd read flat
   float sreg[NTT][4];
@@ -924,42 +937,110 @@ __device__ __forceinline__ void key_side(const float (&a8)[8], const __bf16* pl,
   }
 }
 
+// One 16x16 dq tile over all nk k steps of 4 (keys or positions) on 16x16x4 fp32 MFMA: four
+// independent accumulation chains (step s = 4n + chain), summed in a fixed order by the
+// caller; the next 4 steps' operands load while the current 4 MFMAs issue (two register
+// sets, no copies; loads past the last step stay inside LDS / the buffer's range).
+// WHICH 0: B from the k image (pitch DP); 1: B = pos rows through the buffer descriptor.
+template <int WHICH, int DP>
+__device__ __forceinline__ void dq_job(const float* __restrict__ arow, float live,
+                                       const float* __restrict__ brow,
+                                       __amdgpu_buffer_rsrc_t rs_p, int voff, int C, int sb,
+                                       int se, f32x4 (&ac4)[4]) {
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) ac4[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
+  arow += 4 * sb;
+  if (WHICH == 0) brow += 4 * sb * DP;
+  const int nk = se - sb;
+  const int sbase = 16 * sb * C;  // (WHICH 1: byte offset of row 4 sb)
+  auto ld = [&](int s0, float (&A)[4], float (&B)[4]) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      A[qq] = arow[4 * (s0 + qq)];
+      if (WHICH == 0)
+        B[qq] = brow[4 * (s0 + qq) * DP];
+      else
+        B[qq] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rs_p, voff, sbase + 16 * (s0 + qq) * C, 0));
+    }
+  };
+  float A0[4], B0[4], A1[4], B1[4];
+  ld(0, A0, B0);
+  for (int s0 = 0; s0 < nk; s0 += 8) {
+    ld(s0 + 4, A1, B1);
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) ac4[qq] = mfma4(A0[qq] * live, B0[qq], ac4[qq]);
+    ld(s0 + 8, A0, B0);
+    if (s0 + 4 < nk)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) ac4[qq] = mfma4(A1[qq] * live, B1[qq], ac4[qq]);
+  }
+}
+
 struct FusedLds {  // float offsets into the dynamic LDS of relattn_bwd_fused_kernel
-  int kimg, reg, qu, qv, dO, planes, stats, delta, kb, comb, sums, total;
+  int kimg, reg, qu, qv, dO, planes, stats, delta, dpart, kb, comb, sums, total;
   __host__ __device__ FusedLds(int T, int D, int CT, int nch, int W) {
     const int Tp16 = 16 * ((T + 15) / 16);
-    const int ap = D + 1;                      // A-image pitch (odd: fewer conflicts)
+    const int ap = D + 1;                      // A-image pitch
     kimg = 0;                                  // k rows [Tp][16 CT] (zero pad)
     reg = kimg + Tp16 * 16 * CT;               // prev row [T] + X image / dS' band
     qu = reg + T + 33 * (T + 1);               // (q+u) rows [32][ap]
-    qv = qu + kFQ * ap;                        // (q+v) rows [33][ap]
-    dO = qv + (kFQ + 1) * ap;                  // dO rows [32][ap]
+    qu = (qu + 3) & ~3;
+    qv = qu + kFQ * ap;                        // (q+v) rows [32][ap]
+    dO = qv + kFQ * ap;                        // dO rows [32][ap]
     planes = dO + kFQ * ap;                    // bf16 [3 tensors][3 parts][16 CT][40]
     planes = (planes + 3) & ~3;                // 16-B aligned
     stats = planes + (9 * 16 * CT * kPlanePitch) / 2;
     delta = stats + 2 * kFQ * nch;             // [32]
-    kb = delta + kFQ;                          // keep bits [32][W]
-    comb = kb + kFQ * W;                       // dq parts [2 which][2 a][CT][256]
-    sums = comb + 2 * 2 * CT * 256;            // column sums [2 which][2 a][16 CT]
-    total = sums + 4 * 16 * CT;
+    dpart = delta + kFQ;                       // dO.ctx partials [32][D/4]
+    kb = dpart + kFQ * (D / 4);                // keep bits [32][W]
+    comb = kb + kFQ * W;                       // dq parts [2 which][2 a][CT][2 half][256]
+    sums = comb + 2 * 2 * CT * 2 * 256;        // column sums [2 which][2 a][2 half][16 CT]
+    total = sums + 8 * 16 * CT;
   }
 };
+
+#ifdef OB_ATTN_STAMPS
+// diagnostic build only (tools/attn_stamps.py): per-wave cycles of each phase of the fused
+// backward, written to a buffer nothing else reads
+__device__ uint64_t g_attn_stamps[65536];
+#define OB_STAMP_DECL \
+  uint64_t st_t = __builtin_amdgcn_s_memtime(), st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define OB_STAMP(k)                                          \
+  do {                                                       \
+    const uint64_t st_n = __builtin_amdgcn_s_memtime();      \
+    st_acc[k] += st_n - st_t;                                \
+    st_t = st_n;                                             \
+  } while (0)
+#define OB_STAMP_WRITE                                                                \
+  if (lane == 0 && ((size_t)blockIdx.x * NW + w) * 10 + 10 <= 65536)                  \
+    for (int k_ = 0; k_ < 10; ++k_) g_attn_stamps[((size_t)blockIdx.x * NW + w) * 10 + k_] = st_acc[k_];
+#else
+#define OB_STAMP_DECL
+#define OB_STAMP(k) \
+  do {              \
+  } while (0)
+#define OB_STAMP_WRITE
+#endif
 
 template <int DQ, int NW>
 __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
     const float* __restrict__ dctx, const float* __restrict__ ctxo, const float* __restrict__ q,
     const float* __restrict__ k, const float* __restrict__ v, const float* __restrict__ pos,
     const float* __restrict__ u, const float* __restrict__ vbias, const int* __restrict__ lens,
-    const float* __restrict__ stats, const uint32_t* __restrict__ kbits, int Bp, int T, int H,
-    float inv_sqrt_d, DropCfg dc, float* __restrict__ dq, float* __restrict__ dk,
-    float* __restrict__ dv, float* __restrict__ dp_part, float* __restrict__ du_part,
+    const float* __restrict__ stats, const uint32_t* __restrict__ kbits,
+    const float* __restrict__ anchors, int Bp, int T_, int H, int ns, float inv_sqrt_d,
+    DropCfg dc, float* __restrict__ dq, float* __restrict__ dk, float* __restrict__ dv,
+    size_t kv_split_stride, float* __restrict__ dp_part, float* __restrict__ du_part,
     float* __restrict__ dvb_part) {
+  const int T = T_;
   constexpr int D = 4 * DQ;
   constexpr int CT = (D + 15) / 16;
   constexpr int DP = 16 * CT;           // padded columns
   constexpr int KPW = 16 / NW;          // key / position tiles per wave
   constexpr int NTH = 64 * NW;
-  constexpr int NJ = 4 * CT;            // dq jobs (which, a, ct)
+  constexpr int NJ = 8 * CT;            // dq jobs (which, a, ct, half of the k range)
+  constexpr int JPW = (NJ + NW - 1) / NW;
   extern __shared__ float lds[];
   const int nt = (T + 15) >> 4;
   const int Tp = 16 * nt;
@@ -974,6 +1055,7 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
   __bf16* planes = reinterpret_cast<__bf16*>(lds + off.planes);
   float* st_s = lds + off.stats;
   float* delta_s = lds + off.delta;
+  float* dpart = lds + off.dpart;
   uint32_t* kb_s = reinterpret_cast<uint32_t*>(lds + off.kb);
   float* comb = lds + off.comb;
   float* sums = lds + off.sums;
@@ -981,9 +1063,14 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
   // B plane (tensor z: 0 = q+u, 1 = q+v, 2 = dO; part p): [col][query] bf16
   auto plane = [&](int z, int p) { return planes + (size_t)(3 * z + p) * DP * kPlanePitch; };
 
+  // block = (batch row, head, split of the chunks): the ns splits of one (b, h) are
+  // consecutive logical ids (one XCD: they read the same k / v / pos rows)
   const int L0 = xcd_logical((int)blockIdx.x, (int)gridDim.x);
-  const int h = L0 % H, b = L0 / H;
+  const int sp = L0 % ns, bhl = L0 / ns;
+  const int h = bhl % H, b = bhl / H;
   const int bh = b * H + h;
+  const int cps = (nch + ns - 1) / ns;  // chunks per split
+  const int c0 = sp * cps, c1 = min(nch, c0 + cps);
   const int pass = b / Bp;
   const int C = H * D;
   const int L = min(lens[b], T);
@@ -998,8 +1085,9 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
   const float* ub = u + h * D;
   const float* vbb = vbias + h * D;
   const __amdgpu_buffer_rsrc_t rs_p = slice_rsrc(pb, T, C, D);
+  float* xim = R + T;  // X image: row x (query i0 + x) at pitch T+1, column 0 = 0
 
-  // ---- block setup: k image, statistics, this wave's k / v / pos rows (B operands)
+  // ---- block setup: k image, statistics, this wave's v / pos rows (B operands, registers)
   for (int e = threadIdx.x; e < Tp * CT * 4; e += NTH) {
     const int row = e / (CT * 4), c4 = 4 * (e - row * (CT * 4));
     f32x4 x4 = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1011,83 +1099,154 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
     st_s[2 * e] = in ? stats[2 * ((size_t)bh * Tp + e)] : 0.0f;
     st_s[2 * e + 1] = in ? stats[2 * ((size_t)bh * Tp + e) + 1] : 0.0f;
   }
-  for (int e = threadIdx.x; e < T; e += NTH) R[e] = 0.0f;  // band row "query -1"
-  // this wave's v / pos rows (B operands of dP and X): re-read per chunk (L2-resident) so they
-  // are not live across the whole block; k rows come from the k image
-  auto load_rows = [&](const float* base, int i, float (&dst)[DQ]) {
+  float vreg[KPW][DQ], preg[KPW][DQ];
+#pragma unroll
+  for (int i = 0; i < KPW; ++i) {
     const int row = 16 * (w * KPW + i) + r;
     if (row < T) {
-      load_run<DQ>(base + (size_t)row * C + g * DQ, dst);
+      load_run<DQ>(vb + (size_t)row * C + g * DQ, vreg[i]);
+      load_run<DQ>(pb + (size_t)row * C + g * DQ, preg[i]);
     } else {
 #pragma unroll
-      for (int s = 0; s < DQ; ++s) dst[s] = 0.0f;
+      for (int s = 0; s < DQ; ++s) vreg[i][s] = preg[i][s] = 0.0f;
     }
-  };
+  }
   f32x4 acc_k[KPW][CT], acc_v[KPW][CT], acc_p[KPW][CT];
 #pragma unroll
   for (int i = 0; i < KPW; ++i)
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc_k[i][ct] = acc_v[i][ct] = acc_p[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float csum[(NJ + NW - 1) / NW];
-#pragma unroll
-  for (int jj = 0; jj < (NJ + NW - 1) / NW; ++jj) csum[jj] = 0.0f;
+  for (int e = threadIdx.x; e < 8 * DP; e += NTH) sums[e] = 0.0f;
 
-  for (int c = 0; c < nch; ++c) {
+  // band row 0 of the first chunk: dS' of query i0 - 1, zero or (split > 0) recomputed:
+  // X[ip][j], X[ip+1][j], (q+u)[ip].k[j], dO[ip].v[j] in the MFMA's k order (bitwise the
+  // values the previous split's tiles hold), dO[ip].ctx[ip] as the staging partials sum it
+  if (c0 > 0) {
+    const int ip = kFQ * c0 - 1, j = threadIdx.x;
+    if (j < T) {
+      const float* qr = qb + (size_t)ip * C;
+      const float* qn = qb + (size_t)(ip + 1) * C;
+      const float* dr = dob + (size_t)ip * C;
+      const float* cr = cob + (size_t)ip * C;
+      float prow[D];
+      load_run<D>(pb + (size_t)j * C, prow);
+      float xs = 0.0f, xn = 0.0f, as = 0.0f, ds = 0.0f, dl = 0.0f;
+#pragma unroll
+      for (int s2 = 0; s2 < DQ; ++s2)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int cc = gg * DQ + s2;
+          xs = fmaf(qr[cc] + vbb[cc], prow[cc], xs);
+          xn = fmaf(qn[cc] + vbb[cc], prow[cc], xn);
+          as = fmaf(qr[cc] + ub[cc], kimg[j * DP + cc], as);
+          ds = fmaf(dr[cc], vb[(size_t)j * C + cc], ds);
+        }
+#pragma unroll
+      for (int c4i = 0; c4i < DQ; ++c4i) {
+        float a4 = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) a4 = fmaf(dr[4 * c4i + jj], cr[4 * c4i + jj], a4);
+        dl += a4;
+      }
+      comb[j] = xs;
+      comb[T + j] = xn;
+      comb[2 * T + j] = as;
+      comb[3 * T + j] = ds;
+      if (j == 0) comb[4 * T] = dl;
+    }
+    __syncthreads();
+    if (j < T) {
+      // bd[ip][j] = X.flat[T + ip*T + j]: X[ip][T-1-ip+j] (j <= ip), 0 (j = ip+1),
+      // X[ip+1][j-ip-2] (j >= ip+2)
+      const float bd = j <= ip ? comb[T - 1 - ip + j] : (j == ip + 1 ? 0.0f : comb[T + j - ip - 2]);
+      float sc = (comb[2 * T + j] + bd) * inv_sqrt_d;
+      sc = j < (ip < L ? L : 0) ? sc : -INFINITY;
+      const float p = __expf(sc - st_s[2 * ip]) * st_s[2 * ip + 1];
+      float ks = 1.0f;
+      if (dc.on)
+        ks = (kbits[((size_t)bh * Tp + ip) * W + (j >> 5)] >> (j & 31)) & 1u ? dc.scale : 0.0f;
+      R[j] = (p * (comb[3 * T + j] * ks - comb[4 * T])) * inv_sqrt_d;
+    }
+  } else {
+    for (int e = threadIdx.x; e < T; e += NTH) R[e] = 0.0f;
+  }
+
+  OB_STAMP_DECL
+  for (int c = c0; c < c1; ++c) {
     const int i0 = kFQ * c;
-    __syncthreads();  // the previous chunk's band / image / plane reads are done
-    // ---- phase 0a: finish the previous chunk's dq; stage this chunk's rows
-    if (c > 0) {
+    // LDS addresses derived from T are recomputed per chunk (a few VALU ops) instead of
+    // being hoisted out of the loop and spilled under the register pressure
+    int T = T_;
+    asm volatile("" : "+s"(T));
+    OB_STAMP(0);
+    __syncthreads();  // the previous chunk's band / image / plane / comb reads are done
+    OB_STAMP(1);
+    // ---- phase 0a: the previous chunk's dq; this chunk's rows, dO.ctx partials, X row 32
+    if (c > c0) {
       const int ip = i0 - kFQ;
       for (int e = threadIdx.x; e < kFQ * D; e += NTH) {
         const int x = e / D, col = e - x * D;
         const int a = x >> 4, xr = x & 15, ct = col >> 4, cr = col & 15;
         if (ip + x < T) {
-          const int ci = ((a * CT + ct) * 16 + xr) * 16 + cr;
-          dq[bo + (size_t)(ip + x) * C + col] = comb[ci] + comb[2 * CT * 256 + ci];
+          // dq = (dS' k) + (dX pos), each the sum of its two k-range halves
+          const int ci = ((a * CT + ct) * 2 * 16 + xr) * 16 + cr;
+          const int cv = 2 * CT * 2 * 256;
+          dq[bo + (size_t)(ip + x) * C + col] =
+              (comb[ci] + comb[ci + 256]) + (comb[cv + ci] + comb[cv + ci + 256]);
         }
       }
     }
-    for (int e = threadIdx.x; e < T; e += NTH) R[e] = c > 0 ? R[32 * T + e] : 0.0f;
+    for (int e = threadIdx.x; e < T; e += NTH) {
+      // band row 0: dS' of query i0 - 1 (the first chunk of a split: zero, or recomputed
+      // by the prologue when that row belongs to the previous split)
+      if (c > c0) R[e] = R[32 * T + e];
+      // X row 32 (query i0 + 32), saved by the forward (bitwise the MFMA row)
+      xim[kFQ * (T + 1) + 1 + e] = i0 + kFQ < T ? anchors[((size_t)bh * nch + c) * T + e] : 0.0f;
+    }
     {
       constexpr int nq = kFQ * DQ;  // float4s of 32 rows
-      for (int e = threadIdx.x; e < 2 * nq + DQ; e += NTH) {
-        // [0, nq): q rows 0..31 (+u and +v); [nq, 2nq): dO rows; then q row 32 (+v only)
-        const int kind = e < nq ? 0 : (e < 2 * nq ? 1 : 2);
+      for (int e = threadIdx.x; e < 2 * nq; e += NTH) {
+        // [0, nq): q rows (+u and +v); [nq, 2nq): dO rows, and dO.ctx over the float4
+        const int kind = e < nq ? 0 : 1;
         const int rem = e - kind * nq;
-        const int x = kind == 2 ? kFQ : rem / DQ;
-        const int c4 = 4 * (kind == 2 ? rem : rem - x * DQ);
+        const int x = rem / DQ, c4i = rem - x * DQ, c4 = 4 * c4i;
         const int qi = i0 + x;
-        f32x4 v4 = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (qi < T) v4 = *(const f32x4u*)((kind == 1 ? dob : qb) + (size_t)qi * C + c4);
+        f32x4 v4 = f32x4{0.f, 0.f, 0.f, 0.f}, c4v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (qi < T) {
+          v4 = *(const f32x4u*)((kind == 1 ? dob : qb) + (size_t)qi * C + c4);
+          if (kind == 1) c4v = *(const f32x4u*)(cob + (size_t)qi * C + c4);
+        }
+        if (kind == 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (kind == 1) {
-            do_a[x * AP + c4 + j] = v4[j];
-          } else {
-            if (kind == 0) qu_a[x * AP + c4 + j] = qi < T ? v4[j] + ub[c4 + j] : 0.0f;
+          for (int j = 0; j < 4; ++j) do_a[x * AP + c4 + j] = v4[j];
+          float a = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a = fmaf(v4[j], c4v[j], a);
+          dpart[x * DQ + c4i] = a;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            qu_a[x * AP + c4 + j] = qi < T ? v4[j] + ub[c4 + j] : 0.0f;
             qv_a[x * AP + c4 + j] = qi < T ? v4[j] + vbb[c4 + j] : 0.0f;
           }
         }
       }
-    }
-    if (threadIdx.x < kFQ) {  // delta = dO . ctx (the softmax backward's row term)
-      const int qi = i0 + threadIdx.x;
-      float a = 0.0f;
-      if (qi < T) {
-        const float* dr = dob + (size_t)qi * C;
-        const float* cr = cob + (size_t)qi * C;
-#pragma unroll
-        for (int cc = 0; cc < D; ++cc) a = fmaf(dr[cc], cr[cc], a);
-      }
-      delta_s[threadIdx.x] = a;
     }
     if (dc.on)
       for (int e = threadIdx.x; e < kFQ * W; e += NTH) {
         const int x = e / W;
         kb_s[e] = i0 + x < Tp ? kbits[((size_t)bh * Tp + i0) * W + e] : 0u;
       }
+    OB_STAMP(2);
     __syncthreads();
-    // ---- phase 0b: B planes (split once) ; phase 1: X tiles and the row-32 X on the VALU
+    OB_STAMP(3);
+    // ---- phase 0b: delta, B planes (split once); phase 1: X tiles
+    if (threadIdx.x < kFQ) {
+      float a = 0.0f;
+#pragma unroll
+      for (int cc = 0; cc < DQ; ++cc) a += dpart[threadIdx.x * DQ + cc];
+      delta_s[threadIdx.x] = a;
+    }
     for (int e = threadIdx.x; e < 3 * DP * (kFQ / 4); e += NTH) {
       const int z = e / (DP * (kFQ / 4));
       const int rem = e - z * DP * (kFQ / 4);
@@ -1107,80 +1266,86 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
       *(bf16x4_t*)(plane(z, 1) + col * kPlanePitch + x0) = mp;
       *(bf16x4_t*)(plane(z, 2) + col * kPlanePitch + x0) = lp;
     }
-    float* xim = R + T;  // X image: row x (query i0 + x) at pitch T+1, column 0 = 0
+    {
+      // X[query][pos] = (q+v) pos^T, the KPW x 2 tiles as independent chains
+      f32x4 xa[KPW][2];
 #pragma unroll
-    for (int i = 0; i < KPW; ++i) {
-      const int pt = w * KPW + i;
-      if (pt >= nt) continue;
-      float preg[DQ];
-      load_rows(pb, i, preg);
+      for (int i = 0; i < KPW; ++i) xa[i][0] = xa[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < DQ; ++s) {
+        const float a0 = qv_a[r * AP + g * DQ + s], a1 = qv_a[(16 + r) * AP + g * DQ + s];
 #pragma unroll
-        for (int s = 0; s < DQ; ++s)
-          acc = mfma4(qv_a[(16 * a + r) * AP + g * DQ + s], preg[s], acc);
-        const int m = 16 * pt + r;
+        for (int i = 0; i < KPW; ++i) {
+          xa[i][0] = mfma4(a0, preg[i][s], xa[i][0]);
+          xa[i][1] = mfma4(a1, preg[i][s], xa[i][1]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < KPW; ++i) {
+        const int m = 16 * (w * KPW + i) + r;
         if (m < T)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) xim[(16 * a + 4 * g + e) * (T + 1) + 1 + m] = acc[e];
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xim[(16 * a + 4 * g + e) * (T + 1) + 1 + m] = xa[i][a][e];
       }
     }
-    for (int m = threadIdx.x; m < T; m += NTH) {  // row 32 (query i0 + 32), MFMA k order
-      float pr[D];
-      load_run<D>(pb + (size_t)m * C, pr);
-      float a = 0.0f;
-#pragma unroll
-      for (int s = 0; s < DQ; ++s)
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) a = fmaf(qv_a[kFQ * AP + gg * DQ + s], pr[gg * DQ + s], a);
-      xim[kFQ * (T + 1) + 1 + m] = a;
-    }
     if (threadIdx.x <= kFQ) xim[threadIdx.x * (T + 1)] = 0.0f;
+    OB_STAMP(4);
     __syncthreads();
+    OB_STAMP(5);
     // ---- phase 2: S, P, dP, dS' for this wave's key tiles; key-side products
     float dsv[KPW][8];
+    {
+      f32x4 sa[KPW][2], sd[KPW][2];
 #pragma unroll
-    for (int i = 0; i < KPW; ++i) {
-      const int kt = w * KPW + i;
-      float pdv[8];
+      for (int i = 0; i < KPW; ++i)
+        sa[i][0] = sa[i][1] = sd[i][0] = sd[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) dsv[i][jj] = pdv[jj] = 0.0f;
-      if (kt < nt) {
+      for (int s = 0; s < DQ; ++s) {
+        const float u0 = qu_a[r * AP + g * DQ + s], u1 = qu_a[(16 + r) * AP + g * DQ + s];
+        const float o0 = do_a[r * AP + g * DQ + s], o1 = do_a[(16 + r) * AP + g * DQ + s];
+#pragma unroll
+        for (int i = 0; i < KPW; ++i) {
+          const float kv = kimg[(16 * (w * KPW + i) + r) * DP + g * DQ + s];
+          sa[i][0] = mfma4(u0, kv, sa[i][0]);
+          sa[i][1] = mfma4(u1, kv, sa[i][1]);
+          sd[i][0] = mfma4(o0, vreg[i][s], sd[i][0]);
+          sd[i][1] = mfma4(o1, vreg[i][s], sd[i][1]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < KPW; ++i) {
+        const int kt = w * KPW + i;
         const int key = 16 * kt + r;
-        float vreg[DQ];
-        load_rows(vb, i, vreg);
-        const float* krow = kimg + key * DP + g * DQ;
+        const float tile_live = kt < nt ? 1.0f : 0.0f;
+        float pdv[8];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          f32x4 sa = f32x4{0.f, 0.f, 0.f, 0.f}, sd = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < DQ; ++s) sa = mfma4(qu_a[(16 * a + r) * AP + g * DQ + s], krow[s], sa);
-#pragma unroll
-          for (int s = 0; s < DQ; ++s) sd = mfma4(do_a[(16 * a + r) * AP + g * DQ + s], vreg[s], sd);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int x = 16 * a + 4 * g + e, qi = i0 + x;
-            const int Lq = qi < L ? L : 0;
-            // bd[qi][key] = X.flat[T + qi*T + key] of the padded image (rel_shift, :97-103)
-            const float bd = xim[T + x * T + key - i0];
-            float sc = (sa[e] + bd) * inv_sqrt_d;
-            sc = key < Lq ? sc : -INFINITY;
-            const float p = __expf(sc - st_s[2 * x + 2 * i0]) * st_s[2 * x + 2 * i0 + 1];
-            float ks = 1.0f;
-            if (dc.on) ks = (kb_s[x * W + (key >> 5)] >> (key & 31)) & 1u ? dc.scale : 0.0f;
-            const float dpd = sd[e] * ks;
-            dsv[i][4 * a + e] = (p * (dpd - delta_s[x])) * inv_sqrt_d;
-            pdv[4 * a + e] = dc.on ? p * ks : p;
-          }
+        for (int jj = 0; jj < 8; ++jj) {
+          const int a = jj >> 2, e = jj & 3;
+          const int x = 16 * a + 4 * g + e, qi = i0 + x;
+          const int Lq = qi < L ? L : 0;
+          // bd[qi][key] = X.flat[T + qi*T + key] of the padded image (rel_shift, :97-103)
+          float sc = (sa[i][a][e] + xim[T + x * T + key - i0]) * inv_sqrt_d;
+          sc = key < Lq ? sc : -INFINITY;
+          const float p = __expf(sc - st_s[2 * (i0 + x)]) * st_s[2 * (i0 + x) + 1];
+          // (keep words are unstaged and unused without dropout)
+          const uint32_t kw = kb_s[x * W + (key >> 5)];
+          const float ks = dc.on ? ((kw >> (key & 31)) & 1u ? dc.scale : 0.0f) : 1.0f;
+          dsv[i][jj] = tile_live * ((p * (sd[i][a][e] * ks - delta_s[x])) * inv_sqrt_d);
+          pdv[jj] = tile_live * (dc.on ? p * ks : p);
         }
         // dK += dS'^T (q+u), dV += Pd^T dO: A = this lane's 8 queries of key r (k order
         // 4g..4g+3, 16+4g..16+4g+3), B = the planes read in the same order
-        key_side<CT>(dsv[i], plane(0, 0), g, r, acc_k[i]);
-        key_side<CT>(pdv, plane(2, 0), g, r, acc_v[i]);
+        if (kt < nt) {
+          key_side<CT>(dsv[i], plane(0, 0), g, r, acc_k[i]);
+          key_side<CT>(pdv, plane(2, 0), g, r, acc_v[i]);
+        }
       }
     }
+    OB_STAMP(6);
     __syncthreads();  // every X-image read is done: the band may overwrite it
+    OB_STAMP(7);
 #pragma unroll
     for (int i = 0; i < KPW; ++i) {
       const int key = 16 * (w * KPW + i) + r;
@@ -1191,7 +1356,9 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
           R[(x + 1) * T + key] = dsv[i][jj];
         }
     }
+    OB_STAMP(8);
     __syncthreads();
+    OB_STAMP(9);
     // ---- phase 3: dpos (bf16x6, own position tiles) and the dq jobs (fp32)
 #pragma unroll
     for (int i = 0; i < KPW; ++i) {
@@ -1215,66 +1382,54 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
         acc_p[i][ct] = mfma_x6(ax, bq, acc_p[i][ct]);
       }
     }
-    const int nk = 4 * nt;  // k steps of 4 keys / positions
-#pragma unroll
-    for (int jj = 0; jj < (NJ + NW - 1) / NW; ++jj) {
+    const int nk = 4 * nt;            // k steps of 4 keys / positions
+    const int nk_h = 4 * ((nk + 7) / 8);  // first half: a multiple of 4 steps
+#pragma unroll 1
+    for (int jj = 0; jj < JPW; ++jj) {
       const int j = w + NW * jj;
       if (j >= NJ) continue;
-      const int which = j / (2 * CT), a = (j / CT) & 1, ct = j % CT;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int which = j / (4 * CT), a = (j / (2 * CT)) & 1, ct = (j >> 1) % CT, half = j & 1;
       const int x = 16 * a + r;
-      if (which == 0) {  // dS' k: A = band row x, B = k rows
-        const float* arow = R + (x + 1) * T + g;
-        const float* brow = kimg + g * DP + 16 * ct + r;
-        for (int s = 0; s < nk; ++s) acc = mfma4(arow[4 * s], brow[4 * s * DP], acc);
-      } else {  // dX pos: A = the band read flat, B = pos rows (range check: m >= T reads 0)
-        const bool live = i0 + x < T;
-        const float* arow = R + x * (T + 1) + i0 + 1 + g;
-        const int voff = (g * C + 16 * ct + r) * 4;
-        float bcur[4], bnxt[4];
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq)
-          bcur[qq] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_p, voff, 16 * qq * C, 0));
-        for (int s0 = 0; s0 < nk; s0 += 4) {
-          if (s0 + 4 < nk)
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq)
-              bnxt[qq] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                       rs_p, voff, 16 * (s0 + 4 + qq) * C, 0));
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const float av = live ? arow[4 * (s0 + qq)] : 0.0f;
-            acc = mfma4(av, bcur[qq], acc);
-          }
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) bcur[qq] = bnxt[qq];
-        }
-      }
+      const int sb = half ? nk_h : 0, se = half ? nk : nk_h;
+      f32x4 ac4[4];
+      if (which == 0)  // dS' k: A = band row x, B = k rows of the image (zero past T)
+        dq_job<0, DP>(R + (x + 1) * T + g, 1.0f, kimg + g * DP + 16 * ct + r, rs_p, 0, C, sb, se,
+                      ac4);
+      else  // dX pos: A = the band read flat (0 for rows past T), B = pos rows (range check)
+        dq_job<1, DP>(R + x * (T + 1) + i0 + 1 + g, i0 + x < T ? 1.0f : 0.0f, nullptr, rs_p,
+                      (g * C + 16 * ct + r) * 4, C, sb, se, ac4);
       float cs = 0.0f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        comb[(((which * 2 + a) * CT + ct) * 16 + 4 * g + e) * 16 + r] = acc[e];
-        cs += acc[e];
+        const float vsum = (ac4[0][e] + ac4[1][e]) + (ac4[2][e] + ac4[3][e]);
+        comb[((((which * 2 + a) * CT + ct) * 2 + half) * 16 + 4 * g + e) * 16 + r] = vsum;
+        cs += vsum;
       }
-      csum[jj] += cs;
+      // the job's column sums (du / dvb), accumulated over the chunks in its own LDS slot
+      cs += __shfl_xor(cs, 16);
+      cs += __shfl_xor(cs, 32);
+      if (g == 0) sums[((which * 2 + a) * 2 + half) * DP + 16 * ct + r] += cs;
     }
   }
   __syncthreads();
   // ---- the last chunk's dq; dk, dv, the per-row dpos partial; du / dvb column sums
   {
-    const int ip = kFQ * (nch - 1);
+    const int ip = kFQ * (c1 - 1);
     for (int e = threadIdx.x; e < kFQ * D; e += NTH) {
       const int x = e / D, col = e - x * D;
       const int a = x >> 4, xr = x & 15, ct = col >> 4, cr = col & 15;
       if (ip + x < T) {
-        const int ci = ((a * CT + ct) * 16 + xr) * 16 + cr;
-        dq[bo + (size_t)(ip + x) * C + col] = comb[ci] + comb[2 * CT * 256 + ci];
+        // dq = (dS' k) + (dX pos), each the sum of its two k-range halves
+        const int ci = ((a * CT + ct) * 2 * 16 + xr) * 16 + cr;
+        const int cv = 2 * CT * 2 * 256;
+        dq[bo + (size_t)(ip + x) * C + col] =
+            (comb[ci] + comb[ci + 256]) + (comb[cv + ci] + comb[cv + ci + 256]);
       }
     }
   }
-  float* dkb = dk + bo;
-  float* dvbp = dv + bo;
-  float* dpb = dp_part + (size_t)bh * T * D;
+  float* dkb = dk + sp * kv_split_stride + bo;
+  float* dvbp = dv + sp * kv_split_stride + bo;
+  float* dpb = dp_part + ((size_t)bh * ns + sp) * T * D;
 #pragma unroll
   for (int i = 0; i < KPW; ++i) {
     const int t16 = 16 * (w * KPW + i);
@@ -1292,23 +1447,14 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
       }
     }
   }
-#pragma unroll
-  for (int jj = 0; jj < (NJ + NW - 1) / NW; ++jj) {
-    const int j = w + NW * jj;
-    float cs = csum[jj];
-    cs += __shfl_xor(cs, 16);
-    cs += __shfl_xor(cs, 32);
-    if (j < NJ && g == 0) {
-      const int which = j / (2 * CT), a = (j / CT) & 1, ct = j % CT;
-      sums[(which * 2 + a) * DP + 16 * ct + r] = cs;
-    }
-  }
   __syncthreads();
   if (threadIdx.x < D) {
     const int col = threadIdx.x;
-    du_part[(size_t)bh * D + col] = sums[col] + sums[DP + col];
-    dvb_part[(size_t)bh * D + col] = sums[2 * DP + col] + sums[3 * DP + col];
+    const float* su = sums + col;
+    du_part[((size_t)bh * ns + sp) * D + col] = (su[0] + su[DP]) + (su[2 * DP] + su[3 * DP]);
+    dvb_part[((size_t)bh * ns + sp) * D + col] = (su[4 * DP] + su[5 * DP]) + (su[6 * DP] + su[7 * DP]);
   }
+  OB_STAMP_WRITE
 }
 
 // du, dvb [H][D]: sum over (batch row, query tile) of the per-tile partials. Block = one
@@ -1351,7 +1497,7 @@ __device__ __forceinline__ void relattn_bias_reduce_block(
 // elements x 4 batch slices (slice s: rows s, s+4, ... of the pass); the slices are added
 // in slice order through LDS (fixed order: deterministic).
 __device__ __forceinline__ void relattn_dpos_reduce_block(
-    int bid, const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D,
+    int bid, const float* __restrict__ dp_part, int Bt, int P, int T, int H, int D, int ns,
     float* __restrict__ dpos) {
   __shared__ float red[4][64];
   const int C = H * D;
@@ -1366,8 +1512,9 @@ __device__ __forceinline__ void relattn_dpos_reduce_block(
     const int t = rem / C, hc = rem - t * C, h = hc / D, c = hc - h * D;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     int uu = 0;
-    for (int b = p * Bp + sl; b < (p + 1) * Bp; b += 4, ++uu)
-      a[uu & 3] += dp_part[((((size_t)b * H + h) * T) + t) * D + c];
+    for (int b = p * Bp + sl; b < (p + 1) * Bp; b += 4)
+      for (int sp = 0; sp < ns; ++sp, ++uu)  // (ns query splits per batch row)
+        a[uu & 3] += dp_part[((((size_t)b * H + h) * ns + sp) * T + t) * D + c];
     s = (a[0] + a[1]) + (a[2] + a[3]);
   }
   red[sl][el] = s;
@@ -1378,15 +1525,29 @@ __device__ __forceinline__ void relattn_dpos_reduce_block(
 // Both reductions of the backward in one launch (they read different partials and write
 // different outputs): blocks [0, n_dpos) reduce dpos, the rest du / dvb -- one launch per
 // attention layer fewer at the per-launch floor, the same arithmetic per output.
+// (and, for the flash-style backward with ns > 1 query splits, dk / dv as the fixed-order
+// sum of the splits' partials: [ns][n] each, 4 elements per thread)
 __global__ __launch_bounds__(kThreads) void relattn_reduce_kernel(
     const float* __restrict__ dp_part, const float* __restrict__ du_part,
     const float* __restrict__ dvb_part, int Bt, int P, int T, int H, int D, int nqt, int n_dpos,
-    float* __restrict__ dpos, float* __restrict__ du, float* __restrict__ dvb) {
+    float* __restrict__ dpos, float* __restrict__ du, float* __restrict__ dvb, int ns_dpos,
+    int n_bias, const float* __restrict__ kv_part, int64_t n_kv, float* __restrict__ dk,
+    float* __restrict__ dv) {
   const int bid = (int)blockIdx.x;
-  if (bid < n_dpos)
-    relattn_dpos_reduce_block(bid, dp_part, Bt, P, T, H, D, dpos);
-  else
+  if (bid < n_dpos) {
+    relattn_dpos_reduce_block(bid, dp_part, Bt, P, T, H, D, ns_dpos, dpos);
+  } else if (bid < n_dpos + n_bias) {
     relattn_bias_reduce_block(bid - n_dpos, du_part, dvb_part, Bt, H, D, nqt, du, dvb);
+  } else {
+    const int64_t e = 4 * ((int64_t)(bid - n_dpos - n_bias) * kThreads + threadIdx.x);
+    if (e >= 2 * n_kv) return;
+    const bool isv = e >= n_kv;
+    const int64_t i = isv ? e - n_kv : e;  // n_kv % 4 == 0
+    const float* src = kv_part + (isv ? (int64_t)nqt * n_kv : 0) + i;
+    f32x4 acc = *(const f32x4*)src;
+    for (int sp = 1; sp < nqt; ++sp) acc += *(const f32x4*)(src + sp * n_kv);
+    *(f32x4*)((isv ? dv : dk) + i) = acc;
+  }
 }
 
 // keep mask of n elements in rows of T (element e = row * T + j): the attention kernels'
@@ -1419,12 +1580,22 @@ bool relattn_supported(int64_t T, int64_t d) {
 bool relattn_fused(int64_t T, int64_t d) { return T <= 256 && d <= 36; }
 
 // saved state of the forward for the backward (fp32 elements): row statistics
-// [Bt*H][Tp][2] (max, 1/sum) | keep bits [Bt*H][Tp][W] | (T > 256 or d = 64) probability tiles
+// [Bt*H][Tp][2] (max, 1/sum) | keep bits [Bt*H][Tp][W] | then either (flash-style backward)
+// the X rows below each 32-query chunk [Bt*H][nch][T] or (T > 256 or d = 64) probability tiles
+struct SavedLayout {
+  int64_t stats, kbits, tail, total;
+  SavedLayout(int64_t Bt, int64_t T, int64_t H, int64_t d) {
+    const int64_t nt = (T + 15) / 16, Tp = 16 * nt, W = (nt + 1) / 2, nch = (Tp + 31) / 32;
+    stats = 0;
+    kbits = Bt * H * Tp * 2;
+    tail = kbits + Bt * H * Tp * W;
+    tail = (tail + 3) & ~(int64_t)3;  // 16-B aligned
+    total = tail + (relattn_fused(T, d) ? Bt * H * nch * T : relattn_probs_elems(Bt, T, H));
+  }
+};
+
 int64_t relattn_saved_elems(int64_t Bt, int64_t T, int64_t H, int64_t d) {
-  const int64_t nt = (T + 15) / 16, Tp = 16 * nt, W = (nt + 1) / 2;
-  int64_t n = Bt * H * Tp * (2 + W);
-  if (!relattn_fused(T, d)) n += relattn_probs_elems(Bt, T, H);
-  return n;
+  return SavedLayout(Bt, T, H, d).total;
 }
 
 int64_t relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
@@ -1432,10 +1603,19 @@ int64_t relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
   return Bt * H * nt * nt * 256;
 }
 
-// ws: [probability path: dS' [Bt][H][T][T]] | dpos per batch row [Bt][H][T][d] | du, dvb
-// partials per (batch row, head[, query tile]).
+// query splits of the flash-style backward: two blocks per (batch row, head) once there are
+// two chunks, so Bt*H*2 blocks fill whole rounds of one block per CU (Conformer-S: 768 = 3 x
+// 256) instead of 1.5 rounds; the key-side partials are summed by the reduce launch
+int fused_splits(int64_t T) { return ((16 * ((T + 15) / 16) + 31) / 32) >= 2 ? 2 : 1; }
+
+// ws: [probability path: dS' [Bt][H][T][T]] | dpos per batch row [Bt][H][ns][T][d] | du, dvb
+// partials per (batch row, head, query tile / split) | (ns > 1) dk, dv split partials.
 size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
-  if (relattn_fused(T, d)) return sizeof(float) * (size_t)(Bt * H * T * d + 2 * Bt * H * d + 64);
+  if (relattn_fused(T, d)) {
+    const int64_t ns = fused_splits(T);
+    const int64_t kv = ns > 1 ? 2 * ns * Bt * T * H * d + 4 : 0;
+    return sizeof(float) * (size_t)(Bt * H * ns * T * d + 2 * Bt * H * ns * d + kv + 64);
+  }
   const int64_t nqt = (T + kTile - 1) / kTile;
   return sizeof(float) * (size_t)(Bt * H * T * T + Bt * H * T * d + 2 * Bt * H * nqt * d + 64);
 }
@@ -1462,15 +1642,16 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
   const DropCfg dc = make_drop(p_drop);
   const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
   const size_t lds = fwd_lds_bytes((int)T, (int)d);
-  const int64_t nt = (T + 15) / 16, Tp = 16 * nt;
+  const SavedLayout sl(Bt, T, H, d);
   float* stats = saved;
-  uint32_t* kbits = saved ? reinterpret_cast<uint32_t*>(saved + Bt * H * Tp * 2) : nullptr;
+  uint32_t* kbits = saved ? reinterpret_cast<uint32_t*>(saved + sl.kbits) : nullptr;
+  float* anchors = saved && relattn_fused(T, d) ? saved + sl.tail : nullptr;
   // the probability path's backward reads the tiles from the saved state
-  if (saved && !relattn_fused(T, d)) probs = saved + Bt * H * Tp * (2 + (nt + 1) / 2);
+  if (saved && !relattn_fused(T, d)) probs = saved + sl.tail;
 #define OB_RA_FWD(DQ, NTT)                                                                 \
   hipLaunchKernelGGL((relattn_fwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, q, k, v, pos, \
                      u, vb, lens, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, rng, rng_off, probs, \
-                     stats, kbits, ctx)
+                     stats, kbits, anchors, ctx)
   OB_RA_DISPATCH(OB_RA_FWD);
 #undef OB_RA_FWD
 }
@@ -1486,31 +1667,42 @@ void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, con
   if (relattn_fused(T, d)) {
     const DropCfg dc = make_drop(p_drop);
     const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);
+    const int ns = fused_splits(T);
+    const int64_t C = H * d;
+    const int64_t n_kv = Bt * T * C;
     float* dp_part = (float*)ws;
-    float* du_part = dp_part + (size_t)Bt * H * T * d;
-    float* dvb_part = du_part + (size_t)Bt * H * d;
+    float* du_part = dp_part + (size_t)Bt * H * ns * T * d;
+    float* dvb_part = du_part + (size_t)Bt * H * ns * d;
+    float* kv_part = dvb_part + (size_t)Bt * H * ns * d;
+    kv_part += (16 - ((uintptr_t)kv_part & 15)) / 4 % 4;  // 16-B aligned
+    const SavedLayout sl(Bt, T, H, d);
     const float* stats = saved;
-    const uint32_t* kbits = reinterpret_cast<const uint32_t*>(saved + Bt * H * Tp * 2);
+    const uint32_t* kbits = reinterpret_cast<const uint32_t*>(saved + sl.kbits);
+    const float* anchors = saved + sl.tail;
     const int CT = (int)((d + 15) / 16);
     const size_t lds = sizeof(float) * FusedLds((int)T, (int)d, CT, (int)((Tp + kFQ - 1) / kFQ), (int)W).total;
+    // ns == 1: the key-side results go straight to dk / dv
+    float* dk_out = ns > 1 ? kv_part : dk;
+    float* dv_out = ns > 1 ? kv_part + ns * n_kv : dv;
 #define OB_RA_FUSED(DQ)                                                                           \
-  hipLaunchKernelGGL((relattn_bwd_fused_kernel<DQ, kFusedWaves>), dim3((unsigned)(Bt * H)),        \
+  hipLaunchKernelGGL((relattn_bwd_fused_kernel<DQ, kFusedWaves>), dim3((unsigned)(Bt * H * ns)),   \
                      dim3(64 * kFusedWaves), lds, s, dctx, ctx, q, k, v, pos, u, vb, lens, stats,   \
-                     kbits, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, dq, dk, dv, dp_part,     \
-                     du_part, dvb_part)
+                     kbits, anchors, (int)(Bt / P), (int)T, (int)H, ns, inv_sqrt_d, dc, dq, dk_out, \
+                     dv_out, (size_t)n_kv, dp_part, du_part, dvb_part)
     if (d == 16) OB_RA_FUSED(4);
     else if (d == 32) OB_RA_FUSED(8);
     else OB_RA_FUSED(9);
 #undef OB_RA_FUSED
-    const int64_t C = H * d;
     const int n_dpos = (int)ceil_div(P * T * C, 64);
     const int n_bias = (int)(2 * H * ((d + kBiasCols - 1) / kBiasCols));
-    hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)(n_dpos + n_bias)), dim3(kThreads), 0,
-                       s, (const float*)dp_part, (const float*)du_part, (const float*)dvb_part,
-                       (int)Bt, (int)P, (int)T, (int)H, (int)d, 1, n_dpos, dpos, du, dvb);
+    const int n_kvb = ns > 1 ? (int)ceil_div(2 * n_kv, 4 * kThreads) : 0;
+    hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)(n_dpos + n_bias + n_kvb)),
+                       dim3(kThreads), 0, s, (const float*)dp_part, (const float*)du_part,
+                       (const float*)dvb_part, (int)Bt, (int)P, (int)T, (int)H, (int)d, ns, n_dpos,
+                       dpos, du, dvb, ns, n_bias, (const float*)kv_part, n_kv, dk, dv);
     return;
   }
-  const float* probs = saved + Bt * H * Tp * (2 + W);
+  const float* probs = saved + SavedLayout(Bt, T, H, d).tail;
   const int nqt = (int)((T + kTile - 1) / kTile);
   const dim3 grid((unsigned)(nqt * H * Bt));
   const DropCfg dc = make_drop(p_drop);
@@ -1536,8 +1728,15 @@ void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, con
   const int n_bias = (int)(2 * H * ((d + kBiasCols - 1) / kBiasCols));
   hipLaunchKernelGGL(relattn_reduce_kernel, dim3((unsigned)(n_dpos + n_bias)), dim3(kThreads), 0, s,
                      (const float*)dp_part, (const float*)du_part, (const float*)dvb_part, (int)Bt,
-                     (int)P, (int)T, (int)H, (int)d, nqt, n_dpos, dpos, du, dvb);
+                     (int)P, (int)T, (int)H, (int)d, nqt, n_dpos, dpos, du, dvb, 1, n_bias,
+                     (const float*)nullptr, (int64_t)0, (float*)nullptr, (float*)nullptr);
 }
+
+#ifdef OB_ATTN_STAMPS
+extern "C" int ob_attn_stamps(void* host_dst) {  // diagnostic build only
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? 0 : -6;
+}
+#endif
 
 void launch_relattn_dropout_mask(int64_t n, int64_t T, float p_drop, const uint64_t* rng,
                                  uint64_t rng_off, uint8_t* out, hipStream_t s) {
