@@ -7,9 +7,9 @@ ints or device values, the HIP CTC with device-side lengths, the decoder's causa
 AdamW with a device lr) the whole body is captured once and replayed:
 
 * graph A: zero the flat gradient buffer, the three passes, their losses, backward;
-* [N > 1: one all-reduce (SUM) of the flat gradient buffer over RCCL, outside the graph;]
-* graph B (merged into A when N == 1): clip_grad_norm_(5.0) + AdamW as the three-launch
-  ``FusedAdamW`` (the 1/world average is folded into its gradient scale).
+* N > 1: the gradient exchange, bucketed and overlapped with the backward (below);
+* clip_grad_norm_(5.0) + AdamW as the three-launch ``FusedAdamW`` (the 1/world average is
+  folded into its gradient scale) -- all of it one graph.
 
 Both step bodies capture: the stacked one (``OneBitStep(stacked=True)``) and the
 reference's literal three forwards. Nothing inside the captured region may rely on a
@@ -27,12 +27,24 @@ What changes per step without re-capture:
   shape needs another ``GraphedTrainStep``);
 * dropout masks: torch's philox offsets advance per replay.
 
-With N > 1 gradients live in one flat fp32 buffer (parameter order) so the exchange is a
-single large all-reduce -- the bucket size xGMI ring all-reduce wants -- with no
-flatten/unflatten copies. With N == 1 autograd's own gradient buffers are used as they
-are (``p.grad = None`` before backward, so no accumulate kernels). Parameters that receive
-no gradient in the step are excluded from the optimizer exactly like the reference (AdamW
-skips grad=None).
+With N > 1 gradients live in one flat fp32 buffer (parameter order, no flatten/unflatten
+copies), cut into buckets of contiguous parameters taken in REVERSE order (the backward
+produces the decoder / CTC-head and last-block gradients first). A post-accumulate-grad
+hook counts each bucket's parameters; when a bucket's last gradient has landed its slice is
+all-reduced (SUM) on a communication stream that waited for it, while the backward goes on
+on the compute stream; the update waits for the communication stream (``BucketedAllReduce``;
+reference train.py:116-118 is single-device: loss.backward(), clip, step). The buckets are
+``bucket_mb`` (default 12 MB: 4 buckets for Conformer-S's 47 MB, each large enough for the
+per-link bandwidth of a ring over xGMI). The whole step (forward, backward with the bucket
+all-reduces, update) is captured as one graph; if the process group cannot be captured the
+exchange runs eagerly between graph A and the update graph (flat, one call), as before.
+Without overlap each rank would idle for the whole exchange after its backward. Note: with
+N > 1 the parameter gradients are views of the flat buffer, so the deferred finishes
+(deferred.py) do not apply and every weight-gradient finish runs on the spot (~230 more
+small launches than the single-GPU step). With N == 1 autograd's own gradient buffers are
+used as they are (``p.grad = None`` before backward, so no accumulate kernels). Parameters
+that receive no gradient in the step are excluded from the optimizer exactly like the
+reference (AdamW skips grad=None).
 """
 from __future__ import annotations
 
@@ -46,14 +58,83 @@ from .optim import FusedAdamW
 from .quant import DeviceBits, QuantizedLinear
 from .train_step import WarmupCosine
 
-__all__ = ["GraphedTrainStep"]
+__all__ = ["GraphedTrainStep", "BucketedAllReduce"]
+
+
+class BucketedAllReduce:
+    """SUM all-reduce of a flat gradient buffer in buckets, each started from a
+    post-accumulate-grad hook as soon as its last parameter's gradient has landed. ``params``
+    are laid out in ``flat`` in order; buckets are contiguous runs of them taken from the end
+    (the backward's order). CUDA: the bucket is reduced on ``comm`` after an event on the
+    producing stream; ``finish`` makes the current stream wait. CPU (gloo): async works,
+    waited in ``finish``."""
+
+    def __init__(self, params, flat: torch.Tensor, pg, bucket_bytes: int):
+        self.flat = flat
+        self.pg = pg
+        self.enabled = False
+        offs, off = [], 0
+        for p in params:
+            offs.append(off)
+            off += p.numel()
+        self.buckets = []  # (lo, hi, n_params)
+        self.bucket_of = {}
+        hi, lo, n = off, off, 0
+        for i in range(len(params) - 1, -1, -1):
+            p = params[i]
+            lo = offs[i]
+            self.bucket_of[id(p)] = len(self.buckets)
+            n += 1
+            if (hi - lo) * 4 >= bucket_bytes or i == 0:
+                self.buckets.append((lo, hi, n))
+                hi, n = lo, 0
+        self.count = [0] * len(self.buckets)
+        self.works = []
+        self.cuda = flat.is_cuda
+        self.comm = torch.cuda.Stream(flat.device) if self.cuda else None
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
+
+    def begin(self):
+        self.count = [0] * len(self.buckets)
+        self.works = []
+
+    def _hook(self, p):
+        if not self.enabled:
+            return
+        k = self.bucket_of[id(p)]
+        self.count[k] += 1
+        if self.count[k] == self.buckets[k][2]:
+            self._launch(k)
+
+    def _launch(self, k):
+        lo, hi, _ = self.buckets[k]
+        view = self.flat[lo:hi]
+        if self.cuda:
+            self.comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(self.comm):
+                dist.all_reduce(view, group=self.pg)
+        else:
+            self.works.append(dist.all_reduce(view, group=self.pg, async_op=True))
+
+    def finish(self):
+        """Every bucket has been started (each parameter's hook fired once); make the
+        update wait for the exchange."""
+        if any(c != b[2] for c, b in zip(self.count, self.buckets)):
+            raise RuntimeError("bucketed all-reduce: a bucket did not complete "
+                               f"({self.count} of {[b[2] for b in self.buckets]})")
+        if self.cuda:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)
+        for w in self.works:
+            w.wait()
+        self.works = []
 
 
 class GraphedTrainStep:
     def __init__(self, step_module, n_layers: int, lr: float = 5e-4, warmup_steps: int = 4000,
                  total_steps: int = 100000, max_norm: float = 5.0,
                  process_group: Optional[dist.ProcessGroup] = None, warmup_iters: int = 2,
-                 use_graph: bool = True, fused_optimizer: bool = True):
+                 use_graph: bool = True, fused_optimizer: bool = True,
+                 bucket_mb: Optional[float] = 12.0):
         self.step_module = step_module
         self.n_layers = n_layers
         self.lr0 = lr
@@ -77,6 +158,9 @@ class GraphedTrainStep:
         self.graph_a = self.graph_b = None
         self.loss = self.parts = None
         self.steps_done = 0
+        self.bucket_bytes = int(bucket_mb * 2**20) if bucket_mb else 0
+        self.buckets: Optional[BucketedAllReduce] = None
+        self.comm_in_graph = False
 
     # ------------------------------------------------------------------ setup
     def _set_batch(self, batch):
@@ -109,6 +193,8 @@ class GraphedTrainStep:
                 n = p.numel()
                 p.grad = self.flat[off:off + n].view_as(p)
                 off += n
+            if self.bucket_bytes:
+                self.buckets = BucketedAllReduce(self.params, self.flat, self.pg, self.bucket_bytes)
         if self.device.type == "cuda" and self.fused_optimizer:
             self.fused = True
             self.opt = FusedAdamW(self.params, lr=self.lr0, betas=(0.9, 0.98), eps=1e-8,
@@ -130,15 +216,24 @@ class GraphedTrainStep:
                     off += n
         self.sched = WarmupCosine(self.opt, self.warmup_steps, self.total_steps)
 
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, overlap: bool = False):
+        """Forward + backward; ``overlap``: the buckets' all-reduces start from the backward
+        (finished by ``_allreduce``)."""
         if self.flat is not None:
             self.flat.zero_()
         else:  # N == 1: autograd hands its gradient buffers over (no accumulate kernels)
             for p in self.params:
                 p.grad = None
-        with deferred.scope():  # one finish launch per kind at the end of the backward
-            loss, parts = self.step_module(self.batch, self.bits)
-            loss.backward()
+        if self.buckets is not None:
+            self.buckets.begin()
+            self.buckets.enabled = overlap
+        try:
+            with deferred.scope():  # one finish launch per kind at the end of the backward
+                loss, parts = self.step_module(self.batch, self.bits)
+                loss.backward()
+        finally:
+            if self.buckets is not None:
+                self.buckets.enabled = False
         return loss.detach(), parts
 
     def _update(self):
@@ -150,13 +245,17 @@ class GraphedTrainStep:
         torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, foreach=True)
         self.opt.step()
 
-    def _allreduce(self):
+    def _allreduce(self, overlapped: bool = False):
         if self.world > 1:
-            dist.all_reduce(self.flat, group=self.pg)
+            if overlapped:
+                self.buckets.finish()
+            else:
+                dist.all_reduce(self.flat, group=self.pg)
 
     def _eager(self):
-        loss, parts = self._fwd_bwd()
-        self._allreduce()
+        ov = self.buckets is not None
+        loss, parts = self._fwd_bwd(overlap=ov)
+        self._allreduce(overlapped=ov)
         self._update()
         return loss, parts
 
@@ -232,16 +331,39 @@ class GraphedTrainStep:
             return
         torch.cuda.synchronize(self.device)
         self._drop_code_caches(self.step_module)
-        self.graph_a = torch.cuda.CUDAGraph()
         pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(self.graph_a, pool=pool):
-            self.loss, self.parts = self._fwd_bwd()
-            if self.world == 1:
-                self._update()
-        if self.world > 1:
-            self.graph_b = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_b, pool=pool):
-                self._update()
+        if (self.world > 1 and self.buckets is not None
+                and dist.get_backend(self.pg) == dist.Backend.NCCL):
+            # the whole step in one graph, the bucket all-reduces overlapping the backward
+            # (RCCL collectives capture into a graph; gloo's host staging does not)
+            rng = self._rng_snapshot()  # (a failed attempt must not advance the dropout streams)
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    self.loss, self.parts = self._fwd_bwd(overlap=True)
+                    self._allreduce(overlapped=True)
+                    self._update()
+                self.graph_a, self.comm_in_graph = g, True
+            except Exception as e:  # the process group cannot be captured: exchange eagerly
+                import warnings
+
+                from .fused import rng_restore
+
+                warnings.warn(f"all-reduce capture failed ({e!r}); exchanging between graphs")
+                torch.cuda.synchronize(self.device)
+                rng_restore(self.device, rng[0])
+                torch.cuda.set_rng_state(rng[1], self.device)
+                self.comm_in_graph = False
+        if not self.comm_in_graph:
+            self.graph_a = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_a, pool=pool):
+                self.loss, self.parts = self._fwd_bwd()
+                if self.world == 1:
+                    self._update()
+            if self.world > 1:
+                self.graph_b = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_b, pool=pool):
+                    self._update()
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ step
@@ -258,7 +380,7 @@ class GraphedTrainStep:
             self.loss, self.parts = self._eager()
         else:
             self.graph_a.replay()
-            if self.world > 1:
+            if self.world > 1 and not self.comm_in_graph:
                 self._allreduce()
                 self.graph_b.replay()
             if self.fused:  # the replayed update wrote the parameters in place

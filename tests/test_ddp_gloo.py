@@ -111,7 +111,7 @@ class _HostBitsStep(torch.nn.Module):
         return self.inner(batch, [1 if v == 1 else 0 for v in bits.tensor.tolist()])
 
 
-def _graph_step_worker(rank, world, port, out_dir):
+def _graph_step_worker(rank, world, port, out_dir, bucket_mb=12.0, tag="g"):
     import sys
     from pathlib import Path
 
@@ -124,13 +124,15 @@ def _graph_step_worker(rank, world, port, out_dir):
 
     model = _model()
     gs = GraphedTrainStep(_HostBitsStep(model), n_layers=2, process_group=dist.group.WORLD,
-                          warmup_iters=1, warmup_steps=4, total_steps=10)
+                          warmup_iters=1, warmup_steps=4, total_steps=10, bucket_mb=bucket_mb)
     losses = []
     for mask in ([1, 0], [0, 1], [1, 1]):
         loss, _ = gs.step(_batch(rank), mask)
         losses.append(loss.item())
     params = {k: p.detach().clone() for k, p in model.named_parameters()}
-    torch.save({"params": params, "losses": losses}, os.path.join(out_dir, f"g{rank}.pt"))
+    nb = len(gs.buckets.buckets) if gs.buckets is not None else 0
+    torch.save({"params": params, "losses": losses, "buckets": nb},
+               os.path.join(out_dir, f"{tag}{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -173,3 +175,22 @@ def test_graph_step_flat_allreduce_gloo(tmp_path):
                 assert err <= 1e-5 * p.detach().abs().max().item() + 1e-7, (k, r, err)
     for k in res[0]["params"]:
         assert torch.equal(res[0]["params"][k], res[1]["params"][k]), k
+
+
+@pytest.mark.slow
+def test_bucketed_overlapped_allreduce_equals_flat_gloo(tmp_path):
+    """The exchange started bucket by bucket from the backward's post-accumulate hooks
+    (BucketedAllReduce, tiny buckets: one per few parameters) trains the replicas to exactly
+    the parameters of the single flat all-reduce after the backward (SUM over two ranks does
+    not depend on how the buffer is cut)."""
+    world = 2
+    for bucket_mb, tag in ((None, "flat"), (0.002, "bkt")):
+        mp.spawn(_graph_step_worker, args=(world, _free_port(), str(tmp_path), bucket_mb, tag),
+                 nprocs=world, join=True)
+    flat = [torch.load(tmp_path / f"flat{r}.pt", weights_only=True) for r in range(world)]
+    bkt = [torch.load(tmp_path / f"bkt{r}.pt", weights_only=True) for r in range(world)]
+    assert flat[0]["buckets"] == 0 and bkt[0]["buckets"] > 8, bkt[0]["buckets"]
+    for r in range(world):
+        assert flat[r]["losses"] == bkt[r]["losses"]
+        for k, p in flat[r]["params"].items():
+            assert torch.equal(p, bkt[r]["params"][k]), k
