@@ -654,9 +654,6 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
-    if os.environ.get("OB_BLAS_ALL"):  # A/B experiments: one BLAS library for every GEMM
-        torch.backends.cuda.preferred_blas_library(os.environ["OB_BLAS_ALL"])
-
     from onebit_asr.conformer import ConformerASR
     from onebit_asr.data import CONFORMER_S, synthetic_batch
     from onebit_asr.train_step import OneBitStep, WarmupCosine, make_optimizer, sample_sp_mask, train_step

@@ -297,22 +297,13 @@ struct DgCfg {
 };
 
 // Widest column tile whose image fits one CU's LDS (8 waves) or half of it (4 waves, two
-// blocks per CU), preferring tiles that divide N. OB_DGEMM_NT / OB_DGEMM_WAVES: tuning.
+// blocks per CU), preferring tiles that divide N.
 DgCfg pick_cfg(int64_t N, int64_t K) {
-  static const int env_nt = [] {
-    const char* e = getenv("OB_DGEMM_NT");
-    return e ? atoi(e) : 0;
-  }();
-  static const int env_w = [] {
-    const char* e = getenv("OB_DGEMM_WAVES");
-    return e ? atoi(e) : 0;
-  }();
   const int kpad = dg_kpad((int)K, 0);
   const bool k_special = kpad == 160 || kpad == 288;
   static const int cands[] = {9, 6, 3, 2, 1};
   for (int pass = 0; pass < 2; ++pass)
     for (int nt : cands) {
-      if (env_nt && nt != env_nt) continue;
       if (pass == 0 && N % (16 * nt) != 0) continue;
       if (16 * nt > ((N + 15) & ~int64_t(15))) continue;
       // instantiated combinations (launch_dense_gemm's switch)
@@ -323,7 +314,6 @@ DgCfg pick_cfg(int64_t N, int64_t K) {
       if (!k_special && !(nt == 3 || nt == 1)) continue;
       const size_t lds = dg_lds_bytes(nt, kpad);
       int waves = lds <= kLdsCU / 2 ? 4 : lds <= kLdsCU ? 8 : 0;
-      if (env_w && waves && lds <= kLdsCU / (env_w == 4 ? 2 : 1)) waves = env_w;
       if (waves) return DgCfg{nt, waves};
     }
   return DgCfg{0, 0};

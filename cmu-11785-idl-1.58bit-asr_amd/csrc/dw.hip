@@ -806,21 +806,6 @@ __global__ __launch_bounds__(kThreads) void dw_finish_group_kernel(DwFinishGroup
   dw_finish_body(G.g[i], b - G.start[i], G.start[i + 1] - G.start[i]);
 }
 
-bool use_reg_dw() {  // OB_DW=reg: the register-only bf16x6 kernel (A/B experiments)
-  static const int v = [] {
-    const char* e = getenv("OB_DW");
-    return (e && e[0] == 'r') ? 1 : 0;
-  }();
-  return v != 0;
-}
-
-bool use_f32_dw() {
-  static const int v = [] {
-    const char* e = getenv("OB_GEMM");
-    return (e && e[0] == 'f') ? 1 : 0;
-  }();
-  return v != 0;
-}
 
 }  // namespace
 
@@ -829,7 +814,7 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) { return plan_dw_passes(1, M, N,
 DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
   DwPlan p;
   const int64_t M = P * Mp;  // chunk length is chosen for the whole stacked M
-  if (use_f32_dw() || N % 4 != 0 || K % 4 != 0 || N < 4 || K < 4) {
+  if (N % 4 != 0 || K % 4 != 0 || N < 4 || K < 4) {
     p.variant = 0;
     p.tiles_n = N > 0 ? ceil_div(N, kDwTile) : 1;  // >= 1 so K = 0 still yields db
     p.tiles_k = K > 0 ? ceil_div(K, kDwTile) : 1;
@@ -837,7 +822,7 @@ DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
     int64_t steps = 32;  // chunk = S steps x 16 rows
     while (steps > 8 && tiles * ceil_div(M, 16 * steps) < 256) steps /= 2;
     p.rows_per_chunk = 16 * steps;
-  } else if (N % 48 == 0 && K % 48 == 0 && !use_reg_dw()) {
+  } else if (N % 48 == 0 && K % 48 == 0) {
     // LDS-shared bf16x6: 144x144 block tiles (9 waves) where both widths allow it, else
     // 144x48 / 48x144 (3 waves) or 48x48 (1 wave); chunks of 32-row steps sized for ~256
     // blocks (one per CU).
@@ -860,11 +845,7 @@ DwPlan plan_dw_passes(int64_t P, int64_t Mp, int64_t N, int64_t K) {
     const int64_t tiles = p.tiles_n * p.tiles_k;
     // Chunk = 4 waves x S steps x 32 rows, S in {2, 4, 8}: the longest chunk that still
     // gives >= 256 blocks (one per CU), so the partial slabs stay few.
-    static const int64_t max_steps = [] {  // OB_DW_MAXSTEPS: tuning experiments
-      const char* e = getenv("OB_DW_MAXSTEPS");
-      return (int64_t)(e ? atoi(e) : 8);
-    }();
-    int64_t steps = max_steps;
+    int64_t steps = 8;
     while (steps > 2 && tiles * ceil_div(M, 128 * steps) < 256) steps /= 2;
     p.rows_per_chunk = 128 * steps;
   }

@@ -646,23 +646,10 @@ __global__ __launch_bounds__(kThreads) void ln_param_table_kernel(
   }
 }
 
-// OB_LN_BWD_BLOCKS / OB_LN_RPT: tuning experiments (same arithmetic per row and column)
-int max_bwd_blocks() {
-  static const int v = [] {
-    const char* e = getenv("OB_LN_BWD_BLOCKS");
-    const int n = e ? atoi(e) : 512;
-    return n > 0 ? n : 512;
-  }();
-  return v;
-}
-int fwd_rows_per_group() {
-  static const int v = [] {
-    const char* e = getenv("OB_LN_RPT");
-    const int n = e ? atoi(e) : 1;
-    return n == 2 || n == 4 ? n : 1;
-  }();
-  return v;
-}
+// launch shapes measured in round 3 (profiles/r3/ln/): 512 backward blocks, one row per
+// 16-lane group in the forward
+int max_bwd_blocks() { return 512; }
+int fwd_rows_per_group() { return 1; }
 
 int bwd_blocks(int64_t rows, int* rows_per_block) {
   int64_t nb = ceil_div(rows, kRowsPerBlock);

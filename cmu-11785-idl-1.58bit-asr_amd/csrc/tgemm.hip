@@ -620,13 +620,8 @@ __global__ __launch_bounds__(kThreads) void tgemm_f32_kernel(
   }
 }
 
-bool use_f32_gemm() {
-  static const int v = [] {
-    const char* e = getenv("OB_GEMM");
-    return (e && e[0] == 'f') ? 1 : 0;
-  }();
-  return v != 0;
-}
+// The fp32-MFMA GEMM (tgemm_f32 kernels) serves the shapes the bf16x3 kernels do not take.
+bool use_f32_gemm() { return false; }
 
 size_t bimg_bytes(int nt, int64_t K) {
   const int64_t kpad = (K + 31) & ~int64_t(31);
@@ -636,7 +631,6 @@ size_t bimg_bytes(int nt, int64_t K) {
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // Widest column tile whose bf16 image fits the LDS budget, preferring tiles that divide N.
-// OB_TGEMM_NTMAX (tuning experiments) caps the width.
 // Fused epilogues: widths whose instantiation spills are excluded (checked with
 // -Rpass-analysis=kernel-resource-usage on the row-coalesced (VEC_EPI) kernels: every
 // epilogue is spill-free up to NT 9 at K <= 160 and up to NT 4 beyond).
@@ -646,17 +640,7 @@ bool epi_nt_ok(int nt, int64_t K, int epi_mode) {
 }
 
 int pick_nt(int64_t N, int64_t K, int epi_mode) {
-  static const int env_cap = [] {
-    const char* e = getenv("OB_TGEMM_NTMAX");
-    return e ? atoi(e) : 12;
-  }();
-  const int cap = env_cap;
-  static const int cands_all[] = {12, 9, 6, 4, 3, 2, 1};
-  int cands[7];
-  int nc = 0;
-  for (int c : cands_all)
-    if (c <= cap) cands[nc++] = c;
-  for (int i = nc; i < 7; ++i) cands[i] = 1;
+  static const int cands[] = {12, 9, 6, 4, 3, 2, 1};
   for (int nt : cands)
     if (epi_nt_ok(nt, K, epi_mode) && N % (16 * nt) == 0 &&
         bimg_bytes(nt, K) + 16 + epi_stage_bytes(nt) <= kMaxLds)
@@ -675,11 +659,7 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
                    hipStream_t s) {
   const int n_ct = ep.glayers * (int)ceil_div(N, 16 * NT);  // all layers' column tiles
   const int n_rt = (int)ceil_div(M, kRows);
-  static const int target = [] {  // OB_TGEMM_BLOCKS: tuning experiments
-    const char* e = getenv("OB_TGEMM_BLOCKS");
-    return e ? atoi(e) : kTargetBlocks;
-  }();
-  int rgroups = target / (n_ct * P);
+  int rgroups = kTargetBlocks / (n_ct * P);
   if (rgroups < 1) rgroups = 1;
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);

@@ -22,7 +22,6 @@ reference (conv module "kept full-precision per paper recommendation", :225; sub
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -465,7 +464,6 @@ class ConformerEncoder(nn.Module):
         return self.ln_out(x), key_mask
 
 
-_DEC_RESDROP = os.environ.get("OB_DEC_RESDROP", "1") != "0"  # 0: torch dropout + add
 
 
 def _residual_dropout(x: torch.Tensor, y: torch.Tensor, p: float, training: bool):
@@ -475,7 +473,7 @@ def _residual_dropout(x: torch.Tensor, y: torch.Tensor, p: float, training: bool
     LayerNorm's backward (layernorm.GradScale) instead of a pass of its own."""
     if not (training and p > 0):
         return x + y
-    if not (_DEC_RESDROP and x.is_cuda and x.shape == y.shape):
+    if not (x.is_cuda and x.shape == y.shape):
         return x + F.dropout(y, p, training)
     from .conv import _ResidualDropFn
     from .fused import _rng

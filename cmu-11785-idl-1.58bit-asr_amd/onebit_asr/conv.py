@@ -198,11 +198,14 @@ class _BlasPref:
         return False
 
 
-_PW_BLAS = os.environ.get("OB_PW_BLAS", "cublas")  # "cublas" selects rocBLAS on ROCm
+# pointwise convs the dense kernels do not take run on rocBLAS (measured faster than
+# hipBLASLt for these shapes, tools/blas_pick.py)
+_PW_BLAS = "cublas"  # ("cublas" selects rocBLAS on ROCm)
 
-
-_PW = os.environ.get("OB_PW", "hip")  # "blas": the rocBLAS fp32 GEMMs (A/B checks)
-_PW_RESID = os.environ.get("OB_PW_RESID", "1") != "0"  # 0: pw2, then the residual kernel
+# parity-test hooks (tests/test_dense_gpu.py, tests/test_convmod_gpu.py flip them): "blas"
+# runs the pointwise convs on the library; False runs pw2 and the residual as two launches
+_PW = "hip"
+_PW_RESID = True
 
 
 def _aligned(t: torch.Tensor) -> bool:

@@ -27,11 +27,10 @@ A gradient is deferred only when nothing can read it before the flush:
   no deferral for a parameter carrying a post-accumulate-grad hook.
 The workspaces holding the partials are kept referenced until the flush. A slot is counted
 only once its producing launch returned OB_OK; a scope left by an exception drops the
-pending entries instead of launching them. ``OB_DEFER=0`` finishes everything immediately.
+pending entries instead of launching them.
 """
 from __future__ import annotations
 
-import os
 from contextlib import contextmanager
 from typing import Dict, List, Optional
 
@@ -42,7 +41,7 @@ from . import _lib
 __all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "ln_done", "cm_slot", "keep",
            "add_grad_after_flush", "active"]
 
-_ON = os.environ.get("OB_DEFER", "1") != "0"
+_ON = True  # parity-test hook (tests/test_stacked_step_gpu.py: False = finish on the spot)
 _CAP = 512  # table entries per kind
 
 

@@ -37,8 +37,9 @@ __all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
            "i8_fused_supported", "ffn_residual_i8", "linear_residual_i8", "qkv_projections",
            "i8_linear"]
 
-_DW_GROUP = os.environ.get("OB_DW_GROUP", "1") != "0"  # 0: q/k/v dW one by one
-_QKV_FWD_GROUP = os.environ.get("OB_QKV_FWD_GROUP", "1") != "0"  # 0: q / k / v fwd one by one
+# parity-test hooks (tests/test_fused_gpu.py): False = q / k / v dW, forward one by one
+_DW_GROUP = True
+_QKV_FWD_GROUP = True
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
 

@@ -7,7 +7,6 @@ square root); the backward's dgamma / dbeta are summed in a fixed order.
 """
 from __future__ import annotations
 
-import os
 from typing import NamedTuple
 
 import torch
@@ -18,7 +17,7 @@ from . import _lib, deferred
 __all__ = ["layer_norm", "layer_norm_fork", "layer_norm_amax", "layer_norm_i8", "Int8Act",
            "fused_layernorm_supported", "GradScale", "attach_grad_scale"]
 
-_GSCALE = os.environ.get("OB_LN_GSCALE", "1") != "0"  # 0: consumers run ob_drop_scale_bwd
+_GSCALE = True  # parity-test hook (False: the consumers run ob_drop_scale_bwd)
 
 
 class GradScale:
@@ -94,8 +93,6 @@ def _bwd_call(lib, g2, x2, weight, mean, rstd, rows, d, dres, dx, dw, db, ws, ws
 
 
 def fused_layernorm_supported(x: torch.Tensor, d: int) -> bool:
-    if os.environ.get("OB_LN", "") == "torch":
-        return False
     return x.is_cuda and x.dtype == torch.float32 and 1 <= d <= 512
 
 
@@ -176,8 +173,10 @@ class _LayerNormFn(torch.autograd.Function):
         return dx.view(gy.shape), dw, db, None, None, None, None
 
 
-_PAIR = os.environ.get("OB_LN_PAIR", "1") != "0"  # 0: every LN its own launch
-_PAIR_BWD = os.environ.get("OB_LN_PAIR_BWD", "1") != "0"  # 0: the pair's backwards one by one
+# parity-test hooks (tests/test_stacked_step_gpu.py): False = every LN its own launch /
+# the pair's backwards one by one
+_PAIR = True
+_PAIR_BWD = True
 
 
 class _PairLink:

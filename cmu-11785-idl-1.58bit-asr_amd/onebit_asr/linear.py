@@ -25,7 +25,6 @@ OB_DENSE_LINEAR_DW=0: library weight gradients.
 """
 from __future__ import annotations
 
-import os
 
 from typing import Optional
 
@@ -36,24 +35,19 @@ from . import _lib, deferred
 
 __all__ = ["linear", "colsum"]
 
-_DENSE = os.environ.get("OB_DENSE_LINEAR", "1") != "0"
-_DENSE_DW = _DENSE and os.environ.get("OB_DENSE_LINEAR_DW", "1") != "0"
-# widths that are not multiples of 48 (the V = 5004 CTC head / decoder output layer) on the
-# register bf16x6 dW tiles; 0 keeps them on the library
-_DENSE_DW_WIDE = os.environ.get("OB_DENSE_DW_WIDE", "1") != "0"
 
 
 def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
     """ob_dense_gemm's preconditions (capi.hip: aligned16 of BOTH operands), so an operand
     it would refuse takes the library path instead of raising."""
-    return (_DENSE and k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
+    return (k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
             and w.data_ptr() % 16 == 0 and _lib.load().ob_dense_supported(k, n) == 1)
 
 
 def _dense_dw_ws(g2: torch.Tensor, x2d: torch.Tensor, w: torch.Tensor) -> int:
     """Workspace bytes of ob_dense_dw for this linear's weight gradient, 0 if not taken
     (N, K multiples of 4; 16-byte aligned operands)."""
-    if not (_DENSE_DW and g2.is_cuda and x2d.is_contiguous() and w.is_contiguous()
+    if not (g2.is_cuda and x2d.is_contiguous() and w.is_contiguous()
             and g2.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0):
         return 0
     n, k = w.shape

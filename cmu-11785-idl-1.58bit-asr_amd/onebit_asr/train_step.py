@@ -14,7 +14,6 @@ generator seeded identically on all ranks (train.py:56-59 draws from the global 
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -25,7 +24,6 @@ from . import deferred
 from .losses import att_ce_loss, ctc_loss_from_logits, kl_logits, make_att_targets
 from .seqloss import att_kl_losses, att_kl_supported
 
-_ATT_KL = os.environ.get("OB_ATT_KL", "1") != "0"  # 0: the torch loss expressions
 
 __all__ = ["OneBitStep", "WarmupCosine", "sample_sp_mask", "train_step", "SPECIAL_IDS",
            "make_optimizer"]
@@ -208,7 +206,7 @@ class OneBitStep(nn.Module):
         logits = self.model.decode_logits(enc, mask, t_inp.repeat(P, 1), t_pad.repeat(P, 1))
         # attention CE per pass (losses.py:22-35, label smoothing, scalar-mean quirk) and
         # KL(teacher || student) for the student and SP passes (losses.py:50-59)
-        if _ATT_KL and att_kl_supported(logits, self.label_smoothing):
+        if att_kl_supported(logits, self.label_smoothing):
             # csrc/seqloss.hip: both losses, one row pass per direction
             l_att, l_kl = att_kl_losses(logits, t_out, t_pad, P, sp["pad_id"],
                                         self.label_smoothing)

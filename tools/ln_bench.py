@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """LayerNorm kernel timing at the Conformer-S shape (rows = 3 passes x 32 x 249, d = 144):
 forward, backward with dgamma/dbeta, backward with dres + dy2 (dropout 0.1), graph-replayed
-launches timed with HIP events on the launch stream. The OB_LN_* switches of layernorm.hip
-are read once per process: run one process per setting (tools/gpu_ln_ab.sh).
+launches timed with HIP events on the launch stream (an older library: ONEBIT_HIP_LIB).
 Usage: python tools/ln_bench.py [--reps 100]"""
 import argparse
 import ctypes
