@@ -1576,8 +1576,16 @@ bool relattn_supported(int64_t T, int64_t d) {
   return T >= 1 && T <= 512 && (d == 16 || d == 32 || d == 36 || d == 64);
 }
 
-// the flash-style backward (relattn_bwd_fused_kernel): T <= 256 (16 key tiles), d <= 36
-bool relattn_fused(int64_t T, int64_t d) { return T <= 256 && d <= 36; }
+// the flash-style backward (relattn_bwd_fused_kernel): T <= 256 (16 key tiles), d <= 36, when
+// selected (OB_ATTN_BWD=flash, read per call). It keeps every [T][T] quantity on chip but is
+// slower than the probability path at Conformer-S (measured 400 vs 253 us per call: one fat
+// block per (b, h) split in two, latency-bound chunk phases at 2 waves per SIMD; DESIGN.md
+// "Attention"), so the probability path stays the default.
+bool relattn_fused(int64_t T, int64_t d) {
+  if (!(T <= 256 && d <= 36)) return false;
+  const char* e = getenv("OB_ATTN_BWD");
+  return e && e[0] == 'f';
+}
 
 // saved state of the forward for the backward (fp32 elements): row statistics
 // [Bt*H][Tp][2] (max, 1/sum) | keep bits [Bt*H][Tp][W] | then either (flash-style backward)
@@ -1643,9 +1651,10 @@ void launch_relattn_fwd(const float* q, const float* k, const float* v, const fl
   const float inv_sqrt_d = 1.0f / (float)sqrt((double)d);  // torch: tensor / scalar = * (1/scalar)
   const size_t lds = fwd_lds_bytes((int)T, (int)d);
   const SavedLayout sl(Bt, T, H, d);
-  float* stats = saved;
-  uint32_t* kbits = saved ? reinterpret_cast<uint32_t*>(saved + sl.kbits) : nullptr;
-  float* anchors = saved && relattn_fused(T, d) ? saved + sl.tail : nullptr;
+  const bool flash = saved && relattn_fused(T, d);  // else the probabilities are saved
+  float* stats = flash ? saved : nullptr;
+  uint32_t* kbits = flash ? reinterpret_cast<uint32_t*>(saved + sl.kbits) : nullptr;
+  float* anchors = flash ? saved + sl.tail : nullptr;
   // the probability path's backward reads the tiles from the saved state
   if (saved && !relattn_fused(T, d)) probs = saved + sl.tail;
 #define OB_RA_FWD(DQ, NTT)                                                                 \

@@ -71,10 +71,15 @@ def _close(got, ref, rel, atol, what):
     assert err <= bound, f"{what}: max err {err:.3e} > {bound:.3e}"
 
 
+@pytest.mark.parametrize("bwd", ["probs", "flash"])
 @pytest.mark.parametrize("bt,P,t,H,d,lens", CASES)
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_relattn_matches_reference(gpu, bt, P, t, H, d, lens, p):
+def test_relattn_matches_reference(gpu, bt, P, t, H, d, lens, p, bwd, monkeypatch):
+    """bwd: the backward that reads the stored probabilities (default) or the flash-style one
+    (OB_ATTN_BWD=flash; T <= 256, d <= 36 -- other shapes take the probability path)."""
     from onebit_asr import attention as at
+
+    monkeypatch.setenv("OB_ATTN_BWD", "flash" if bwd == "flash" else "")
 
     q, k, v, pos, u, vb = _inputs(bt, P, t, H, d, seed=bt * 1000 + t)
     lens_t = torch.tensor(lens)
