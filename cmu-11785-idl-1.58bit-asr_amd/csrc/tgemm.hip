@@ -10,8 +10,10 @@
 // `a` is applied once in the epilogue (Y = a*(X.Q^T)).
 //
 // Block = 4 waves, 64 rows x BN = 16*NT columns. At entry the block decodes its BN code
-// rows into a bf16 image of Q in LDS ([BN][Kpad+8], the row pad keeps the B-fragment
-// ds_read_b128 conflict-free at K = 144 / 576), then loops over its row tiles: each wave
+// rows into a bf16 image of Q in LDS ([BN][Kpad+16]: a row pitch of Kpad/2 + 8 dwords puts
+// the 16 lanes of every ds_read_b128 lane group of the B fragments on disjoint banks at
+// K = 144 and 576 -- the round-3 pad of 8 left 2-way conflicts at K = 576), then loops over
+// its row tiles: each wave
 // streams 16 rows of A (two dwordx4 per lane per 32-wide k-chunk, all chunks of a row in
 // flight at once when K is a compile-time size), splits them in registers and issues 3
 // MFMAs per 16-column tile. Blocks sharing a row tile are dealt to the same XCD so their
@@ -26,9 +28,8 @@
 // the block copies its rows into the LDS image instead of decoding codes, and the scale is
 // 1 -- the same kernel, tiles and fused epilogues, only the weight format differs.
 //
-// OB_GEMM=f32 in the environment selects an fp32-MFMA kernel (v_mfma_f32_16x16x4_f32,
-// exact fp32 fma chain) for A/B checks; it is also the path for shapes the bf16x3 kernel
-// does not take (K % 4 != 0, misaligned A, B image over 64 KB).
+// An fp32-MFMA kernel (v_mfma_f32_16x16x4_f32, exact fp32 fma chain) is the path for shapes
+// the bf16x3 kernel does not take (K % 4 != 0, misaligned A, B image over the LDS budget).
 #include <cstdlib>
 
 #include "ob_drop.h"
@@ -48,6 +49,7 @@ constexpr int kThreads = 256;  // 4 waves
 constexpr int kRows = 64;      // rows per row tile (16 per wave)
 constexpr size_t kMaxLds = 80 * 1024;  // B image + epilogue staging: 2 blocks per CU
 constexpr int kTargetBlocks = 512;  // 2 per CU
+constexpr int kBPad = 16;           // B-image row pad (bf16 elements), see the header
 
 __device__ __forceinline__ uint32_t code_bf16(uint32_t c) {
   return ((c & 1u) * 0x3F80u) | ((c & 2u) << 14);  // 0 -> 0, 1 -> +1.0, 3 -> -1.0
@@ -168,7 +170,7 @@ __device__ __forceinline__ void select_pass(const float* __restrict__& A, float*
 
 // byte offset of the epilogue staging tiles (after the B image, 16-B aligned) and their size
 __host__ __device__ inline size_t epi_stage_off(int nt, int kpad) {
-  return ((size_t)2 * 16 * nt * (kpad + 8) + 15) & ~(size_t)15;
+  return ((size_t)2 * 16 * nt * (kpad + kBPad) + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t epi_stage_bytes(int nt) {
   const int cw = nt < 4 ? nt : 4;
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
   const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
-  const int stride = kpad + 8;
+  const int stride = kpad + kBPad;
   const int kwp = kpad >> 4;
   // row-coalesced epilogue (vec_epi): per-wave staging [16][kEpiCC + 4] after the B image
   constexpr int kEpiCW = NT < 4 ? NT : 4, kEpiCC = 16 * kEpiCW, kEpiLd = kEpiCC + 4;
@@ -625,7 +627,7 @@ bool use_f32_gemm() { return false; }
 
 size_t bimg_bytes(int nt, int64_t K) {
   const int64_t kpad = (K + 31) & ~int64_t(31);
-  return sizeof(uint16_t) * (size_t)(16 * nt) * (size_t)(kpad + 8);
+  return sizeof(uint16_t) * (size_t)(16 * nt) * (size_t)(kpad + kBPad);
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
