@@ -51,8 +51,6 @@ def _dense_dw_ws(g2: torch.Tensor, x2d: torch.Tensor, w: torch.Tensor) -> int:
             and g2.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0):
         return 0
     n, k = w.shape
-    if not _DENSE_DW_WIDE and (n % 48 or k % 48):
-        return 0
     return int(_lib.load().ob_dense_dw_workspace(g2.shape[0], n, k))
 
 
