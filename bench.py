@@ -419,12 +419,84 @@ def cpu_baseline(seconds: float, bsz: int = 4, progress=lambda msg: None):
     except Exception:
         pass
     tried = ", ".join(f"{k} threads {bsz * 1000 / v:.0f}" for k, v in sorted(trial.items()))
-    return {"value": round(bsz * 1000 / t, 1), "unit": "mel-frames/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle (CPU fp32 restatement) full 3-pass step + AdamW on Conformer-S, "
-                      f"B={bsz} x 1000 frames, median of {len(times)} steps after warm-up; "
-                      f"{threads} torch threads on {cpu} (affinity {n_aff} cores, "
-                      f"os.cpu_count() {n_cpu}; one-step trial mel-frames/s: {tried})"}
+    out = {"value": round(bsz * 1000 / t, 1), "unit": "mel-frames/s", "cores": threads,
+           "kind": "port",
+           "sample": f"oracle (CPU fp32 restatement) full 3-pass step + AdamW on Conformer-S, "
+                     f"B={bsz} x 1000 frames, median of {len(times)} steps after warm-up; "
+                     f"{threads} torch threads on {cpu} (affinity {n_aff} cores, "
+                     f"os.cpu_count() {n_cpu}; one-step trial mel-frames/s: {tried})"}
+    out["cfg1"] = cpu_cfg1(progress)
+    out["ql_microbench"] = cpu_ql_microbench(progress)
+    return out
+
+
+def cpu_cfg1(progress=lambda msg: None, steps: int = 10):
+    """SURVEY 8(d)'s parity config on the host: the oracle step (3 passes + losses + backward
+    + clip + AdamW) of the 2-block d_model 64 Conformer at B = 2, feat_lens [734, 349], 10
+    steps after one warm-up, at the thread count cpu_baseline chose."""
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CFG1, synthetic_batch
+    from onebit_asr.train_step import sample_sp_mask
+    from oracle.conformer_oracle import OracleConformer, oracle_step_loss
+
+    torch.manual_seed(0)
+    prod = ConformerASR(N_MELS, VOCAB, **CFG1)
+    orc = OracleConformer(prod.state_dict(), input_dim=N_MELS, vocab_size=VOCAB, d_model=64,
+                          n_layers=2, n_heads=4, d_ff=256, conv_kernel=31, dec_layers=2,
+                          dec_heads=4, dec_d_ff=1024, dropout=0.0)
+    opt = torch.optim.AdamW(orc.parameters(), lr=5e-4, betas=(0.9, 0.98), weight_decay=1e-2)
+    b = synthetic_batch([734, 349], [27, 12], seed=0)
+    g = torch.Generator().manual_seed(1)
+
+    def one():
+        loss, _ = oracle_step_loss(orc, b, sample_sp_mask(2, generator=g))
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(orc.parameters(), 5.0)
+        opt.step()
+
+    one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = (time.perf_counter() - t0) / steps
+    progress(f"cpu baseline: cfg1 step {dt * 1e3:.0f} ms")
+    return {"value": round((734 + 349) / dt, 1), "unit": "mel-frames/s",
+            "ms_per_step": round(dt * 1e3, 2), "threads": torch.get_num_threads(),
+            "sample": f"oracle step, 2 blocks d_model 64, B = 2 (734 + 349 frames), {steps} steps"}
+
+
+def cpu_ql_microbench(progress=lambda msg: None, reps: int = 3):
+    """QuantizedLinear alone on the host (the oracle's torch restatement of quant.py:38-127:
+    quantize + F.linear forward, autograd backward for dX, dW, dalpha, db) at each
+    Conformer-S shape with the 3 stacked passes' rows (M = 3 x 32 x 249), 2-bit; median of
+    ``reps`` after one warm-up, at the thread count cpu_baseline chose."""
+    from oracle.quant_oracle import ref_layer_init, ref_quantized_linear
+
+    gen = torch.Generator().manual_seed(5)
+    rows = 3 * 32 * 249
+    res = []
+    for name, k, n in (("lin1", 144, 576), ("lin2", 576, 144), ("qkvo", 144, 144)):
+        w, a, bias = ref_layer_init(k, n, gen)
+        w.requires_grad_()
+        a.requires_grad_()
+        bias.requires_grad_()
+        x = torch.randn(rows, k, generator=gen, requires_grad=True)
+        gy = torch.randn(rows, n, generator=gen)
+        ts = []
+        for i in range(reps + 1):
+            t0 = time.perf_counter()
+            y = ref_quantized_linear(x, w, a, bias, 2)
+            y.backward(gy)
+            if i:
+                ts.append(time.perf_counter() - t0)
+            x.grad = w.grad = a.grad = bias.grad = None
+        t = sorted(ts)[len(ts) // 2]
+        flop = 6.0 * rows * k * n
+        res.append({"layer": name, "M": rows, "K": k, "N": n, "fwd_bwd_ms": round(t * 1e3, 2),
+                    "GFLOPs": round(flop / t / 1e9, 1)})
+        progress(f"cpu baseline: QL {name} fwd+bwd {t * 1e3:.0f} ms")
+    return res
 
 
 # ------------------------------------------------------------------------- inference

@@ -245,16 +245,12 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     for (int m = threadIdx.x; m < T; m += kThreads) {
       float pr[D];
       load_run<D>(pb + (size_t)m * C, pr);
-      // the MFMA's k order (step s, then k = g: column g*DQ + s), so this row is bitwise the
-      // one an MFMA tile would produce (the fused backward recomputes it that way)
+      // (columns in order: this row only feeds the upper rel_shift part of row 63 of the tile;
+      // the flash-style backward recomputes that row from the MFMA-computed anchor, which can
+      // differ from this one in the last bit)
       float a = 0.0f;
 #pragma unroll
-      for (int s = 0; s < DQ; ++s)
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-          const int c = gg * DQ + s;
-          a = fmaf(qe[c] + vbb[c], pr[c], a);
-        }
+      for (int c = 0; c < D; ++c) a = fmaf(qe[c] + vbb[c], pr[c], a);
       img[kTile * ldi + 1 + m] = a;
     }
     if (threadIdx.x == 0) img[kTile * ldi] = 0.0f;
