@@ -51,6 +51,53 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16x6 products: exact fp32 from bf16 MFMA (every operand x = hi + mid + lo)
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_bf(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// x = hi + mid + lo exactly (each part the bf16 rounding of what is left)
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8_t (&p)[3]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __bf16 h, m, l;
+    split3(x[j], h, m, l);
+    p[0][j] = h;
+    p[1][j] = m;
+    p[2][j] = l;
+  }
+}
+
+// the six products of weight >= 2^-16 (smallest first), as dw.hip's bf16x6 GEMM
+__device__ __forceinline__ f32x4 mfma_x6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4 c) {
+  c = mfma_bf(a[1], b[1], c);
+  c = mfma_bf(a[2], b[0], c);
+  c = mfma_bf(a[0], b[2], c);
+  c = mfma_bf(a[1], b[0], c);
+  c = mfma_bf(a[0], b[1], c);
+  return mfma_bf(a[0], b[0], c);
+}
+
+// hi / mid / lo of two values as three packed dwords (value 0 in the low half)
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t (&w)[3]) {
+  __bf16 h0, m0, l0, h1, m1, l1;
+  split3(x0, h0, m0, l0);
+  split3(x1, h1, m1, l1);
+  w[0] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+  w[1] = (uint32_t)__builtin_bit_cast(uint16_t, m0) | ((uint32_t)__builtin_bit_cast(uint16_t, m1) << 16);
+  w[2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+}
+
 // N consecutive floats from a 4-byte-aligned address as dwordx4 runs + a dword tail
 // (gfx950 global loads take unaligned vector addresses).
 typedef f32x4 f32x4u __attribute__((aligned(4)));
@@ -360,30 +407,66 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     }
   }
 
-  // ctx = A v: A = the lane's probabilities (row r, k = 4g+j of tile t), B = v rows.
-  // v [16 nt keys][D] of (b, h) is staged once per block into the image (free once every
-  // wave has passed the scores phase) with coalesced dwordx4 loads; the MFMA operands then
-  // come from LDS (row pitch D: the 4 key rows a B fragment touches sit 16 banks apart).
+  // ctx = A v on bf16x6 (16x16x32, exact fp32 products): k step c = keys 32c .. 32c+31;
+  // A = the lane's 8 probabilities of its query (keys 32c+4g..+3 of tile 2c and
+  // 32c+16+4g..+3 of tile 2c+1: a permuted k order), split in registers; B = v^T parts
+  // [col][key] in LDS read in the same order (two ds_read_b64 per part). v of (b, h) is staged
+  // once per block into the image space (free once every wave has passed the scores phase):
+  // each thread splits two consecutive keys of 4 columns, one packed dword per part.
   __syncthreads();
-  float* vs = img;
-  for (int e = threadIdx.x; e < 16 * nt * DQ; e += kThreads) {
-    const int key = e / DQ, c4 = 4 * (e - key * DQ);
-    const f32x4 v4 = key < T ? *(const f32x4u*)(vbp + (size_t)key * C + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    *(f32x4*)(vs + key * D + c4) = v4;
+  constexpr int DPc = 16 * CT;
+  const int KPc = 32 * ((nt + 1) >> 1);  // keys covered by the k steps (zero past T)
+  const int VP = KPc + 8;                // bf16 per part row (pad: conflict-free b64 reads)
+  __bf16* vpl = reinterpret_cast<__bf16*>(img);
+  for (int e = threadIdx.x; e < (KPc / 2) * DQ; e += kThreads) {
+    const int kp = e / DQ, cq = e - kp * DQ;
+    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (2 * kp < T) v0 = *(const f32x4u*)(vbp + (size_t)(2 * kp) * C + 4 * cq);
+    if (2 * kp + 1 < T) v1 = *(const f32x4u*)(vbp + (size_t)(2 * kp + 1) * C + 4 * cq);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t wds[3];
+      split_pair(v0[j], v1[j], wds);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint32_t*>(vpl + ((size_t)p * DPc + 4 * cq + j) * VP + 2 * kp) = wds[p];
+    }
+  }
+  for (int e = threadIdx.x; e < 3 * (DPc - D) * (KPc / 2); e += kThreads) {  // columns >= D
+    const int pc = e / (KPc / 2), kp = e - pc * (KPc / 2);
+    const int p = pc / (DPc - D), col = D + pc % (DPc - D);
+    *reinterpret_cast<uint32_t*>(vpl + ((size_t)p * DPc + col) * VP + 2 * kp) = 0u;
   }
   __syncthreads();
   f32x4 o[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // (columns 16ct + r >= D read the next row: they only feed output columns never stored)
 #pragma unroll
-  for (int t = 0; t < NTT; ++t) {
-    if (t >= nt) continue;
+  for (int kc = 0; kc < (NTT + 1) / 2; ++kc) {
+    if (2 * kc >= nt) continue;
+    float a8[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float* vrow = vs + (16 * t + 4 * g + j) * D + r;
+      a8[j] = sreg[2 * kc][j];
+      a8[4 + j] = 2 * kc + 1 < nt ? sreg[2 * kc + 1][j] : 0.0f;
+    }
+    bf16x8_t af[3];
+    split8(a8, af);
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) o[ct] = mfma4(sreg[t][j], vrow[16 * ct], o[ct]);
+    for (int ct = 0; ct < CT; ++ct) {
+      bf16x8_t bfr[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const __bf16* row = vpl + ((size_t)p * DPc + 16 * ct + r) * VP + 32 * kc + 4 * g;
+        const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(row);
+        const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(row + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bfr[p][j] = lo[j];
+          bfr[p][4 + j] = hi[j];
+        }
+      }
+      o[ct] = mfma_x6(af, bfr, o[ct]);
     }
   }
 #pragma unroll
@@ -869,42 +952,6 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
 // dealt round-robin (waves w and w+4 share a SIMD: 3 jobs per SIMD at CT = 3, NW = 8).
 // du / dvb: per-(b, h) column sums of the dq parts (relattn_reduce_kernel, nqt = 1).
 // ------------------------------------------------------------------------------------
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 mfma_bf(const bf16x8_t& a, const bf16x8_t& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// x = hi + mid + lo exactly (each part the bf16 rounding of what is left)
-__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-  h = (__bf16)x;
-  const float r1 = x - (float)h;
-  m = (__bf16)r1;
-  l = (__bf16)(r1 - (float)m);
-}
-
-__device__ __forceinline__ void split8(const float (&x)[8], bf16x8_t (&p)[3]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    __bf16 h, m, l;
-    split3(x[j], h, m, l);
-    p[0][j] = h;
-    p[1][j] = m;
-    p[2][j] = l;
-  }
-}
-
-// the six products of weight >= 2^-16 (smallest first), as dw.hip's bf16x6 GEMM
-__device__ __forceinline__ f32x4 mfma_x6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4 c) {
-  c = mfma_bf(a[1], b[1], c);
-  c = mfma_bf(a[2], b[0], c);
-  c = mfma_bf(a[0], b[2], c);
-  c = mfma_bf(a[1], b[0], c);
-  c = mfma_bf(a[0], b[1], c);
-  return mfma_bf(a[0], b[0], c);
-}
-
 constexpr int kFQ = 32;        // query rows per chunk
 constexpr int kPlanePitch = 40;  // bf16 per column row of a B plane (80 B: 16-B aligned rows)
 
@@ -1453,6 +1500,222 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
   OB_STAMP_WRITE
 }
 
+// ------------------------------------------------------------------------------------
+// Backward, key side on bf16x6 MFMA (the probability path): block = (key tile of 64, head,
+// batch row), wave w = keys 16w..16w+15 of the tile, every query row visited:
+//   dK[key]  = sum_i dS'[i][key] (q+u)[i]       dV[key] = sum_i Pd[i][key] dO[i]
+//   dpos[m]  = sum_i dX[i][m] (q+v)[i]          (per batch row; summed over the pass later)
+// Queries go in chunks of 32 = ONE k step of v_mfma_f32_16x16x32_bf16 per product and
+// 16-column tile. Per chunk the block splits every staged value once into exact hi / mid /
+// lo bf16 parts (x = hi + mid + lo) and stores the parts as planes in LDS: the A tiles
+// dS' / Pd (dropout applied) / dX as [64 keys][32 queries] (dX gathered by the rel_shift
+// adjoint), the B tiles q+u / q+v / dO as [16 CT columns][32 queries]; a lane's fragment is
+// 8 consecutive queries of its key / column (two ds_read_b64 per part). The six products of
+// weight >= 2^-16 accumulate in fp32 (dropped terms < 2^-24 relative: fp32-equivalent), 2.7x
+// fewer MFMA cycles than the 16x16x4 fp32 chain it replaces. Each thread stages two
+// consecutive queries of 4 keys (A) or 4 columns (B), so every part write is one packed
+// dword; the next chunk's global loads are in flight in registers while the current chunk's
+// MFMAs issue.
+// ------------------------------------------------------------------------------------
+constexpr int kKvQ = 32;     // queries per chunk (one 16x16x32 k step)
+constexpr int kKvPitch = 36; // bf16 per plane row: 32 queries + pad (72 B: 8-B aligned reads)
+
+template <int D>
+struct KvX6Stage {
+  static constexpr int CT = (D + 15) / 16;
+  static constexpr int DP = 16 * CT;
+  // A parts: [tile 0 dS', 1 Pd, 2 dX][part][key 64][query 36]; B parts: [tensor 0 q+u, 1 q+v,
+  // 2 dO][part][column DP][query 36]
+  alignas(16) __bf16 a[3][3][64][kKvPitch];
+  alignas(16) __bf16 b[3][3][DP][kKvPitch];
+};
+
+template <int DQ>
+__global__ __launch_bounds__(kThreads) void relattn_bwd_kv_x6_kernel(
+    const float* __restrict__ dsg, const float* __restrict__ probs, const float* __restrict__ q,
+    const float* __restrict__ dctx, const float* __restrict__ u, const float* __restrict__ vbias,
+    int T, int H, DropCfg dc, float* __restrict__ dk, float* __restrict__ dv,
+    float* __restrict__ dp_part) {
+  constexpr int D = 4 * DQ;
+  using St = KvX6Stage<D>;
+  constexpr int CT = St::CT, DP = St::DP;
+  constexpr int kBItems = DQ * (kKvQ / 2);                  // (column quad, query pair) per tensor
+  constexpr int kBSlots = (2 * kBItems + kThreads - 1) / kThreads;
+  __shared__ St st;
+  const int nt = (T + 15) >> 4;
+  const int nkt = (T + kTile - 1) / kTile;
+  const BlockId bid = block_id(nkt, H);
+  const int b = bid.b, h = bid.h, k0 = bid.qt * kTile;
+  const int bh = b * H + h;
+  const int C = H * D;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const size_t bo = (size_t)b * T * C + h * D;
+  const float* qb = q + bo;
+  const float* dob = dctx + bo;
+  const float* ub = u + h * D;
+  const float* vbb = vbias + h * D;
+  const float* dsb = dsg + (size_t)bh * T * T;
+  const float* prb = probs + frag_off(bh, 0, 0, nt);
+
+  // B columns >= D stay zero (their output columns are discarded)
+  for (int e = threadIdx.x; e < 3 * 3 * (DP - D) * kKvPitch; e += kThreads) {
+    const int rw = e / ((DP - D) * kKvPitch), rem = e - rw * (DP - D) * kKvPitch;
+    (&st.b[0][0][0][0])[(size_t)rw * DP * kKvPitch + (size_t)D * kKvPitch + rem] = (__bf16)0.0f;
+  }
+
+  // A staging: thread = (key quad kq: keys k0 + 4kq .. +3, query pair qp: rows 2qp, 2qp+1)
+  const int kq = threadIdx.x & 15, qp = threadIdx.x >> 4;
+  const int key0 = k0 + 4 * kq;
+  const size_t pcol = (size_t)256 * (key0 >> 4) + 64 * ((key0 & 15) >> 2);
+  const __amdgpu_buffer_rsrc_t rs_ds = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(dsb), (short)0, (int)((size_t)T * T * sizeof(float)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_pr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(prb), (short)0, (int)((size_t)nt * nt * 256 * sizeof(float)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_q = slice_rsrc(qb, T, C, D), rs_do = slice_rsrc(dob, T, C, D);
+  const bool kfull = key0 + 3 < T;
+  f32x4 ra_k[2], ra_v[2], ra_p[2], rb[kBSlots][2];
+  auto fetch = [&](int i0) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int i = i0 + 2 * qp + hf;
+      const int fk = i * T + key0, fx = i * (T + 1) + key0 + 1 - T;
+      if (kfull && i < T && fx >= 0) {
+        ra_k[hf] = __builtin_amdgcn_raw_buffer_load_b128(rs_ds, 4 * fk, 0, 0);
+        ra_p[hf] = __builtin_amdgcn_raw_buffer_load_b128(rs_ds, 4 * fx, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = i < T && key0 + j < T;
+          const float xk = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_ds, 4 * (fk + j), 0, 0));
+          const float xp = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_ds, 4 * max(fx + j, 0), 0, 0));
+          ra_k[hf][j] = ok ? xk : 0.0f;
+          ra_p[hf][j] = ok && fx + j >= 0 ? xp : 0.0f;
+        }
+      }
+      ra_v[hf] = key0 < 16 * nt
+                     ? __builtin_amdgcn_raw_buffer_load_b128(
+                           rs_pr, 4 * (int)((size_t)(i >> 4) * nt * 256 + pcol + 4 * (i & 15)), 0, 0)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // Pd = P * keep * scale (the keep bit rides in the sign)
+        if (dc.on) ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
+    }
+#pragma unroll
+    for (int sl = 0; sl < kBSlots; ++sl) {
+      const int e = threadIdx.x + kThreads * sl;
+      const int e2 = e < kBItems ? e : e - kBItems;  // (column quad, query pair)
+      const int cq = e2 % DQ, pr = e2 / DQ;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int row = i0 + 2 * pr + hf;
+        rb[sl][hf] = e < 2 * kBItems ? __builtin_amdgcn_raw_buffer_load_b128(
+                                           e < kBItems ? rs_q : rs_do, 4 * (row * C + 4 * cq), 0, 0)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto put_a = [&](int tile, const f32x4 (&v)[2]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t wds[3];
+      split_pair(v[0][j], v[1][j], wds);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint32_t*>(&st.a[tile][p][4 * kq + j][2 * qp]) = wds[p];
+    }
+  };
+  auto stage = [&]() {
+    put_a(0, ra_k);
+    put_a(1, ra_v);
+    put_a(2, ra_p);
+#pragma unroll
+    for (int sl = 0; sl < kBSlots; ++sl) {
+      const int e = threadIdx.x + kThreads * sl;
+      if (e >= 2 * kBItems) continue;
+      const int e2 = e < kBItems ? e : e - kBItems;
+      const int cq = e2 % DQ, pr = e2 / DQ;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = 4 * cq + j;
+        uint32_t wds[3];
+        if (e < kBItems) {
+          split_pair(rb[sl][0][j] + ub[col], rb[sl][1][j] + ub[col], wds);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) *reinterpret_cast<uint32_t*>(&st.b[0][p][col][2 * pr]) = wds[p];
+          split_pair(rb[sl][0][j] + vbb[col], rb[sl][1][j] + vbb[col], wds);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) *reinterpret_cast<uint32_t*>(&st.b[1][p][col][2 * pr]) = wds[p];
+        } else {
+          split_pair(rb[sl][0][j], rb[sl][1][j], wds);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) *reinterpret_cast<uint32_t*>(&st.b[2][p][col][2 * pr]) = wds[p];
+        }
+      }
+    }
+  };
+  // (rows >= T: q / dO rows read 0 through the range check, so q+u / q+v there are u / v;
+  // they multiply A entries that are 0 for rows >= T)
+  auto frag = [&](const __bf16* rowp) {  // 8 consecutive queries 8g .. 8g+7 of one row
+    const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(rowp + 8 * g);
+    const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(rowp + 8 * g + 4);
+    bf16x8_t f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = lo[j];
+      f[4 + j] = hi[j];
+    }
+    return f;
+  };
+
+  f32x4 ak[CT], av[CT], ap[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) ak[ct] = av[ct] = ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kl = 16 * w + r;  // the lane's key within the tile (A row)
+  fetch(0);
+  for (int i0 = 0; i0 < T; i0 += kKvQ) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    stage();
+    __syncthreads();
+    if (i0 + kKvQ < T) fetch(i0 + kKvQ);
+    bf16x8_t fa_k[3], fa_v[3], fa_p[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      fa_k[p] = frag(&st.a[0][p][kl][0]);
+      fa_v[p] = frag(&st.a[1][p][kl][0]);
+      fa_p[p] = frag(&st.a[2][p][kl][0]);
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      bf16x8_t bu[3], bq[3], bd[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        bu[p] = frag(&st.b[0][p][16 * ct + r][0]);
+        bq[p] = frag(&st.b[1][p][16 * ct + r][0]);
+        bd[p] = frag(&st.b[2][p][16 * ct + r][0]);
+      }
+      ak[ct] = mfma_x6(fa_k, bu, ak[ct]);
+      av[ct] = mfma_x6(fa_v, bd, av[ct]);
+      ap[ct] = mfma_x6(fa_p, bq, ap[ct]);
+    }
+  }
+  float* dkb = dk + bo;
+  float* dvb = dv + bo;
+  float* dpb = dp_part + ((size_t)b * H + h) * T * D;  // [b][h][T][D]
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = 16 * ct + r;
+    if (col >= D) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kk = k0 + 16 * w + 4 * g + j;
+      if (kk >= T) continue;
+      dkb[(size_t)kk * C + col] = ak[ct][j];
+      dvb[(size_t)kk * C + col] = av[ct][j];
+      dpb[(size_t)kk * D + col] = ap[ct][j];
+    }
+  }
+}
+
 // du, dvb [H][D]: sum over (batch row, query tile) of the per-tile partials. Block = one
 // (which, head) x 4 columns x 64 slices (slice s: pairs s, s+64, ..., four accumulators),
 // the slices added in order through LDS (fixed order). 2*H*ceil(D/4) blocks: each thread
@@ -1560,9 +1823,11 @@ __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, int64
 }
 
 size_t fwd_lds_bytes(int T, int D) {
-  const size_t img = (size_t)(kTile + 1) * (T + 1);
-  const size_t vst = (size_t)16 * ((T + 15) / 16) * D;
-  return sizeof(float) * (img > vst ? img : vst);
+  const size_t img = sizeof(float) * (size_t)(kTile + 1) * (T + 1);
+  // v^T parts: 3 x [16 CT cols][32 ceil(nt/2) keys + 8] bf16
+  const size_t nt = (T + 15) / 16;
+  const size_t vst = sizeof(uint16_t) * 3 * (size_t)(16 * ((D + 15) / 16)) * (32 * ((nt + 1) / 2) + 8);
+  return img > vst ? img : vst;
 }
 size_t bwd_lds_bytes(int T) { return sizeof(float) * ((size_t)(kTile + 1) * T + 128); }
 
@@ -1723,8 +1988,8 @@ void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, con
                      du_part, dvb_part)
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
-#define OB_RA_KV(DQ, NTT)                                                                       \
-  hipLaunchKernelGGL((relattn_bwd_kv_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg, \
+#define OB_RA_KV(DQ, NTT)                                                                          \
+  hipLaunchKernelGGL((relattn_bwd_kv_x6_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg, \
                      probs, q, dctx, u, vb, (int)T, (int)H, dc, dk, dv, dp_part)
   OB_RA_DISPATCH(OB_RA_KV);
 #undef OB_RA_KV
