@@ -35,6 +35,8 @@
 // backward kernels read the keep bit back with the probability.
 #include <math.h>
 
+#include <algorithm>
+
 #include "ob_drop.h"
 #include "ob_launch.h"
 
@@ -46,6 +48,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
 constexpr int kTile = 64;  // query rows per block (16 per wave)
+constexpr int kFwdKeyChunk = 256;  // keys of v staged per pass of the forward's ctx product
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -201,6 +204,44 @@ __device__ __forceinline__ void keep4(uint32_t key, uint64_t idx, const DropCfg&
   keep[3] = (h1 >> 16) >= dc.thresh;
 }
 
+#ifdef OB_ATTN_STAMPS
+// diagnostic build only (tools/attn_stamps.py): per-wave cycles of up to 10 phases of ONE
+// kernel (OB_ATTN_STAMPS = 1 flash-style backward, 2 query-side backward, 3 forward,
+// 4 key-side backward), written to a buffer nothing else reads
+__device__ uint64_t g_attn_stamps[65536];
+__device__ uint64_t g_attn_rt[16384];  // per wave: s_memrealtime (100 MHz) at start and end
+#define OB_STAMP_DECL(K)                                                       \
+  constexpr bool st_on = OB_ATTN_STAMPS == (K);                                \
+  uint64_t st_t = st_on ? __builtin_amdgcn_s_memtime() : 0,                   \
+           st_rt0 = st_on ? __builtin_amdgcn_s_memrealtime() : 0,             \
+           st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define OB_STAMP(k)                                          \
+  do {                                                       \
+    if constexpr (st_on) {                                   \
+      const uint64_t st_n = __builtin_amdgcn_s_memtime();    \
+      st_acc[k] += st_n - st_t;                              \
+      st_t = st_n;                                           \
+    }                                                        \
+  } while (0)
+#define OB_STAMP_WRITE(NWV)                                                             \
+  if constexpr (st_on) {                                                                \
+    const uint64_t st_rt1 = __builtin_amdgcn_s_memrealtime();                           \
+    const size_t st_w = (size_t)blockIdx.x * (NWV) + w;                                 \
+    if (lane == 0 && st_w * 10 + 10 <= 65536)                                           \
+      for (int k_ = 0; k_ < 10; ++k_) g_attn_stamps[st_w * 10 + k_] = st_acc[k_];       \
+    if (lane == 0 && st_w * 2 + 2 <= 16384) {                                           \
+      g_attn_rt[st_w * 2] = st_rt0;                                                     \
+      g_attn_rt[st_w * 2 + 1] = st_rt1;                                                 \
+    }                                                                                   \
+  }
+#else
+#define OB_STAMP_DECL(K)
+#define OB_STAMP(k) \
+  do {              \
+  } while (0)
+#define OB_STAMP_WRITE(NWV)
+#endif
+
 // ------------------------------------------------------------------------------------
 // Forward: block = (query tile of 64, head, batch row). The Xpad image of rows i0 .. i0+64
 // lives in LDS (row 64 = the next tile's first query, read by the last rows' j >= i+2
@@ -234,6 +275,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   const float* vbb = vbias + h * D;
   const __amdgpu_buffer_rsrc_t rs_p = slice_rsrc(pb, T, C, D), rs_k = slice_rsrc(kb, T, C, D);
   const int voff_a = (r * C + g * DQ) * 4;  // this lane's A-operand run in a 16-row group
+  OB_STAMP_DECL(3)
 
   const int ir = 16 * w + r;  // this lane's query row in the tile (scores phase)
   const int qi = i0 + ir;
@@ -256,6 +298,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   // (two operand buffers used alternately by the fully unrolled group loop: no copies)
   float opb[2][4][DQ];
   load_group_buf<DQ>(rs_p, voff_a, C, 0, opb[0]);
+  OB_STAMP(0);
 #pragma unroll
   for (int t0 = 0; t0 < NTT; t0 += 4) {
     if (t0 >= nt) continue;
@@ -284,6 +327,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     }
   }
   if (g == 0) img[ir * ldi] = 0.0f;
+  OB_STAMP(1);
   // the first key group of the scores phase, in flight over the row-64 work and barrier
   load_group_buf<DQ>(rs_k, voff_a, C, 0, opb[0]);
   // Xpad row 64: the next tile's first query (fp32 fma chain on the VALU)
@@ -302,7 +346,9 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     }
     if (threadIdx.x == 0) img[kTile * ldi] = 0.0f;
   }
+  OB_STAMP(2);
   __syncthreads();
+  OB_STAMP(3);
   // X rows of the queries 32, 64, 96, ... (< T): the rows just below each 32-query chunk of
   // the flash-style backward, which reads them instead of recomputing them
   if (anchors) {
@@ -347,6 +393,25 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16));
   mx = fmaxf(mx, __shfl_xor(mx, 32));
+  OB_STAMP(4);
+  // v rows of the ctx product's first key chunk, in flight over the softmax (DQ <= 9: the
+  // registers are free; wider heads load at staging)
+  constexpr int kVSlots = (kFwdKeyChunk / 2 * DQ + kThreads - 1) / kThreads;
+  constexpr bool kVPre = DQ <= 9;
+  const int nkp0 = min(kFwdKeyChunk, 32 * ((nt + 1) >> 1)) / 2;  // key pairs of chunk 0
+  f32x4 vpre[kVPre ? kVSlots : 1][2];
+  if constexpr (kVPre) {
+#pragma unroll
+    for (int sl = 0; sl < kVSlots; ++sl) {
+      const int e = threadIdx.x + kThreads * sl;
+      const int kp = e / DQ, cq = e - kp * DQ;
+      const bool ok = e < nkp0 * DQ;
+      vpre[sl][0] = ok && 2 * kp < T ? *(const f32x4u*)(vbp + (size_t)(2 * kp) * C + 4 * cq)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+      vpre[sl][1] = ok && 2 * kp + 1 < T ? *(const f32x4u*)(vbp + (size_t)(2 * kp + 1) * C + 4 * cq)
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   const bool row_live = mx != -INFINITY;  // all -inf -> softmax NaN -> nan_to_num 0
   const float mxs = row_live ? mx : 0.0f;
   float sum = 0.0f;
@@ -411,62 +476,89 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
   // A = the lane's 8 probabilities of its query (keys 32c+4g..+3 of tile 2c and
   // 32c+16+4g..+3 of tile 2c+1: a permuted k order), split in registers; B = v^T parts
   // [col][key] in LDS read in the same order (two ds_read_b64 per part). v of (b, h) is staged
-  // once per block into the image space (free once every wave has passed the scores phase):
-  // each thread splits two consecutive keys of 4 columns, one packed dword per part.
-  __syncthreads();
+  // into the image space (free once every wave has passed the scores phase), up to
+  // kFwdKeyChunk keys at a time: each thread splits two consecutive keys of 4 columns, one
+  // packed dword per part.
   constexpr int DPc = 16 * CT;
-  const int KPc = 32 * ((nt + 1) >> 1);  // keys covered by the k steps (zero past T)
-  const int VP = KPc + 8;                // bf16 per part row (pad: conflict-free b64 reads)
+  const int KPc = 32 * ((nt + 1) >> 1);      // keys covered by the k steps (zero past T)
+  const int VP = min(KPc, kFwdKeyChunk) + 8;  // bf16 per part row (pad: conflict-free b64 reads)
   __bf16* vpl = reinterpret_cast<__bf16*>(img);
-  for (int e = threadIdx.x; e < (KPc / 2) * DQ; e += kThreads) {
-    const int kp = e / DQ, cq = e - kp * DQ;
-    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (2 * kp < T) v0 = *(const f32x4u*)(vbp + (size_t)(2 * kp) * C + 4 * cq);
-    if (2 * kp + 1 < T) v1 = *(const f32x4u*)(vbp + (size_t)(2 * kp + 1) * C + 4 * cq);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t wds[3];
-      split_pair(v0[j], v1[j], wds);
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        *reinterpret_cast<uint32_t*>(vpl + ((size_t)p * DPc + 4 * cq + j) * VP + 2 * kp) = wds[p];
-    }
-  }
-  for (int e = threadIdx.x; e < 3 * (DPc - D) * (KPc / 2); e += kThreads) {  // columns >= D
-    const int pc = e / (KPc / 2), kp = e - pc * (KPc / 2);
-    const int p = pc / (DPc - D), col = D + pc % (DPc - D);
-    *reinterpret_cast<uint32_t*>(vpl + ((size_t)p * DPc + col) * VP + 2 * kp) = 0u;
-  }
-  __syncthreads();
   f32x4 o[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) o[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // keys in chunks of kFwdKeyChunk (one chunk up to T = 256): stage, then the chunk's k steps
 #pragma unroll
-  for (int kc = 0; kc < (NTT + 1) / 2; ++kc) {
-    if (2 * kc >= nt) continue;
-    float a8[8];
+  for (int ch = 0; ch < (16 * NTT + kFwdKeyChunk - 1) / kFwdKeyChunk; ++ch) {
+    const int kb0 = ch * kFwdKeyChunk;
+    if (kb0 >= KPc) continue;
+    const int nkp = min(kFwdKeyChunk, KPc - kb0) / 2;  // key pairs staged
+    OB_STAMP(5);
+    __syncthreads();  // the image (first chunk) / the previous chunk's parts are read
+    OB_STAMP(6);
+    auto put_v = [&](int kp, int cq, const f32x4& v0, const f32x4& v1) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      a8[j] = sreg[2 * kc][j];
-      a8[4 + j] = 2 * kc + 1 < nt ? sreg[2 * kc + 1][j] : 0.0f;
-    }
-    bf16x8_t af[3];
-    split8(a8, af);
+      for (int j = 0; j < 4; ++j) {
+        uint32_t wds[3];
+        split_pair(v0[j], v1[j], wds);
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      bf16x8_t bfr[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const __bf16* row = vpl + ((size_t)p * DPc + 16 * ct + r) * VP + 32 * kc + 4 * g;
-        const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(row);
-        const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(row + 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          bfr[p][j] = lo[j];
-          bfr[p][4 + j] = hi[j];
-        }
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint32_t*>(vpl + ((size_t)p * DPc + 4 * cq + j) * VP + 2 * kp) = wds[p];
       }
-      o[ct] = mfma_x6(af, bfr, o[ct]);
+    };
+    if (kVPre && ch == 0) {
+#pragma unroll
+      for (int sl = 0; sl < kVSlots; ++sl) {
+        const int e = threadIdx.x + kThreads * sl;
+        if (e < nkp * DQ) put_v(e / DQ, e % DQ, vpre[sl][0], vpre[sl][1]);
+      }
+    } else {
+      for (int e = threadIdx.x; e < nkp * DQ; e += kThreads) {
+        const int kp = e / DQ, cq = e - kp * DQ;
+        const int key = kb0 + 2 * kp;
+        f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (key < T) v0 = *(const f32x4u*)(vbp + (size_t)key * C + 4 * cq);
+        if (key + 1 < T) v1 = *(const f32x4u*)(vbp + (size_t)(key + 1) * C + 4 * cq);
+        put_v(kp, cq, v0, v1);
+      }
+    }
+    if constexpr (DPc > D) {
+      for (int e = threadIdx.x; e < 3 * (DPc - D) * nkp; e += kThreads) {  // columns >= D
+        const int pc = e / nkp, kp = e - pc * nkp;
+        const int p = pc / (DPc - D), col = D + pc % (DPc - D);
+        *reinterpret_cast<uint32_t*>(vpl + ((size_t)p * DPc + col) * VP + 2 * kp) = 0u;
+      }
+    }
+    OB_STAMP(7);
+    __syncthreads();
+    OB_STAMP(8);
+#pragma unroll
+    for (int kl = 0; kl < kFwdKeyChunk / 32; ++kl) {
+      const int kc = ch * (kFwdKeyChunk / 32) + kl;  // k step: keys 32kc .. 32kc+31
+      if (kc >= (NTT + 1) / 2 || 2 * kc >= nt) continue;
+      float a8[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a8[j] = sreg[2 * kc][j];
+        a8[4 + j] = 2 * kc + 1 < nt ? sreg[2 * kc + 1][j] : 0.0f;
+      }
+      bf16x8_t af[3];
+      split8(a8, af);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        bf16x8_t bfr[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const __bf16* row = vpl + ((size_t)p * DPc + 16 * ct + r) * VP + 32 * kl + 4 * g;
+          const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(row);
+          const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(row + 16);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            bfr[p][j] = lo[j];
+            bfr[p][4 + j] = hi[j];
+          }
+        }
+        o[ct] = mfma_x6(af, bfr, o[ct]);
+      }
     }
   }
 #pragma unroll
@@ -479,6 +571,8 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       if (row < T) ctx[((size_t)b * T + row) * C + h * D + col] = o[ct][j];
     }
   }
+  OB_STAMP(9);
+  OB_STAMP_WRITE(kThreads / 64)
 }
 
 // ------------------------------------------------------------------------------------
@@ -524,6 +618,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   };
   // the band's slack past its 65 rows (read only by rows >= T and padded positions)
   if (threadIdx.x < 128) band[(kTile + 1) * T + threadIdx.x] = 0.0f;
+  OB_STAMP_DECL(2)
 
   const int ir = 16 * w + r;
   const int qi = i0 + ir;
@@ -541,6 +636,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     a += __shfl_xor(a, 32);
     delta = a;
   }
+  OB_STAMP(0);
 
   // dPd[query qi][key] = dO . v (A = v rows, B = dO row); P from the fragment tiles;
   // dS' = P (dPd * keep * scale - delta) / sqrt(d) (softmax backward, then the 1/sqrt(d))
@@ -590,6 +686,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     }
   }
 
+  OB_STAMP(1);
   // band row 0: query i0-1 on the VALU, the same formula (zero row when i0 == 0)
   if (i0 > 0) {
     const int ip = i0 - 1;
@@ -611,6 +708,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
   } else {
     for (int jj = threadIdx.x; jj < T; jj += kThreads) band[jj] = 0.0f;
   }
+  OB_STAMP(2);
 
   // dQu = dS' k (A = dS' row r, k = 4g+j of tile t; B = k rows)
   f32x4 oq[CT];
@@ -641,18 +739,20 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
         for (int ct = 0; ct < CT; ++ct) oq[ct] = mfma4(dsr[t][j], kbb[t & 1][j][ct], oq[ct]);
     }
   }
+  OB_STAMP(3);
   __syncthreads();  // the band is complete (row 0 and every wave's rows)
+  OB_STAMP(4);
 
   // dQv = dX p, dX read flat from the band: dX[qi][m] = dS'.flat[qi(T+1) + m + 1 - T]
   // = band[i0 + 1 + ir(T+1) + m] (band row 0 = query i0-1, zero for the first tile).
-  // Positions m = 4mk+g go four MFMA steps at a time, the next four's p operands loading
+  // Positions m = 4mk+g go eight MFMA steps at a time, the next eight's p operands loading
   // meanwhile; positions past T multiply p = 0.
   f32x4 ov[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) ov[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* xrow = band + i0 + 1 + ir * (T + 1) + g;  // dX[qi][4mk + g] = xrow[4mk]
   const int nk = (T + 3) >> 2;
-  constexpr int kMK = 4;
+  constexpr int kMK = 8;  // eight MFMA steps per round, the next round's p loading meanwhile
   // p[4mk + g][16ct + r]: positions >= T read 0 (range check)
   const int voff_pm = (g * C + r) * 4;
   auto load_p = [&](int mk0, float (&dst)[kMK][CT]) {
@@ -670,7 +770,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     if (mk0 + kMK < nk) load_p(mk0 + kMK, pv_nxt);
 #pragma unroll
     for (int qq = 0; qq < kMK; ++qq) {
-      const float av = xrow[4 * (mk0 + qq)];
+      const float av = mk0 + qq < nk ? xrow[4 * (mk0 + qq)] : 0.0f;
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) ov[ct] = mfma4(av, pv_cur[qq][ct], ov[ct]);
     }
@@ -679,6 +779,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) pv_cur[qq][ct] = pv_nxt[qq][ct];
   }
+  OB_STAMP(5);
   // dq = dQu + dQv; per-tile column sums of dQu / dQv for du / dvb
   float su[CT], sv[CT];
 #pragma unroll
@@ -709,7 +810,9 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
       red[w][1][col] = sv[ct];
     }
   }
+  OB_STAMP(6);
   __syncthreads();
+  OB_STAMP(7);
   if (threadIdx.x < D) {
     const int c = threadIdx.x;
     du_part[tile_id * D + c] = ((red[0][0][c] + red[1][0][c]) + red[2][0][c]) + red[3][0][c];
@@ -736,6 +839,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
       if (e < n) dsb[e] = v8[q8];
     }
   }
+  OB_STAMP(8);
+  OB_STAMP_WRITE(kThreads / 64)
 }
 
 // ------------------------------------------------------------------------------------
@@ -895,11 +1000,16 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
     ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const int kl = 16 * w + r;  // the lane's key within the tile (A row)
+  OB_STAMP_DECL(4)
   fetch(0);
+  OB_STAMP(0);
   for (int i0 = 0; i0 < T; i0 += kQ) {
     __syncthreads();  // the previous chunk's LDS reads are done
+    OB_STAMP(1);
     stage();
+    OB_STAMP(2);
     __syncthreads();
+    OB_STAMP(3);
     if (i0 + kQ < T) fetch(i0 + kQ);
 #pragma unroll
     for (int s4 = 0; s4 < kQ / 4; ++s4) {
@@ -913,6 +1023,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
         ap[ct] = mfma4(a_p, st.qv[qq][col], ap[ct]);
       }
     }
+    OB_STAMP(4);
   }
   float* dkb = dk + bo;
   float* dvb = dv + bo;
@@ -930,6 +1041,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kv_kernel(
       dpb[(size_t)kk * D + col] = ap[ct][j];
     }
   }
+  OB_STAMP(5);
+  OB_STAMP_WRITE(kThreads / 64)
 }
 
 // ------------------------------------------------------------------------------------
@@ -1043,28 +1156,6 @@ struct FusedLds {  // float offsets into the dynamic LDS of relattn_bwd_fused_ke
   }
 };
 
-#ifdef OB_ATTN_STAMPS
-// diagnostic build only (tools/attn_stamps.py): per-wave cycles of each phase of the fused
-// backward, written to a buffer nothing else reads
-__device__ uint64_t g_attn_stamps[65536];
-#define OB_STAMP_DECL \
-  uint64_t st_t = __builtin_amdgcn_s_memtime(), st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#define OB_STAMP(k)                                          \
-  do {                                                       \
-    const uint64_t st_n = __builtin_amdgcn_s_memtime();      \
-    st_acc[k] += st_n - st_t;                                \
-    st_t = st_n;                                             \
-  } while (0)
-#define OB_STAMP_WRITE                                                                \
-  if (lane == 0 && ((size_t)blockIdx.x * NW + w) * 10 + 10 <= 65536)                  \
-    for (int k_ = 0; k_ < 10; ++k_) g_attn_stamps[((size_t)blockIdx.x * NW + w) * 10 + k_] = st_acc[k_];
-#else
-#define OB_STAMP_DECL
-#define OB_STAMP(k) \
-  do {              \
-  } while (0)
-#define OB_STAMP_WRITE
-#endif
 
 template <int DQ, int NW>
 __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
@@ -1214,7 +1305,7 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
     for (int e = threadIdx.x; e < T; e += NTH) R[e] = 0.0f;
   }
 
-  OB_STAMP_DECL
+  OB_STAMP_DECL(1)
   for (int c = c0; c < c1; ++c) {
     const int i0 = kFQ * c;
     // LDS addresses derived from T are recomputed per chunk (a few VALU ops) instead of
@@ -1497,223 +1588,7 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
     du_part[((size_t)bh * ns + sp) * D + col] = (su[0] + su[DP]) + (su[2 * DP] + su[3 * DP]);
     dvb_part[((size_t)bh * ns + sp) * D + col] = (su[4 * DP] + su[5 * DP]) + (su[6 * DP] + su[7 * DP]);
   }
-  OB_STAMP_WRITE
-}
-
-// ------------------------------------------------------------------------------------
-// Backward, key side on bf16x6 MFMA (the probability path): block = (key tile of 64, head,
-// batch row), wave w = keys 16w..16w+15 of the tile, every query row visited:
-//   dK[key]  = sum_i dS'[i][key] (q+u)[i]       dV[key] = sum_i Pd[i][key] dO[i]
-//   dpos[m]  = sum_i dX[i][m] (q+v)[i]          (per batch row; summed over the pass later)
-// Queries go in chunks of 32 = ONE k step of v_mfma_f32_16x16x32_bf16 per product and
-// 16-column tile. Per chunk the block splits every staged value once into exact hi / mid /
-// lo bf16 parts (x = hi + mid + lo) and stores the parts as planes in LDS: the A tiles
-// dS' / Pd (dropout applied) / dX as [64 keys][32 queries] (dX gathered by the rel_shift
-// adjoint), the B tiles q+u / q+v / dO as [16 CT columns][32 queries]; a lane's fragment is
-// 8 consecutive queries of its key / column (two ds_read_b64 per part). The six products of
-// weight >= 2^-16 accumulate in fp32 (dropped terms < 2^-24 relative: fp32-equivalent), 2.7x
-// fewer MFMA cycles than the 16x16x4 fp32 chain it replaces. Each thread stages two
-// consecutive queries of 4 keys (A) or 4 columns (B), so every part write is one packed
-// dword; the next chunk's global loads are in flight in registers while the current chunk's
-// MFMAs issue.
-// ------------------------------------------------------------------------------------
-constexpr int kKvQ = 32;     // queries per chunk (one 16x16x32 k step)
-constexpr int kKvPitch = 36; // bf16 per plane row: 32 queries + pad (72 B: 8-B aligned reads)
-
-template <int D>
-struct KvX6Stage {
-  static constexpr int CT = (D + 15) / 16;
-  static constexpr int DP = 16 * CT;
-  // A parts: [tile 0 dS', 1 Pd, 2 dX][part][key 64][query 36]; B parts: [tensor 0 q+u, 1 q+v,
-  // 2 dO][part][column DP][query 36]
-  alignas(16) __bf16 a[3][3][64][kKvPitch];
-  alignas(16) __bf16 b[3][3][DP][kKvPitch];
-};
-
-template <int DQ>
-__global__ __launch_bounds__(kThreads) void relattn_bwd_kv_x6_kernel(
-    const float* __restrict__ dsg, const float* __restrict__ probs, const float* __restrict__ q,
-    const float* __restrict__ dctx, const float* __restrict__ u, const float* __restrict__ vbias,
-    int T, int H, DropCfg dc, float* __restrict__ dk, float* __restrict__ dv,
-    float* __restrict__ dp_part) {
-  constexpr int D = 4 * DQ;
-  using St = KvX6Stage<D>;
-  constexpr int CT = St::CT, DP = St::DP;
-  constexpr int kBItems = DQ * (kKvQ / 2);                  // (column quad, query pair) per tensor
-  constexpr int kBSlots = (2 * kBItems + kThreads - 1) / kThreads;
-  __shared__ St st;
-  const int nt = (T + 15) >> 4;
-  const int nkt = (T + kTile - 1) / kTile;
-  const BlockId bid = block_id(nkt, H);
-  const int b = bid.b, h = bid.h, k0 = bid.qt * kTile;
-  const int bh = b * H + h;
-  const int C = H * D;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
-  const size_t bo = (size_t)b * T * C + h * D;
-  const float* qb = q + bo;
-  const float* dob = dctx + bo;
-  const float* ub = u + h * D;
-  const float* vbb = vbias + h * D;
-  const float* dsb = dsg + (size_t)bh * T * T;
-  const float* prb = probs + frag_off(bh, 0, 0, nt);
-
-  // B columns >= D stay zero (their output columns are discarded)
-  for (int e = threadIdx.x; e < 3 * 3 * (DP - D) * kKvPitch; e += kThreads) {
-    const int rw = e / ((DP - D) * kKvPitch), rem = e - rw * (DP - D) * kKvPitch;
-    (&st.b[0][0][0][0])[(size_t)rw * DP * kKvPitch + (size_t)D * kKvPitch + rem] = (__bf16)0.0f;
-  }
-
-  // A staging: thread = (key quad kq: keys k0 + 4kq .. +3, query pair qp: rows 2qp, 2qp+1)
-  const int kq = threadIdx.x & 15, qp = threadIdx.x >> 4;
-  const int key0 = k0 + 4 * kq;
-  const size_t pcol = (size_t)256 * (key0 >> 4) + 64 * ((key0 & 15) >> 2);
-  const __amdgpu_buffer_rsrc_t rs_ds = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(dsb), (short)0, (int)((size_t)T * T * sizeof(float)), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_pr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(prb), (short)0, (int)((size_t)nt * nt * 256 * sizeof(float)), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_q = slice_rsrc(qb, T, C, D), rs_do = slice_rsrc(dob, T, C, D);
-  const bool kfull = key0 + 3 < T;
-  f32x4 ra_k[2], ra_v[2], ra_p[2], rb[kBSlots][2];
-  auto fetch = [&](int i0) {
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const int i = i0 + 2 * qp + hf;
-      const int fk = i * T + key0, fx = i * (T + 1) + key0 + 1 - T;
-      if (kfull && i < T && fx >= 0) {
-        ra_k[hf] = __builtin_amdgcn_raw_buffer_load_b128(rs_ds, 4 * fk, 0, 0);
-        ra_p[hf] = __builtin_amdgcn_raw_buffer_load_b128(rs_ds, 4 * fx, 0, 0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool ok = i < T && key0 + j < T;
-          const float xk = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_ds, 4 * (fk + j), 0, 0));
-          const float xp = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_ds, 4 * max(fx + j, 0), 0, 0));
-          ra_k[hf][j] = ok ? xk : 0.0f;
-          ra_p[hf][j] = ok && fx + j >= 0 ? xp : 0.0f;
-        }
-      }
-      ra_v[hf] = key0 < 16 * nt
-                     ? __builtin_amdgcn_raw_buffer_load_b128(
-                           rs_pr, 4 * (int)((size_t)(i >> 4) * nt * 256 + pcol + 4 * (i & 15)), 0, 0)
-                     : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)  // Pd = P * keep * scale (the keep bit rides in the sign)
-        if (dc.on) ra_v[hf][j] = __builtin_signbit(ra_v[hf][j]) ? 0.0f : ra_v[hf][j] * dc.scale;
-    }
-#pragma unroll
-    for (int sl = 0; sl < kBSlots; ++sl) {
-      const int e = threadIdx.x + kThreads * sl;
-      const int e2 = e < kBItems ? e : e - kBItems;  // (column quad, query pair)
-      const int cq = e2 % DQ, pr = e2 / DQ;
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int row = i0 + 2 * pr + hf;
-        rb[sl][hf] = e < 2 * kBItems ? __builtin_amdgcn_raw_buffer_load_b128(
-                                           e < kBItems ? rs_q : rs_do, 4 * (row * C + 4 * cq), 0, 0)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-  auto put_a = [&](int tile, const f32x4 (&v)[2]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t wds[3];
-      split_pair(v[0][j], v[1][j], wds);
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        *reinterpret_cast<uint32_t*>(&st.a[tile][p][4 * kq + j][2 * qp]) = wds[p];
-    }
-  };
-  auto stage = [&]() {
-    put_a(0, ra_k);
-    put_a(1, ra_v);
-    put_a(2, ra_p);
-#pragma unroll
-    for (int sl = 0; sl < kBSlots; ++sl) {
-      const int e = threadIdx.x + kThreads * sl;
-      if (e >= 2 * kBItems) continue;
-      const int e2 = e < kBItems ? e : e - kBItems;
-      const int cq = e2 % DQ, pr = e2 / DQ;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = 4 * cq + j;
-        uint32_t wds[3];
-        if (e < kBItems) {
-          split_pair(rb[sl][0][j] + ub[col], rb[sl][1][j] + ub[col], wds);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) *reinterpret_cast<uint32_t*>(&st.b[0][p][col][2 * pr]) = wds[p];
-          split_pair(rb[sl][0][j] + vbb[col], rb[sl][1][j] + vbb[col], wds);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) *reinterpret_cast<uint32_t*>(&st.b[1][p][col][2 * pr]) = wds[p];
-        } else {
-          split_pair(rb[sl][0][j], rb[sl][1][j], wds);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) *reinterpret_cast<uint32_t*>(&st.b[2][p][col][2 * pr]) = wds[p];
-        }
-      }
-    }
-  };
-  // (rows >= T: q / dO rows read 0 through the range check, so q+u / q+v there are u / v;
-  // they multiply A entries that are 0 for rows >= T)
-  auto frag = [&](const __bf16* rowp) {  // 8 consecutive queries 8g .. 8g+7 of one row
-    const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(rowp + 8 * g);
-    const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(rowp + 8 * g + 4);
-    bf16x8_t f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f[j] = lo[j];
-      f[4 + j] = hi[j];
-    }
-    return f;
-  };
-
-  f32x4 ak[CT], av[CT], ap[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) ak[ct] = av[ct] = ap[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kl = 16 * w + r;  // the lane's key within the tile (A row)
-  fetch(0);
-  for (int i0 = 0; i0 < T; i0 += kKvQ) {
-    __syncthreads();  // the previous chunk's LDS reads are done
-    stage();
-    __syncthreads();
-    if (i0 + kKvQ < T) fetch(i0 + kKvQ);
-    bf16x8_t fa_k[3], fa_v[3], fa_p[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      fa_k[p] = frag(&st.a[0][p][kl][0]);
-      fa_v[p] = frag(&st.a[1][p][kl][0]);
-      fa_p[p] = frag(&st.a[2][p][kl][0]);
-    }
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      bf16x8_t bu[3], bq[3], bd[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        bu[p] = frag(&st.b[0][p][16 * ct + r][0]);
-        bq[p] = frag(&st.b[1][p][16 * ct + r][0]);
-        bd[p] = frag(&st.b[2][p][16 * ct + r][0]);
-      }
-      ak[ct] = mfma_x6(fa_k, bu, ak[ct]);
-      av[ct] = mfma_x6(fa_v, bd, av[ct]);
-      ap[ct] = mfma_x6(fa_p, bq, ap[ct]);
-    }
-  }
-  float* dkb = dk + bo;
-  float* dvb = dv + bo;
-  float* dpb = dp_part + ((size_t)b * H + h) * T * D;  // [b][h][T][D]
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    const int col = 16 * ct + r;
-    if (col >= D) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kk = k0 + 16 * w + 4 * g + j;
-      if (kk >= T) continue;
-      dkb[(size_t)kk * C + col] = ak[ct][j];
-      dvb[(size_t)kk * C + col] = av[ct][j];
-      dpb[(size_t)kk * D + col] = ap[ct][j];
-    }
-  }
+  OB_STAMP_WRITE(NW)
 }
 
 // du, dvb [H][D]: sum over (batch row, query tile) of the per-tile partials. Block = one
@@ -1824,9 +1699,10 @@ __global__ __launch_bounds__(kThreads) void relattn_mask_kernel(int64_t n, int64
 
 size_t fwd_lds_bytes(int T, int D) {
   const size_t img = sizeof(float) * (size_t)(kTile + 1) * (T + 1);
-  // v^T parts: 3 x [16 CT cols][32 ceil(nt/2) keys + 8] bf16
+  // v^T parts: 3 x [16 CT cols][min(32 ceil(nt/2), kFwdKeyChunk) keys + 8] bf16
   const size_t nt = (T + 15) / 16;
-  const size_t vst = sizeof(uint16_t) * 3 * (size_t)(16 * ((D + 15) / 16)) * (32 * ((nt + 1) / 2) + 8);
+  const size_t kp = std::min<size_t>(32 * ((nt + 1) / 2), kFwdKeyChunk);
+  const size_t vst = sizeof(uint16_t) * 3 * (size_t)(16 * ((D + 15) / 16)) * (kp + 8);
   return img > vst ? img : vst;
 }
 size_t bwd_lds_bytes(int T) { return sizeof(float) * ((size_t)(kTile + 1) * T + 128); }
@@ -1983,13 +1859,13 @@ void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, con
   float* du_part = dp_part + (size_t)Bt * H * T * d;
   float* dvb_part = du_part + (size_t)Bt * H * nqt * d;
 #define OB_RA_BWD(DQ, NTT)                                                                     \
-  hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, ctx, k, \
+  hipLaunchKernelGGL((relattn_bwd_kernel<DQ, NTT>), grid, dim3(kThreads), lds, s, dctx, ctx, k,    \
                      v, pos, (int)(Bt / P), (int)T, (int)H, inv_sqrt_d, dc, probs, dq, dsg,        \
                      du_part, dvb_part)
   OB_RA_DISPATCH(OB_RA_BWD);
 #undef OB_RA_BWD
 #define OB_RA_KV(DQ, NTT)                                                                          \
-  hipLaunchKernelGGL((relattn_bwd_kv_x6_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg, \
+  hipLaunchKernelGGL((relattn_bwd_kv_kernel<DQ>), grid, dim3(kThreads), 0, s, (const float*)dsg,    \
                      probs, q, dctx, u, vb, (int)T, (int)H, dc, dk, dv, dp_part)
   OB_RA_DISPATCH(OB_RA_KV);
 #undef OB_RA_KV
@@ -2005,6 +1881,9 @@ void launch_relattn_bwd(const float* dctx, const float* ctx, const float* q, con
 #ifdef OB_ATTN_STAMPS
 extern "C" int ob_attn_stamps(void* host_dst) {  // diagnostic build only
   return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? 0 : -6;
+}
+extern "C" int ob_attn_rt(void* host_dst) {  // diagnostic build only
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_attn_rt), sizeof(g_attn_rt)) == hipSuccess ? 0 : -6;
 }
 #endif
 

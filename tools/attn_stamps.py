@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
-"""Per-phase cycles of the flash-style attention backward from a diagnostic build
-(-DOB_ATTN_STAMPS: s_memtime stamps per wave, written to a device buffer of their own).
-Build:  make -C cmu-11785-idl-1.58bit-asr_amd/csrc OUT=$PWD/exp/libstamp.so BUILD=$PWD/exp/stamp \
-        HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -DOB_ATTN_STAMPS"
-Run:    ONEBIT_HIP_LIB=exp/libstamp.so python tools/attn_stamps.py"""
+"""Per-phase cycles of one attention kernel from a diagnostic build (-DOB_ATTN_STAMPS=K:
+s_memtime stamps per wave, written to a device buffer of their own). K = 1 flash-style
+backward, 2 query-side backward, 3 forward, 4 key-side backward.
+Build:  make -C cmu-11785-idl-1.58bit-asr_amd/csrc OUT=$PWD/exp/libstampK.so BUILD=$PWD/exp/stampK \
+        HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -DOB_ATTN_STAMPS=K"
+Run:    ONEBIT_HIP_LIB=exp/libstampK.so python tools/attn_stamps.py K [waves] [blocks per (b,h)]"""
 import ctypes
+import os
 import sys
 from pathlib import Path
 
@@ -16,11 +18,23 @@ import torch  # noqa: E402
 
 from onebit_asr import _lib  # noqa: E402
 
-PHASES = ["p3 work", "top wait", "0a stage", "0a wait", "X", "X wait", "S/dP/dK/dV", "wait",
-          "band", "band wait"]
+PHASES = {
+    1: ["p3 work", "top wait", "0a stage", "0a wait", "X", "X wait", "S/dP/dK/dV", "wait",
+        "band", "band wait"],
+    2: ["dO/delta", "dPd", "band row0", "dQu", "band sync", "dQv", "dq+sums", "red sync",
+        "dS' out", "-"],
+    3: ["q", "X", "row64", "sync1", "anchors+scores", "softmax", "sync2", "v stage", "sync3",
+        "ctx"],
+    4: ["first fetch", "sync a", "stage", "sync b", "mfma", "store", "-", "-", "-", "-"],
+}
+# (waves per block, blocks per (b, h)) at T = 249
+GRID = {1: (8, 2), 2: (4, 4), 3: (4, 4), 4: (4, 4)}
 
 
 def main():
+    kern = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    if kern == 1:
+        os.environ["OB_ATTN_BWD"] = "flash"
     lib = _lib.load()
     dev = torch.device("cuda:0")
     Bt, P, T, H, d = 96, 3, 249, 4, 36
@@ -53,14 +67,31 @@ def main():
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p]
     assert fn(buf.ctypes.data) == 0
-    nw = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    nblk = Bt * H * (int(sys.argv[2]) if len(sys.argv) > 2 else 2)
+    nw = int(sys.argv[2]) if len(sys.argv) > 2 else GRID[kern][0]
+    nblk = Bt * H * (int(sys.argv[3]) if len(sys.argv) > 3 else GRID[kern][1])
     st = buf[: nblk * nw * 10].reshape(nblk, nw, 10).astype(np.float64)
     tot = st.sum(axis=2)
     print(f"block cycles: median {np.median(tot):.0f} (wave-summed over phases)")
+    # block concurrency and the shader clock from s_memrealtime (100 MHz) at wave start / end
+    rt = np.zeros(16384, dtype=np.uint64)
+    fr = lib.ob_attn_rt
+    fr.restype = ctypes.c_int
+    fr.argtypes = [ctypes.c_void_p]
+    assert fr(rt.ctypes.data) == 0
+    rt = rt[: nblk * nw * 2].reshape(nblk, nw, 2).astype(np.float64)
+    b0, b1 = rt[:, :, 0].min(axis=1), rt[:, :, 1].max(axis=1)
+    span_us = (b1.max() - b0.min()) / 100.0
+    dur_us = (b1 - b0) / 100.0
+    clk = np.median(tot / np.maximum((rt[:, :, 1] - rt[:, :, 0]) / 100.0, 1e-9))  # cycles / us
+    print(f"kernel span {span_us:.1f} us; block duration median {np.median(dur_us):.1f} us, "
+          f"max {dur_us.max():.1f}; blocks in flight on average {dur_us.sum() / span_us:.1f}; "
+          f"shader clock ~{clk / 1e3:.2f} GHz")
+    starts = np.sort(b0 - b0.min()) / 100.0
+    print("block start offsets (us) at quantiles 0/25/50/75/100 %:",
+          " ".join(f"{np.quantile(starts, q):.1f}" for q in (0, 0.25, 0.5, 0.75, 1)))
     for wv in range(nw):
         med = np.median(st[:, wv, :], axis=0)
-        print(f"wave {wv}: " + "  ".join(f"{n} {m:.0f}" for n, m in zip(PHASES, med)))
+        print(f"wave {wv}: " + "  ".join(f"{n} {m:.0f}" for n, m in zip(PHASES[kern], med)))
 
 
 if __name__ == "__main__":
