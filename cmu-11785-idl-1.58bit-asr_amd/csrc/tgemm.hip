@@ -49,7 +49,48 @@ constexpr int kThreads = 256;  // 4 waves
 constexpr int kRows = 64;      // rows per row tile (16 per wave)
 constexpr size_t kMaxLds = 80 * 1024;  // B image + epilogue staging: 2 blocks per CU
 constexpr int kTargetBlocks = 512;  // 2 per CU
+// K > 256 (K = 576: 18 chunks a row tile, NT 3): one block per CU. The 504-block grid left
+// 13 of 56 row groups with a third 64-row tile (125 row tiles a pass) and CUs holding two
+// such blocks: waves in flight averaged 1.27 per SIMD (tools/tgemm_stamps.py) and the
+// launch ended on that tail. 252 blocks of <= 5 tiles: lin2 fwd 31.3 -> 27.4 us, lin1 dX
+// 32.8 -> 29.2 us same box; the K = 144 launches stay at 512 (256 measured 2-6 us slower).
+// (profiles/r4/tgemm_blocks/)
+constexpr int kTargetBlocksLongK = 256;
 constexpr int kBPad = 16;           // B-image row pad (bf16 elements), see the header
+
+#ifdef OB_TGEMM_STAMPS
+// diagnostic build only (tools/tgemm_stamps.py): per wave the cycles of the prologue (B
+// decode + barrier), of the main loops and of the epilogues, the row tiles done, and
+// s_memrealtime (100 MHz) at start and end -- into buffers nothing else reads
+__device__ uint64_t g_tg_stamps[32768];
+__device__ uint64_t g_tg_rt[16384];
+#define TG_DECL                                                              \
+  uint64_t tg_t = __builtin_amdgcn_s_memtime(), tg_rt0 = __builtin_amdgcn_s_memrealtime(), \
+           tg_acc[4] = {0, 0, 0, 0};
+#define TG_STAMP(k)                                       \
+  do {                                                    \
+    const uint64_t tg_n = __builtin_amdgcn_s_memtime();   \
+    tg_acc[k] += tg_n - tg_t;                             \
+    tg_t = tg_n;                                          \
+  } while (0)
+#define TG_WRITE                                                                          \
+  {                                                                                       \
+    const uint64_t tg_rt1 = __builtin_amdgcn_s_memrealtime();                             \
+    const size_t tg_w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;         \
+    if (lane == 0 && tg_w * 4 + 4 <= 32768)                                               \
+      for (int k_ = 0; k_ < 4; ++k_) g_tg_stamps[tg_w * 4 + k_] = tg_acc[k_];             \
+    if (lane == 0 && tg_w * 2 + 2 <= 16384) {                                             \
+      g_tg_rt[tg_w * 2] = tg_rt0;                                                         \
+      g_tg_rt[tg_w * 2 + 1] = tg_rt1;                                                     \
+    }                                                                                     \
+  }
+#else
+#define TG_DECL
+#define TG_STAMP(k) \
+  do {              \
+  } while (0)
+#define TG_WRITE
+#endif
 
 __device__ __forceinline__ uint32_t code_bf16(uint32_t c) {
   return ((c & 1u) * 0x3F80u) | ((c & 2u) << 14);  // 0 -> 0, 1 -> +1.0, 3 -> -1.0
@@ -219,6 +260,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
     const int* __restrict__ pass_bits, EpiArgs ep) {
+  TG_DECL
   const int L = xcd_logical(blockIdx.x, gridDim.x);
   const int n_ct_l = n_ct / ep.glayers;  // column tiles of one layer
   if (ep.glayers > 1) {
@@ -343,6 +385,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     for (int idx = threadIdx.x; idx < nwords; idx += kThreads) decode_store(idx, word_at(idx));
   }
   __syncthreads();
+  TG_STAMP(0);
 
   const __bf16* brow = bimg + r * stride + kg;
   const float a_eff = effective_alpha(alpha, alpha_raw);
@@ -430,6 +473,10 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     // keep the epilogue's loads (residual / pre-activation) from being hoisted into the
     // main loop, where they would hold NT*4 VGPRs across it
     __builtin_amdgcn_sched_barrier(0);
+    TG_STAMP(1);
+#ifdef OB_TGEMM_STAMPS
+    ++tg_acc[3];
+#endif
     if constexpr (VEC_EPI) {
       // Row-coalesced epilogue: each chunk of <= 4 column tiles goes through the wave's LDS
       // staging tile, then every lane handles 4 consecutive columns of one row (dwordx4 R
@@ -489,6 +536,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
       }
+      TG_STAMP(2);
       continue;
     }
     if constexpr (!VEC_EPI) {
@@ -535,8 +583,10 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       // exp/div sequences and spill
       if constexpr (EPI != kEpiNone) __builtin_amdgcn_sched_barrier(0);
     }
+    TG_STAMP(2);
     }
   }
+  TG_WRITE
 }
 
 // ---------------------------------------------------------------------------------
@@ -661,7 +711,7 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
                    hipStream_t s) {
   const int n_ct = ep.glayers * (int)ceil_div(N, 16 * NT);  // all layers' column tiles
   const int n_rt = (int)ceil_div(M, kRows);
-  int rgroups = kTargetBlocks / (n_ct * P);
+  int rgroups = (K > 256 ? kTargetBlocksLongK : kTargetBlocks) / (n_ct * P);
   if (rgroups < 1) rgroups = 1;
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
@@ -792,5 +842,12 @@ void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* c
                          hipStream_t s) {
   launch_ternary_gemm_passes(A, 1, M, K, codes, codes, nullptr, N, alpha, alpha_raw, bias, C, s);
 }
+
+#ifdef OB_TGEMM_STAMPS
+extern "C" int ob_tgemm_stamps(void* host_stamps, void* host_rt) {  // diagnostic build only
+  if (hipMemcpyFromSymbol(host_stamps, HIP_SYMBOL(g_tg_stamps), sizeof(g_tg_stamps)) != hipSuccess) return -6;
+  return hipMemcpyFromSymbol(host_rt, HIP_SYMBOL(g_tg_rt), sizeof(g_tg_rt)) == hipSuccess ? 0 : -6;
+}
+#endif
 
 }  // namespace ob
