@@ -57,6 +57,36 @@ constexpr int kTargetBlocks = 512;  // 2 per CU
 // (profiles/r4/tgemm_blocks/)
 constexpr int kTargetBlocksLongK = 256;
 constexpr int kBPad = 16;           // B-image row pad (bf16 elements), see the header
+// Byte image (K = 576 and N a multiple of 144: all 144 columns of a row tile in one block,
+// so each A element is split once instead of once per 48 columns): one byte per weight,
+// the high byte of the bf16 of Q/2 (0x00 -> 0, 0x3F -> +0.5, 0xBF -> -0.5; the low byte
+// 0); the epilogue scales by 2a, so every product and sum is the bf16-image one halved
+// exactly. 84 KB of LDS: one block (4 waves, up to 512 registers each) per CU. Row pitch
+// Kpad + 8 bytes = 146 dwords at K = 576: the 16 lanes of a ds_read_b64 group on disjoint
+// bank pairs. Same box: lin2 fwd 26.9 -> 20.9 us, lin1 dX 28.4 -> 22.8 us, lin2 fwd +
+// residual 29.7 -> 26.8 us (profiles/r4/tgemm_blocks/kbench_byte_image.log).
+constexpr int kBytePad = 8;
+
+// code word (16 two-bit codes) -> 16 image bytes as 4 dwords (byte p of dword q = code 4q+p)
+__device__ __forceinline__ void code_bytes(uint32_t word, u32x4& out) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t x = (word >> (8 * q)) & 0xFFu;                         // codes 4q .. 4q+3
+    x = (x | (x << 6) | (x << 12) | (x << 18)) & 0x03030303u;       // one code per byte
+    const uint32_t lo = x & 0x01010101u, hi = x & 0x02020202u;
+    out[q] = ((lo << 6) - lo) | (hi << 6);                          // 1 -> 0x3F, 3 -> 0xBF
+  }
+}
+
+// 8 image bytes (k .. k+7) -> the bf16x8 B fragment (byte = high byte, low byte 0)
+__device__ __forceinline__ bf16x8 bytes_bf16x8(uint32_t d0, uint32_t d1) {
+  u32x4 o;
+  o[0] = __builtin_amdgcn_perm(d1, d0, 0x010C000Cu);
+  o[1] = __builtin_amdgcn_perm(d1, d0, 0x030C020Cu);
+  o[2] = __builtin_amdgcn_perm(d1, d0, 0x050C040Cu);
+  o[3] = __builtin_amdgcn_perm(d1, d0, 0x070C060Cu);
+  return __builtin_bit_cast(bf16x8, o);
+}
 
 #ifdef OB_TGEMM_STAMPS
 // diagnostic build only (tools/tgemm_stamps.py): per wave the cycles of the prologue (B
@@ -210,8 +240,9 @@ __device__ __forceinline__ void select_pass(const float* __restrict__& A, float*
 }
 
 // byte offset of the epilogue staging tiles (after the B image, 16-B aligned) and their size
-__host__ __device__ inline size_t epi_stage_off(int nt, int kpad) {
-  return ((size_t)2 * 16 * nt * (kpad + kBPad) + 15) & ~(size_t)15;
+__host__ __device__ inline size_t epi_stage_off(int nt, int kpad, bool byte = false) {
+  return ((byte ? (size_t)16 * nt * (kpad + kBytePad) : (size_t)2 * 16 * nt * (kpad + kBPad)) + 15) &
+         ~(size_t)15;
 }
 __host__ __device__ inline size_t epi_stage_bytes(int nt) {
   const int cw = nt < 4 ? nt : 4;
@@ -254,8 +285,8 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
   *reinterpret_cast<f32x4*>(c) = out;
 }
 
-template <int NT, int NCH, int EPI, bool VEC_EPI>
-__global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
+template <int NT, int NCH, int EPI, bool VEC_EPI, bool BYTE = false>
+__global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
@@ -276,7 +307,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
   const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
-  const int stride = kpad + kBPad;
+  const int stride = BYTE ? kpad + kBytePad : kpad + kBPad;  // image row pitch (bytes / bf16)
   const int kwp = kpad >> 4;
   // row-coalesced epilogue (vec_epi): per-wave staging [16][kEpiCC + 4] after the B image
   constexpr int kEpiCW = NT < 4 ? NT : 4, kEpiCC = 16 * kEpiCW, kEpiLd = kEpiCC + 4;
@@ -294,6 +325,12 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   auto decode_store = [&](int idx, uint32_t word) {
     const int nl = idx / kwp, w = idx - nl * kwp;
     word = (n0 + nl < N && w < KW && idx < nwords) ? word : 0u;
+    if constexpr (BYTE) {
+      u32x4 b4;
+      code_bytes(word, b4);
+      if (idx < nwords) *reinterpret_cast<u32x4*>(smem + nl * stride + 16 * w) = b4;
+      return;
+    }
     u32x4 lo4, hi4;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -338,6 +375,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   // quant-off (alpha_raw 2): the LDS image is a copy of the block's rows of the bf16 weight
   // image [N][K]. Unit = 8 consecutive k of one row (one 16-byte load and store).
   auto weight_image = [&]() {
+    if constexpr (BYTE) return;  // (the host never pairs the byte image with alpha_raw 2)
     const uint16_t* Wb = reinterpret_cast<const uint16_t*>(codes);
     const int upr = kpad >> 3;
     for (int u = threadIdx.x; u < 16 * NT * upr; u += kThreads) {
@@ -388,7 +426,8 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
   TG_STAMP(0);
 
   const __bf16* brow = bimg + r * stride + kg;
-  const float a_eff = effective_alpha(alpha, alpha_raw);
+  const unsigned char* brow8 = reinterpret_cast<const unsigned char*>(smem) + r * stride + kg;
+  const float a_eff = BYTE ? 2.0f * effective_alpha(alpha, alpha_raw) : effective_alpha(alpha, alpha_raw);
   const uint32_t dkey = (EPI != kEpiNone && ep.dc.on) ? drop_key(ep.rng[0], ep.rng[1] + ep.rng_off) : 0u;
   float bcol[NT];
 #pragma unroll
@@ -410,12 +449,31 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
     // flight; each tile's MFMAs then wait only for their own read (counted lgkmcnt).
     auto compute = [&](const f32x4& x0, const f32x4& x1, int kc) {
       bf16x8 bq[NT];
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      u32x2 bb[BYTE ? NT : 1];
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        bq[t] = *reinterpret_cast<const bf16x8*>(brow + t * 16 * stride + kc);
+      for (int t = 0; t < NT; ++t) {
+        if constexpr (BYTE)
+          bb[t] = *reinterpret_cast<const u32x2*>(brow8 + t * 16 * stride + kc);
+        else
+          bq[t] = *reinterpret_cast<const bf16x8*>(brow + t * 16 * stride + kc);
+      }
       __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (hipcc would pair them up)
       bf16x8 hi, mid, lo;
       split3(x0, x1, hi, mid, lo);
+      if constexpr (BYTE) {
+        // tile-major: a fragment is converted right before its three MFMAs (one live at a
+        // time; dependent 16x16x32 MFMAs issue back to back at full rate), the same
+        // per-accumulator order lo, mid, hi as the part-major loops below
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const bf16x8 b = bytes_bf16x8(bb[t][0], bb[t][1]);
+          acc[t] = mfma_bf16(lo, b, acc[t]);
+          acc[t] = mfma_bf16(mid, b, acc[t]);
+          acc[t] = mfma_bf16(hi, b, acc[t]);
+        }
+        return;
+      }
       // part-major: consecutive MFMAs update different accumulators (no back-to-back
       // dependence on the MFMA just issued)
 #pragma unroll
@@ -482,7 +540,7 @@ __global__ __launch_bounds__(kThreads, 2) void tgemm_bf16x3_kernel(
       // staging tile, then every lane handles 4 consecutive columns of one row (dwordx4 R
       // loads and C / C2 stores; 16 lanes = 256 contiguous bytes). The wave's LDS ops run
       // in issue order; the waitcnt + sched barriers keep hipcc from reordering across them.
-      float* stg = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad)) + wave * 16 * kEpiLd;
+      float* stg = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad, BYTE)) + wave * 16 * kEpiLd;
       constexpr int kQ = kEpiCC / 4;  // float4s per staged row
       constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
 #pragma unroll
@@ -708,7 +766,7 @@ template <int NT>
 void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
                    const float* alpha, int alpha_raw, const float* bias, float* C,
                    const uint32_t* codes1, const int* pass_bits, int P, const EpiArgs& ep,
-                   hipStream_t s) {
+                   hipStream_t s, bool byte = false) {
   const int n_ct = ep.glayers * (int)ceil_div(N, 16 * NT);  // all layers' column tiles
   const int n_rt = (int)ceil_div(M, kRows);
   int rgroups = (K > 256 ? kTargetBlocksLongK : kTargetBlocks) / (n_ct * P);
@@ -716,7 +774,7 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
   const int kpad = (int)((K + 31) & ~int64_t(31));
-  const size_t lds = epi_stage_off(NT, kpad) + epi_stage_bytes(NT);
+  const size_t lds = epi_stage_off(NT, kpad, byte) + epi_stage_bytes(NT);
   const int KW = (int)ceil_div(K, 16);
   const bool vec = (N % 4 == 0) && aligned16(C) && (ep.mode != kEpiSwishDrop || aligned16(ep.C2)) &&
                    ((ep.mode != kEpiResidual && ep.mode != kEpiSwishDropBwd) || aligned16(ep.R));
@@ -729,6 +787,23 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
     hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E, false>), grid, dim3(kThreads), lds, s, \
                        A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,  \
                        bias, C, codes1, pass_bits, ep)
+  if constexpr (NT == 9) {
+    if (byte) {  // byte image: K = 576 (18 chunks), codes (alpha_raw < 2), plain / residual
+#define OB_TGEMM_B(E)                                                                            \
+  if (vec)                                                                                      \
+    hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, 18, E, true, true>), grid, dim3(kThreads), lds, s, \
+                       A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,    \
+                       bias, C, codes1, pass_bits, ep);                                           \
+  else                                                                                          \
+    hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, 18, E, false, true>), grid, dim3(kThreads), lds,  \
+                       s, A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, \
+                       bias, C, codes1, pass_bits, ep)
+      if (ep.mode == kEpiResidual) OB_TGEMM_B(kEpiResidual);
+      else OB_TGEMM_B(kEpiNone);
+#undef OB_TGEMM_B
+      return;
+    }
+  }
 #define OB_TGEMM(NCH)                                                   \
   switch (ep.mode) {                                                    \
     case kEpiSwishDrop: OB_TGEMM_E(NCH, kEpiSwishDrop); break;          \
@@ -771,6 +846,13 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
   }
   const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const int nt = vec && !use_f32_gemm() ? pick_nt(N, K, ep.mode) : 0;
+  // K = 576 with N a multiple of 144: every column in one block on the byte image (the A
+  // split once per 144 columns instead of once per 48)
+  if (nt > 0 && (K + 31) / 32 == 18 && N % 144 == 0 && alpha_raw < 2 &&
+      (ep.mode == kEpiNone || ep.mode == kEpiResidual)) {
+    launch_bf16x3<9>(A, M, K, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s, true);
+    return;
+  }
 #define OB_NT(V)                                                                            \
   case V:                                                                                   \
     launch_bf16x3<V>(A, M, K, codes, N, alpha, alpha_raw, bias, C, codes1, pass_bits, P, ep, s); \
