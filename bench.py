@@ -225,6 +225,14 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
     # MFMA-busy (north_star: "MFMA-busy against gfx950 peak"): the MFMA pipe cycles the
     # family's instructions take, over the 1024 SIMDs x 2.4 GHz x its measured time
     mfma_busy = cyc / 1024 / (t_us * 1e-6 * 2.4e9)
+    # both families against both roofs (the dominant one is the line's roofline)
+    fams = {}
+    for k, (ft, fb, ff, fn_, _c) in fam.items():
+        if fn_:
+            fams[k] = {"ms_per_step": round(ft / 1e3, 3), "launches_per_step": fn_,
+                       "frac_hbm": round((fb / ft * 1e6) / 1e9 / PEAK_HBM_GBS, 4),
+                       "frac_fp32_mfma": round((ff / ft * 1e6) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4)}
+    roof["families"] = fams
     roof.update({"kernel": dom, "avg_launch_us": round(avg_t, 3),
                  "mfma_busy": round(mfma_busy, 4),
                  "mfma_busy_basis": "issued v_mfma_f32_16x16x32_bf16 cycles (16/SIMD each: 3 per "
