@@ -424,6 +424,39 @@ __global__ __launch_bounds__(kThreads, 2) void dw_bf16x6_kernel(
 // step. Loader unit = 4 rows x 4 columns of one operand (row quad fastest across lanes:
 // conflict-free ds_write_b64).
 // ---------------------------------------------------------------------------------
+#ifdef OB_DW_STAMPS
+// diagnostic build only (tools/dw_stamps.py): per wave the cycles of the prologue, the
+// steps' MFMA phases, split / LDS-store phases, load issue and barrier waits, the partial /
+// alpha epilogue and the db epilogue, and s_memrealtime at start and end
+__device__ uint64_t g_dw_stamps[8 * 4096];
+__device__ uint64_t g_dw_rt[2 * 4096];
+#define DW_DECL \
+  uint64_t dw_t = __builtin_amdgcn_s_memtime(), dw_rt0 = __builtin_amdgcn_s_memrealtime(), \
+           dw_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define DW_STAMP(k)                                     \
+  do {                                                  \
+    const uint64_t dw_n = __builtin_amdgcn_s_memtime(); \
+    dw_acc[k] += dw_n - dw_t;                           \
+    dw_t = dw_n;                                        \
+  } while (0)
+#define DW_WRITE                                                                        \
+  {                                                                                     \
+    const uint64_t dw_rt1 = __builtin_amdgcn_s_memrealtime();                           \
+    const size_t dw_w = (size_t)blockIdx.x * (blockDim.x / 64) + wave;                  \
+    if (lane == 0 && dw_w < 4096) {                                                     \
+      for (int k_ = 0; k_ < 8; ++k_) g_dw_stamps[dw_w * 8 + k_] = dw_acc[k_];           \
+      g_dw_rt[dw_w * 2] = dw_rt0;                                                       \
+      g_dw_rt[dw_w * 2 + 1] = dw_rt1;                                                   \
+    }                                                                                   \
+  }
+#else
+#define DW_DECL
+#define DW_STAMP(k) \
+  do {              \
+  } while (0)
+#define DW_WRITE
+#endif
+
 constexpr int kLdsPitch = 224;  // bytes per column slot: 3 planes x 32 bf16 rows + 32 B pad
 constexpr int kStepRows = 32;
 
@@ -478,6 +511,7 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wave / WK, wk = wave - wn * WK;
+  DW_DECL
   const int r = lane & 15, g = lane >> 4;
   const int tiles_nl = N / C::BN;  // n-tiles of one layer
   const int tiles = grp.layers * tiles_nl * tiles_k;
@@ -619,6 +653,7 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   store(ra, 0);
   if (steps > 2) load(ra, 2);
   __syncthreads();
+  DW_STAMP(0);
   // Waves 0-3 compute before they store, waves 4.. store first (a stagger: the waves
   // sharing a SIMD -- w and w+4 -- then run their MFMA and their split/store phases at
   // different times instead of in lockstep between the barriers). Compute-first code issues
@@ -628,19 +663,26 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   auto phase = [&](int cb, Raw& nxt, int sb, bool do_store, int ld_step) {
     if (late) {
       if (do_store) store(nxt, sb);
+      DW_STAMP(2);
       compute(cb);
+      DW_STAMP(1);
     } else {
       compute(cb);
+      DW_STAMP(1);
       if (do_store) store(nxt, sb);
+      DW_STAMP(2);
     }
     if (do_store && ld_step >= 0) load(nxt, ld_step);
+    DW_STAMP(3);
   };
   for (int s = 0; s < steps; s += 2) {
     phase(0, rb, 1, s + 1 < steps, s + 3 < steps ? s + 3 : -1);
     __syncthreads();
+    DW_STAMP(4);
     if (s + 1 >= steps) break;
     phase(1, ra, 0, s + 2 < steps, s + 4 < steps ? s + 4 : -1);
     __syncthreads();
+    DW_STAMP(4);
   }
   // partial tile: D[row = 4g + reg][col = r] of tile (t, u) -> n = n0 + 48wn + 16t + 4g + reg,
   // k = k0 + 48wk + 16u + r. The same loop forms this block's share of the alpha gradient
@@ -672,6 +714,7 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
   };
   if (has_al) emit(std::true_type{});
   else emit(std::false_type{});
+  DW_STAMP(5);
   if (has_al) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) prod += __shfl_xor(prod, off, 64);
@@ -702,6 +745,8 @@ __global__ __launch_bounds__(64 * WN * WK) void dw_lds_kernel(
       part_db[chunk * N + n0 + c] = v;
     }
   }
+  DW_STAMP(6);
+  DW_WRITE
 }
 
 
@@ -976,5 +1021,12 @@ void launch_dw_finish_group(const DwFinish* a, int n, hipStream_t s) {
   G.start[n] = (int)total;
   hipLaunchKernelGGL(dw_finish_group_kernel, dim3((unsigned)total), dim3(kThreads), 0, s, G);
 }
+
+#ifdef OB_DW_STAMPS
+extern "C" int ob_dw_stamps(void* host_stamps, void* host_rt) {  // diagnostic build only
+  if (hipMemcpyFromSymbol(host_stamps, HIP_SYMBOL(g_dw_stamps), sizeof(g_dw_stamps)) != hipSuccess) return -6;
+  return hipMemcpyFromSymbol(host_rt, HIP_SYMBOL(g_dw_rt), sizeof(g_dw_rt)) == hipSuccess ? 0 : -6;
+}
+#endif
 
 }  // namespace ob
