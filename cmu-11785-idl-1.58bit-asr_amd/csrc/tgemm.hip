@@ -543,6 +543,24 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
       float* stg = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad, BYTE)) + wave * 16 * kEpiLd;
       constexpr int kQ = kEpiCC / 4;  // float4s per staged row
       constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
+      // residual rows past their utterance's length (pad-zeroed): a lane's rows are the same
+      // in every column chunk, so each is tested once per row tile (32-bit division below
+      // 2^31 rows)
+      bool rvalid[kEpiCW];
+#pragma unroll
+      for (int it = 0; it < kEpiCW; ++it) {
+        rvalid[it] = true;
+        if (EPI == kEpiResidual && ep.lens) {
+          const int64_t grow = rowbase + m0 + (it * 64 + lane) / kQ;
+          if (grow < ((int64_t)1 << 31)) {
+            const uint32_t bb = (uint32_t)grow / (uint32_t)ep.T;
+            rvalid[it] = (int)((uint32_t)grow - bb * (uint32_t)ep.T) < ep.lens[bb];
+          } else {
+            const int64_t bb = grow / ep.T;
+            rvalid[it] = (grow - bb * ep.T) < ep.lens[bb];
+          }
+        }
+      }
 #pragma unroll
       for (int c0 = 0; c0 < NT; c0 += kEpiCW) {
         // the chunk's residual / pre-activation operand, loaded unconditionally from clamped
@@ -580,13 +598,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
               if (EPI == kEpiSwishDrop)
                 *reinterpret_cast<f32x4*>(ep.C2 + (rowbase + orow) * N + col) = y;
             } else {
-              bool valid = true;
-              if (EPI == kEpiResidual && ep.lens) {
-                const int64_t grow = rowbase + orow;
-                const int64_t bb = grow / ep.T;
-                valid = (grow - bb * ep.T) < ep.lens[bb];
-              }
-              epi_store4<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, valid,
+              epi_store4<EPI>(ep, dkey, C + orow * N + col, rowbase + orow, col, N, y, rvalid[it],
                               rpre[it]);
             }
           }

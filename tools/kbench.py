@@ -119,6 +119,10 @@ def main():
             pre = torch.randn(P * M, K, device=dev)
             rng = torch.tensor([1234, 5], dtype=torch.int64, device=dev)
             pd = 0.1
+            # the step's residual epilogue zeroes rows past each utterance's length:
+            # 249-row utterances (M = 32 x 249 at Conformer-S), ragged lengths
+            Tq = 249 if M % 249 == 0 else M
+            lens = torch.randint(Tq // 2, Tq + 1, (P * M // Tq,), dtype=torch.int32, device=dev)
             fns.update({
                 "fswish": lambda cs=s: lib.ob_bitlinear_fwd_swish_drop(
                     X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
@@ -128,6 +132,10 @@ def main():
                     X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
                     alpha.data_ptr(), 1, b.data_ptr(), N, R.data_ptr(), 0.5, pd, rng.data_ptr(), 0,
                     None, 0, Y.data_ptr(), cs),
+                "fresl": lambda cs=s: lib.ob_bitlinear_fwd_residual(
+                    X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                    alpha.data_ptr(), 1, b.data_ptr(), N, R.data_ptr(), 0.5, pd, rng.data_ptr(), 0,
+                    lens.data_ptr(), Tq, Y.data_ptr(), cs),
                 "dxswish": lambda cs=s: lib.ob_bitlinear_bwd_dx_swish_drop(
                     dY.data_ptr(), P, M, N, codes_t.data_ptr(), c1t.data_ptr(), pbits.data_ptr(),
                     alpha.data_ptr(), 1, K, pre.data_ptr(), pd, rng.data_ptr(), 0, dX.data_ptr(),
@@ -158,7 +166,8 @@ def main():
             print(f"{'':6s} int8: absmax {res['absmax']:7.2f}  fwd_i8 {res['fwd_i8']:7.2f} us "
                   f"({gb_i8:.0f} GB/s fp32-in/out, {tops:.1f} TOP/s)  vs bf16x3 fwd {res['fwd']:7.2f} us")
         if "fswish" in res:
-            print(f"{'':6s} fused: fwd+swish {res['fswish']:7.2f}  fwd+residual {res['fres']:7.2f}  "
+            print(f"{'':6s} fused: fwd+swish {res['fswish']:7.2f}  fwd+residual {res['fres']:7.2f} "
+                  f"(with lengths {res['fresl']:7.2f})  "
                   f"dx+swish-bwd {res['dxswish']:7.2f}  drop-scale-bwd {res['dropbwd']:7.2f} us")
 
 
