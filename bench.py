@@ -230,8 +230,9 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
     for k, (ft, fb, ff, fn_, _c) in fam.items():
         if fn_:
             fams[k] = {"ms_per_step": round(ft / 1e3, 3), "launches_per_step": fn_,
-                       "frac_hbm": round((fb / ft * 1e6) / 1e9 / PEAK_HBM_GBS, 4),
-                       "frac_fp32_mfma": round((ff / ft * 1e6) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4)}
+                       "frac_hbm": round((fb / ft * 1e6) / 1e9 / PEAK_HBM_GBS, 4)}
+            if k != "ternary_gemm":  # (2-bit weights: no fp32 x fp32 product to price)
+                fams[k]["frac_fp32_mfma"] = round((ff / ft * 1e6) / 1e12 / PEAK_FP32_MFMA_TFLOPS, 4)
     roof["families"] = fams
     roof.update({"kernel": dom, "avg_launch_us": round(avg_t, 3),
                  "mfma_busy": round(mfma_busy, 4),
