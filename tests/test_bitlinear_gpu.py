@@ -20,6 +20,9 @@ pytestmark = pytest.mark.gpu
 SHAPES = [  # (M, K, N)
     (1, 3, 2), (5, 7, 37), (16, 16, 16), (100, 100, 37), (364, 64, 256), (364, 256, 64),
     (249, 144, 144), (7968, 144, 144), (7968, 144, 576), (7968, 576, 144), (33, 13, 130),
+    # the K = 576 byte-image launches (all 144 columns of a row tile in one block) with
+    # ragged row counts: forward at N = 288 and at K = 560 (padded to 576), dX of K = 144
+    (65, 576, 288), (130, 560, 144), (65, 144, 576),
 ]
 
 

@@ -70,6 +70,21 @@ def main():
         report(lib, name + " dX", lambda: lib.ob_bitlinear_bwd_dx_passes(
             dY.data_ptr(), P, M, N, codes_t.data_ptr(), c1t.data_ptr(), pbits.data_ptr(),
             alpha.data_ptr(), 1, K, dX.data_ptr(), s))
+        if N == 576:  # the FFN's fused launches: lin1 fwd + swish + dropout, lin2 dX + swish bwd
+            rng = torch.tensor([1234, 5], dtype=torch.int64, device=dev)
+            Y2 = torch.empty_like(Y)
+            report(lib, name + " fwd + swish + dropout", lambda: lib.ob_bitlinear_fwd_swish_drop(
+                X.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                alpha.data_ptr(), 1, b.data_ptr(), N, 0.1, rng.data_ptr(), 0, Y2.data_ptr(),
+                Y.data_ptr(), s))
+            dY2 = torch.randn(P * M, K, device=dev)
+            pre = torch.randn(P * M, N, device=dev)
+            dX2 = torch.empty(P * M, N, device=dev)
+            report(lib, "lin2 dX + dropout / swish bwd (K 144, N 576)",
+                   lambda: lib.ob_bitlinear_bwd_dx_swish_drop(
+                       dY2.data_ptr(), P, M, K, codes.data_ptr(), c1.data_ptr(), pbits.data_ptr(),
+                       alpha.data_ptr(), 1, N, pre.data_ptr(), 0.1, rng.data_ptr(), 0,
+                       dX2.data_ptr(), s))
 
 
 if __name__ == "__main__":
