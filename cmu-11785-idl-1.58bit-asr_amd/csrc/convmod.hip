@@ -584,19 +584,48 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
     float acc[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = 0.0f;
-    float gr[8];
+    if (KT > 0 && j0 + 7 < KT) {
+      // all 8 taps are weights: 8 frames per round from a 16-value window of g (one move per
+      // frame instead of seven, no per-tap select); the same fma order per accumulator
+      float win[16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) gr[q] = gs[min(j0 + q, W - 1) * CG + c];
-    for (int tl = 0; tl < n_t; ++tl) {
-      const float d = dzs[(tl + P) * CG + c];
+      for (int q = 0; q < 8; ++q) win[q] = gs[(j0 + q) * CG + c];
+      int tl = 0;
+      for (; tl + 8 <= n_t; tl += 8) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int j = j0 + q;
-        acc[q] = fmaf(d, j < KT ? gr[q] : (j == KT ? 1.0f : 0.0f), acc[q]);
+        for (int q = 0; q < 8; ++q) win[8 + q] = gs[(tl + 8 + j0 + q) * CG + c];
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const float d = dzs[(tl + st + P) * CG + c];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = fmaf(d, win[st + q], acc[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) win[q] = win[8 + q];
       }
+      for (; tl < n_t; ++tl) {  // the last tile's remaining frames
+        const float d = dzs[(tl + P) * CG + c];
 #pragma unroll
-      for (int q = 0; q < 7; ++q) gr[q] = gr[q + 1];
-      gr[7] = gs[min(tl + 1 + j0 + 7, W - 1) * CG + c];
+        for (int q = 0; q < 8; ++q) acc[q] = fmaf(d, win[q], acc[q]);
+#pragma unroll
+        for (int q = 0; q < 7; ++q) win[q] = win[q + 1];
+        win[7] = gs[min(tl + 1 + j0 + 7, W - 1) * CG + c];
+      }
+    } else {
+      float gr[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) gr[q] = gs[min(j0 + q, W - 1) * CG + c];
+      for (int tl = 0; tl < n_t; ++tl) {
+        const float d = dzs[(tl + P) * CG + c];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int j = j0 + q;
+          acc[q] = fmaf(d, j < KT ? gr[q] : (j == KT ? 1.0f : 0.0f), acc[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 7; ++q) gr[q] = gr[q + 1];
+        gr[7] = gs[min(tl + 1 + j0 + 7, W - 1) * CG + c];
+      }
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
