@@ -48,6 +48,7 @@ reference (AdamW skips grad=None).
 """
 from __future__ import annotations
 
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -129,6 +130,13 @@ class BucketedAllReduce:
         self.works = []
 
 
+# Test hook: run the multi-rank exchange path (flat buffer, buckets, the all-reduce captured
+# into the step graph) at world size 1, so a single-GPU test can capture RCCL collectives
+# (tests/test_rccl_capture_gpu.py). Not read from the environment.
+_MULTI_RANK_PATH_AT_WORLD_1 = False
+_WATCHDOG_DRAIN_S = 2.0  # > the watchdog's poll interval (ProcessGroupNCCL: ~100 ms... 1 s)
+
+
 class GraphedTrainStep:
     def __init__(self, step_module, n_layers: int, lr: float = 5e-4, warmup_steps: int = 4000,
                  total_steps: int = 100000, max_norm: float = 5.0,
@@ -143,6 +151,8 @@ class GraphedTrainStep:
         self.max_norm = max_norm
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if process_group is not None else 1
+        # the multi-rank path: flat gradient buffer + the exchange (world > 1, or the test hook)
+        self.multi = self.world > 1 or (_MULTI_RANK_PATH_AT_WORLD_1 and process_group is not None)
         self.warmup_iters = warmup_iters
         self.use_graph = use_graph
         self.fused_optimizer = fused_optimizer
@@ -184,7 +194,7 @@ class GraphedTrainStep:
         self.params = [p for p in self.step_module.parameters() if p.grad is not None]
         for p in self.step_module.parameters():
             p.grad = None
-        if self.world > 1:
+        if self.multi:
             # one flat gradient buffer: the all-reduce is a single large RCCL call
             total = sum(p.numel() for p in self.params)
             self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
@@ -206,7 +216,7 @@ class GraphedTrainStep:
             lr = torch.tensor(self.lr0, dtype=torch.float32, device=self.device) if cap else self.lr0
             self.opt = torch.optim.AdamW(self.params, lr=lr, betas=(0.9, 0.98),
                                          weight_decay=1e-2, foreach=True, capturable=cap)
-            if self.world == 1 and cap:  # N == 1 torch path needs stable grads for capture
+            if not self.multi and cap:  # N == 1 torch path needs stable grads for capture
                 total = sum(p.numel() for p in self.params)
                 self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
                 off = 0
@@ -240,13 +250,13 @@ class GraphedTrainStep:
         if self.fused:  # clip + AdamW in three launches (grad_scale = 1/world)
             self.opt.step()
             return
-        if self.world > 1:
+        if self.multi:
             self.flat.div_(self.world)
         torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, foreach=True)
         self.opt.step()
 
     def _allreduce(self, overlapped: bool = False):
-        if self.world > 1:
+        if self.multi:
             if overlapped:
                 self.buckets.finish()
             else:
@@ -332,11 +342,17 @@ class GraphedTrainStep:
         torch.cuda.synchronize(self.device)
         self._drop_code_caches(self.step_module)
         pool = torch.cuda.graph_pool_handle()
-        if (self.world > 1 and self.buckets is not None
+        if (self.multi and self.buckets is not None
                 and dist.get_backend(self.pg) == dist.Backend.NCCL):
             # the whole step in one graph, the bucket all-reduces overlapping the backward
             # (RCCL collectives capture into a graph; gloo's host staging does not)
             rng = self._rng_snapshot()  # (a failed attempt must not advance the dropout streams)
+            # the warm-up's collectives must have left the process group's watchdog before any
+            # collective is captured (it polls their events and may not touch captured ones)
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.pg, device_ids=[self.device.index])
+            torch.cuda.synchronize(self.device)
+            time.sleep(_WATCHDOG_DRAIN_S)
             try:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
@@ -358,9 +374,9 @@ class GraphedTrainStep:
             self.graph_a = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_a, pool=pool):
                 self.loss, self.parts = self._fwd_bwd()
-                if self.world == 1:
+                if not self.multi:
                     self._update()
-            if self.world > 1:
+            if self.multi:
                 self.graph_b = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph_b, pool=pool):
                     self._update()
@@ -380,7 +396,7 @@ class GraphedTrainStep:
             self.loss, self.parts = self._eager()
         else:
             self.graph_a.replay()
-            if self.world > 1 and not self.comm_in_graph:
+            if self.multi and not self.comm_in_graph:
                 self._allreduce()
                 self.graph_b.replay()
             if self.fused:  # the replayed update wrote the parameters in place
