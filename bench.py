@@ -712,6 +712,20 @@ def replicas_equal(model, dev) -> bool:
     return bool(torch.equal(hi, lo))
 
 
+def exchange_desc(args, gs):
+    """The gradient exchange the timed steps ran (graph path: the bucket plan and whether the
+    collectives were captured into the step graph)."""
+    via = "RCCL" if args.dist_backend == "nccl" else "gloo"
+    if gs is None:
+        return f"DDP (eager) over {via}"
+    if gs.buckets is None:
+        return f"one flat fp32 gradient all-reduce per step over {via}, between two graph replays"
+    where = ("captured in the step graph, overlapping the backward" if gs.comm_in_graph
+             else "between two graph replays")
+    return (f"{len(gs.buckets.buckets)} bucketed fp32 all-reduces per step (~{gs.bucket_bytes >> 20} MB, "
+            f"reverse parameter order) over {via}, {where}")
+
+
 def main():
     args = parse()
     if args.mode.startswith("infer"):
@@ -838,9 +852,8 @@ def main():
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
                    "d_model": 144, "blocks": 16, "d_ff": 576, "heads": 4, "vocab": VOCAB,
                    "parallelism": f"dp{world}",
-                   "exchange": (f"one flat fp32 gradient all-reduce per step over "
-                                f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'}"
-                                if distributed else None),
+                   "exchange": exchange_desc(args, gs if not args.eager else None)
+                               if distributed else None,
                    "passes": "teacher 2-bit + student 1-bit + SP",
                    "subsampling": "computed once, shared by the 3 stacked passes (exact: no "
                                   "dropout, full-precision weights; the reference runs it 3x)",
