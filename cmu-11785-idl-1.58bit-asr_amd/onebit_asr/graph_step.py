@@ -27,24 +27,32 @@ What changes per step without re-capture:
   shape needs another ``GraphedTrainStep``);
 * dropout masks: torch's philox offsets advance per replay.
 
-With N > 1 gradients live in one flat fp32 buffer (parameter order, no flatten/unflatten
-copies), cut into buckets of contiguous parameters taken in REVERSE order (the backward
-produces the decoder / CTC-head and last-block gradients first). A post-accumulate-grad
-hook counts each bucket's parameters; when a bucket's last gradient has landed its slice is
-all-reduced (SUM) on a communication stream that waited for it, while the backward goes on
-on the compute stream; the update waits for the communication stream (``BucketedAllReduce``;
-reference train.py:116-118 is single-device: loss.backward(), clip, step). The buckets are
-``bucket_mb`` (default 12 MB: 4 buckets for Conformer-S's 47 MB, each large enough for the
-per-link bandwidth of a ring over xGMI). The whole step (forward, backward with the bucket
-all-reduces, update) is captured as one graph; if the process group cannot be captured the
-exchange runs eagerly between graph A and the update graph (flat, one call), as before.
-Without overlap each rank would idle for the whole exchange after its backward. Note: with
-N > 1 the parameter gradients are views of the flat buffer, so the deferred finishes
-(deferred.py) do not apply and every weight-gradient finish runs on the spot (~230 more
-small launches than the single-GPU step). With N == 1 autograd's own gradient buffers are
-used as they are (``p.grad = None`` before backward, so no accumulate kernels). Parameters
-that receive no gradient in the step are excluded from the optimizer exactly like the
-reference (AdamW skips grad=None).
+N > 1 (reference train.py:116-118 is single-device: loss.backward(), clip, step), the
+``exchange``:
+
+* ``"deferred"`` (default): the backward runs exactly as at N == 1 -- autograd's own
+  gradient buffers, every weight-gradient finish deferred to one table launch per kind at
+  the end (deferred.py) -- then the gradients are packed into one flat fp32 buffer (one
+  ``cat``), all-reduced (SUM) in one call and copied back (one ``foreach`` copy), all
+  inside the step graph with RCCL. Measured per rank on one GPU (world size 1 through the
+  test hook below, ``tools/multi_path_bench.py``): the bucketed path's on-the-spot finishes
+  cost ~2.3 ms/step (28.6 vs 26.3 ms) -- more than the exchange it overlaps (47 MB: a few
+  hundred us on a ring over xGMI) -- so the deferred exchange is the default.
+* ``"bucketed"``: gradients are views of the flat buffer (parameter order), cut into
+  ``bucket_mb`` buckets (default 12 MB: 4 for Conformer-S's 47 MB) of contiguous parameters
+  taken in REVERSE order (the backward produces the decoder / CTC-head and last-block
+  gradients first). A post-accumulate-grad hook counts each bucket's parameters; when a
+  bucket's last gradient has landed its slice is all-reduced on a communication stream
+  while the backward goes on (``BucketedAllReduce``); the update waits for it. Deferral
+  cannot apply (a hook needs its finished gradient): ~230 more small launches per step.
+* ``"flat"``: the gradient views of the flat buffer, one all-reduce after the backward.
+
+With RCCL the whole step (forward, backward, the exchange, update) is captured as one
+graph; if the process group cannot be captured (gloo) the exchange runs eagerly between
+graph A and the update graph. With N == 1 autograd's own gradient buffers are used as they
+are (``p.grad = None`` before backward, so no accumulate kernels). Parameters that receive
+no gradient in the step are excluded from the optimizer exactly like the reference (AdamW
+skips grad=None).
 """
 from __future__ import annotations
 
@@ -142,7 +150,9 @@ class GraphedTrainStep:
                  total_steps: int = 100000, max_norm: float = 5.0,
                  process_group: Optional[dist.ProcessGroup] = None, warmup_iters: int = 2,
                  use_graph: bool = True, fused_optimizer: bool = True,
-                 bucket_mb: Optional[float] = 12.0):
+                 bucket_mb: Optional[float] = 12.0, exchange: str = "deferred"):
+        if exchange not in ("deferred", "bucketed", "flat"):
+            raise ValueError(f"exchange must be 'deferred', 'bucketed' or 'flat', got {exchange!r}")
         self.step_module = step_module
         self.n_layers = n_layers
         self.lr0 = lr
@@ -168,7 +178,9 @@ class GraphedTrainStep:
         self.graph_a = self.graph_b = None
         self.loss = self.parts = None
         self.steps_done = 0
-        self.bucket_bytes = int(bucket_mb * 2**20) if bucket_mb else 0
+        self.exchange = exchange
+        self.bucket_bytes = int(bucket_mb * 2**20) if (bucket_mb and exchange == "bucketed") else 0
+        self.flat_views: List[torch.Tensor] = []
         self.buckets: Optional[BucketedAllReduce] = None
         self.comm_in_graph = False
 
@@ -195,14 +207,17 @@ class GraphedTrainStep:
         for p in self.step_module.parameters():
             p.grad = None
         if self.multi:
-            # one flat gradient buffer: the all-reduce is a single large RCCL call
+            # one flat gradient buffer: the exchange's all-reduce(s) run on it
             total = sum(p.numel() for p in self.params)
             self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
             off = 0
             for p in self.params:
                 n = p.numel()
-                p.grad = self.flat[off:off + n].view_as(p)
+                self.flat_views.append(self.flat[off:off + n].view_as(p))
                 off += n
+            if self.exchange != "deferred":  # the gradients ARE the flat buffer's views
+                for p, v in zip(self.params, self.flat_views):
+                    p.grad = v
             if self.bucket_bytes:
                 self.buckets = BucketedAllReduce(self.params, self.flat, self.pg, self.bucket_bytes)
         if self.device.type == "cuda" and self.fused_optimizer:
@@ -229,9 +244,9 @@ class GraphedTrainStep:
     def _fwd_bwd(self, overlap: bool = False):
         """Forward + backward; ``overlap``: the buckets' all-reduces start from the backward
         (finished by ``_allreduce``)."""
-        if self.flat is not None:
+        if self.flat is not None and (not self.multi or self.exchange != "deferred"):
             self.flat.zero_()
-        else:  # N == 1: autograd hands its gradient buffers over (no accumulate kernels)
+        else:  # autograd hands its gradient buffers over (no accumulate kernels)
             for p in self.params:
                 p.grad = None
         if self.buckets is not None:
@@ -250,17 +265,27 @@ class GraphedTrainStep:
         if self.fused:  # clip + AdamW in three launches (grad_scale = 1/world)
             self.opt.step()
             return
-        if self.multi:
+        if self.multi and self.exchange != "deferred":
             self.flat.div_(self.world)
         torch.nn.utils.clip_grad_norm_(self.params, max_norm=self.max_norm, foreach=True)
         self.opt.step()
 
     def _allreduce(self, overlapped: bool = False):
-        if self.multi:
-            if overlapped:
-                self.buckets.finish()
-            else:
-                dist.all_reduce(self.flat, group=self.pg)
+        if not self.multi:
+            return
+        if self.exchange == "deferred":
+            # pack (one cat), one all-reduce, unpack (one foreach copy); the non-fused update
+            # takes the average here (the fused one scales by 1/world)
+            grads = [p.grad for p in self.params]
+            torch.cat([g.reshape(-1) for g in grads], out=self.flat)
+            dist.all_reduce(self.flat, group=self.pg)
+            if not self.fused:
+                self.flat.div_(self.world)
+            torch._foreach_copy_(grads, self.flat_views)
+        elif overlapped:
+            self.buckets.finish()
+        else:
+            dist.all_reduce(self.flat, group=self.pg)
 
     def _eager(self):
         ov = self.buckets is not None
@@ -342,10 +367,9 @@ class GraphedTrainStep:
         torch.cuda.synchronize(self.device)
         self._drop_code_caches(self.step_module)
         pool = torch.cuda.graph_pool_handle()
-        if (self.multi and self.buckets is not None
-                and dist.get_backend(self.pg) == dist.Backend.NCCL):
-            # the whole step in one graph, the bucket all-reduces overlapping the backward
-            # (RCCL collectives capture into a graph; gloo's host staging does not)
+        if self.multi and dist.get_backend(self.pg) == dist.Backend.NCCL:
+            # the whole step in one graph with its exchange (bucketed: the all-reduces overlap
+            # the backward); RCCL collectives capture into a graph, gloo's host staging does not
             rng = self._rng_snapshot()  # (a failed attempt must not advance the dropout streams)
             # the warm-up's collectives must have left the process group's watchdog before any
             # collective is captured (it polls their events and may not touch captured ones)
@@ -355,9 +379,10 @@ class GraphedTrainStep:
             time.sleep(_WATCHDOG_DRAIN_S)
             try:
                 g = torch.cuda.CUDAGraph()
+                ov = self.buckets is not None
                 with torch.cuda.graph(g, pool=pool):
-                    self.loss, self.parts = self._fwd_bwd(overlap=True)
-                    self._allreduce(overlapped=True)
+                    self.loss, self.parts = self._fwd_bwd(overlap=ov)
+                    self._allreduce(overlapped=ov)
                     self._update()
                 self.graph_a, self.comm_in_graph = g, True
             except Exception as e:  # the process group cannot be captured: exchange eagerly

@@ -1,8 +1,9 @@
 """Worker of tests/test_rccl_capture_gpu.py (a child process on the box's one GPU): the
-multi-rank step path over RCCL at world size 1 -- flat gradient buffer, the bucketed
-all-reduce started from the backward's gradient hooks and captured into the same graph as
-the forward, backward and update (graph_step._MULTI_RANK_PATH_AT_WORLD_1). With one rank the
-all-reduce is an identity, so two steps must give the parameters of the single-GPU path.
+multi-rank step path over RCCL at world size 1 (graph_step._MULTI_RANK_PATH_AT_WORLD_1),
+both exchanges captured into the same graph as the forward, backward and update: the
+bucketed all-reduce started from the backward's gradient hooks, and the default deferred
+one (pack, one all-reduce, unpack). With one rank the all-reduce is an identity, so two
+steps must give the parameters of the single-GPU path.
 Writes result.pt: whether the collectives were captured, bucket count, the parameters of
 both runs."""
 import os
@@ -35,13 +36,14 @@ def main():
     batch = synthetic_batch([400, 333], [20, 13], seed=100, device=dev)
     sp_mask = sample_sp_mask(CFG1["enc_layers"], generator=torch.Generator().manual_seed(9))
 
-    def run(multi):
+    def run(multi, exchange="deferred"):
         graph_step._MULTI_RANK_PATH_AT_WORLD_1 = multi
         torch.manual_seed(0)
         model = ConformerASR(80, 5004, **CFG1).to(dev)
         # small buckets: several captured collectives (Conformer cfg1 has ~2 MB of gradients)
         gs = GraphedTrainStep(OneBitStep(model, n_layers=CFG1["enc_layers"]), CFG1["enc_layers"],
-                              process_group=dist.group.WORLD, warmup_iters=1, bucket_mb=0.25)
+                              process_group=dist.group.WORLD, warmup_iters=1, bucket_mb=0.25,
+                              exchange=exchange)
         for _ in range(2):
             gs.step(batch, sp_mask)
         torch.cuda.synchronize()
@@ -49,10 +51,13 @@ def main():
         params = {k: p.detach().clone().cpu() for k, p in model.named_parameters()}
         return gs.comm_in_graph, nb, gs.multi, params
 
-    cap, nb, multi, p_multi = run(True)
+    cap, nb, multi, p_multi = run(True, "bucketed")
+    cap_d, nb_d, multi_d, p_dfr = run(True, "deferred")
     _, _, plain_multi, p_plain = run(False)
     torch.save({"captured": cap, "buckets": nb, "multi": multi, "plain_multi": plain_multi,
-                "p_multi": p_multi, "p_plain": p_plain}, os.path.join(out_dir, "result.pt"))
+                "p_multi": p_multi, "p_plain": p_plain, "captured_deferred": cap_d,
+                "buckets_deferred": nb_d, "multi_deferred": multi_d, "p_deferred": p_dfr},
+               os.path.join(out_dir, "result.pt"))
     dist.destroy_process_group()
 
 

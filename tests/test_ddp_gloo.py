@@ -111,7 +111,7 @@ class _HostBitsStep(torch.nn.Module):
         return self.inner(batch, [1 if v == 1 else 0 for v in bits.tensor.tolist()])
 
 
-def _graph_step_worker(rank, world, port, out_dir, bucket_mb=12.0, tag="g"):
+def _graph_step_worker(rank, world, port, out_dir, bucket_mb=12.0, tag="g", exchange="deferred"):
     import sys
     from pathlib import Path
 
@@ -124,7 +124,8 @@ def _graph_step_worker(rank, world, port, out_dir, bucket_mb=12.0, tag="g"):
 
     model = _model()
     gs = GraphedTrainStep(_HostBitsStep(model), n_layers=2, process_group=dist.group.WORLD,
-                          warmup_iters=1, warmup_steps=4, total_steps=10, bucket_mb=bucket_mb)
+                          warmup_iters=1, warmup_steps=4, total_steps=10, bucket_mb=bucket_mb,
+                          exchange=exchange)
     losses = []
     for mask in ([1, 0], [0, 1], [1, 1]):
         loss, _ = gs.step(_batch(rank), mask)
@@ -179,18 +180,24 @@ def test_graph_step_flat_allreduce_gloo(tmp_path):
 
 @pytest.mark.slow
 def test_bucketed_overlapped_allreduce_equals_flat_gloo(tmp_path):
-    """The exchange started bucket by bucket from the backward's post-accumulate hooks
-    (BucketedAllReduce, tiny buckets: one per few parameters) trains the replicas to exactly
-    the parameters of the single flat all-reduce after the backward (SUM over two ranks does
-    not depend on how the buffer is cut)."""
+    """The three exchanges train the replicas to exactly the same parameters (SUM over two
+    ranks does not depend on how the buffer is cut or packed): the bucketed one started
+    bucket by bucket from the backward's post-accumulate hooks (BucketedAllReduce, tiny
+    buckets: one per few parameters), the single flat all-reduce over the gradient views,
+    and the default deferred one (autograd's gradient buffers packed into the flat buffer,
+    one all-reduce, copied back)."""
     world = 2
-    for bucket_mb, tag in ((None, "flat"), (0.002, "bkt")):
-        mp.spawn(_graph_step_worker, args=(world, _free_port(), str(tmp_path), bucket_mb, tag),
+    runs = ((None, "flat", "flat"), (0.002, "bkt", "bucketed"), (None, "dfr", "deferred"))
+    for bucket_mb, tag, exchange in runs:
+        mp.spawn(_graph_step_worker,
+                 args=(world, _free_port(), str(tmp_path), bucket_mb, tag, exchange),
                  nprocs=world, join=True)
-    flat = [torch.load(tmp_path / f"flat{r}.pt", weights_only=True) for r in range(world)]
-    bkt = [torch.load(tmp_path / f"bkt{r}.pt", weights_only=True) for r in range(world)]
-    assert flat[0]["buckets"] == 0 and bkt[0]["buckets"] > 8, bkt[0]["buckets"]
+    res = {tag: [torch.load(tmp_path / f"{tag}{r}.pt", weights_only=True) for r in range(world)]
+           for _, tag, _ in runs}
+    flat, bkt, dfr = res["flat"], res["bkt"], res["dfr"]
+    assert flat[0]["buckets"] == 0 and dfr[0]["buckets"] == 0 and bkt[0]["buckets"] > 8, bkt[0]["buckets"]
     for r in range(world):
-        assert flat[r]["losses"] == bkt[r]["losses"]
-        for k, p in flat[r]["params"].items():
-            assert torch.equal(p, bkt[r]["params"][k]), k
+        for other in (bkt, dfr):
+            assert flat[r]["losses"] == other[r]["losses"]
+            for k, p in flat[r]["params"].items():
+                assert torch.equal(p, other[r]["params"][k]), k

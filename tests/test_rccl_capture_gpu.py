@@ -1,8 +1,8 @@
 """The multi-rank step path on its real transport (RCCL never ran): at world size
 1 over RCCL (graph_step._MULTI_RANK_PATH_AT_WORLD_1), in a child process
 (tests/rccl_capture_worker.py):
-  * the bucketed all-reduce is captured into the step's single graph (no fallback to the
-    eager exchange), with several buckets;
+  * both exchanges (the default deferred one and the bucketed one, several buckets) are
+    captured into the step's single graph (no fallback to the eager exchange);
   * two graphed steps give the parameters of the single-GPU path (the one-rank all-reduce is
     an identity; the multi-rank path finishes its gradients on the spot instead of deferring
     them, which is bit-identical)."""
@@ -28,10 +28,12 @@ def test_bucketed_allreduce_captured_over_rccl(gpu, tmp_path):
                         str(tmp_path), str(port)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = torch.load(tmp_path / "result.pt", weights_only=True)
-    assert res["multi"] and not res["plain_multi"]
-    assert res["captured"], "the RCCL all-reduce was not captured into the step graph"
-    assert res["buckets"] > 2
-    for k, p in res["p_plain"].items():
-        q = res["p_multi"][k]
-        err = (q.double() - p.double()).abs().max().item()
-        assert err <= 1e-6 * max(p.abs().max().item(), 1e-30), (k, err)
+    assert res["multi"] and res["multi_deferred"] and not res["plain_multi"]
+    assert res["captured"], "the bucketed RCCL all-reduce was not captured into the step graph"
+    assert res["captured_deferred"], "the deferred exchange was not captured into the step graph"
+    assert res["buckets"] > 2 and res["buckets_deferred"] == 0
+    for key in ("p_multi", "p_deferred"):
+        for k, p in res["p_plain"].items():
+            q = res[key][k]
+            err = (q.double() - p.double()).abs().max().item()
+            assert err <= 1e-6 * max(p.abs().max().item(), 1e-30), (key, k, err)
