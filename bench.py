@@ -718,12 +718,14 @@ def exchange_desc(args, gs):
     via = "RCCL" if args.dist_backend == "nccl" else "gloo"
     if gs is None:
         return f"DDP (eager) over {via}"
+    where = "captured in the step graph" if gs.comm_in_graph else "between two graph replays"
+    if gs.exchange == "deferred":
+        return (f"deferred gradient finishes, then one fp32 all-reduce of the packed 47 MB "
+                f"gradients per step over {via}, {where}")
     if gs.buckets is None:
-        return f"one flat fp32 gradient all-reduce per step over {via}, between two graph replays"
-    where = ("captured in the step graph, overlapping the backward" if gs.comm_in_graph
-             else "between two graph replays")
+        return f"one flat fp32 gradient all-reduce per step over {via}, {where}"
     return (f"{len(gs.buckets.buckets)} bucketed fp32 all-reduces per step (~{gs.bucket_bytes >> 20} MB, "
-            f"reverse parameter order) over {via}, {where}")
+            f"reverse parameter order, started from the backward) over {via}, {where}")
 
 
 def main():
