@@ -63,8 +63,11 @@ def parse():
     ap.add_argument("--roofline-only", action="store_true", help="skip the step timing")
     ap.add_argument("--progress", action="store_true", help="progress lines on stderr")
     ap.add_argument("--mode", default="train",
-                    choices=["train", "quant-off", "quant-off-lib", "infer", "infer-fp32act"],
-                    help="train: configs[1]/[2] (default); quant-off: configs[3] (BitLinear -> "
+                    choices=["train", "train-i8", "quant-off", "quant-off-lib", "infer",
+                             "infer-fp32act"],
+                    help="train: configs[1]/[2] (default); train-i8: the same step with "
+                         "absmax-int8 activations on every BitLinear (opt-in north-star mode, "
+                         "not the reference's arithmetic); quant-off: configs[3] (BitLinear -> "
                          "bf16 weights on the same fused kernels, set_quant_off 'bf16w'); "
                          "quant-off-lib: the same with bf16 library GEMMs (hipBLASLt); "
                          "infer / infer-fp32act: configs[4] (B=256, 2-bit, int8 / fp32 "
@@ -620,6 +623,91 @@ def roofline_i8(batch, frames, dev, act_quant, reps=20):
             "ql_kernel_ms_per_step": round(tot_t / 1e3, 3), "shapes": detail, "traffic": None}
 
 
+def roofline_i8_train(batch, frames, dev, reps=20, log=lambda m: None):
+    """``--mode train-i8``: the training step's int8 forward GEMMs (ob_bitlinear_fwd_i8 on
+    the stacked 3-pass rows, fp32 X quantised in registers at its per-pass absmax, i8 MFMA)
+    at their Conformer-S shapes, and the per-call absmax launch that precedes each one (in
+    training no LN / swish producer emits the scale). dX and dW stay on the fp32 kernels
+    (STE; quant.py _BitLinearI8Fn). Algorithmic bytes of the GEMM: fp32 X read once, fp32 Y
+    written once, the codes; FLOPs 2MKN. HIP events around `reps` graph-replayed launches."""
+    from onebit_asr import _lib
+    from onebit_asr.quant import pack_codes
+
+    lib = _lib.load()
+    side = torch.cuda.Stream(dev)
+    pbits = torch.tensor(PASS_BITS, dtype=torch.int32, device=dev)
+    tot = {"gemm_t": 0.0, "absmax_t": 0.0, "b": 0.0, "f": 0.0, "n": 0}
+    detail = []
+    for name, M, K, N, count in ql_shapes(batch, frames):  # qkvo: four module calls a block
+        rows = PASSES * M
+        g = torch.Generator(device=dev).manual_seed(M + K + N)
+        X = torch.randn(rows, K, device=dev, generator=g)
+        W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
+        alpha = W.abs().mean()
+        b = torch.zeros(N, device=dev)
+        c2, _ = pack_codes(W, alpha, 2)
+        c1, _ = pack_codes(W, alpha, 1)
+        Y = torch.empty(rows, N, device=dev)
+        amax = torch.empty(PASSES, device=dev)
+        wsb = lib.ob_act_absmax_workspace(PASSES)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        _lib.check(lib.ob_act_absmax(X.data_ptr(), PASSES, M * K, amax.data_ptr(), ws.data_ptr(),
+                                     wsb, torch.cuda.current_stream(dev).cuda_stream), "absmax")
+
+        def absmax(s):
+            return lib.ob_act_absmax(X.data_ptr(), PASSES, M * K, amax.data_ptr(), ws.data_ptr(),
+                                     wsb, s)
+
+        def gemm(s):
+            return lib.ob_bitlinear_fwd_i8(X.data_ptr(), PASSES, M, K, c2.data_ptr(), c1.data_ptr(),
+                                           pbits.data_ptr(), alpha.data_ptr(), 1, amax.data_ptr(),
+                                           b.data_ptr(), N, Y.data_ptr(), s)
+
+        def timed(fn):
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    _lib.check(fn(side.cuda_stream), "roofline warm-up")
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=side):
+                    for _ in range(reps):
+                        fn(torch.cuda.current_stream(dev).cuda_stream)
+                graph.replay()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+                graph.replay()
+                e1.record(side)
+            e1.synchronize()
+            return e0.elapsed_time(e1) * 1e3 / reps
+
+        tg, ta = timed(gemm), timed(absmax)
+        by = 4 * rows * K + 4 * rows * N + 4 * N + 2 * 4 * N * ((K + 15) // 16)
+        fl = 2.0 * rows * K * N
+        tot["gemm_t"] += count * tg
+        tot["absmax_t"] += count * ta
+        tot["b"] += count * by
+        tot["f"] += count * fl
+        tot["n"] += count
+        detail.append({"layer": name, "rows": rows, "K": K, "N": N, "launches_per_step": count,
+                       "gemm_us": round(tg, 2), "absmax_us": round(ta, 2), "alg_bytes": int(by),
+                       "GBs": round(by / (tg * 1e-6) / 1e9, 1),
+                       "TOPs": round(fl / (tg * 1e-6) / 1e12, 2)})
+        log(f"roofline train-i8 {name}: gemm {tg:.2f} us, absmax {ta:.2f} us")
+    n = tot["n"]
+    avg = tot["gemm_t"] / n
+    gbs = (tot["b"] / n) / (avg * 1e-6) / 1e9
+    tops = (tot["f"] / n) / (avg * 1e-6) / 1e12
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "kernel": "tgemm_i8 (ob_bitlinear_fwd_i8: fp32 X quantised in registers, i8 MFMA)",
+            "avg_launch_us": round(avg, 3), "bytes_per_launch": int(tot["b"] / n),
+            "flops_per_launch": int(tot["f"] / n), "achieved_TOPs": round(tops, 2),
+            "mfma_peak_TOPs": PEAK_I8_MFMA_TOPS, "mfma_frac": round(tops / PEAK_I8_MFMA_TOPS, 4),
+            "i8_gemm_ms_per_step": round(tot["gemm_t"] / 1e3, 3),
+            "absmax_ms_per_step": round(tot["absmax_t"] / 1e3, 3), "shapes": detail,
+            "traffic": None}
+
+
 def run_infer(args):
     from onebit_asr.conformer import ConformerASR
     from onebit_asr.data import CONFORMER_S, synthetic_batch
@@ -759,6 +847,11 @@ def main():
     model = ConformerASR(N_MELS, VOCAB, **CONFORMER_S,
                          quantize_conv_pointwise=args.conv_pw_ternary).to(dev)
     quant_off = args.mode.startswith("quant-off")
+    train_i8 = args.mode == "train-i8"
+    if train_i8:  # every BitLinear on absmax-int8 activations (quant.py _BitLinearI8Fn)
+        from onebit_asr.quant import set_act_quant
+
+        set_act_quant(model, "absmax_int8")
     if quant_off:  # configs[3]: every BitLinear -> bf16 weights, same step body
         from onebit_asr.quant import set_quant_off
 
@@ -831,7 +924,10 @@ def main():
     value = frames_total / elapsed
     out = {
         "metric": ("mel-frames/sec (Conformer-S quant-off train step, BitLinear -> bf16 nn.Linear)"
-                   if quant_off else "mel-frames/sec (Conformer-S 1.58-bit train step)"),
+                   if quant_off else
+                   "mel-frames/sec (Conformer-S 1.58-bit train step, absmax-int8 activations: "
+                   "opt-in, not the reference's arithmetic)" if train_i8 else
+                   "mel-frames/sec (Conformer-S 1.58-bit train step)"),
         "quant_off": (None if not quant_off else
                       "bf16 weights on the fused ternary-GEMM kernels (exact fp32 activations)"
                       if args.mode == "quant-off" else "bf16 F.linear on hipBLASLt"),
@@ -846,9 +942,12 @@ def main():
         "vs_baseline": None,
         "dtype": ("bf16 weights x fp32 activations (fused kernels), fp32 elsewhere"
                   if args.mode == "quant-off" else
-                  "bf16 linears (hipBLASLt), fp32 elsewhere" if quant_off else "fp32"),
+                  "bf16 linears (hipBLASLt), fp32 elsewhere" if quant_off else
+                  "int8 x ternary forward GEMMs (i8 MFMA); fp32 dX / dW and elsewhere"
+                  if train_i8 else "fp32"),
         "data": "synthetic (N(0,1) 80-mel x 1000-frame padded batches, random-init weights)",
         "config": {"workload": ("conformer-s-quant-off-bf16-train-step" if quant_off
+                                else "conformer-s-1.58bit-train-step-int8-act" if train_i8
                                 else "conformer-s-1.58bit-train-step"), "global_batch": args.batch * world,
                    "execution": "eager" if args.eager else "hip-graph",
                    "per_gpu_batch": args.batch, "frames": args.frames, "tokens": args.tokens,
@@ -866,6 +965,10 @@ def main():
         out["replicas_bitwise_equal"] = same
     if quant_off:  # no ternary kernel runs: the line is the ceiling the 1.58-bit step is read against
         out["roofline"] = None
+    elif train_i8:  # the int8 forward GEMMs; the fp32 oracle step is no baseline for this mode
+        out["roofline"] = (None if args.no_roofline or rank != 0 or world != 1 else
+                           roofline_i8_train(args.batch, args.frames, dev,
+                                             log=lambda m: log(args, m)))
     elif rank == 0 and world == 1 and not args.no_roofline:
         roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
         roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
@@ -873,7 +976,7 @@ def main():
         roof["in_step_fused"] = roofline_fused(args.batch, args.frames, dev,
                                                log=lambda m: log(args, m))
         out["roofline"] = roof
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not quant_off:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not quant_off and not train_i8:
         # (progress always on stderr: the CPU leg runs minutes without other output)
         out["cpu_baseline"] = cpu_baseline(
             args.cpu_seconds,
