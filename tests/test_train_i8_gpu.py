@@ -9,9 +9,16 @@ north-star mode; not the reference's arithmetic, which keeps activations fp32 --
   model and batch: loss within 3% and the whole gradient vector at cosine >= 0.98 (the
   per-tensor int8 rounding is the only difference);
 * GraphedTrainStep (``bench.py --mode train-i8``) replays == the same class run eagerly
-  over 3 steps (losses rel <= 1e-5).
+  over 3 steps (losses rel <= 1e-5);
+* ``bench.py --mode train-i8`` (small batch) prints its line with the int8-GEMM roofline.
 Module-level int8 forward / backward parity against the numpy oracle is in
 test_bitlinear_i8_gpu.py."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
 import pytest
 import torch
 
@@ -86,3 +93,21 @@ def test_int8_graphed_train_step(gpu):
     assert all(torch.isfinite(torch.tensor(l_g)))
     for a, b in zip(l_g, l_e):
         assert abs(a - b) <= 1e-5 * abs(b), (l_g, l_e)
+
+
+def test_bench_train_i8_line(gpu):
+    root = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, str(root / "bench.py"), "--mode", "train-i8", "--steps", "2",
+           "--warmup", "1", "--batch", "4", "--frames", "600", "--tokens", "20"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["config"]["workload"] == "conformer-s-1.58bit-train-step-int8-act"
+    assert res["value"] > 0 and "cpu_baseline" not in res
+    roof = res["roofline"]
+    assert roof["kernel"].startswith("tgemm_i8") and 0 < roof["frac"] < 1
+    assert {s["layer"] for s in roof["shapes"]} == {"lin1", "lin2", "qkvo", "pos"}
