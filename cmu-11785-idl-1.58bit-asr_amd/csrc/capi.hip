@@ -1,6 +1,7 @@
 // capi.hip — the C ABI declared in include/onebit_hip.h: argument validation, workspace
 // carving and launch-error reporting around the launchers in quant.hip / gemm.hip.
 #include <algorithm>
+#include <vector>
 
 #include "../../include/onebit_hip.h"
 #include "ob_launch.h"
@@ -924,6 +925,97 @@ int ob_dw_finish_table(const void* table, int64_t n, int64_t total_blocks, void*
   if (n > 0 && !table) return OB_ERR_NULL;
   launch_dw_finish_table(static_cast<const DwFinishEntry*>(table), (int)n, total_blocks,
                          as_stream(stream));
+  return launched();
+}
+
+int ob_dw_grouped_supported(int64_t N, int64_t K) {
+  return N > 0 && K > 0 && N % kDwgTile == 0 && K % kDwgTile == 0 && N <= (1 << 20) &&
+         K <= (1 << 20);
+}
+
+namespace {
+struct DwgPlan {
+  std::vector<DwgDesc> d;
+  int64_t steps = 0;
+  int tiles = 0, blocks = 0;
+  size_t table = 0, slots = 0, talpha = 0, total = 0;
+};
+
+// validates the descriptors and lays out the linear work space (gemm-major, tile, pass, step)
+int dwg_plan(const ob_dwg_gemm* g, int64_t G, DwgPlan& pl) {
+  if (G < 1 || G > (1 << 16)) return OB_ERR_SHAPE;
+  if (!g) return OB_ERR_NULL;
+  pl.d.resize((size_t)G);
+  int64_t tiles = 0;
+  for (int64_t i = 0; i < G; ++i) {
+    const ob_dwg_gemm& e = g[i];
+    // 32-bit offsets in the kernel: one pass of an operand, the weight, the step count
+    if (!ob_dw_grouped_supported(e.N, e.K) || e.M < 1 || e.P < 1 || e.P > kMaxPasses ||
+        e.M * e.P >= ((int64_t)1 << 30) || e.M * std::max(e.N, e.K) * 4 >= ((int64_t)1 << 31) ||
+        e.N * e.K * 4 >= ((int64_t)1 << 31))
+      return OB_ERR_SHAPE;
+    if (!e.dY || !e.X || !e.dW) return OB_ERR_NULL;
+    if (e.W && (!e.alpha || !e.dalpha)) return OB_ERR_NULL;
+    if (e.W && !e.pass_bits && check_bits(e.bits) != OB_OK) return OB_ERR_BITWIDTH;
+    if (!aligned4(e.dY) || !aligned4(e.X) || ((reinterpret_cast<uintptr_t>(e.dY) |
+                                               reinterpret_cast<uintptr_t>(e.X)) & 15))
+      return OB_ERR_ALIGN;
+    DwgDesc& d = pl.d[(size_t)i];
+    d.dY = e.dY;
+    d.X = e.X;
+    d.W = e.W;
+    d.alpha = e.alpha;
+    d.pass_bits = e.pass_bits;
+    d.dW = e.dW;
+    d.db = e.db;
+    d.dalpha = e.dalpha;
+    d.N = (int)e.N;
+    d.K = (int)e.K;
+    d.Mp = (int)e.M;
+    d.P = (int)e.P;
+    d.alpha_raw = e.alpha_raw;
+    d.bits = e.bits;
+    d.spp = (int)ceil_div(e.M, 32);
+    d.tiles_k = (int)(e.K / kDwgTile);
+    d.tiles = (int)((e.N / kDwgTile) * d.tiles_k);
+    d.tile0 = (int)tiles;
+    d.work0 = pl.steps;
+    tiles += d.tiles;
+    pl.steps += (int64_t)d.tiles * d.P * d.spp;
+  }
+  if (tiles > (1 << 24) || pl.steps >= ((int64_t)1 << 31)) return OB_ERR_SHAPE;
+  pl.tiles = (int)tiles;
+  pl.blocks = dwg_blocks(pl.steps);
+  pl.table = align_up(sizeof(DwgDesc) * (size_t)G);
+  pl.slots = align_up(dwg_slot_bytes() * 2 * (size_t)pl.blocks);
+  pl.talpha = align_up(sizeof(float) * (size_t)tiles);
+  pl.total = pl.table + pl.slots + pl.talpha;
+  return OB_OK;
+}
+}  // namespace
+
+size_t ob_dw_grouped_workspace(const ob_dwg_gemm* gemms, int64_t G) {
+  DwgPlan pl;
+  return dwg_plan(gemms, G, pl) == OB_OK ? pl.total : 0;
+}
+
+size_t ob_dw_grouped_tickets(const ob_dwg_gemm* gemms, int64_t G) {
+  DwgPlan pl;
+  return dwg_plan(gemms, G, pl) == OB_OK ? (size_t)pl.tiles + (size_t)G : 0;
+}
+
+int ob_dw_grouped(const ob_dwg_gemm* gemms, int64_t G, void* ws, size_t ws_bytes, void* tickets,
+                  size_t ticket_words, void* stream) {
+  DwgPlan pl;
+  const int st = dwg_plan(gemms, G, pl);
+  if (st != OB_OK) return st;
+  if (!ws || !tickets) return OB_ERR_NULL;
+  if (ws_bytes < pl.total || ticket_words < (size_t)pl.tiles + (size_t)G) return OB_ERR_WORKSPACE;
+  unsigned char* base = static_cast<unsigned char*>(ws);
+  launch_dw_grouped(pl.d.data(), (int)G, pl.steps, pl.blocks, reinterpret_cast<DwgDesc*>(base),
+                    reinterpret_cast<float*>(base + pl.table),
+                    reinterpret_cast<float*>(base + pl.table + pl.slots),
+                    static_cast<uint32_t*>(tickets), pl.tiles, as_stream(stream));
   return launched();
 }
 

@@ -852,6 +852,432 @@ __global__ __launch_bounds__(kThreads) void dw_finish_group_kernel(DwFinishGroup
 }
 
 
+// ---------------------------------------------------------------------------------
+// Grouped deferred dW, stream-K (ob_dw_grouped). Every deferred weight gradient of a
+// backward (N, K multiples of 144) in ONE persistent launch after the backward. The work
+// space is linear in steps -- gemm-major, then 144 x 144 tile, then pass, then 32-row step
+// -- and block b (one 9-wave block per CU) owns steps [b W / nb, (b + 1) W / nb). It walks
+// its range tile by tile with the dw_lds_kernel<3,3> main loop (same LDS planes, same six
+// products), so each segment runs hundreds of steps instead of the 12 a per-layer split-M
+// launch gave one block, and no per-layer prologue / epilogue / finish launch remains.
+//   * A tile one block covers entirely is finished from that block's registers: dW = G *
+//     1[|W/a| <= 1] (quant.py:80-82), db, the tile's alpha partial.
+//   * A tile split between blocks (only the first and the last tile of a block's range, so
+//     <= 2 slabs per block) is finished by the block whose ticket add arrives last; it sums
+//     the segments' slabs in block order (the partition is static: deterministic).
+//   * Alpha (quant.py:84-91) is linear in G, so a segment that crosses a pass boundary i adds
+//     sum_e A_i[e] (term_{b_i}[e] - term_{b_i+1}[e]) there (A_i = its accumulator at the
+//     boundary) and sum_e A[e] term_b[e] at its end: the telescoped sum over passes of each
+//     pass's rows against the term at that pass's bitwidth. Tiles' partials are summed in tile
+//     order by the last tile of the gemm (second ticket).
+// Hand-offs are write-through: sc1 stores, every storing wave's vmcnt(0), the block barrier,
+// one agent-scope ticket add; the last arriver reads every handed-off byte with sc1 loads
+// (MI355X_MICROARCH.md, Valid forms, row 1). The last arriver resets its ticket to 0.
+// ---------------------------------------------------------------------------------
+constexpr int kDwgSlotF = kDwgTile * kDwgTile + 256;  // floats: tile (fragment order), db, alpha
+constexpr int kDwgDb = kDwgTile * kDwgTile;
+constexpr int kDwgAl = kDwgDb + kDwgTile;
+constexpr unsigned kSc1 = 16;  // buffer cache policy: sc1 (write-through store / L1-bypass load)
+
+__device__ __forceinline__ int dwg_start(int b, int nb, int W) {
+  return (int)((long long)b * W / nb);
+}
+// the block whose range holds linear step x (the largest b with dwg_start(b) <= x; nb <= W)
+__device__ __forceinline__ int dwg_owner(int x, int nb, int W) {
+  return (int)(((long long)(x + 1) * nb - 1) / W);
+}
+
+// An opaque copy of x: values derived from it cannot be hoisted above this point (keeps the
+// epilogue's per-lane addresses out of the main loop's registers: hoisted out of the segment
+// loop they stayed live across it and spilled the main loop).
+// fp32 through the 32-bit buffer builtins (they move integers: bit-cast, not convert)
+__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, int voff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+__device__ __forceinline__ void st_f32(float v, __amdgpu_buffer_rsrc_t r, int voff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, 0, 0);
+}
+
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// 8 waves, two per SIMD: per 32-row step a SIMD issues the MFMAs of 21 or 20 16 x 16
+// sub-tiles, against 27 on the busiest SIMD of the 9-wave dw_lds tiling (3/2/2/2 waves), and a
+// wave may use 256 registers, which leaves the segment loop room (the 9-wave main loop needs
+// all of its 168 and spilled inside the loop nest). Wave w owns the 3 x 3 block (w / 3, w % 3)
+// of the 144 x 144 tile's 9 x 9 sub-tiles and sub-tile w of the ninth block (2, 2); wave 7 also
+// owns that block's last sub-tile (8, 8).
+constexpr int kDwgWaves = 8, kDwgThreads = 64 * kDwgWaves;
+constexpr int kDwgBuf = 2 * kDwgTile * kLdsPitch;  // one step: dY columns, then X columns
+constexpr int kDwgLds = 2 * kDwgBuf + 16 * kDwgTile * 4 + 16;
+
+__global__ __launch_bounds__(kDwgThreads) void dw_grouped_kernel(
+    const DwgDesc* __restrict__ descs, int G, int Wtot, float* __restrict__ slots,
+    float* __restrict__ talpha, uint32_t* __restrict__ tickets, int total_tiles) {
+  constexpr int BN = kDwgTile;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bn = wave / 3, bk = wave - 3 * bn;  // main 3 x 3 block of sub-tiles
+  const int tie = 6 + bn, tue = 6 + bk;         // extra sub-tile of block (2, 2)
+  const bool two = wave == 7;                   // wave 7: also sub-tile (8, 8)
+  const int r = lane & 15, g = lane >> 4;
+  const int nb = gridDim.x, blk = blockIdx.x;
+  const int beg = dwg_start(blk, nb, Wtot), end = dwg_start(blk + 1, nb, Wtot);
+  // LDS: two step buffers, the db column partials [16 row pairs][144], a flag
+  float* const s_db = reinterpret_cast<float*>(lds + 2 * kDwgBuf);
+  int* const s_flag = reinterpret_cast<int*>(lds + 2 * kDwgBuf + 16 * kDwgTile * 4);
+  float* const fl = reinterpret_cast<float*>(lds);  // epilogue scratch (step buffers free)
+  // loader units (2 rows x 4 columns of each operand): unit tid, and for wave 0 also unit
+  // 512 + tid (576 units per operand)
+  const bool u2 = wave == 0;
+  const int rp0 = threadIdx.x & 15, cq0 = 4 * (threadIdx.x >> 4);
+  const int cq1 = 128 + cq0;  // the second unit (wave 0): same row pair, columns 128..143
+
+  int gi = 0;  // the gemm holding `beg`
+  {
+    int lo = 0, hi = G - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (descs[mid].work0 <= beg) lo = mid;
+      else hi = mid - 1;
+    }
+    gi = lo;
+  }
+
+  auto put = [&](unsigned char* base, int col, const f32x4& r0, const f32x4& r1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float h0, h1, m0, m1, l0, l1;
+      const uint32_t ph = cvt2(r0[e], r1[e], h0, h1);
+      const float s0 = r0[e] - h0, s1 = r1[e] - h1;
+      const uint32_t pm = cvt2(s0, s1, m0, m1);
+      const uint32_t pl = cvt2(s0 - m0, s1 - m1, l0, l1);
+      unsigned char* cb = base + (col + e) * kLdsPitch + rp0 * 4;
+      *reinterpret_cast<uint32_t*>(cb) = ph;
+      *reinterpret_cast<uint32_t*>(cb + 64) = pm;
+      *reinterpret_cast<uint32_t*>(cb + 128) = pl;
+    }
+  };
+  auto frag = [&](const unsigned char* base, int col, int plane) {
+    return *reinterpret_cast<const bf16x8*>(base + col * kLdsPitch + 64 * plane + 16 * g);
+  };
+
+  int pos = beg;
+  while (pos < end) {
+    const DwgDesc& d = descs[gi];
+    const int tsteps = d.P * d.spp;
+    if (pos >= (int)d.work0 + tsteps * d.tiles) {
+      ++gi;
+      continue;
+    }
+    const int t = (pos - (int)d.work0) / tsteps;
+    const int T0 = (int)d.work0 + t * tsteps, T1 = T0 + tsteps;
+    const int send = end < T1 ? end : T1;
+    const int N = d.N, K = d.K, Mp = d.Mp, spp = d.spp;
+    const int tn = t / d.tiles_k, tk = t - tn * d.tiles_k;
+    const int n0 = tn * kDwgTile, k0 = tk * kDwgTile;
+    const bool has_al = d.W != nullptr;
+    const bool do_db = d.db != nullptr && tk == 0;
+    const float a = has_al ? effective_alpha(d.alpha, d.alpha_raw) : 1.0f;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(d.W, has_al ? (int64_t)N * K * 4 : 0);
+    auto pass_bits = [&](int p) {
+      const int b = d.pass_bits ? d.pass_bits[p] : d.bits;
+      return b == 1 ? 1 : 2;
+    };
+
+    f32x4 acc[3][3], acce[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acce[0] = acce[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fn(accumulator, sub-tile row ti, sub-tile column tu) for every sub-tile of this wave
+    auto for_tiles = [&](auto&& fn) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int u = 0; u < 3; ++u) fn(acc[i][u], 3 * bn + i, 3 * bk + u);
+      fn(acce[0], tie, tue);
+      if (two) fn(acce[1], 8, 8);
+    };
+    // byte offset of element (reg 0) of this lane in sub-tile (ti, tu): row 16 ti + 4g + reg,
+    // column 16 tu + r (D[row = 4g + reg][col = r]); formed from an opaque lane id where used
+    auto elem_base = [&]() {
+      const int ln = opaque(lane);
+      return ((n0 + 4 * (ln >> 4)) * K + k0 + (ln & 15)) * 4;
+    };
+    float aprod = 0.0f;
+    // sum over this wave's elements of acc * (term_b1(W/a) - term_b2(W/a)) (b2 = 0: none)
+    auto alpha_dot = [&](int b1, int b2) {
+      const int eb = elem_base();
+      for_tiles([&](f32x4& ac, int ti, int tu) {
+        float w[4];
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+          w[reg] = ld_f32(rw, eb + ((16 * ti + reg) * K + 16 * tu) * 4);
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const float wa = w[reg] / a;
+          aprod += ac[reg] * (alpha_term(wa, b1) - (b2 ? alpha_term(wa, b2) : 0.0f));
+        }
+      });
+    };
+    // db: each thread sums its units' columns into thread-private LDS slots
+    f32x4* const db0 = reinterpret_cast<f32x4*>(s_db + rp0 * kDwgTile + cq0);
+    f32x4* const db1 = reinterpret_cast<f32x4*>(s_db + rp0 * kDwgTile + cq1);
+
+    __syncthreads();  // the previous segment's epilogue scratch is free
+    if (do_db) {
+      *db0 = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (u2) *db1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    int j = pos - T0;
+    const int j1 = send - T0;
+    while (j < j1) {
+      // one pass piece: rows [r0, r1) of pass p
+      const int p = j / spp;
+      const int je = j1 < (p + 1) * spp ? j1 : (p + 1) * spp;
+      const int r0 = p * Mp + (j - p * spp) * kStepRows;
+      const int rl = p * Mp + (je - p * spp) * kStepRows;
+      const int r1 = rl < (p + 1) * Mp ? rl : (p + 1) * Mp;
+      const int steps = je - j;
+      const __amdgpu_buffer_rsrc_t ry =
+          make_rsrc(d.dY + (int64_t)r0 * N, (int64_t)(r1 - r0) * N * 4);
+      const __amdgpu_buffer_rsrc_t rx =
+          make_rsrc(d.X + (int64_t)r0 * K, (int64_t)(r1 - r0) * K * 4);
+      // the second unit through descriptors of length 0 outside wave 0: those loads return 0
+      // without touching memory, and every wave issues the same loads (a wave-dependent load
+      // count made the compiler wait for all of them at every step)
+      const __amdgpu_buffer_rsrc_t ry2 = u2 ? ry : make_rsrc(d.dY, 0);
+      const __amdgpu_buffer_rsrc_t rx2 = u2 ? rx : make_rsrc(d.X, 0);
+      const int yv0 = (2 * rp0 * N + n0 + cq0) * 4, xv0 = (2 * rp0 * K + k0 + cq0) * 4;
+      struct Raw {
+        f32x4 y[2][2];  // [unit][row]
+        f32x4 x[2][2];
+      };
+      auto load = [&](Raw& raw, int step) {
+        const int soy = step * kStepRows * N * 4, sox = step * kStepRows * K * 4;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // (row offset in soffset)
+          raw.y[0][i] = __builtin_amdgcn_raw_buffer_load_b128(ry, yv0, soy + i * N * 4, 0);
+          raw.x[0][i] = __builtin_amdgcn_raw_buffer_load_b128(rx, xv0, sox + i * K * 4, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          raw.y[1][i] = __builtin_amdgcn_raw_buffer_load_b128(ry2, yv0 + 512, soy + i * N * 4, 0);
+          raw.x[1][i] = __builtin_amdgcn_raw_buffer_load_b128(rx2, xv0 + 512, sox + i * K * 4, 0);
+        }
+      };
+      auto store = [&](const Raw& raw, int buf) {
+        unsigned char* base = lds + buf * kDwgBuf;
+        if (do_db) *db0 = *db0 + (raw.y[0][0] + raw.y[0][1]);
+        put(base, cq0, raw.y[0][0], raw.y[0][1]);
+        put(base, BN + cq0, raw.x[0][0], raw.x[0][1]);
+        if (u2) {
+          if (do_db) *db1 = *db1 + (raw.y[1][0] + raw.y[1][1]);
+          put(base, cq1, raw.y[1][0], raw.y[1][1]);
+          put(base, BN + cq1, raw.x[1][0], raw.x[1][1]);
+        }
+      };
+      auto compute = [&](int buf) {
+        const unsigned char* base = lds + buf * kDwgBuf;
+        bf16x8 bq[3][3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bq[u][q] = frag(base, BN + 48 * bk + 16 * u + r, q);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          bf16x8 aq[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) aq[q] = frag(base, 48 * bn + 16 * i + r, q);
+#pragma unroll
+          for (int pr = 0; pr < 6; ++pr)
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+              acc[i][u] = mfma_bf16(aq[kProdA[pr]], bq[u][kProdB[pr]], acc[i][u]);
+        }
+        bf16x8 ae[3], be[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ae[q] = frag(base, 16 * tie + r, q);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) be[q] = frag(base, BN + 16 * tue + r, q);
+#pragma unroll
+        for (int pr = 0; pr < 6; ++pr) acce[0] = mfma_bf16(ae[kProdA[pr]], be[kProdB[pr]], acce[0]);
+        if (two) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) be[q] = frag(base, BN + 16 * 8 + r, q);
+#pragma unroll
+          for (int pr = 0; pr < 6; ++pr)
+            acce[1] = mfma_bf16(ae[kProdA[pr]], be[kProdB[pr]], acce[1]);
+        }
+      };
+      // Every phase issues its loads unconditionally: steps past the piece read zeros through
+      // the descriptors' range check (no memory traffic). With the loads conditional the
+      // compiler's wait counts had to cover the path without them, and each store then
+      // waited for the NEXT step's loads too (one step of prefetch instead of two).
+      auto phase = [&](int cb, Raw& nxt, int sb, bool do_store, int ld_step) {
+        compute(cb);
+        (void)do_store;  // (the last phase stores the zeros read past the piece: never read)
+        store(nxt, sb);
+        load(nxt, ld_step);
+      };
+      Raw ra, rb;
+      load(ra, 0);
+      load(rb, 1);
+      store(ra, 0);
+      load(ra, 2);
+      __syncthreads();
+      // an even number of steps (an odd piece ends with a step of zeros: adds nothing), so
+      // the loop body has no exit between its two phases (with one, the compiler's wait
+      // counts at the loop head had to cover that path and waited for the next step's loads)
+      for (int s = 0; s < steps; s += 2) {
+        phase(0, rb, 1, true, s + 3);
+        __syncthreads();
+        phase(1, ra, 0, true, s + 4);
+        __syncthreads();
+      }
+      if (has_al) {
+        const int bp = pass_bits(p);
+        if (je == j1) {
+          alpha_dot(bp, 0);
+        } else {
+          const int bq = pass_bits(p + 1);
+          if (bq != bp) alpha_dot(bp, bq);
+        }
+      }
+      j = je;
+    }
+
+    // block sums of db and of the alpha partial (fixed order through LDS)
+    const int tid = opaque((int)threadIdx.x);
+    const int ln = tid & 63;
+    if (has_al) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) aprod += __shfl_xor(aprod, off, 64);
+      if (ln == 0) fl[wave] = aprod;
+    }
+    __syncthreads();
+    float dbv = 0.0f, ap = 0.0f;
+    if (do_db && tid < kDwgTile) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dbv += s_db[q * kDwgTile + tid];
+    }
+    if (has_al && tid == 0) {
+      for (int w = 0; w < kDwgWaves; ++w) ap += fl[w];
+    }
+    // slab offset of sub-tile (ti, tu) for this lane: [ti][tu][lane] f32x4
+    auto slab_off = [&](int ti, int tu) { return ((ti * 9 + tu) * 64) * 16; };
+
+    bool finish = pos == T0 && send == T1;  // the whole tile is this block's
+    if (!finish) {
+      // publish this segment's slab
+      const int nsl = dwg_owner(T1 - 1, nb, Wtot) - dwg_owner(T0, nb, Wtot) + 1;
+      float* slab = slots + (int64_t)(2 * blk + (beg >= T0 ? 0 : 1)) * kDwgSlotF;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(slab, (int64_t)kDwgSlotF * 4);
+      for_tiles([&](f32x4& ac, int ti, int tu) {
+        __builtin_amdgcn_raw_buffer_store_b128(ac, rs, ln * 16, slab_off(ti, tu), kSc1);
+      });
+      if (do_db && tid < kDwgTile)
+        __hip_atomic_store(slab + kDwgDb + tid, dbv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (has_al && tid == 0)
+        __hip_atomic_store(slab + kDwgAl, ap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+      __syncthreads();
+      if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(tickets + d.tile0 + t, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = old == (uint32_t)(nsl - 1);
+      }
+      __syncthreads();
+      finish = *s_flag != 0;
+      if (finish) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below
+        // sum the segments' slabs in block order (own slab included: read back)
+        const int bf = dwg_owner(T0, nb, Wtot);
+        dbv = 0.0f;
+        ap = 0.0f;
+        for (int q = 0; q < nsl; ++q) {
+          const int bb = bf + q;
+          const float* sl =
+              slots + (int64_t)(2 * bb + (dwg_start(bb, nb, Wtot) >= T0 ? 0 : 1)) * kDwgSlotF;
+          const __amdgpu_buffer_rsrc_t rl = make_rsrc(sl, (int64_t)kDwgSlotF * 4);
+          for_tiles([&](f32x4& ac, int ti, int tu) {
+            const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rl, ln * 16, slab_off(ti, tu), kSc1);
+            ac = q == 0 ? v : ac + v;
+          });
+          if (do_db && tid < kDwgTile) {
+            const float v =
+                __hip_atomic_load(sl + kDwgDb + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dbv = q == 0 ? v : dbv + v;
+          }
+          if (has_al && tid == 0) {
+            const float v =
+                __hip_atomic_load(sl + kDwgAl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ap = q == 0 ? v : ap + v;
+          }
+        }
+        if (tid == 0)
+          __hip_atomic_store(tickets + d.tile0 + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (finish) {
+      // dW = G * 1[|W/a| <= 1] (quant.py:80-82; dense: G)
+      const __amdgpu_buffer_rsrc_t rd = make_rsrc(d.dW, (int64_t)N * K * 4);
+      const int eb = elem_base();
+      for_tiles([&](f32x4& ac, int ti, int tu) {
+        float w[4];
+        if (has_al) {
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            w[reg] = ld_f32(rw, eb + ((16 * ti + reg) * K + 16 * tu) * 4);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          float v = ac[reg];
+          if (has_al) v *= ste_indicator(w[reg] / a);
+          st_f32(v, rd, eb + ((16 * ti + reg) * K + 16 * tu) * 4);
+        }
+      });
+      if (do_db && tid < kDwgTile) d.db[n0 + tid] = dbv;
+      if (has_al && tid == 0) {
+        const float chain = alpha_chain(d.alpha, d.alpha_raw);
+        if (d.tiles == 1) {
+          *d.dalpha = ap * chain;
+        } else {
+          __hip_atomic_store(talpha + d.tile0 + t, ap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          uint32_t* gt = tickets + total_tiles + gi;
+          const uint32_t old =
+              __hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (old == (uint32_t)(d.tiles - 1)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float s2 = 0.0f;
+            for (int q = 0; q < d.tiles; ++q)
+              s2 += __hip_atomic_load(talpha + d.tile0 + q, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+            *d.dalpha = s2 * chain;
+            __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+    }
+    pos = send;
+  }
+}
+
+constexpr int kDwgChunk = 16;
+struct DwgChunk {
+  DwgDesc d[kDwgChunk];
+};
+__global__ void dwg_table_kernel(DwgDesc* table, int off, int n, DwgChunk c) {
+  if ((int)threadIdx.x < n) table[off + threadIdx.x] = c.d[threadIdx.x];
+}
+
+
 }  // namespace
 
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K) { return plan_dw_passes(1, M, N, K); }
@@ -1007,6 +1433,32 @@ void launch_dw_finish_table(const DwFinishEntry* table, int n, int64_t total_blo
   if (n <= 0 || total_blocks <= 0) return;
   hipLaunchKernelGGL(dw_finish_table_kernel, dim3((unsigned)total_blocks), dim3(kThreads), 0, s,
                      table, n, total_blocks);
+}
+
+int dwg_blocks(int64_t total_steps) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  return (int)(total_steps < cus ? total_steps : cus);
+}
+
+size_t dwg_slot_bytes() { return sizeof(float) * (size_t)kDwgSlotF; }
+
+void launch_dw_grouped(const DwgDesc* host_descs, int G, int64_t total_steps, int blocks,
+                       DwgDesc* table, float* slots, float* talpha, uint32_t* tickets,
+                       int total_tiles, hipStream_t s) {
+  // the descriptors reach the device as kernel arguments (capture-safe: no host copy)
+  for (int off = 0; off < G; off += kDwgChunk) {
+    DwgChunk c{};
+    const int n = G - off < kDwgChunk ? G - off : kDwgChunk;
+    for (int i = 0; i < n; ++i) c.d[i] = host_descs[off + i];
+    hipLaunchKernelGGL(dwg_table_kernel, dim3(1), dim3(kDwgChunk), 0, s, table, off, n, c);
+  }
+  hipLaunchKernelGGL(dw_grouped_kernel, dim3((unsigned)blocks), dim3(kDwgThreads),
+                     (size_t)kDwgLds, s, table, G, (int)total_steps, slots,
+                     talpha, tickets, total_tiles);
 }
 
 void launch_dw_finish_group(const DwFinish* a, int n, hipStream_t s) {

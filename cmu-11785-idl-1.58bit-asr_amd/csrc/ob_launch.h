@@ -233,6 +233,33 @@ void launch_dw_partial_group_defer(const float* const* dY, int G, const float* X
                                    DwFinishEntry* table, int slot, const DwFinishEntry* ent,
                                    hipStream_t s);
 
+// Grouped deferred dW (dw.hip, ob_dw_grouped): one descriptor per weight gradient; the host
+// fills the work-space fields (work0 .. tile0) and the launcher copies the table to the device.
+struct DwgDesc {
+  const float* dY;
+  const float* X;
+  const float* W;  // nullptr: dense
+  const float* alpha;
+  const int* pass_bits;
+  float* dW;
+  float* db;
+  float* dalpha;
+  int64_t work0;  // first linear step (32 rows of one 144 x 144 tile) of this gemm
+  int N, K, Mp, P, alpha_raw, bits;
+  int spp;      // 32-row steps per pass
+  int tiles_k;  // K / 144
+  int tiles;    // (N / 144) * tiles_k
+  int tile0;    // first tile index (tile tickets, tile alpha slots)
+};
+constexpr int kDwgTile = 144;
+int dwg_blocks(int64_t total_steps);  // one block per CU (at most total_steps)
+size_t dwg_slot_bytes();              // one partial slab (tile + db + alpha)
+// table: device [G] descriptors; slots: 2 * blocks slabs; talpha: [total tiles] floats;
+// tickets: [total tiles + G] zeroed words (left zero)
+void launch_dw_grouped(const DwgDesc* host_descs, int G, int64_t total_steps, int blocks,
+                       DwgDesc* table, float* slots, float* talpha, uint32_t* tickets,
+                       int total_tiles, hipStream_t s);
+
 // dgemm.hip (dense exact-fp32 GEMM of the pointwise convs): false = shape not taken
 bool dense_gemm_supported(int64_t K, int64_t N);
 // Optional residual epilogue: C = R + dropout(A W^T + b) (R [M][N], the flat index

@@ -155,6 +155,10 @@ SIGNATURES = {
         _int, [_i64, _c_f, _c_f, _i64, _i64, _i64, _i64, _c_f, _c_f, _int, _c_f, _c_f, _c_f, _c_f,
                _c_f, _sz, _c_f, _i64, _i64, _c_f, _c_f]),
     "ob_dw_finish_table": (_int, [_c_f, _i64, _i64, _c_f]),
+    "ob_dw_grouped_supported": (_int, [_i64, _i64]),
+    "ob_dw_grouped_workspace": (_sz, [_c_f, _i64]),
+    "ob_dw_grouped_tickets": (_sz, [_c_f, _i64]),
+    "ob_dw_grouped": (_int, [_c_f, _i64, _c_f, _sz, _c_f, _sz, _c_f]),
     "ob_dense_dw_defer": (_int, [_c_f, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _sz, _c_f, _i64,
                                  _i64, _c_f, _c_f]),
     "ob_layernorm_bwd_workspace": (_sz, [_i64, _i64]),

@@ -31,6 +31,7 @@ pending entries instead of launching them.
 """
 from __future__ import annotations
 
+import ctypes
 from contextlib import contextmanager
 from typing import Dict, List, Optional
 
@@ -39,10 +40,21 @@ import torch
 from . import _lib
 
 __all__ = ["scope", "note", "can_defer", "dw_slot", "ln_slot", "ln_done", "cm_slot", "keep",
-           "add_grad_after_flush", "active"]
+           "add_grad_after_flush", "active", "dwg_take"]
 
 _ON = True  # parity-test hook (tests/test_stacked_step_gpu.py: False = finish on the spot)
+_DWG = True  # grouped dW launch (ob_dw_grouped); tests flip it to compare with per-layer dW
 _CAP = 512  # table entries per kind
+_TICKETS = 1 << 16  # ob_dw_grouped ticket words per device (zeroed once, left zero by every launch)
+
+
+class DwgGemm(ctypes.Structure):
+    """ob_dwg_gemm (include/onebit_hip.h)."""
+    _fields_ = [("dY", ctypes.c_void_p), ("X", ctypes.c_void_p), ("W", ctypes.c_void_p),
+                ("alpha", ctypes.c_void_p), ("pass_bits", ctypes.c_void_p),
+                ("dW", ctypes.c_void_p), ("db", ctypes.c_void_p), ("dalpha", ctypes.c_void_p),
+                ("N", ctypes.c_int64), ("K", ctypes.c_int64), ("M", ctypes.c_int64),
+                ("P", ctypes.c_int64), ("alpha_raw", ctypes.c_int32), ("bits", ctypes.c_int32)]
 
 
 class _State:
@@ -60,6 +72,7 @@ class _State:
         self.cm_n = 0
         self.cm_nmax = 0
         self.refs: List[torch.Tensor] = []
+        self.dwg: List[DwgGemm] = []  # weight gradients for the grouped launch
         self.post: List[tuple] = []  # (param, src): param.grad += src after the tables
         self.stream: Optional[int] = None
         self.dev: Optional[int] = None
@@ -127,7 +140,8 @@ def _tables(dev: torch.device):
         dw = torch.zeros((_CAP * lib.ob_dw_finish_entry_bytes(),), dtype=torch.uint8, device=dev)
         ln = torch.zeros((_CAP * lib.ob_ln_param_entry_bytes(),), dtype=torch.uint8, device=dev)
         cm = torch.zeros((_CAP * lib.ob_cm_wgrad_entry_bytes(),), dtype=torch.uint8, device=dev)
-        t = (dw, ln, cm)
+        tk = torch.zeros((_TICKETS,), dtype=torch.int32, device=dev)
+        t = (dw, ln, cm, tk)
         _S.tables[idx] = t
     return idx, t
 
@@ -147,7 +161,7 @@ def dw_slot(dev: torch.device, stream: int, n: int = 1):
     if _S.dw_n + n > _CAP:
         return None
     _begin(dev, stream)
-    _, (dw, _, _) = _tables(dev)
+    _, (dw, _, _, _) = _tables(dev)
     return dw.data_ptr(), _S.dw_n, _S.dw_blocks
 
 
@@ -163,7 +177,7 @@ def ln_slot(dev: torch.device, stream: int, d: int, n: int = 1):
     if _S.ln_n + n > _CAP:
         return None
     _begin(dev, stream)
-    _, (_, ln, _) = _tables(dev)
+    _, (_, ln, _, _) = _tables(dev)
     return ln.data_ptr(), _S.ln_n
 
 
@@ -178,7 +192,7 @@ def cm_slot(dev: torch.device, stream: int):
     if _S.cm_n + 1 > _CAP:
         return None
     _begin(dev, stream)
-    _, (_, _, cm) = _tables(dev)
+    _, (_, _, cm, _) = _tables(dev)
     return cm.data_ptr(), _S.cm_n
 
 
@@ -188,11 +202,40 @@ def cm_done(n_out: int) -> None:
     _S.cm_nmax = max(_S.cm_nmax, n_out)
 
 
+def dwg_take(dy, x, P, m, n, k, gw, gb, stream, weight, bias, alpha=None, ga=None,
+             pass_bits=None, bits=2) -> bool:
+    """Queue one weight gradient for the grouped launch at the end of the backward
+    (ob_dw_grouped: every queued dW of the backward in ONE persistent launch). A BitLinear's
+    when ``alpha`` is given (dW with the STE mask, dalpha at pass_bits[p] -- or ``bits`` -- for
+    the rows p*m .. p*m+m-1, db), else a dense linear's (dW, db). False: not taken (the
+    parameters cannot be deferred, or the shape is off the grouped kernel): finish here."""
+    if not (_DWG and _ON and _S.active):
+        return False
+    params = (weight, alpha, bias) if alpha is not None else (weight, bias)
+    if not can_defer(*params) or not all(p.requires_grad for p in params if p is not None):
+        return False  # (a gradient autograd drops would be freed before the launch writes it)
+    lib = _lib.load()
+    if (not lib.ob_dw_grouped_supported(n, k) or m < 1 or not 1 <= P <= 4
+            or dy.data_ptr() % 16 or x.data_ptr() % 16
+            or not dy.is_contiguous() or not x.is_contiguous()):
+        return False
+    _begin(dy.device, stream)
+    _tables(dy.device)
+    _S.dwg.append(DwgGemm(dy.data_ptr(), x.data_ptr(),
+                          weight.data_ptr() if alpha is not None else None,
+                          _lib.ptr(alpha), _lib.ptr(pass_bits), gw.data_ptr(), _lib.ptr(gb),
+                          _lib.ptr(ga), n, k, m, P, 1, bits))
+    # the inputs stay allocated until the launch; the outputs are NOT referenced here: an extra
+    # reference would make AccumulateGrad install a copy (unwritten) instead of the tensor
+    keep(dy, x, pass_bits)
+    return True
+
+
 def dense_dw(g2, x2d, m, n, k, gw, gb, ws, wsb, stream, weight, bias) -> None:
     """ob_dense_dw (full-precision weight gradient on the dW kernels), its finish deferred
-    when the parameters qualify."""
-    import ctypes
-
+    when the parameters qualify; queued for the grouped launch when its shape allows."""
+    if dwg_take(g2, x2d, 1, m, n, k, gw, gb, stream, weight, bias):
+        return
     lib = _lib.load()
     slot = dw_slot(g2.device, stream) if can_defer(weight, bias) else None
     if slot is not None:
@@ -225,7 +268,20 @@ def _flush() -> None:
         _S.reset()
         return
     lib = _lib.load()
-    dw, ln, cm = _S.tables[_S.dev]
+    dw, ln, cm, tk = _S.tables[_S.dev]
+    if _S.dwg:
+        n = len(_S.dwg)
+        arr = (DwgGemm * n)(*_S.dwg)
+        ad = ctypes.addressof(arr)
+        wsb = lib.ob_dw_grouped_workspace(ad, n)
+        need = lib.ob_dw_grouped_tickets(ad, n)
+        if not wsb or need > tk.numel():
+            raise _lib.OneBitHipError(f"ob_dw_grouped: {n} gradients do not fit "
+                                      f"(workspace {wsb}, tickets {need} > {tk.numel()})")
+        ws = torch.empty((wsb,), dtype=torch.uint8, device=tk.device)
+        _lib.check(lib.ob_dw_grouped(ad, n, ws.data_ptr(), wsb, tk.data_ptr(), tk.numel(),
+                                     _S.stream), "ob_dw_grouped")
+        keep(ws)
     if _S.dw_n:
         _lib.check(lib.ob_dw_finish_table(dw.data_ptr(), _S.dw_n, _S.dw_blocks, _S.stream),
                    "ob_dw_finish_table")

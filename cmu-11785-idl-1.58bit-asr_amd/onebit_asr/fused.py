@@ -161,6 +161,9 @@ def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream, bias=
         deferred.dense_dw(dy, x, P * m, n, k, gw, gb, ws, wsb, stream, weight, bias)
         return gw, None, gb
     ga = torch.empty((), dtype=torch.float32, device=dy.device)
+    if pb is not None and deferred.dwg_take(dy, x, P, m, n, k, gw, gb, stream, weight, bias,
+                                            alpha=alpha, ga=ga, pass_bits=pb):
+        return gw, ga, gb  # computed by the grouped launch at the end of the backward
     slot = (deferred.dw_slot(dy.device, stream)
             if pb is not None and deferred.can_defer(weight, alpha, bias) else None)
     if slot is not None:
@@ -367,7 +370,15 @@ class _QKVFn(torch.autograd.Function):
                     a.data_ptr(), c.dx_raw, None, k, gh.data_ptr(), 1.0, 0.0, None, 0, None, 0,
                     gh.data_ptr(), stream), "ob_bitlinear_fwd_residual (dX accumulate)")
         grads = {}
-        if _DW_GROUP and pb is not None and len(layers) == 3 and not codes[0].dense and \
+        if pb is not None and not codes[0].dense:  # the grouped launch at the end of the backward
+            for g, w, a, c, hb in layers:
+                b = ctx.biases[[id(t) for t in (wq, wk, wv)].index(id(w))]
+                o = (torch.empty_like(w), torch.empty((), dtype=torch.float32, device=h.device),
+                     torch.empty((w.shape[0],), dtype=torch.float32, device=h.device) if hb else None)
+                if deferred.dwg_take(g, h, P, m, w.shape[0], k, o[0], o[2], stream, w, b, alpha=a,
+                                     ga=o[1], pass_bits=pb):
+                    grads[id(w)] = o
+        if _DW_GROUP and not grads and pb is not None and len(layers) == 3 and not codes[0].dense and \
                 len({w.shape for _, w, _, _, _ in layers}) == 1:
             # the three dW GEMMs share X = h: their finishes in one launch
             n = layers[0][1].shape[0]

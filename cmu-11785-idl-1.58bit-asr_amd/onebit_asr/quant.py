@@ -331,6 +331,9 @@ class _BitLinearPassesFn(torch.autograd.Function):
             gw = torch.empty_like(weight)
             galpha = torch.empty((), dtype=torch.float32, device=gy.device)
             gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            if deferred.dwg_take(gy, x2d, P, m, n, k, gw, gb, stream, weight, ctx.bias,
+                                 alpha=alpha, ga=galpha, pass_bits=pass_bits):
+                return gx, gw, galpha, gb, None, None, None, None, None, None
             ws_bytes = lib.ob_bitlinear_bwd_dw_passes_workspace(P, m, n, k)
             ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=gy.device)
             slot = (deferred.dw_slot(gy.device, stream)

@@ -389,6 +389,34 @@ OB_API int ob_bitlinear_bwd_dw_passes_group_defer(
     void* stream);
 OB_API int ob_dw_finish_table(const void* table, int64_t n, int64_t total_blocks, void* stream);
 
+/* Grouped deferred weight gradients. Every weight gradient of a backward whose N and K are
+ * multiples of 144 -- a BitLinear's (autograd of quant.py:126 through quant.py:72-92: dW with
+ * the STE mask, dalpha at each stacked pass's bitwidth, db) or a dense linear's (W == NULL:
+ * dW = dY^T X, db) -- computed in ONE persistent launch after the backward (the reference reads
+ * parameter gradients only after loss.backward(), train.py:104-111), instead of one split-M
+ * launch per layer plus the finish table. Rows of pass p are rows p*M .. p*M+M-1 of dY and X.
+ * `gemms` is a HOST array of G descriptors (device pointers inside). `tickets`: a caller-owned
+ * device buffer of ob_dw_grouped_tickets(...) uint32 words, all zero before the first call;
+ * every call leaves it zero. Deterministic: fixed partition of the rows, fixed summation order.
+ * dY / X / W / alpha / pass_bits must stay valid until the launch has run. */
+typedef struct ob_dwg_gemm {
+  const float* dY;          /* [P*M][N] */
+  const float* X;           /* [P*M][K] */
+  const float* W;           /* [N][K] BitLinear weight; NULL = dense (no STE mask, no dalpha) */
+  const float* alpha;       /* BitLinear: 0-dim alpha (alpha_raw as ob_bitlinear_bwd_dw) */
+  const int32_t* pass_bits; /* DEVICE [P] bitwidths (1 or 2); NULL: `bits` for every pass */
+  float* dW;                /* [N][K] */
+  float* db;                /* [N] or NULL */
+  float* dalpha;            /* 0-dim (BitLinear; unused when W == NULL) */
+  int64_t N, K, M, P;       /* M = rows of one pass (>= 1), 1 <= P <= 4 */
+  int32_t alpha_raw, bits;
+} ob_dwg_gemm;
+OB_API int ob_dw_grouped_supported(int64_t N, int64_t K);
+OB_API size_t ob_dw_grouped_workspace(const ob_dwg_gemm* gemms, int64_t G);
+OB_API size_t ob_dw_grouped_tickets(const ob_dwg_gemm* gemms, int64_t G);
+OB_API int ob_dw_grouped(const ob_dwg_gemm* gemms, int64_t G, void* ws, size_t ws_bytes,
+                         void* tickets, size_t ticket_words, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * The decoder's attention core (onebit_asr/conformer.py:275-299: the stock
  * nn.TransformerDecoderLayer self- and cross-attention, torch's

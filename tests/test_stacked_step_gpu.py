@@ -84,6 +84,7 @@ def test_deferred_finishes_equal_immediate(gpu, monkeypatch):
     batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
     res = {}
     used = {}
+    monkeypatch.setattr(deferred, "_DWG", False)  # the per-layer dW GEMMs, finishes deferred
     for on in (False, True):
         monkeypatch.setattr(deferred, "_ON", on)
         torch.manual_seed(0)
@@ -188,3 +189,50 @@ def test_layernorm_pair_backward_matches_separate(gpu, monkeypatch):
         exact += int(torch.equal(a, b))
         assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-12, k
     print(f"bit-identical gradients: {exact} / {len(res[False])}")
+
+
+def test_grouped_dw_matches_immediate(gpu, monkeypatch):
+    """With the grouped launch (deferred._DWG, ob_dw_grouped) every qualifying weight gradient
+    of the stacked step -- the BitLinears and the 144-multiple dense linears -- is computed by
+    one launch at the end of the backward: the same products as the per-layer dW kernels in
+    another summation order, so every gradient equals the on-the-spot path within 2e-6 of
+    its max (alpha: 1e-4, biases 1e-5), the loss is identical, and the grouped launch took the gradients."""
+    from onebit_asr import deferred
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CFG1, synthetic_batch
+    from onebit_asr.train_step import OneBitStep
+
+    cfg = dict(CFG1, enc_d_model=144, enc_d_ff=576)
+    batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
+    res, losses, taken = {}, {}, {}
+    for on in (False, True):
+        monkeypatch.setattr(deferred, "_ON", on)
+        torch.manual_seed(0)
+        m = ConformerASR(80, 5004, **cfg).to(gpu)
+        step = OneBitStep(m, n_layers=2, stacked=True)
+        counts = []
+
+        def spy(orig=deferred._flush, counts=counts):
+            counts.append(len(deferred._S.dwg))
+            orig()
+
+        monkeypatch.setattr(deferred, "_flush", spy)
+        with deferred.scope():
+            loss, _ = step(batch, [1, 1])
+            loss.backward()
+        torch.cuda.synchronize()
+        taken[on] = max(counts, default=0)
+        losses[on] = loss.detach().clone()
+        res[on] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    assert taken[False] == 0 and taken[True] >= 2 * 9, taken
+    assert torch.equal(losses[False], losses[True])
+    assert res[False].keys() == res[True].keys()
+    scale = max(g.abs().max().item() for g in res[False].values())
+    for k in res[False]:
+        a, b = res[True][k], res[False][k]
+        if any(n in k for n in NOISE_ONLY):  # exact gradient 0: rounding noise only
+            assert (a - b).abs().max().item() <= 1e-6 * scale, k
+            continue
+        # alpha and bias gradients are cancellation-prone sums (over N*K products / rows)
+        bar = 1e-4 if k.endswith(".alpha") else 1e-5 if k.endswith("bias") else 2e-6
+        assert (a - b).abs().max().item() <= bar * b.abs().max().item() + 1e-12, k
