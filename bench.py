@@ -105,18 +105,115 @@ PASSES = 3
 PASS_BITS = [2, 1, 1]  # teacher, student, an SP pass at 1 bit
 
 
-def roofline(batch, frames, dev, reps=20, log=lambda m: None):
+def dwg_bitlinear_shapes(batch, frames):
+    """(N, K, M per pass, P, bitlinear) of the BitLinear weight gradients of one step: the
+    grouped launch's composition when no step has run (--roofline-only)."""
+    out = []
+    for _name, M, K, N, count in ql_shapes(batch, frames):
+        for _ in range(count):
+            out.append((N, K, M, PASSES, True, len(out)))
+    return out
+
+
+def roofline_dwg(dev, shapes, from_step, reps=5, log=lambda m: None, graph_replay=True):
+    """The grouped weight-gradient launch (ob_dw_grouped: every deferred dW of a backward in
+    ONE stream-K launch) with the composition the step's backward issued (deferred.LAST_DWG:
+    the BitLinear dWs with their STE mask / dalpha, plus the full-precision dWs of the same
+    launch), on fresh buffers (every gemm its own dY; X shared exactly where the step shares it,
+    q / k / v of one LayerNorm output). Timed with HIP events around graph-replayed
+    launches on the launch stream. Returns (us per launch, algorithmic bytes, FLOPs, MFMA
+    cycles summed over SIMDs, detail)."""
+    from onebit_asr import _lib, deferred
+
+    lib = _lib.load()
+    g = torch.Generator(device=dev).manual_seed(11)
+    pmax = max(sh[3] for sh in shapes)
+    bits_t = torch.tensor((PASS_BITS * pmax)[:pmax], dtype=torch.int32, device=dev)
+    keep, descs = [], []
+    by = fl = cyc = 0.0
+    n_bl = 0
+    t16 = lambda a: -(-a // 16)  # noqa: E731
+    t32 = lambda a: -(-a // 32)  # noqa: E731
+    xs = {}
+    for i, (N, K, M, P, bl, xid) in enumerate(shapes):
+        rows = P * M
+        if xid == i:  # q / k / v of one LN output share X, as in the step
+            xs[i] = torch.randn(rows, K, device=dev, generator=g)
+        X = xs[xid]
+        dY = torch.randn(rows, N, device=dev, generator=g)
+        dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+        W = alpha = da = None
+        if bl:
+            W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) * (2 / math.sqrt(K))
+            alpha, da = W.abs().mean(), torch.empty((), device=dev)
+            n_bl += 1
+        keep += [X, dY, dW, db, W, alpha, da]
+        descs.append(deferred.DwgGemm(dY.data_ptr(), X.data_ptr(), _lib.ptr(W), _lib.ptr(alpha),
+                                      bits_t.data_ptr() if bl else None, dW.data_ptr(),
+                                      db.data_ptr(), _lib.ptr(da), N, K, M, P, 1, 2))
+        # dY, X read; dW (and db) written; a BitLinear also reads W (STE mask, dalpha)
+        by += 4 * (rows * (N + K) + N * K * (2 if bl else 1) + N)
+        fl += 2.0 * rows * N * K
+        cyc += 16 * 6 * t16(N) * t16(K) * t32(rows)  # bf16x6: 6 16x16x32 MFMAs per block
+    G = len(descs)
+    arr = (deferred.DwgGemm * G)(*descs)
+    ad = ctypes.addressof(arr)
+    wsb = lib.ob_dw_grouped_workspace(ad, G)
+    nt = lib.ob_dw_grouped_tickets(ad, G)
+    if not wsb:
+        raise RuntimeError("roofline: grouped dW composition not supported")
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    tk = torch.zeros(nt, dtype=torch.int32, device=dev)
+    side = torch.cuda.Stream(dev)
+
+    def fn(s):
+        return lib.ob_dw_grouped(ad, G, ws.data_ptr(), wsb, tk.data_ptr(), nt, s)
+
+    log(f"roofline dw_grouped: {G} gemms ({n_bl} BitLinear)")
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            _lib.check(fn(side.cuda_stream), "roofline warm-up")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if graph_replay:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=side):
+                for _ in range(reps):
+                    fn(torch.cuda.current_stream(dev).cuda_stream)
+            graph.replay()
+            e0.record(side)
+            graph.replay()
+            e1.record(side)
+        else:  # eager launches (PMC passes: tools/dwg_bench.py)
+            e0.record(side)
+            for _ in range(reps):
+                _lib.check(fn(side.cuda_stream), "roofline dw_grouped")
+            e1.record(side)
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    detail = {"gemms": G, "bitlinear_gemms": n_bl, "us_per_launch": round(us, 1),
+              "composition": ("the step's backward (deferred.LAST_DWG)" if from_step else
+                              "the step's BitLinear dWs only (no step ran)")}
+    del keep
+    return us, by, fl, cyc, detail
+
+
+def roofline(batch, frames, dev, reps=20, log=lambda m: None, dwg_shapes=None):
     """Time each BitLinear kernel family at the step's stacked shapes with HIP events on the
     launch stream (kernels captured in a HIP graph and replayed, so the events bracket
-    device time, not Python launch gaps); the dominant family (largest time per step) is
-    reported against its roof. Algorithmic bytes / FLOPs per launch are counted for the P
-    passes one launch covers."""
+    device time, not Python launch gaps). The forward / dX ternary GEMMs are one family of
+    launches (272 a step); the weight gradients are ONE grouped launch a step (ob_dw_grouped,
+    timed at the composition the step issued). The line's roofline is the dominant KERNEL --
+    the one with the most time per step: the grouped dW launch whenever it takes more than the
+    whole ternary family would in one kernel's share, i.e. more than any single ternary launch
+    kind (roofline_fused) -- against its roof; both families are listed. Algorithmic bytes /
+    FLOPs per launch are counted for the P passes one launch covers."""
     from onebit_asr import _lib
     from onebit_asr.quant import pack_codes
 
     lib = _lib.load()
     P = PASSES
-    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0, 0.0], "dw_lds+dw_finish": [0.0, 0.0, 0.0, 0, 0.0]}
+    fam = {"ternary_gemm": [0.0, 0.0, 0.0, 0, 0.0], "dw_grouped": [0.0, 0.0, 0.0, 0, 0.0]}
     # fam value: [total_time_us_per_step, total_bytes_per_step, total_flops_per_step, launches,
     #             MFMA pipe cycles per step summed over SIMDs]
     detail = []
@@ -133,11 +230,6 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
         c1, c1t = pack_codes(W, alpha, 1)
         Y = torch.empty(P * M, N, device=dev)
         dX = torch.empty(P * M, K, device=dev)
-        dW = torch.empty(N, K, device=dev)
-        da = torch.empty((), device=dev)
-        db = torch.empty(N, device=dev)
-        wsb = lib.ob_bitlinear_bwd_dw_passes_workspace(P, M, N, K)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
         def fwd(s):
             return lib.ob_bitlinear_fwd_passes(X.data_ptr(), P, M, K, c2.data_ptr(), c1.data_ptr(),
@@ -148,12 +240,6 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
             return lib.ob_bitlinear_bwd_dx_passes(dY.data_ptr(), P, M, N, c2t.data_ptr(),
                                                   c1t.data_ptr(), bits_t.data_ptr(),
                                                   alpha.data_ptr(), 1, K, dX.data_ptr(), s)
-
-        def bdw(s):
-            return lib.ob_bitlinear_bwd_dw_passes(dY.data_ptr(), X.data_ptr(), P, M, N, K,
-                                                  W.data_ptr(), alpha.data_ptr(), 1,
-                                                  bits_t.data_ptr(), dW.data_ptr(), da.data_ptr(),
-                                                  db.data_ptr(), ws.data_ptr(), wsb, s)
 
         def timed(fn):
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -176,13 +262,10 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
         t_f = timed(fwd)
         log(f"roofline {name}: dx")
         t_dx = timed(bdx)
-        log(f"roofline {name}: dw")
-        t_dw = timed(bdw)
         cw = 4 * N * ((K + 15) // 16)
         rows = P * M
         by_f = 4 * (rows * K + rows * N + N) + 2 * cw      # X, Y, bias, codes (2 bitwidths)
         by_dx = 4 * (rows * N + rows * K) + 2 * cw          # dY, dX, codes_t
-        by_dw = 4 * (rows * N + rows * K + 2 * N * K + N)   # dY, X, W, dW, db
         fl = 2.0 * rows * K * N
         n_dx = 0 if name == "pos" else count  # pos_emb needs no input gradient
         # MFMA instructions the kernels issue: v_mfma_f32_16x16x32_bf16 (16 cycles per SIMD,
@@ -192,23 +275,21 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
         t32 = lambda a: -(-a // 32)  # noqa: E731
         cyc_f = 16 * 3 * t16(rows) * t16(N) * t32(K)
         cyc_dx = 16 * 3 * t16(rows) * t16(K) * t32(N)
-        cyc_dw = 16 * 6 * t16(N) * t16(K) * t32(rows)
         f = fam["ternary_gemm"]
         f[0] += count * t_f + n_dx * t_dx
         f[1] += count * by_f + n_dx * by_dx
         f[2] += (count + n_dx) * fl
         f[3] += count + n_dx
         f[4] += count * cyc_f + n_dx * cyc_dx
-        f = fam["dw_lds+dw_finish"]
-        f[0] += count * t_dw
-        f[1] += count * by_dw
-        f[2] += count * fl
-        f[3] += count
-        f[4] += count * cyc_dw
         detail.append({"layer": name, "M_per_pass": M, "passes": P, "K": K, "N": N,
                        "launches_per_step": count, "fwd_us": round(t_f, 2),
-                       "dx_us": round(t_dx, 2), "dw_us": round(t_dw, 2)})
-    dom = max(fam, key=lambda k: fam[k][0])
+                       "dx_us": round(t_dx, 2)})
+    shapes = dwg_shapes or dwg_bitlinear_shapes(batch, frames)
+    t_g, by_g, fl_g, cyc_g, det_g = roofline_dwg(dev, shapes, bool(dwg_shapes), log=log)
+    fam["dw_grouped"] = [t_g, by_g, fl_g, 1, cyc_g]
+    # the dominant kernel: one grouped dW launch vs the ternary family's launches (the
+    # largest single ternary launch kind is well below the family total)
+    dom = "dw_grouped" if t_g >= fam["ternary_gemm"][0] / 6 else "ternary_gemm"
     t_us, by, fl, n, cyc = fam[dom]
     avg_t = t_us / n
     gbs = (by / n) / (avg_t * 1e-6) / 1e9
@@ -245,7 +326,7 @@ def roofline(batch, frames, dev, reps=20, log=lambda m: None):
                  "bytes_per_launch": int(by / n), "flops_per_launch": int(fl / n),
                  "achieved_GBs": round(gbs, 1), "achieved_TFLOPs": round(tfs, 2),
                  "ql_kernel_ms_per_step": {k: round(v[0] / 1e3, 3) for k, v in fam.items()},
-                 "shapes": detail})
+                 "dw_grouped": det_g, "shapes": detail})
     return roof
 
 
@@ -970,7 +1051,10 @@ def main():
                            roofline_i8_train(args.batch, args.frames, dev,
                                              log=lambda m: log(args, m)))
     elif rank == 0 and world == 1 and not args.no_roofline:
-        roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m))
+        from onebit_asr import deferred
+
+        roof = roofline(args.batch, args.frames, dev, log=lambda m: log(args, m),
+                        dwg_shapes=list(deferred.LAST_DWG) or None)
         roof["traffic"] = traffic_from(args.traffic_json, roof["kernel"])
         # the same family as the step launches it (fused epilogues, dX accumulations)
         roof["in_step_fused"] = roofline_fused(args.batch, args.frames, dev,

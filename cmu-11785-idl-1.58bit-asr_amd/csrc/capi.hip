@@ -11,7 +11,7 @@ using namespace ob;
 
 namespace {
 
-constexpr int kAbiVersion = 2;
+constexpr int kAbiVersion = 3;  // 3 (round 5): ob_relattn_bwd takes saved_elems
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -1409,6 +1409,8 @@ size_t ob_relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d) {
   return align_up(relattn_bwd_workspace(Bt, T, H, d));
 }
 
+int ob_relattn_set_bwd_mode(int mode) { return relattn_set_flash(mode); }
+
 int64_t ob_relattn_probs_elems(int64_t Bt, int64_t T, int64_t H) {
   if (Bt < 1 || H < 1 || T < 1) return 0;
   return relattn_probs_elems(Bt, T, H);
@@ -1418,12 +1420,14 @@ int ob_relattn_bwd(const float* dctx, const float* ctx, const float* q, const fl
                    const float* v, const float* pos, const float* u, const float* vb,
                    const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H, int64_t d,
                    float p_drop, const int64_t* rng, int64_t rng_offset, const float* saved,
-                   float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb, void* ws,
-                   size_t ws_bytes, void* stream) {
+                   int64_t saved_elems, float* dq, float* dk, float* dv, float* dpos, float* du,
+                   float* dvb, void* ws, size_t ws_bytes, void* stream) {
   if (int st = relattn_check(Bt, P, T, H, d, p_drop)) return st;
   if (!dctx || !ctx || !q || !k || !v || !pos || !u || !vb || !lens || !saved || !dq || !dk ||
       !dv || !dpos || !du || !dvb || !ws)
     return OB_ERR_NULL;
+  // `saved` laid out under the other backward mode (ob_relattn_set_bwd_mode in between)
+  if (saved_elems != relattn_saved_elems(Bt, T, H, d)) return OB_ERR_SHAPE;
   (void)rng;  // the forward's keep decisions are in the saved state
   (void)rng_offset;
   if ((uintptr_t)saved & 15) return OB_ERR_ALIGN;

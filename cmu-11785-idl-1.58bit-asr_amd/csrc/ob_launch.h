@@ -433,6 +433,7 @@ bool relattn_supported(int64_t T, int64_t d);
 size_t relattn_bwd_workspace(int64_t Bt, int64_t T, int64_t H, int64_t d);
 int64_t relattn_probs_elems(int64_t Bt, int64_t T, int64_t H);
 int64_t relattn_saved_elems(int64_t Bt, int64_t T, int64_t H, int64_t d);
+int relattn_set_flash(int on);  // 0 / 1 sets the process-wide backward mode; returns the previous
 void launch_relattn_fwd(const float* q, const float* k, const float* v, const float* pos,
                         const float* u, const float* vb, const int* lens, int64_t Bt, int64_t P,
                         int64_t T, int64_t H, int64_t d, float p_drop, const uint64_t* rng,

@@ -33,6 +33,7 @@
 // rounded up to even (so the two keys of a pair share a row); the forward stores each kept
 // probability as P and each dropped one as -P (P >= 0, so the sign bit is free), and the
 // backward kernels read the keep bit back with the probability.
+#include <atomic>
 #include <math.h>
 
 #include <algorithm>
@@ -1714,15 +1715,31 @@ bool relattn_supported(int64_t T, int64_t d) {
 }
 
 // the flash-style backward (relattn_bwd_fused_kernel): T <= 256 (16 key tiles), d <= 36, when
-// selected (OB_ATTN_BWD=flash, read per call). It keeps every [T][T] quantity on chip but is
-// slower than the probability path at Conformer-S (measured 400 vs 253 us per call: one fat
-// block per (b, h) split in two, latency-bound chunk phases at 2 waves per SIMD; DESIGN.md
-// "Attention"), so the probability path stays the default.
-bool relattn_fused(int64_t T, int64_t d) {
-  if (!(T <= 256 && d <= 36)) return false;
-  const char* e = getenv("OB_ATTN_BWD");
-  return e && e[0] == 'f';
+// selected (OB_ATTN_BWD=flash). It keeps every [T][T] quantity on chip but is slower than the
+// probability path at Conformer-S (measured 400 vs 253 us per call: one fat block per (b, h)
+// split in two, latency-bound chunk phases at 2 waves per SIMD; DESIGN.md "Attention"), so the
+// probability path stays the default. The mode is process-wide: OB_ATTN_BWD read once (the
+// first query), then only ob_relattn_set_bwd_mode changes it. The saved buffer's layout, the
+// backward's work space and the backward kernel all follow it; ob_relattn_bwd checks the
+// caller's saved size against the layout of the current mode, so a backward never reads a
+// buffer the forward laid out under the other mode.
+static std::atomic<int> g_flash{-1};
+static bool flash_selected() {
+  int m = g_flash.load(std::memory_order_relaxed);
+  if (m < 0) {
+    const char* e = getenv("OB_ATTN_BWD");
+    int want = (e != nullptr && e[0] == 'f') ? 1 : 0;
+    g_flash.compare_exchange_strong(m, want);
+    m = g_flash.load(std::memory_order_relaxed);
+  }
+  return m == 1;
 }
+int relattn_set_flash(int on) {
+  const int prev = flash_selected() ? 1 : 0;
+  if (on == 0 || on == 1) g_flash.store(on, std::memory_order_relaxed);
+  return prev;
+}
+bool relattn_fused(int64_t T, int64_t d) { return T <= 256 && d <= 36 && flash_selected(); }
 
 // saved state of the forward for the backward (fp32 elements): row statistics
 // [Bt*H][Tp][2] (max, 1/sum) | keep bits [Bt*H][Tp][W] | then either (flash-style backward)

@@ -328,7 +328,14 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     if constexpr (BYTE) {
       u32x4 b4;
       code_bytes(word, b4);
-      if (idx < nwords) *reinterpret_cast<u32x4*>(smem + nl * stride + 16 * w) = b4;
+      // the byte image's row pitch (kpad + 8 bytes) makes odd rows 8-byte aligned only: two
+      // 8-byte stores (ds_write_b64), no reliance on unaligned-DS mode for a 16-byte one
+      if (idx < nwords) {
+        typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(8)));
+        u32x2a* dst = reinterpret_cast<u32x2a*>(smem + nl * stride + 16 * w);
+        dst[0] = u32x2a{b4[0], b4[1]};
+        dst[1] = u32x2a{b4[2], b4[3]};
+      }
       return;
     }
     u32x4 lo4, hi4;

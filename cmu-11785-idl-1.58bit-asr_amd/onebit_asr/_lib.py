@@ -200,7 +200,8 @@ SIGNATURES = {
     "ob_relattn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64]),
     "ob_relattn_bwd": (
         _int, [_c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _i64, _i64, _i64, _i64, _i64,
-               _f32, _c_f, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+               _f32, _c_f, _i64, _c_f, _i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_relattn_set_bwd_mode": (_int, [_int]),
     "ob_relattn_dropout_mask": (_int, [_i64, _i64, _f32, _c_f, _i64, _c_f, _c_f]),
     "ob_embedding_bwd": (_int, [_c_f, _i64, _c_f, _i64, _i64, _i64, _c_f, _c_f]),
     "ob_adamw_plan": (_i64, [_c_f, _i64, _c_f]),
@@ -210,7 +211,7 @@ SIGNATURES = {
                _sz, _c_f]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3  # 3 (round 5): ob_relattn_bwd takes saved_elems
 
 _lib = None
 
@@ -248,12 +249,23 @@ def check_digest(lib, expected: str | None = None) -> None:
     if expected is None:
         if os.environ.get("ONEBIT_HIP_LIB"):
             return
+        if not _sources_present():
+            # a packaged library without its sources: nothing to compare against
+            import warnings
+
+            warnings.warn(f"{LIB_PATH.name}: no csrc/ sources beside it; build digest not checked")
+            return
         expected = source_digest()
     got = lib.ob_source_digest().decode()
     if got != expected:
         raise OneBitHipError(
             f"{LIB_PATH.name} was built from other sources (digest {got[:12]} != {expected[:12]} "
             "of csrc/ and include/): rebuild with `make -C cmu-11785-idl-1.58bit-asr_amd/csrc`")
+
+
+def _sources_present() -> bool:
+    csrc = Path(__file__).resolve().parents[1] / "csrc"
+    return csrc.is_dir() and any(csrc.glob("*.hip"))
 
 
 def ptr_array(ptrs):

@@ -6,9 +6,11 @@ Reference: onebit_asr/conformer.py:115-127 (between MHSA's projections and out_p
 projection outputs in their natural [B, T, H*d] layout and returns the context in the
 layout out_proj consumes, with one forward kernel and one backward kernel (+ a small
 reduction); see csrc/relattn.hip. Gradients flow to q, k, v, pos, pos_bias_u, pos_bias_v.
-The forward saves only per-row softmax statistics and the dropout keep bits; for
-T <= 256 and d_head <= 36 (every Conformer call site) the backward is flash style and
-recomputes the probabilities on chip (no [B, H, T, T] tensor in HBM).
+By default the forward saves the softmax probabilities as MFMA-fragment tiles and the
+backward reads them. The flash-style backward (``set_backward_mode("flash")`` or
+``OB_ATTN_BWD=flash``; T <= 256 and d_head <= 36) saves only per-row softmax statistics, the
+dropout keep bits and a few rel_shift rows, and recomputes the probabilities on chip; it is
+slower at Conformer-S, hence opt-in.
 
 Dropout uses the kernels' counter-based hash of (seed, counter + offset): the device state
 and per-call host offsets are the fused BitLinear call sites' (fused._rng), whose counter
@@ -25,7 +27,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["rel_pos_attention", "fused_attention_supported", "dropout_mask", "probs_dense"]
+__all__ = ["rel_pos_attention", "fused_attention_supported", "dropout_mask", "probs_dense",
+           "set_backward_mode"]
 
 # device -> (rng tensor, offset) of the latest call with dropout (tests read the mask back)
 LAST_RNG: Dict[torch.device, Tuple[torch.Tensor, int]] = {}
@@ -79,12 +82,21 @@ class _RelAttnFn(torch.autograd.Function):
             lib.ob_relattn_bwd(g.data_ptr(), out.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), bt,
                                P, t, n_heads, d, p_drop, _lib.ptr(rng), rng_off, saved.data_ptr(),
-                               dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(),
+                               saved.numel(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(),
                                du.data_ptr(), dvb.data_ptr(), ws.data_ptr(), wsb,
                                _lib.stream_of(g)),
             "ob_relattn_bwd",
         )
         return dq, dk, dv, dpos, du, dvb, None, None, None, None, None
+
+
+def set_backward_mode(mode: str) -> str:
+    """'probs' (default) or 'flash': the process-wide attention backward (csrc/relattn.hip).
+    Returns the previous mode. A backward whose forward ran under the other mode raises."""
+    if mode not in ("probs", "flash"):
+        raise ValueError(f"mode must be 'probs' or 'flash', got {mode!r}")
+    prev = _lib.load().ob_relattn_set_bwd_mode(1 if mode == "flash" else 0)
+    return "flash" if prev == 1 else "probs"
 
 
 def rel_pos_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, pos: torch.Tensor,

@@ -46,6 +46,9 @@ _ON = True  # parity-test hook (tests/test_stacked_step_gpu.py: False = finish o
 _DWG = True  # grouped dW launch (ob_dw_grouped); tests flip it to compare with per-layer dW
 _CAP = 512  # table entries per kind
 _TICKETS = 1 << 16  # ob_dw_grouped ticket words per device (zeroed once, left zero by every launch)
+# (N, K, M, P, bitlinear, index of the first gemm with the same X) of every gemm of the latest
+# grouped launch (bench.py's roofline times a launch of the same composition)
+LAST_DWG: List[tuple] = []
 
 
 class DwgGemm(ctypes.Structure):
@@ -271,6 +274,8 @@ def _flush() -> None:
     dw, ln, cm, tk = _S.tables[_S.dev]
     if _S.dwg:
         n = len(_S.dwg)
+        xs = [g.X for g in _S.dwg]  # (q / k / v of one LN output share X)
+        LAST_DWG[:] = [(g.N, g.K, g.M, g.P, bool(g.W), xs.index(g.X)) for g in _S.dwg]
         arr = (DwgGemm * n)(*_S.dwg)
         ad = ctypes.addressof(arr)
         wsb = lib.ob_dw_grouped_workspace(ad, n)

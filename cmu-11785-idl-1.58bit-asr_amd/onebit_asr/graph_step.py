@@ -48,15 +48,28 @@ N > 1 (reference train.py:116-118 is single-device: loss.backward(), clip, step)
 * ``"flat"``: the gradient views of the flat buffer, one all-reduce after the backward.
 
 With RCCL the whole step (forward, backward, the exchange, update) is captured as one
-graph; if the process group cannot be captured (gloo) the exchange runs eagerly between
-graph A and the update graph. With N == 1 autograd's own gradient buffers are used as they
+graph; with gloo (host staging, not capturable) the exchange runs eagerly between graph A
+and the update graph. A failed RCCL capture raises: the communicator's state after a broken
+capture is not something to build on.
+
+The captured collectives run on a process group of their own (``capture_group``: the same
+ranks, a second RCCL communicator connected eagerly, before capture, by
+``eager_connect_single_device`` -- no collective). ProcessGroupNCCL's watchdog thread polls
+the completion event of every eager collective it is handed, and HIP refuses that query
+(hipErrorCapturedEvent, "operation not permitted on an event last recorded in a capturing
+stream") once the communicator's stream has joined a capture: an eager collective still on
+the watchdog's list when the capture starts (the warm-up steps' exchanges, the barrier)
+aborted the process in round 4. The capture group never runs an eager collective, so its
+watchdog never holds an event to query; the warm-up and the barrier use the caller's group.
+Captured collectives are not handed to the watchdog (torch skips ``workEnqueue`` while the
+stream captures). Capture also runs in ``thread_local`` error mode, so no other thread's
+call can invalidate it. With N == 1 autograd's own gradient buffers are used as they
 are (``p.grad = None`` before backward, so no accumulate kernels). Parameters that receive
 no gradient in the step are excluded from the optimizer exactly like the reference (AdamW
 skips grad=None).
 """
 from __future__ import annotations
 
-import time
 from typing import Dict, List, Optional
 
 import torch
@@ -142,7 +155,16 @@ class BucketedAllReduce:
 # into the step graph) at world size 1, so a single-GPU test can capture RCCL collectives
 # (tests/test_rccl_capture_gpu.py). Not read from the environment.
 _MULTI_RANK_PATH_AT_WORLD_1 = False
-_WATCHDOG_DRAIN_S = 2.0  # > the watchdog's poll interval (ProcessGroupNCCL: ~100 ms... 1 s)
+
+
+def capture_group(pg: dist.ProcessGroup, device: torch.device) -> dist.ProcessGroup:
+    """A second RCCL process group over ``pg``'s ranks for the collectives captured into the
+    step graph, its communicator connected now (no collective, so its watchdog never tracks
+    an eager event; module docstring). Every rank of ``pg`` calls this in the same order."""
+    ranks = dist.get_process_group_ranks(pg)
+    g = dist.new_group(ranks=ranks, backend="nccl", use_local_synchronization=True)
+    g._get_backend(device).eager_connect_single_device(device)
+    return g
 
 
 class GraphedTrainStep:
@@ -183,6 +205,7 @@ class GraphedTrainStep:
         self.flat_views: List[torch.Tensor] = []
         self.buckets: Optional[BucketedAllReduce] = None
         self.comm_in_graph = False
+        self.xpg = process_group  # the group the exchange's collectives run on
 
     # ------------------------------------------------------------------ setup
     def _set_batch(self, batch):
@@ -278,14 +301,14 @@ class GraphedTrainStep:
             # takes the average here (the fused one scales by 1/world)
             grads = [p.grad for p in self.params]
             torch.cat([g.reshape(-1) for g in grads], out=self.flat)
-            dist.all_reduce(self.flat, group=self.pg)
+            dist.all_reduce(self.flat, group=self.xpg)
             if not self.fused:
                 self.flat.div_(self.world)
             torch._foreach_copy_(grads, self.flat_views)
         elif overlapped:
             self.buckets.finish()
         else:
-            dist.all_reduce(self.flat, group=self.pg)
+            dist.all_reduce(self.flat, group=self.xpg)
 
     def _eager(self):
         ov = self.buckets is not None
@@ -370,31 +393,27 @@ class GraphedTrainStep:
         if self.multi and dist.get_backend(self.pg) == dist.Backend.NCCL:
             # the whole step in one graph with its exchange (bucketed: the all-reduces overlap
             # the backward); RCCL collectives capture into a graph, gloo's host staging does not
-            rng = self._rng_snapshot()  # (a failed attempt must not advance the dropout streams)
-            # the warm-up's collectives must have left the process group's watchdog before any
-            # collective is captured (it polls their events and may not touch captured ones)
+            # the captured collectives go to a group that has never run an eager one (module
+            # docstring: its watchdog holds no event HIP would refuse to query mid-capture)
+            self.xpg = capture_group(self.pg, self.device)
+            if self.buckets is not None:
+                self.buckets.pg = self.xpg
             torch.cuda.synchronize(self.device)
             dist.barrier(group=self.pg, device_ids=[self.device.index])
             torch.cuda.synchronize(self.device)
-            time.sleep(_WATCHDOG_DRAIN_S)
+            g = torch.cuda.CUDAGraph()
+            ov = self.buckets is not None
             try:
-                g = torch.cuda.CUDAGraph()
-                ov = self.buckets is not None
-                with torch.cuda.graph(g, pool=pool):
+                with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                     self.loss, self.parts = self._fwd_bwd(overlap=ov)
                     self._allreduce(overlapped=ov)
                     self._update()
-                self.graph_a, self.comm_in_graph = g, True
-            except Exception as e:  # the process group cannot be captured: exchange eagerly
-                import warnings
-
-                from .fused import rng_restore
-
-                warnings.warn(f"all-reduce capture failed ({e!r}); exchanging between graphs")
-                torch.cuda.synchronize(self.device)
-                rng_restore(self.device, rng[0])
-                torch.cuda.set_rng_state(rng[1], self.device)
-                self.comm_in_graph = False
+            except Exception as e:
+                raise RuntimeError("capturing the step with its RCCL exchange failed; the "
+                                   "communicator is not reused after a broken capture") from e
+            self.graph_a, self.comm_in_graph = g, True
+        else:
+            self.xpg = self.pg
         if not self.comm_in_graph:
             self.graph_a = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_a, pool=pool):

@@ -456,10 +456,13 @@ OB_API int ob_decattn_bwd(const float* dctx, const float* ctx, const float* q, i
  *           16-B aligned; NULL when no backward follows): row statistics [Bt*H][Tp][2]
  *           (max of the scaled masked scores, 1/sum; Tp = 16*ceil(T/16)), the dropout keep
  *           bits [Bt*H][Tp][W] (uint32, W = ceil(Tp/32), key j of row i = bit j%32 of word
- *           j/32), and for T > 256 or d = 64 the probability tiles below. For T <= 256 and
- *           d <= 36 the backward is flash style: it recomputes the probabilities of 32-query
- *           chunks from q, k, pos and the statistics (bitwise the forward's) and keeps every
- *           [T][T] quantity on chip.
+ *           j/32), then (default backward mode) the probability tiles below -- the
+ *           statistics region is reserved but not written -- or, in the flash backward mode
+ *           (ob_relattn_set_bwd_mode(1) or OB_ATTN_BWD=flash; only T <= 256 and d <= 36, other
+ *           shapes always take the probability tiles), the statistics, the keep bits and the
+ *           X rows below each 32-query chunk: that backward recomputes the probabilities of
+ *           32-query chunks (bitwise the forward's) and keeps every [T][T] quantity on chip.
+ *           It is slower at Conformer-S, hence opt-in.
  *   probs : optional (NULL: not written) MFMA-fragment tiles [Bt*H][nt][nt][64][4],
  *           nt = ceil(T/16), of the softmax before dropout (ob_relattn_probs_elems floats):
  *           tile (a, t), lane r + 16g, element e holds P[16a + r][16t + 4g + e] (rows / keys
@@ -486,9 +489,15 @@ OB_API int ob_relattn_bwd(const float* dctx, const float* ctx, const float* q, c
                           const float* v, const float* pos, const float* u, const float* vb,
                           const int32_t* lens, int64_t Bt, int64_t P, int64_t T, int64_t H,
                           int64_t d, float p_drop, const int64_t* rng, int64_t rng_offset,
-                          const float* saved,
+                          const float* saved, int64_t saved_elems,
                           float* dq, float* dk, float* dv, float* dpos, float* du, float* dvb,
                           void* ws, size_t ws_bytes, void* stream);
+/* The attention backward mode, process-wide: 0 = probability tiles (default), 1 = flash style
+ * (T <= 256, d <= 36); any other value only queries. Returns the previous mode. The initial
+ * mode is OB_ATTN_BWD (read once). ob_relattn_saved_elems / ob_relattn_bwd_workspace follow the
+ * current mode; ob_relattn_bwd returns OB_ERR_SHAPE when `saved_elems` (the size the forward's
+ * buffer was allocated with) is not the current mode's -- the mode changed in between. */
+OB_API int ob_relattn_set_bwd_mode(int mode);
 /* The dropout keep-mask (1 = kept) of n elements laid out in rows of row_len: the attention
  * kernels' mask of [rows][T] probabilities with row_len = T, the BitLinear / LayerNorm /
  * residual-dropout kernels' mask of a flat tensor with row_len = n. */

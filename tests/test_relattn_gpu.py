@@ -74,12 +74,21 @@ def _close(got, ref, rel, atol, what):
 @pytest.mark.parametrize("bwd", ["probs", "flash"])
 @pytest.mark.parametrize("bt,P,t,H,d,lens", CASES)
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_relattn_matches_reference(gpu, bt, P, t, H, d, lens, p, bwd, monkeypatch):
+def test_relattn_matches_reference(gpu, bt, P, t, H, d, lens, p, bwd):
     """bwd: the backward that reads the stored probabilities (default) or the flash-style one
-    (OB_ATTN_BWD=flash; T <= 256, d <= 36 -- other shapes take the probability path)."""
+    (set_backward_mode("flash"); T <= 256, d <= 36 -- other shapes take the probability path)."""
     from onebit_asr import attention as at
 
-    monkeypatch.setenv("OB_ATTN_BWD", "flash" if bwd == "flash" else "")
+    prev = at.set_backward_mode(bwd)
+    try:
+        _check_case(gpu, bt, P, t, H, d, lens, p)
+    finally:
+        at.set_backward_mode(prev)
+
+
+def _check_case(gpu, bt, P, t, H, d, lens, p):
+    from onebit_asr import attention as at
+
 
     q, k, v, pos, u, vb = _inputs(bt, P, t, H, d, seed=bt * 1000 + t)
     lens_t = torch.tensor(lens)
@@ -161,3 +170,22 @@ def test_mhsa_fused_matches_torch_path(gpu, monkeypatch):
     for a, b in zip(outs["fused"], outs["torch"]):
         err = (a - b).abs().max().item()
         assert err <= 1e-4 * b.abs().max().item() + 1e-6, err
+
+
+def test_backward_refuses_saved_state_of_the_other_mode(gpu):
+    """The backward mode is process-wide: a backward whose forward saved its state
+    under the other mode is refused (OB_ERR_SHAPE from the saved-size check), not run on a
+    buffer of the wrong layout."""
+    from onebit_asr import attention as at
+
+    bt, P, t, H, d = 2, 1, 249, 4, 36
+    dev = [x.to(gpu).requires_grad_() for x in _inputs(bt, P, t, H, d, seed=11)]
+    lens = torch.tensor([249, 100], device=gpu)
+    prev = at.set_backward_mode("probs")
+    try:
+        ctx = at.rel_pos_attention(*dev, lens, H)
+        at.set_backward_mode("flash")
+        with pytest.raises(RuntimeError, match="ob_relattn_bwd"):
+            ctx.backward(torch.ones_like(ctx))
+    finally:
+        at.set_backward_mode(prev)

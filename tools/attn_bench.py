@@ -48,7 +48,8 @@ def main():
     def bwd(s):
         return lib.ob_relattn_bwd(do.data_ptr(), ctx.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
                                   pos.data_ptr(), u.data_ptr(), vb.data_ptr(), lens.data_ptr(), Bt,
-                                  P, T, H, d, a.p, rng.data_ptr(), 0, saved.data_ptr(), dq.data_ptr(),
+                                  P, T, H, d, a.p, rng.data_ptr(), 0, saved.data_ptr(), saved.numel(),
+                                  dq.data_ptr(),
                                   dk.data_ptr(), dv.data_ptr(), dpos.data_ptr(), du.data_ptr(),
                                   dvb.data_ptr(), ws.data_ptr(), wsb, s)
 

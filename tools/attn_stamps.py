@@ -59,7 +59,7 @@ def main():
         _lib.check(lib.ob_relattn_bwd(do.data_ptr(), ctx.data_ptr(), q.data_ptr(), k.data_ptr(),
                                       v.data_ptr(), pos.data_ptr(), u.data_ptr(), vb.data_ptr(),
                                       lens.data_ptr(), Bt, P, T, H, d, 0.1, rng.data_ptr(), 0,
-                                      saved.data_ptr(), *(o.data_ptr() for o in outs),
+                                      saved.data_ptr(), saved.numel(), *(o.data_ptr() for o in outs),
                                       ws.data_ptr(), wsb, s), "bwd")
     torch.cuda.synchronize()
     buf = np.zeros(65536, dtype=np.uint64)

@@ -1,15 +1,18 @@
 #!/bin/bash
-# usage: bash exp/r5run.sh TAG "pytest selection" [bench] [prof]
+# usage: bash tools/r5run.sh TAG "pytest selection" [bench] [prof]
 set -o pipefail
 TAG=$1; TESTS=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG; mkdir -p $O
 if [ "$TESTS" != "-" ]; then
-  timeout -k 10 700 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+  timeout -k 10 700 python -u -m pytest $TESTS ${XFLAG--x} -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 1
 fi
 for st in "$@"; do case $st in
   bench) timeout -k 10 300 python bench.py --no-cpu-baseline --no-roofline > $O/bench.log 2>&1 || exit 1 ;;
   benchfull) timeout -k 10 400 python bench.py > $O/benchfull.log 2>&1 || exit 1 ;;
-  prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-roofline > $O/prof.log 2>&1) || exit 1 ;;
+  traffic) timeout -k 10 900 bash tools/traffic.sh $TAG/traffic > $O/traffic.log 2>&1 || exit 1 ;;
+  dwg) timeout -k 10 300 python tools/dwg_bench.py > $O/dwg.log 2>&1 || exit 1 ;;
+  probe) timeout -k 10 400 python -u tools/rccl_watchdog_probe.py sep same_tl same > $O/probe.log 2>&1 || exit 1 ;;
+  prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline > $O/prof.log 2>&1) || exit 1 ;;
 esac; done
 echo done

@@ -4,8 +4,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. gfx950 correction (MI355X_MICROARCH.md,
 HBM/rocprofv3 section): FETCH_SIZE reports half the bytes of a wide coalesced streaming
 read, so it is doubled; WRITE_SIZE is taken as is. Per (shape, op) the median over the
-timed dispatches of each kernel is used; one "launch" of the dW family is one dw_lds
-dispatch plus its dw_finish dispatch. Families are weighted by launches per training
+timed dispatches of each kernel is used; the weight gradients are one grouped launch a step
+(dw_grouped_kernel). Families are weighted by launches per training
 step exactly as bench.py's roofline() weights its time and algorithmic bytes.
 
 usage: python tools/traffic_json.py gpurun_out/TAG > profiles/pmc_traffic.json"""
@@ -20,7 +20,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 # launches per step (bench.py ql_shapes at Conformer-S: 16 blocks, 2 FFNs, 4 q/k/v/out)
 COUNT = {"lin1": 32, "lin2": 32, "qkvo": 64, "pos": 16}
-KERNELS = {"fwd": ("tgemm",), "dx": ("tgemm",), "dw": ("dw_lds", "dw_finish")}
+KERNELS = {"fwd": ("tgemm",), "dx": ("tgemm",)}
 
 
 def per_dispatch(path, sub):
@@ -52,11 +52,19 @@ def main():
                     raise SystemExit(f"missing counters for {shape} {op} {sub}")
                 tot += (2.0 * f + w) * 1024.0
             out[f"{shape}_{op}_hbm_bytes"] = int(tot)
-            key = "dw_lds+dw_finish" if op == "dw" else "ternary_gemm"
+            key = "ternary_gemm"
             b, n = fam.get(key, (0.0, 0))
             fam[key] = (b + cnt * tot, n + cnt)
     for key, (b, n) in fam.items():
         out[key] = {"hbm_bytes_per_launch": int(b / n), "launches_per_step": n}
+    # the grouped dW launch: one a step (median over the eager dispatches of dwg_bench.py,
+    # its composition recorded from a step's backward)
+    f = per_dispatch(f"{d}/dwg_FETCH_SIZE", "dw_grouped")
+    w = per_dispatch(f"{d}/dwg_WRITE_SIZE", "dw_grouped")
+    if f is None or w is None:
+        raise SystemExit("missing counters for dw_grouped")
+    out["dw_grouped"] = {"hbm_bytes_per_launch": int((2.0 * f + w) * 1024.0),
+                         "launches_per_step": 1}
     print(json.dumps(out, indent=1))
 
 
