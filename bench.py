@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--roofline-only", action="store_true", help="skip the step timing")
+    ap.add_argument("--branch-streams", action="store_true",
+                    help="A/B: the decoder branch on a side stream beside the CTC branch "
+                         "(OneBitStep branch_streams=True; measured slower, off by default)")
     ap.add_argument("--progress", action="store_true", help="progress lines on stderr")
     ap.add_argument("--mode", default="train",
                     choices=["train", "train-i8", "quant-off", "quant-off-lib", "infer",
@@ -940,7 +943,7 @@ def main():
         # differs); quant-off-lib: bf16 F.linear on hipBLASLt
         set_quant_off(model, "bf16w" if args.mode == "quant-off" else torch.bfloat16)
     n_layers = CONFORMER_S["enc_layers"]
-    step_mod = OneBitStep(model, n_layers=n_layers)
+    step_mod = OneBitStep(model, n_layers=n_layers, branch_streams=args.branch_streams)
     batch = synthetic_batch([args.frames] * args.batch, [args.tokens] * args.batch,
                             seed=1234 + rank, device=dev)
     sp_gen = torch.Generator().manual_seed(4321)  # same SP masks on every rank

@@ -613,7 +613,10 @@ class ConformerASR(nn.Module):
 
     def forward(self, batch, precision: int, sp_mask=None):
         enc_out, enc_mask = self.encoder(batch["feats"], batch["feat_lens"], precision, sp_mask)
-        return enc_out, enc_mask, linear(enc_out, self.ctc_head.weight, self.ctc_head.bias)
+        return enc_out, enc_mask, self.ctc_logits(enc_out)
+
+    def ctc_logits(self, enc_out):
+        return linear(enc_out, self.ctc_head.weight, self.ctc_head.bias)
 
     def decode_logits(self, enc_out, enc_mask, tgt_inp, tgt_pad_mask):
         return self.decoder(tgt_inp, enc_out, enc_mask, tgt_pad_mask)

@@ -28,6 +28,13 @@ A gradient is deferred only when nothing can read it before the flush:
 The workspaces holding the partials are kept referenced until the flush. A slot is counted
 only once its producing launch returned OB_OK; a scope left by an exception drops the
 pending entries instead of launching them.
+
+Streams: the step may run branches of its backward on several streams (train_step.py: the
+decoder branch on a side stream beside the CTC branch). The flush runs on the stream that
+was current when the scope opened (the step's own stream, the one the optimizer then uses),
+after an event wait on every other stream that produced an entry; the tensors kept for the
+flush are recorded on the flush stream (record_stream), so the allocator does not hand them
+to their producing stream's next allocation while the flush still reads them.
 """
 from __future__ import annotations
 
@@ -65,6 +72,7 @@ class _State:
         self.active = False
         self.uses: Dict[int, int] = {}
         self.tables: Dict[int, tuple] = {}  # device index -> (dw, ln, cm tables)
+        self.home: Optional[int] = None  # the stream current when the scope opened
         self.reset()
 
     def reset(self):
@@ -78,6 +86,7 @@ class _State:
         self.dwg: List[DwgGemm] = []  # weight gradients for the grouped launch
         self.post: List[tuple] = []  # (param, src): param.grad += src after the tables
         self.stream: Optional[int] = None
+        self.streams = set()  # every stream that produced an entry
         self.dev: Optional[int] = None
         self.queued = False
 
@@ -97,6 +106,8 @@ def scope(enabled: bool = True):
     prev = _S.active
     _S.active = bool(enabled)
     _S.uses = {}
+    _S.home = (torch.cuda.current_stream().cuda_stream
+               if enabled and torch.cuda.is_available() and torch.cuda.is_initialized() else None)
     ok = False
     try:
         yield
@@ -151,8 +162,12 @@ def _tables(dev: torch.device):
 
 def _begin(dev: torch.device, stream: int) -> None:
     if _S.stream is None:
-        _S.stream = stream
-        _S.dev = dev.index if dev.index is not None else torch.cuda.current_device()
+        # the flush stream: the scope's own (home) stream when it is on this device
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        home_ok = _S.home is not None and torch.cuda.current_device() == idx
+        _S.stream = _S.home if home_ok else stream
+        _S.dev = idx
+    _S.streams.add(stream)
     if not _S.queued:
         torch.autograd.Variable._execution_engine.queue_callback(_flush)
         _S.queued = True
@@ -270,8 +285,27 @@ def _flush() -> None:
     if _S.stream is None:
         _S.reset()
         return
+    # (the final callback runs on the engine's thread, whose current stream is whatever the
+    # last node used: allocations and torch ops of the flush belong to the flush stream)
+    with torch.cuda.stream(torch.cuda.ExternalStream(_S.stream,
+                                                     device=torch.device("cuda", _S.dev))):
+        _flush_tables()
+
+
+def _flush_tables() -> None:
     lib = _lib.load()
     dw, ln, cm, tk = _S.tables[_S.dev]
+    others = sorted(x for x in _S.streams if x != _S.stream)
+    if others:  # entries produced on other streams: the flush waits for them (module docstring)
+        dev = torch.device("cuda", _S.dev)
+        home = torch.cuda.ExternalStream(_S.stream, device=dev)
+        for x in others:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.ExternalStream(x, device=dev))
+            home.wait_event(ev)
+        for t in _S.refs:
+            if t.is_cuda:
+                t.record_stream(home)
     if _S.dwg:
         n = len(_S.dwg)
         xs = [g.X for g in _S.dwg]  # (q / k / v of one LN output share X)

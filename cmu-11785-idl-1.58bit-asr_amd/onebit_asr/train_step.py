@@ -96,11 +96,15 @@ class OneBitStep(nn.Module):
     keeps per-pass statistics, and the losses are formed per pass exactly as in the
     reference. Each pass computes what the reference computes; only the order in which
     the passes' gradient contributions are summed differs. ``stacked=False`` is the
-    reference's literal three forwards."""
+    reference's literal three forwards. ``branch_streams`` (stacked, CUDA; off by default):
+    the decoder branch runs on a side stream beside the CTC branch (``_forward_stacked``);
+    measured same-box in the graphed step it is 0.2 ms SLOWER (24.53 vs 24.33 ms/step,
+    profiles/r5/branch_ab/), so the step keeps one stream."""
 
     def __init__(self, model: nn.Module, n_layers: int, special: Optional[Dict[str, int]] = None,
                  gamma_ctc: float = 0.2, lambda1: float = 0.5, lambda2: float = 1.0,
-                 label_smoothing: float = 0.1, stacked: Optional[bool] = None):
+                 label_smoothing: float = 0.1, stacked: Optional[bool] = None,
+                 branch_streams: bool = False):
         super().__init__()
         self.model = model
         self.n_layers = n_layers
@@ -110,6 +114,8 @@ class OneBitStep(nn.Module):
         self.lambda2 = lambda2
         self.label_smoothing = label_smoothing
         self.stacked = stacked
+        self.branch_streams = branch_streams
+        self._side = None
         self._bits = None
         self._packer = None
 
@@ -187,6 +193,25 @@ class OneBitStep(nn.Module):
         l_kl = (kl * keep.unsqueeze(0)).sum(dim=(1, 2)) / keep.sum().clamp_min(1.0)
         return l_att, l_kl
 
+    def _decoder_losses(self, enc, mask, tgt_inp, tgt_pad, t_out, t_pad, P):
+        logits = self.model.decode_logits(enc, mask, tgt_inp, tgt_pad)
+        # attention CE per pass (losses.py:22-35, label smoothing, scalar-mean quirk) and
+        # KL(teacher || student) for the student and SP passes (losses.py:50-59)
+        if att_kl_supported(logits, self.label_smoothing):
+            # csrc/seqloss.hip: both losses, one row pass per direction
+            return att_kl_losses(logits, t_out, t_pad, P, self.special["pad_id"],
+                                 self.label_smoothing)
+        return self._att_kl_torch(logits, t_out, t_pad, P)
+
+    def _side_stream(self, enc):
+        """The decoder branch's stream (one per device), or None (branches off -- tests compare
+        both -- or a CPU tensor)."""
+        if not (self.branch_streams and enc.is_cuda):
+            return None
+        if self._side is None or self._side.device != enc.device:
+            self._side = torch.cuda.Stream(enc.device)
+        return self._side
+
     def _forward_stacked(self, batch, bits):
         from .ctc import ctc_loss_logits_groups
 
@@ -202,21 +227,38 @@ class OneBitStep(nn.Module):
         bsz = batch["feats"].size(0)
         t_inp, t_out, t_pad = make_att_targets(batch["tokens"], sp["bos_id"], sp["eos_id"], sp["pad_id"])
         # the encoder repeats the (pass-independent) subsampling output P times itself
-        enc, mask, ctc = self.model(batch, precision=2, sp_mask=bits)
-        logits = self.model.decode_logits(enc, mask, t_inp.repeat(P, 1), t_pad.repeat(P, 1))
-        # attention CE per pass (losses.py:22-35, label smoothing, scalar-mean quirk) and
-        # KL(teacher || student) for the student and SP passes (losses.py:50-59)
-        if att_kl_supported(logits, self.label_smoothing):
-            # csrc/seqloss.hip: both losses, one row pass per direction
-            l_att, l_kl = att_kl_losses(logits, t_out, t_pad, P, sp["pad_id"],
-                                        self.label_smoothing)
+        enc, mask = self.model.encoder(batch["feats"], batch["feat_lens"], 2, bits)
+        tgt_inp, tgt_pad = t_inp.repeat(P, 1), t_pad.repeat(P, 1)
+        side = self._side_stream(enc)
+        if side is not None:
+            # Two independent branches from here to the loss: the decoder + attention-CE / KL
+            # (decoder.py call sites, losses.py:22-35,50-59) on a side stream, the CTC head +
+            # CTC (losses.py:41-47) on this one. Both are chains of small, latency-bound
+            # launches; side by side they overlap (also in the captured graph, where the fork
+            # and join are graph edges). Autograd runs each node's backward on its forward's
+            # stream, so the two backward branches overlap too; deferred.py joins the streams
+            # before its end-of-backward finishes.
+            main = torch.cuda.current_stream(enc.device)
+            side.wait_stream(main)
+            # this stream's tensors read on the side stream (also by the decoder's backward):
+            # their blocks must not return to this stream's pool before the side stream has
+            # read them (the engine records the gradients that cross back itself)
+            for t in (enc, mask, tgt_inp, tgt_pad, t_out, t_pad):
+                t.record_stream(side)
+            with torch.cuda.stream(side):
+                l_att, l_kl = self._decoder_losses(enc, mask, tgt_inp, tgt_pad, t_out, t_pad, P)
         else:
-            l_att, l_kl = self._att_kl_torch(logits, t_out, t_pad, P)
+            l_att, l_kl = self._decoder_losses(enc, mask, tgt_inp, tgt_pad, t_out, t_pad, P)
+        ctc = self.model.ctc_logits(enc)
         # CTC per pass (losses.py:41-47: log_softmax + CTC), straight from the head's logits
         in_lens = mask.sum(dim=1).long()
         # the P passes' CTC losses in one launch per direction (each pass its own mean)
         l_ctc = ctc_loss_logits_groups(ctc, batch["tokens"].repeat(P, 1), in_lens,
                                        batch["token_lens"].repeat(P), sp["blank_id"], P)
+        if side is not None:  # join: the loss below reads the decoder branch's results
+            main.wait_stream(side)
+            l_att.record_stream(main)
+            l_kl.record_stream(main)
         l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
         loss = l_int[0] + self.lambda1 * (l_int[1] + l_int[2]) + self.lambda2 * (l_kl[0] + l_kl[1])
         parts = torch.stack([l_int[0], l_int[1], l_int[2], l_kl[0], l_kl[1],

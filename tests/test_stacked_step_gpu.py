@@ -236,3 +236,42 @@ def test_grouped_dw_matches_immediate(gpu, monkeypatch):
         # alpha and bias gradients are cancellation-prone sums (over N*K products / rows)
         bar = 1e-4 if k.endswith(".alpha") else 1e-5 if k.endswith("bias") else 2e-6
         assert (a - b).abs().max().item() <= bar * b.abs().max().item() + 1e-12, k
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_branch_streams_equal_single_stream(gpu, graphed):
+    """OneBitStep(branch_streams=True), opt-in: the decoder branch on a side stream beside
+    the CTC branch (forward and backward), deferred finishes joined across the two streams.
+    Same kernels, same per-node arithmetic: the loss, its parts and every gradient equal the
+    single-stream step bit for bit, eagerly (with the deferred finishes) and as the captured
+    graph replayed twice (the fork / join as graph edges)."""
+    from onebit_asr import deferred
+    from onebit_asr.data import synthetic_batch
+    from onebit_asr.graph_step import GraphedTrainStep
+    from onebit_asr.train_step import OneBitStep
+
+    batch = synthetic_batch([734, 349], [27, 12], seed=3, device=gpu)
+    res = {}
+    for branch in (False, True):
+        m = _model(gpu)
+        step = OneBitStep(m, n_layers=2, stacked=True, branch_streams=branch)
+        if graphed:
+            gs = GraphedTrainStep(step, 2, warmup_iters=1)
+            outs = [gs.step(batch, [1, 0]) for _ in range(2)]
+            torch.cuda.synchronize()
+            res[branch] = ([(lo.item(), pa.cpu()) for lo, pa in outs],
+                           {k: p.detach().cpu().clone() for k, p in m.named_parameters()})
+        else:
+            with deferred.scope():
+                loss, parts = step(batch, [1, 0])
+                loss.backward()
+            torch.cuda.synchronize()
+            res[branch] = ([(loss.item(), parts.cpu())],
+                           {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()
+                            if p.grad is not None})
+    (o0, t0), (o1, t1) = res[False], res[True]
+    for (l0, p0), (l1, p1) in zip(o0, o1):
+        assert l0 == l1 and torch.equal(p0, p1)
+    assert t0.keys() == t1.keys()
+    for k in t0:
+        assert torch.equal(t0[k], t1[k]), k
