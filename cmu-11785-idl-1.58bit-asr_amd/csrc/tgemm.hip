@@ -373,7 +373,10 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   // the barrier run under their latency), and while a tile computes its last chunks the
   // next tile's first chunks are already loading (so the epilogue runs under them too).
   // vmcnt counts in issue order: the code words go first so the decode waits only on them.
-  constexpr int kWmax = NT > 6 ? 3 : 5;
+#ifndef OB_TG_KWMAX_WIDE
+#define OB_TG_KWMAX_WIDE 3
+#endif
+  constexpr int kWmax = NT > 6 ? OB_TG_KWMAX_WIDE : 5;
   // NT 12: the cross-tile live range spills (and a 2-deep window measured slower), so it
   // keeps the per-tile window (issued at the top of each row tile)
   constexpr bool kCross = NT <= 9;

@@ -275,8 +275,8 @@ def _pointwise_backward(ctx, g, need_x, need_w, need_b):
             _lib.check(lib.ob_dense_gemm(g.data_ptr(), m, n, w.data_ptr(), 1, None, k,
                                          gx.data_ptr(), st), "ob_dense_gemm")
         if need_w or need_b:
-            gw = torch.empty(ctx.wshape, dtype=torch.float32, device=g.device)  # [out, in, 1]
-            gb = torch.empty((n,), dtype=torch.float32, device=g.device) if need_b else None
+            gw = deferred.grad_buf(ctx.wparam, ctx.wshape, g.device)  # [out, in, 1]
+            gb = deferred.grad_buf(ctx.bias, (n,), g.device) if need_b else None
             wsb = lib.ob_dense_dw_workspace(m, n, k)
             ws = torch.empty((wsb,), dtype=torch.uint8, device=g.device)
             deferred.dense_dw(g, x2d, m, n, k, gw, gb, ws, wsb, st, ctx.wparam, ctx.bias)

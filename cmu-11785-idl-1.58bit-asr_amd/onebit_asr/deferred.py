@@ -98,6 +98,39 @@ def active() -> bool:
     return _ON and _S.active
 
 
+# The N > 1 exchange's flat gradient buffer (graph_step, exchange "deferred"): id(param) ->
+# (flat, element offset, shape). A backward site that allocates a parameter's gradient takes
+# it from grad_buf(): a fresh view of the flat buffer, which AccumulateGrad adopts as .grad
+# (the gradient is written in place, no pack copy before the all-reduce).
+_ARENA: Dict[int, tuple] = {}
+
+
+def set_arena(entries) -> None:
+    """entries: [(param, flat, offset)] or None (no arena)."""
+    _ARENA.clear()
+    for p, flat, off in entries or ():
+        _ARENA[id(p)] = (flat, off, tuple(p.shape))
+
+
+def grad_buf(param, shape=None, device=None) -> torch.Tensor:
+    """The tensor a backward writes ``param``'s gradient into: its view of the registered flat
+    buffer when autograd will adopt it (inside an active scope, ``param.grad`` None), else a
+    new fp32 tensor of ``shape`` (default: the parameter's). A NEW view object every call:
+    an extra reference held here would make AccumulateGrad copy instead of adopt."""
+    if param is not None and _S.active and _ARENA:
+        e = _ARENA.get(id(param))
+        if e is not None and param.grad is None:
+            flat, off, shp = e
+            n = 1
+            for d in shp:
+                n *= d
+            return flat[off:off + n].view(shp)
+    if shape is None:
+        shape = param.shape
+    return torch.empty(shape, dtype=torch.float32,
+                       device=device if device is not None else param.device)
+
+
 @contextmanager
 def scope(enabled: bool = True):
     """Forward + backward of one training step: deferrable gradients are finished by one

@@ -149,8 +149,8 @@ def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream, bias=
     """dW / dalpha / db of one BitLinear; the finish deferred to the end of the backward
     (deferred.py) when nothing can read these gradients before it. dense (quant-off): the
     plain dW = dY^T X and db on the same kernels, no STE mask, no alpha gradient."""
-    gw = torch.empty_like(weight)
-    gb = torch.empty((n,), dtype=torch.float32, device=dy.device) if has_bias else None
+    gw = deferred.grad_buf(weight)
+    gb = deferred.grad_buf(bias, (n,), dy.device) if has_bias else None
     if dense:
         wsb = lib.ob_dense_dw_workspace(P * m, n, k)
         if not wsb:  # shapes off the dW kernels: library fp32
@@ -160,7 +160,7 @@ def _dw(lib, dy, x, P, m, n, k, weight, alpha, has_bias, pb, bits, stream, bias=
         ws = torch.empty((wsb,), dtype=torch.uint8, device=dy.device)
         deferred.dense_dw(dy, x, P * m, n, k, gw, gb, ws, wsb, stream, weight, bias)
         return gw, None, gb
-    ga = torch.empty((), dtype=torch.float32, device=dy.device)
+    ga = deferred.grad_buf(alpha, (), dy.device)
     if pb is not None and deferred.dwg_take(dy, x, P, m, n, k, gw, gb, stream, weight, bias,
                                             alpha=alpha, ga=ga, pass_bits=pb):
         return gw, ga, gb  # computed by the grouped launch at the end of the backward
@@ -373,8 +373,8 @@ class _QKVFn(torch.autograd.Function):
         if pb is not None and not codes[0].dense:  # the grouped launch at the end of the backward
             for g, w, a, c, hb in layers:
                 b = ctx.biases[[id(t) for t in (wq, wk, wv)].index(id(w))]
-                o = (torch.empty_like(w), torch.empty((), dtype=torch.float32, device=h.device),
-                     torch.empty((w.shape[0],), dtype=torch.float32, device=h.device) if hb else None)
+                o = (deferred.grad_buf(w), deferred.grad_buf(a, (), h.device),
+                     deferred.grad_buf(b, (w.shape[0],), h.device) if hb else None)
                 if deferred.dwg_take(g, h, P, m, w.shape[0], k, o[0], o[2], stream, w, b, alpha=a,
                                      ga=o[1], pass_bits=pb):
                     grads[id(w)] = o

@@ -91,14 +91,13 @@ class BucketedAllReduce:
     producing stream; ``finish`` makes the current stream wait. CPU (gloo): async works,
     waited in ``finish``."""
 
-    def __init__(self, params, flat: torch.Tensor, pg, bucket_bytes: int):
+    def __init__(self, params, flat: torch.Tensor, pg, bucket_bytes: int, offs=None):
         self.flat = flat
         self.pg = pg
         self.enabled = False
-        offs, off = [], 0
-        for p in params:
-            offs.append(off)
-            off += p.numel()
+        if offs is None:
+            offs = flat_offsets(params)
+        off = flat.numel()
         self.buckets = []  # (lo, hi, n_params)
         self.bucket_of = {}
         hi, lo, n = off, off, 0
@@ -149,6 +148,17 @@ class BucketedAllReduce:
         for w in self.works:
             w.wait()
         self.works = []
+
+
+def flat_offsets(params, align: int = 4):
+    """Element offset of every parameter in the flat gradient buffer: each one starts on a
+    16-byte boundary (the HIP kernels that write gradients in place store dwordx4), the gaps
+    stay zero."""
+    offs, off = [], 0
+    for p in params:
+        offs.append(off)
+        off += -(-p.numel() // align) * align
+    return offs
 
 
 # Test hook: run the multi-rank exchange path (flat buffer, buckets, the all-reduce captured
@@ -203,6 +213,8 @@ class GraphedTrainStep:
         self.exchange = exchange
         self.bucket_bytes = int(bucket_mb * 2**20) if (bucket_mb and exchange == "bucketed") else 0
         self.flat_views: List[torch.Tensor] = []
+        self.arena = None  # [(param, flat, offset)]: the deferred exchange's in-place gradients
+        self.copied = 0    # gradients the deferred exchange copies in and out (last exchange)
         self.buckets: Optional[BucketedAllReduce] = None
         self.comm_in_graph = False
         self.xpg = process_group  # the group the exchange's collectives run on
@@ -231,18 +243,22 @@ class GraphedTrainStep:
             p.grad = None
         if self.multi:
             # one flat gradient buffer: the exchange's all-reduce(s) run on it
-            total = sum(p.numel() for p in self.params)
+            offs = flat_offsets(self.params)
+            last = self.params[-1].numel() if self.params else 0
+            total = (offs[-1] + -(-last // 4) * 4) if self.params else 0
             self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
-            off = 0
-            for p in self.params:
-                n = p.numel()
-                self.flat_views.append(self.flat[off:off + n].view_as(p))
-                off += n
+            for p, off in zip(self.params, offs):
+                self.flat_views.append(self.flat[off:off + p.numel()].view_as(p))
             if self.exchange != "deferred":  # the gradients ARE the flat buffer's views
                 for p, v in zip(self.params, self.flat_views):
                     p.grad = v
+            elif self.device.type == "cuda":
+                # the backward's gradient sites write into the flat buffer's views
+                # (deferred.grad_buf): only the gradients formed elsewhere are copied in
+                self.arena = [(p, self.flat, off) for p, off in zip(self.params, offs)]
             if self.bucket_bytes:
-                self.buckets = BucketedAllReduce(self.params, self.flat, self.pg, self.bucket_bytes)
+                self.buckets = BucketedAllReduce(self.params, self.flat, self.pg, self.bucket_bytes,
+                                                 offs)
         if self.device.type == "cuda" and self.fused_optimizer:
             self.fused = True
             self.opt = FusedAdamW(self.params, lr=self.lr0, betas=(0.9, 0.98), eps=1e-8,
@@ -275,11 +291,13 @@ class GraphedTrainStep:
         if self.buckets is not None:
             self.buckets.begin()
             self.buckets.enabled = overlap
+        deferred.set_arena(self.arena)
         try:
             with deferred.scope():  # one finish launch per kind at the end of the backward
                 loss, parts = self.step_module(self.batch, self.bits)
                 loss.backward()
         finally:
+            deferred.set_arena(None)
             if self.buckets is not None:
                 self.buckets.enabled = False
         return loss.detach(), parts
@@ -297,14 +315,19 @@ class GraphedTrainStep:
         if not self.multi:
             return
         if self.exchange == "deferred":
-            # pack (one cat), one all-reduce, unpack (one foreach copy); the non-fused update
-            # takes the average here (the fused one scales by 1/world)
-            grads = [p.grad for p in self.params]
-            torch.cat([g.reshape(-1) for g in grads], out=self.flat)
+            # the gradients the backward wrote into the flat buffer (deferred.grad_buf) are in
+            # place; the rest are copied in (one foreach copy), one all-reduce, and copied back
+            # out; the non-fused update takes the average here (the fused one scales by 1/world)
+            out = [(p.grad, v) for p, v in zip(self.params, self.flat_views)
+                   if p.grad.data_ptr() != v.data_ptr()]
+            self.copied = len(out)
+            if out:
+                torch._foreach_copy_([v for _, v in out], [g for g, _ in out])
             dist.all_reduce(self.flat, group=self.xpg)
             if not self.fused:
                 self.flat.div_(self.world)
-            torch._foreach_copy_(grads, self.flat_views)
+            if out:
+                torch._foreach_copy_([g for g, _ in out], [v for _, v in out])
         elif overlapped:
             self.buckets.finish()
         else:

@@ -117,9 +117,9 @@ class _LinearFn(torch.autograd.Function):
             wsb = _dense_dw_ws(g2, x2d, weight) if ctx.needs_input_grad[1] else 0
             if wsb:  # dW (and db) on the dW kernel family: exact-fp32 products, fixed order
                 m, n, k = g2.shape[0], weight.shape[0], weight.shape[1]
-                gw = torch.empty_like(weight)
+                gw = deferred.grad_buf(weight)
                 if has_b and ctx.needs_input_grad[2]:
-                    gb = torch.empty((n,), dtype=torch.float32, device=g2.device)
+                    gb = deferred.grad_buf(ctx.bias, (n,), g2.device)
                 ws = torch.empty((wsb,), dtype=torch.uint8, device=g2.device)
                 deferred.dense_dw(g2, x2d, m, n, k, gw, gb, ws, wsb, _lib.stream_of(g2), weight,
                                   ctx.bias)

@@ -317,8 +317,8 @@ class _BitLinearPassesFn(torch.autograd.Function):
         if ctx.dense and (ctx.needs_input_grad[1] or ctx.needs_input_grad[3]):
             wsb = lib.ob_dense_dw_workspace(rows, n, k)
             if wsb and gy.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0:
-                gw = torch.empty_like(weight)
-                gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+                gw = deferred.grad_buf(weight)
+                gb = deferred.grad_buf(ctx.bias, (n,), gy.device) if ctx.has_bias else None
                 ws = torch.empty((wsb,), dtype=torch.uint8, device=gy.device)
                 deferred.dense_dw(gy, x2d, rows, n, k, gw, gb, ws, wsb, stream, weight, ctx.bias)
             else:  # shapes off the dW kernels (N or K not a multiple of 48): library fp32
@@ -328,9 +328,9 @@ class _BitLinearPassesFn(torch.autograd.Function):
                 gb = colsum(gy) if ctx.has_bias else None
             return gx, gw, None, gb, None, None, None, None, None, None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
-            gw = torch.empty_like(weight)
-            galpha = torch.empty((), dtype=torch.float32, device=gy.device)
-            gb = torch.empty((n,), dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            gw = deferred.grad_buf(weight)
+            galpha = deferred.grad_buf(alpha, (), gy.device)
+            gb = deferred.grad_buf(ctx.bias, (n,), gy.device) if ctx.has_bias else None
             if deferred.dwg_take(gy, x2d, P, m, n, k, gw, gb, stream, weight, ctx.bias,
                                  alpha=alpha, ga=galpha, pass_bits=pass_bits):
                 return gx, gw, galpha, gb, None, None, None, None, None, None

@@ -53,8 +53,12 @@ def main():
         torch.cuda.synchronize()
         ms = 1e3 * (time.perf_counter() - t0) / steps
         nb = len(gs.buckets.buckets) if gs.buckets is not None else 0
+        cp = [p for p, v in zip(gs.params, gs.flat_views)
+              if p.grad is not None and p.grad.data_ptr() != v.data_ptr()] if multi else []
         print(f"{('multi-rank path, ' + exchange) if multi else 'single-GPU path'}: {ms:.3f} ms/step "
-              f"(buckets {nb}, all-reduce in the graph: {gs.comm_in_graph})", flush=True)
+              f"(buckets {nb}, all-reduce in the graph: {gs.comm_in_graph}; gradients copied "
+              f"around the exchange: {len(cp)} of {len(gs.params)}, "
+              f"{sum(p.numel() for p in cp) * 4 / 2**20:.1f} MiB)", flush=True)
         del gs, model
         torch.cuda.empty_cache()
     dist.destroy_process_group()
