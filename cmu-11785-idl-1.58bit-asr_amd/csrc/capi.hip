@@ -1201,6 +1201,21 @@ int ob_att_kl_loss_bwd(const float* logits, const int64_t* tgt_out, const uint8_
   return launched();
 }
 
+int ob_loss_combine_fwd(const float* l_att, const float* l_ctc, const float* l_kl, float gamma,
+                        float lambda1, float lambda2, float* loss, float* parts, void* stream) {
+  if (!l_att || !l_ctc || !l_kl || !loss || !parts) return OB_ERR_NULL;
+  launch_loss_combine_fwd(l_att, l_ctc, l_kl, gamma, lambda1, lambda2, loss, parts,
+                          as_stream(stream));
+  return launched();
+}
+
+int ob_loss_combine_bwd(const float* g_loss, float gamma, float lambda1, float lambda2,
+                        float* d_att, float* d_ctc, float* d_kl, void* stream) {
+  if (!g_loss || !d_att || !d_ctc || !d_kl) return OB_ERR_NULL;
+  launch_loss_combine_bwd(g_loss, gamma, lambda1, lambda2, d_att, d_ctc, d_kl, as_stream(stream));
+  return launched();
+}
+
 int ob_ctc_greedy_decode(const float* logits, const int64_t* lens, int64_t B, int64_t T,
                          int64_t V, int blank, int32_t* ids, int32_t* out, int32_t* out_len,
                          void* stream) {

@@ -407,6 +407,12 @@ void launch_att_kl_fwd(const float* x, const int64_t* tgt, const uint8_t* pad, i
 void launch_att_kl_bwd(const float* x, const int64_t* tgt, const uint8_t* pad, int64_t P,
                        int64_t BU, int64_t V, float ls, const float* g_att, const float* g_kl,
                        float* grad, const void* ws, hipStream_t s);
+// the step's loss from its per-pass parts (P = 3): loss [1], parts [8]; and its backward
+void launch_loss_combine_fwd(const float* l_att, const float* l_ctc, const float* l_kl,
+                             float gamma, float lam1, float lam2, float* loss, float* parts,
+                             hipStream_t s);
+void launch_loss_combine_bwd(const float* gl, float gamma, float lam1, float lam2, float* d_att,
+                             float* d_ctc, float* d_kl, hipStream_t s);
 
 // adamw.hip (clip_grad_norm_ + AdamW over a tensor table; layout = ob_adamw_tensor)
 struct AdamwTensor {

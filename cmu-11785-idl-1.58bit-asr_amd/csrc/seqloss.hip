@@ -216,4 +216,73 @@ void launch_att_kl_bwd(const float* x, const int64_t* tgt, const uint8_t* pad, i
                      pad, (int)BU, (int)V, off, c2, stats, aux, g_att, g_kl, grad);
 }
 
+// ---------------------------------------------------------------------------------------
+// The step's loss from its per-pass parts (train.py:95-111, the stacked form of
+// train_step.OneBitStep): l_int = (1 - gamma) l_att + gamma l_ctc per pass, then
+// loss = l_int[0] + lambda1 (l_int[1] + l_int[2]) + lambda2 (l_kl[0] + l_kl[1]) and the eight
+// logged parts -- ONE single-thread launch, the rounding sequence of the torch expression it
+// replaces (each mul and add rounded, in that order; no contraction), instead of ~20 scalar
+// torch kernels forward and ~25 (index backwards: fills, copies, adds) backward.
+namespace {
+__device__ __forceinline__ float rmul(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float radd(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+
+__global__ void loss_combine_fwd_kernel(const float* __restrict__ l_att,
+                                        const float* __restrict__ l_ctc,
+                                        const float* __restrict__ l_kl, float g1, float g,
+                                        float lam1, float lam2, float* __restrict__ loss,
+                                        float* __restrict__ parts) {
+  if (threadIdx.x != 0) return;
+  float li[3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) li[p] = radd(rmul(g1, l_att[p]), rmul(g, l_ctc[p]));
+  const float a = radd(li[0], rmul(lam1, radd(li[1], li[2])));
+  loss[0] = radd(a, rmul(lam2, radd(l_kl[0], l_kl[1])));
+  parts[0] = li[0];
+  parts[1] = li[1];
+  parts[2] = li[2];
+  parts[3] = l_kl[0];
+  parts[4] = l_kl[1];
+  parts[5] = l_ctc[0];
+  parts[6] = l_ctc[1];
+  parts[7] = l_ctc[2];
+}
+
+// autograd of the same expression: dl_int = (gL, lam1 gL, lam1 gL), dl_att = (1 - gamma)
+// dl_int, dl_ctc = gamma dl_int, dl_kl = (lam2 gL, lam2 gL)
+__global__ void loss_combine_bwd_kernel(const float* __restrict__ gl, float g1, float g,
+                                        float lam1, float lam2, float* __restrict__ d_att,
+                                        float* __restrict__ d_ctc, float* __restrict__ d_kl) {
+  if (threadIdx.x != 0) return;
+  const float gv = gl[0];
+  const float di[3] = {gv, rmul(lam1, gv), rmul(lam1, gv)};
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    d_att[p] = rmul(g1, di[p]);
+    d_ctc[p] = rmul(g, di[p]);
+  }
+  d_kl[0] = rmul(lam2, gv);
+  d_kl[1] = rmul(lam2, gv);
+}
+}  // namespace
+
+void launch_loss_combine_fwd(const float* l_att, const float* l_ctc, const float* l_kl,
+                             float gamma, float lam1, float lam2, float* loss, float* parts,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(loss_combine_fwd_kernel, dim3(1), dim3(64), 0, s, l_att, l_ctc, l_kl,
+                     1.0f - gamma, gamma, lam1, lam2, loss, parts);
+}
+
+void launch_loss_combine_bwd(const float* gl, float gamma, float lam1, float lam2, float* d_att,
+                             float* d_ctc, float* d_kl, hipStream_t s) {
+  hipLaunchKernelGGL(loss_combine_bwd_kernel, dim3(1), dim3(64), 0, s, gl, 1.0f - gamma, gamma,
+                     lam1, lam2, d_att, d_ctc, d_kl);
+}
+
 }  // namespace ob

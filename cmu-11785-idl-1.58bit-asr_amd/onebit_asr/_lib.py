@@ -100,6 +100,8 @@ SIGNATURES = {
     "ob_att_kl_workspace": (_sz, [_i64, _i64]),
     "ob_att_kl_loss_fwd": (
         _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _int, _f32, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_loss_combine_fwd": (_int, [_c_f, _c_f, _c_f, _f32, _f32, _f32, _c_f, _c_f, _c_f]),
+    "ob_loss_combine_bwd": (_int, [_c_f, _f32, _f32, _f32, _c_f, _c_f, _c_f, _c_f]),
     "ob_att_kl_loss_bwd": (
         _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _f32, _c_f, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_quant_dequant": (_int, [_c_f, _c_f, _int, _int, _i64, _c_f, _c_f]),

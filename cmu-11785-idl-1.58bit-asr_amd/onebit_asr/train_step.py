@@ -259,11 +259,50 @@ class OneBitStep(nn.Module):
             main.wait_stream(side)
             l_att.record_stream(main)
             l_kl.record_stream(main)
+        if l_att.is_cuda and P == 3:  # one HIP launch each way (csrc/seqloss.hip)
+            return _LossCombine.apply(l_att, l_ctc, l_kl, self.gamma_ctc, self.lambda1,
+                                      self.lambda2)
         l_int = (1 - self.gamma_ctc) * l_att + self.gamma_ctc * l_ctc
         loss = l_int[0] + self.lambda1 * (l_int[1] + l_int[2]) + self.lambda2 * (l_kl[0] + l_kl[1])
         parts = torch.stack([l_int[0], l_int[1], l_int[2], l_kl[0], l_kl[1],
                              l_ctc[0], l_ctc[1], l_ctc[2]]).detach()
         return loss, parts
+
+
+class _LossCombine(torch.autograd.Function):
+    """train.py:95-111's combination of the three passes' losses (the stacked step's form of
+    the expression in ``_forward_stacked``'s fallback, same rounding sequence) and the eight
+    logged parts in ONE launch, its backward in one more (ob_loss_combine_*): the torch
+    expression is ~20 scalar kernels forward and ~25 backward (index backwards: fills,
+    copies, adds)."""
+
+    @staticmethod
+    def forward(ctx, l_att, l_ctc, l_kl, gamma, lam1, lam2):
+        from . import _lib
+
+        l_att, l_ctc, l_kl = (t.contiguous() for t in (l_att, l_ctc, l_kl))
+        loss = torch.empty((), dtype=torch.float32, device=l_att.device)
+        parts = torch.empty((8,), dtype=torch.float32, device=l_att.device)
+        _lib.check(_lib.load().ob_loss_combine_fwd(
+            l_att.data_ptr(), l_ctc.data_ptr(), l_kl.data_ptr(), gamma, lam1, lam2,
+            loss.data_ptr(), parts.data_ptr(), _lib.stream_of(l_att)), "ob_loss_combine_fwd")
+        ctx.meta = (gamma, lam1, lam2)
+        ctx.mark_non_differentiable(parts)
+        return loss, parts
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_parts):
+        from . import _lib
+
+        gamma, lam1, lam2 = ctx.meta
+        g_loss = g_loss.contiguous()
+        d_att = torch.empty((3,), dtype=torch.float32, device=g_loss.device)
+        d_ctc = torch.empty((3,), dtype=torch.float32, device=g_loss.device)
+        d_kl = torch.empty((2,), dtype=torch.float32, device=g_loss.device)
+        _lib.check(_lib.load().ob_loss_combine_bwd(
+            g_loss.data_ptr(), gamma, lam1, lam2, d_att.data_ptr(), d_ctc.data_ptr(),
+            d_kl.data_ptr(), _lib.stream_of(g_loss)), "ob_loss_combine_bwd")
+        return d_att, d_ctc, d_kl, None, None, None
 
 
 PART_NAMES = ["Lint2", "Lint1", "Lint_s", "Lkl1", "Lkl_s", "Lctc2", "Lctc1", "Lctc_s"]

@@ -248,6 +248,17 @@ OB_API int ob_att_kl_loss_bwd(const float* logits, const int64_t* tgt_out,
                               const uint8_t* tgt_pad, int64_t P, int64_t BU, int64_t V,
                               float label_smoothing, const float* g_att, const float* g_kl,
                               float* grad, const void* ws, size_t ws_bytes, void* stream);
+/* The training step's loss from its per-pass parts (train.py:95-111 with the three passes
+ * stacked: teacher 2-bit, student 1-bit, SP): l_int[p] = (1 - gamma) l_att[p] + gamma l_ctc[p],
+ * loss = l_int[0] + lambda1 (l_int[1] + l_int[2]) + lambda2 (l_kl[0] + l_kl[1]) -- each
+ * multiply and add rounded in that order (the torch expression's sequence) -- and
+ * parts[8] = (l_int[0..2], l_kl[0..1], l_ctc[0..2]). DEVICE pointers, one launch each way.
+ * bwd: from g_loss [1]: d_att[3], d_ctc[3], d_kl[2] (the expression's autograd). */
+OB_API int ob_loss_combine_fwd(const float* l_att, const float* l_ctc, const float* l_kl,
+                               float gamma, float lambda1, float lambda2, float* loss,
+                               float* parts, void* stream);
+OB_API int ob_loss_combine_bwd(const float* g_loss, float gamma, float lambda1, float lambda2,
+                               float* d_att, float* d_ctc, float* d_kl, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Stacked passes. The reference's training step runs every BitLinear three times per

@@ -91,3 +91,26 @@ def test_att_kl_rejects_bad_shapes(gpu):
                       torch.zeros(2, 4, dtype=torch.bool, device=gpu), 3, PAD, 0.1)
     lib = _lib.load()
     assert lib.ob_att_kl_loss_fwd(0, 0, 0, 3, 4, 10, 0, 0.1, 0, 0, 0, 0, 0) != 0
+
+
+def test_loss_combine_equals_torch_expression(gpu):
+    """ob_loss_combine_fwd / _bwd (train_step._LossCombine) against the torch expression it
+    replaces (train.py:95-111 in the stacked form): loss, the eight parts and the gradients of
+    l_att, l_ctc, l_kl bit for bit (same rounding sequence), for a unit and a non-unit seed."""
+    from onebit_asr.train_step import _LossCombine
+
+    g = torch.Generator().manual_seed(5)
+    gam, lam1, lam2 = 0.2, 0.5, 1.0
+    for seed in (1.0, 0.37):
+        base = [torch.rand(n, generator=g) * 5 for n in (3, 3, 2)]
+        la, lc, lk = (t.to(gpu).requires_grad_() for t in base)
+        loss, parts = _LossCombine.apply(la, lc, lk, gam, lam1, lam2)
+        loss.backward(torch.tensor(seed, device=gpu))
+        ta, tc, tk = (t.to(gpu).requires_grad_() for t in base)
+        li = (1 - gam) * ta + gam * tc
+        tl = li[0] + lam1 * (li[1] + li[2]) + lam2 * (tk[0] + tk[1])
+        tp = torch.stack([li[0], li[1], li[2], tk[0], tk[1], tc[0], tc[1], tc[2]])
+        tl.backward(torch.tensor(seed, device=gpu))
+        assert torch.equal(loss, tl.detach()) and torch.equal(parts, tp.detach())
+        for a, b in ((la, ta), (lc, tc), (lk, tk)):
+            assert torch.equal(a.grad, b.grad), (a.grad, b.grad)
