@@ -776,6 +776,23 @@ int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int64_t N,
   return launched();
 }
 
+int ob_bitlinear_bwd_dx_passes_sum(int64_t G, const float* const* dY, int64_t P, int64_t M,
+                                   int64_t N, const uint32_t* const* codes2_t,
+                                   const uint32_t* const* codes1_t, const int32_t* pass_bits,
+                                   const float* const* alpha, int alpha_raw, int64_t K, float* dX,
+                                   void* stream) {
+  if (G < 1 || G > 3 || M < 0 || K < 0 || N < 0 || P < 1 || P > 65535) return OB_ERR_SHAPE;
+  if (!dY || !codes2_t || !codes1_t || !alpha || !pass_bits || !dX) return OB_ERR_NULL;
+  for (int64_t i = 0; i < G; ++i)
+    if (!dY[i] || !codes2_t[i] || !codes1_t[i] || !alpha[i]) return OB_ERR_NULL;
+  if (!aligned4(pass_bits)) return OB_ERR_ALIGN;
+  if (!launch_ternary_dx_sum((int)G, dY, (int)P, M, N, codes2_t, codes1_t,
+                             reinterpret_cast<const int*>(pass_bits), alpha, alpha_raw, K, dX,
+                             as_stream(stream)))
+    return OB_ERR_SHAPE;  // not this kernel's shape: one ob_bitlinear_bwd_dx_passes per source
+  return launched();
+}
+
 size_t ob_bitlinear_bwd_dw_passes_workspace(int64_t P, int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0 || P < 1 || P > kMaxPasses) return 0;
   return dw_layout(P, M, N, K).total;

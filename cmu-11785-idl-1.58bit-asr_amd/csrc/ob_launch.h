@@ -66,6 +66,14 @@ bool launch_ternary_gemm_passes_group(const float* A, int P, int64_t M, int64_t 
                                       const uint32_t* const* codes1, const int* pass_bits,
                                       int64_t N, const float* const* alpha, int alpha_raw,
                                       const float* const* bias, float* const* C, hipStream_t s);
+// dX = sum_g alpha_g dY_g . Q_g^T over G = 3 sources of width N = 144 (the q / k / v input
+// gradients of one LayerNorm output) in one launch; codes_t / codes_t1: the sources' dX code
+// images (2-bit / 1-bit), per-pass bitwidths from pass_bits. false: shape not taken (the
+// caller runs one dX launch per source).
+bool launch_ternary_dx_sum(int G, const float* const* dY, int P, int64_t M, int64_t N,
+                           const uint32_t* const* codes_t, const uint32_t* const* codes_t1,
+                           const int* pass_bits, const float* const* alpha, int alpha_raw,
+                           int64_t K, float* dX, hipStream_t s);
 
 // Fused epilogues of the ternary GEMM, y = a * acc + bias; element (row, col) of the
 // P*M x N output has dropout index row * N + col (ob_drop.h):

@@ -156,6 +156,9 @@ struct EpiArgs {
   const float* galpha[3];
   const float* gbias[3];
   float* gC[3];
+  // MS > 1 (the dX of q / k / v summed in one launch): the A operand of source s (its rows
+  // [P][M][K]); source s reduces against gcodes[s] / gcodes1[s], scaled by galpha[s]
+  const float* gA[3];
   int mode;
   const float* R;
   float* C2;
@@ -285,7 +288,13 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
   *reinterpret_cast<f32x4*>(c) = out;
 }
 
-template <int NT, int NCH, int EPI, bool VEC_EPI, bool BYTE = false>
+// MS (multi-source, > 1 only with BYTE): C = sum_s alpha_s A_s . Q_s over MS sources that share
+// the output (the k / v / q input gradients of one LayerNorm output): the reduction runs over
+// MS segments of NCH / MS chunks (K per source, zero-padded to 32 * NCH / MS), each chunk's A
+// from its source, pre-scaled by that source's alpha (fp32 multiply: the product the
+// reference forms with its alpha * Q weight, quant.py:126), the byte image holding the MS
+// code blocks side by side.
+template <int NT, int NCH, int EPI, bool VEC_EPI, bool BYTE = false, int MS = 1>
 __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
     int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
@@ -304,6 +313,24 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   }
   select_pass(A, C, codes, codes1, pass_bits, M, K, N);
   const int64_t rowbase = pass_bits ? (int64_t)blockIdx.y * M : 0;
+  static_assert(MS == 1 || (BYTE && NCH % MS == 0 && MS <= 3), "multi-source: byte image");
+  constexpr int NCHS = NCH / MS;  // chunks per source
+  // (three named scalars, not arrays: a runtime-indexed private array lives in scratch)
+  const float *As0 = A, *As1 = A, *As2 = A;
+  const uint32_t *Cs0 = codes, *Cs1 = codes, *Cs2 = codes;
+  float al0 = 1.0f, al1 = 1.0f, al2 = 1.0f;
+  if constexpr (MS > 1) {
+    const bool one = pass_bits && pass_bits[blockIdx.y] == 1;
+    As0 = ep.gA[0] + rowbase * (int64_t)K;
+    As1 = ep.gA[1] + rowbase * (int64_t)K;
+    As2 = ep.gA[2] + rowbase * (int64_t)K;
+    Cs0 = one ? ep.gcodes1[0] : ep.gcodes[0];
+    Cs1 = one ? ep.gcodes1[1] : ep.gcodes[1];
+    Cs2 = one ? ep.gcodes1[2] : ep.gcodes[2];
+    al0 = effective_alpha(ep.galpha[0], alpha_raw);
+    al1 = effective_alpha(ep.galpha[1], alpha_raw);
+    al2 = effective_alpha(ep.galpha[2], alpha_raw);
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
   const int kpad = NCH > 0 ? 32 * NCH : ((K + 31) & ~31);
@@ -324,7 +351,8 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   const int nwords = 16 * NT * kwp;
   auto decode_store = [&](int idx, uint32_t word) {
     const int nl = idx / kwp, w = idx - nl * kwp;
-    word = (n0 + nl < N && w < KW && idx < nwords) ? word : 0u;
+    // (multi-source: the pad words of each source block are zeroed by word_at)
+    word = (n0 + nl < N && (MS > 1 || w < KW) && idx < nwords) ? word : 0u;
     if constexpr (BYTE) {
       u32x4 b4;
       code_bytes(word, b4);
@@ -355,6 +383,12 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     const int nl = idx / kwp, w = idx - nl * kwp;
     int64_t n = n0 + nl;
     n = n < N ? n : N - 1;
+    if constexpr (MS > 1) {  // source block q = w / (kwp / MS), its word ws
+      const int wps = kwp / MS, q = w / wps, ws = w - q * wps;
+      const uint32_t* cq = q == 0 ? Cs0 : (q == 1 ? Cs1 : Cs2);
+      const uint32_t v = cq[n * KW + (ws < KW ? ws : KW - 1)];
+      return ws < KW ? v : 0u;
+    }
     const int wc = w < KW ? w : KW - 1;
     return codes[n * KW + wc];  // clamped, always valid; out-of-range words are zeroed above
   };
@@ -367,6 +401,17 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     const int64_t m0 = (int64_t)rt * kRows + wave * 16;
     const int64_t row = m0 + r < M ? m0 + r : M - 1;
     return A + row * (int64_t)K;
+  };
+  // chunk c of a row tile (arow = arow_of's pointer): multi-source, chunk c is chunk c % NCHS
+  // of source c / NCHS (c is a compile-time constant wherever the chunk loops are unrolled)
+  auto ldc = [&](const float* arow, int c, f32x4& x, f32x4& y) {
+    if constexpr (MS > 1) {
+      const int q = c / NCHS;
+      const float* src = q == 0 ? As0 : (q == 1 ? As1 : As2);
+      load8(src + (arow - A), 32 * (c - q * NCHS) + kg, K, x, y);
+    } else {
+      load8(arow, 32 * c + kg, K, x, y);
+    }
   };
   // K compile-time (NCH > 0): A chunks are software-pipelined ACROSS row tiles. The first
   // tile's first kWin chunks are issued right after the code words (so the B decode and
@@ -409,7 +454,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
       if constexpr (kCross) {
         const float* a0 = arow_of(rg);
 #pragma unroll
-        for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+        for (int c = 0; c < kWin; ++c) ldc(a0, c, buf[c][0], buf[c][1]);
       }
       __builtin_amdgcn_sched_barrier(0);
       weight_image();
@@ -421,7 +466,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
       if constexpr (kCross) {
         const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
 #pragma unroll
-        for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
+        for (int c = 0; c < kWin; ++c) ldc(a0, c, buf[c][0], buf[c][1]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -437,7 +482,9 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
 
   const __bf16* brow = bimg + r * stride + kg;
   const unsigned char* brow8 = reinterpret_cast<const unsigned char*>(smem) + r * stride + kg;
-  const float a_eff = BYTE ? 2.0f * effective_alpha(alpha, alpha_raw) : effective_alpha(alpha, alpha_raw);
+  const float a_eff = MS > 1 ? 2.0f
+                      : BYTE ? 2.0f * effective_alpha(alpha, alpha_raw)
+                             : effective_alpha(alpha, alpha_raw);
   const uint32_t dkey = (EPI != kEpiNone && ep.dc.on) ? drop_key(ep.rng[0], ep.rng[1] + ep.rng_off) : 0u;
   float bcol[NT];
 #pragma unroll
@@ -457,7 +504,17 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
 
     // All B fragments of the chunk are read first and the split runs while they are in
     // flight; each tile's MFMAs then wait only for their own read (counted lgkmcnt).
-    auto compute = [&](const f32x4& x0, const f32x4& x1, int kc) {
+    auto compute = [&](const f32x4& x0in, const f32x4& x1in, int kc) {
+      f32x4 x0 = x0in, x1 = x1in;
+      if constexpr (MS > 1) {  // alpha of the chunk's source, applied before the exact split
+        const int q = (kc >> 5) / NCHS;
+        const float al = q == 0 ? al0 : (q == 1 ? al1 : al2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // rounded products (no contraction into the split)
+          x0[j] = nc_mul(x0[j], al);
+          x1[j] = nc_mul(x1[j], al);
+        }
+      }
       bf16x8 bq[NT];
       typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
       u32x2 bb[BYTE ? NT : 1];
@@ -501,7 +558,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
       // The last tile re-reads its own rows as the "next" tile (L2 hits, never used).
       if constexpr (!kCross) {  // NT 12: this tile's window is issued here (no cross-tile)
 #pragma unroll
-        for (int c = 0; c < kWin; ++c) load8(arow, 32 * c + kg, K, buf[c][0], buf[c][1]);
+        for (int c = 0; c < kWin; ++c) ldc(arow, c, buf[c][0], buf[c][1]);
         __builtin_amdgcn_sched_barrier(0);
       }
       const int rt_next = rt + rgroups < n_rt ? rt + rgroups : rt;
@@ -509,15 +566,14 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + kWin < NCH)
-          load8(arow, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
+          ldc(arow, c + kWin, buf[c + kWin][0], buf[c + kWin][1]);
         __builtin_amdgcn_sched_barrier(0);
         compute(buf[c][0], buf[c][1], 32 * c);
         // next tile's chunk into the slot just consumed (slot c + kWin - NCH <= c; it IS
         // slot c when kWin == NCH, so the load must follow this chunk's compute)
         if constexpr (kCross) {
           if (c + kWin >= NCH) {
-            load8(anext, 32 * (c + kWin - NCH) + kg, K, buf[c + kWin - NCH][0],
-                  buf[c + kWin - NCH][1]);
+            ldc(anext, c + kWin - NCH, buf[c + kWin - NCH][0], buf[c + kWin - NCH][1]);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -939,6 +995,40 @@ bool launch_ternary_gemm_passes_group(const float* A, int P, int64_t M, int64_t 
     default: return false;
   }
 #undef OB_NTG
+}
+
+bool launch_ternary_dx_sum(int G, const float* const* dY, int P, int64_t M, int64_t N,
+                           const uint32_t* const* codes_t, const uint32_t* const* codes_t1,
+                           const int* pass_bits, const float* const* alpha, int alpha_raw,
+                           int64_t K, float* dX, hipStream_t s) {
+  // the Conformer shape: three 144-wide sources (q / k / v), outputs a multiple of 144
+  if (G != 3 || N != 144 || K <= 0 || K % 144 != 0 || alpha_raw >= 2 || use_f32_gemm())
+    return false;
+  for (int i = 0; i < G; ++i)
+    if (!aligned16(dY[i])) return false;
+  if (!aligned16(dX)) return false;
+  if (M == 0 || P == 0) return true;
+  EpiArgs ep{};
+  ep.glayers = 1;
+  ep.mode = kEpiNone;
+  for (int i = 0; i < G; ++i) {
+    ep.gA[i] = dY[i];
+    ep.gcodes[i] = codes_t[i];
+    ep.gcodes1[i] = codes_t1[i];
+    ep.galpha[i] = alpha[i];
+  }
+  constexpr int kNch = 15;  // 3 sources x 5 chunks (144 zero-padded to 160)
+  const int n_ct = (int)(K / 144);
+  const int n_rt = (int)ceil_div(M, kRows);
+  int rgroups = kTargetBlocksLongK / (n_ct * P);
+  if (rgroups < 1) rgroups = 1;
+  if (rgroups > n_rt) rgroups = n_rt;
+  const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
+  const size_t lds = epi_stage_off(9, 32 * kNch, true) + epi_stage_bytes(9);
+  hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, kNch, kEpiNone, true, true, 3>), grid, dim3(kThreads),
+                     lds, s, dY[0], M, (int)N, codes_t[0], (int)ceil_div(N, 16), (int)K, n_ct,
+                     n_rt, rgroups, alpha[0], alpha_raw, nullptr, dX, codes_t1[0], pass_bits, ep);
+  return true;
 }
 
 void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,

@@ -21,6 +21,7 @@ LIB_NAME = "libonebit_hip.so"
 LIB_PATH = Path(os.environ.get("ONEBIT_HIP_LIB") or Path(__file__).with_name(LIB_NAME))
 
 OB_OK = 0
+OB_ERR_SHAPE = -2
 OB_ERR_BITWIDTH = -3
 
 _c_f = ctypes.c_void_p  # device pointers are passed as raw addresses
@@ -100,6 +101,8 @@ SIGNATURES = {
     "ob_att_kl_workspace": (_sz, [_i64, _i64]),
     "ob_att_kl_loss_fwd": (
         _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _int, _f32, _c_f, _c_f, _c_f, _sz, _c_f]),
+    "ob_bitlinear_bwd_dx_passes_sum": (
+        _int, [_i64, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _i64, _c_f, _c_f]),
     "ob_loss_combine_fwd": (_int, [_c_f, _c_f, _c_f, _f32, _f32, _f32, _c_f, _c_f, _c_f]),
     "ob_loss_combine_bwd": (_int, [_c_f, _f32, _f32, _f32, _c_f, _c_f, _c_f, _c_f]),
     "ob_att_kl_loss_bwd": (

@@ -39,6 +39,9 @@ __all__ = ["ffn_residual", "linear_residual", "fused_supported", "advance_step",
 
 # parity-test hooks (tests/test_fused_gpu.py): False = q / k / v dW, forward one by one
 _DW_GROUP = True
+# q / k / v input gradients summed in one launch (tests flip it to compare with the three
+# launches: plain dX of q, then k and v accumulated through the residual epilogue)
+_DX_SUM = True
 _QKV_FWD_GROUP = True
 _STATE: Dict[torch.device, list] = {}  # device -> [rng tensor {seed, counter}, host offset]
 
@@ -357,7 +360,22 @@ class _QKVFn(torch.autograd.Function):
                   zip((gq, gk, gv), (wq, wk, wv), (aq, ak, av), codes, ctx.has_bias)
                   if g is not None]
         gh = None
-        if ctx.needs_input_grad[0]:
+        if (ctx.needs_input_grad[0] and _DX_SUM and pb is not None and len(layers) == 3
+                and len({c.dx_raw for c in codes}) == 1 and not codes[0].dense):
+            # the three input gradients summed in ONE launch (ob_bitlinear_bwd_dx_passes_sum)
+            n = wq.shape[0]
+            out = torch.empty((rows, k), dtype=torch.float32, device=h.device)
+            arrs = [_lib.ptr_array(v) for v in (
+                [g.data_ptr() for g, _, _, _, _ in layers], [c[2].data_ptr() for c in codes],
+                [c[3].data_ptr() for c in codes], [a.data_ptr() for _, _, a, _, _ in layers])]
+            ad = [ctypes.addressof(x) for x in arrs]
+            st = lib.ob_bitlinear_bwd_dx_passes_sum(3, ad[0], P, m, n, ad[1], ad[2], pb.data_ptr(),
+                                                    ad[3], codes[0].dx_raw, k, out.data_ptr(),
+                                                    stream)
+            if st != _lib.OB_ERR_SHAPE:  # (shape not taken: the per-layer launches below)
+                _lib.check(st, "ob_bitlinear_bwd_dx_passes_sum")
+                gh = out
+        if ctx.needs_input_grad[0] and gh is None:
             for g, w, a, c, _ in layers:
                 n = w.shape[0]
                 if gh is None:

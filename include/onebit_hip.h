@@ -354,6 +354,19 @@ OB_API int ob_bitlinear_bwd_dx_passes(const float* dY, int64_t P, int64_t M, int
                                       const uint32_t* codes2_t, const uint32_t* codes1_t,
                                       const int32_t* pass_bits, const float* alpha,
                                       int alpha_raw, int64_t K, float* dX, void* stream);
+/* The summed input gradient of G BitLinears that read the same input (the q / k / v
+ * projections of one LayerNorm output, conformer.py:111-113; autograd sums their input
+ * gradients): dX = sum_g alpha_g dY_g . Q_g (autograd of quant.py:126 per layer, summed) in
+ * ONE launch, each dY_g [P*M][N] against its own codes (codes2_t[g] / codes1_t[g] as
+ * ob_bitlinear_bwd_dx_passes, per-pass bitwidths from pass_bits), each product formed as
+ * (alpha_g dY_g) Q_g (the reference's dY (alpha Q) product rounding). Host arrays of G
+ * device pointers. Taken for G = 3, N = 144, K a multiple of 144, 16-byte aligned dY / dX;
+ * otherwise OB_ERR_SHAPE with nothing launched (run ob_bitlinear_bwd_dx_passes per source). */
+OB_API int ob_bitlinear_bwd_dx_passes_sum(int64_t G, const float* const* dY, int64_t P,
+                                          int64_t M, int64_t N, const uint32_t* const* codes2_t,
+                                          const uint32_t* const* codes1_t,
+                                          const int32_t* pass_bits, const float* const* alpha,
+                                          int alpha_raw, int64_t K, float* dX, void* stream);
 OB_API size_t ob_bitlinear_bwd_dw_passes_workspace(int64_t P, int64_t M, int64_t N, int64_t K);
 OB_API int ob_bitlinear_bwd_dw_passes(const float* dY, const float* X, int64_t P, int64_t M,
                                       int64_t N, int64_t K, const float* W, const float* alpha,

@@ -343,3 +343,42 @@ def test_qkv_forward_group_equals_separate(gpu, monkeypatch):
             outs[grp] = fused.qkv_projections(h, *layers, bits[0])
     for a, b in zip(outs[True], outs[False]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("sp", [1, 0])
+def test_qkv_input_gradient_summed_in_one_launch(gpu, monkeypatch, sp):
+    """The q / k / v node's input gradient from ONE launch (ob_bitlinear_bwd_dx_passes_sum:
+    the three sources' codes side by side, each chunk pre-scaled by its layer's alpha) against
+    the three launches it replaces (q's plain dX, then k's and v's accumulated through the
+    residual epilogue) and against float64 of the reference's sum of the three layers'
+    dY (alpha Q) products: 1e-6 / 1e-5 of max (only the rounding order differs). Stacked
+    passes at 2 / 1 / (1 or 2) bits, Conformer-S width, rows not a multiple of the tiles."""
+    from onebit_asr import fused
+    from onebit_asr.quant import QuantizedLinear, StackedBits
+    from oracle.quant_oracle import ref_quantize_weight
+
+    P, m, d = 3, 997, 144
+    pass_bits = [2, 1, 1 if sp else 2]
+    torch.manual_seed(0)
+    layers = [QuantizedLinear(d, d).to(gpu) for _ in range(3)]
+    sb = StackedBits(1, gpu)
+    sb.set([sp])
+    h = torch.randn(P * m, d, device=gpu)
+    gouts = [torch.randn(P * m, d, device=gpu) for _ in range(3)]
+    res = {}
+    for on in (False, True):
+        monkeypatch.setattr(fused, "_DX_SUM", on)
+        x = h.clone().requires_grad_()
+        outs = fused.qkv_projections(x, *layers, sb[0])
+        torch.autograd.backward(outs, gouts)
+        res[on] = x.grad.detach().clone()
+    ref = torch.zeros(P * m, d, dtype=torch.float64)
+    with torch.no_grad():
+        for lay, go in zip(layers, gouts):
+            for p in range(P):
+                wq = ref_quantize_weight(lay.weight.detach().cpu(), lay.alpha.detach().cpu(),
+                                         pass_bits[p])
+                ref[p * m:(p + 1) * m] += go[p * m:(p + 1) * m].cpu().double() @ wq.double()
+    scale = ref.abs().max().item()
+    assert (res[True].cpu().double() - res[False].cpu().double()).abs().max().item() <= 1e-6 * scale
+    assert (res[True].cpu().double() - ref).abs().max().item() <= 1e-5 * scale
