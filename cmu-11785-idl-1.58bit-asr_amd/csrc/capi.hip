@@ -350,6 +350,59 @@ int ob_bitlinear_fwd_residual(const float* X, int64_t P, int64_t M, int64_t K,
   return launched();
 }
 
+int ob_bitlinear_fwd_residual_ln(const float* X, int64_t P, int64_t M, int64_t K,
+                                 const uint32_t* codes2, const uint32_t* codes1,
+                                 const int32_t* pass_bits, const float* alpha, int alpha_raw,
+                                 const float* bias, int64_t N, const float* R, float rscale,
+                                 float p_drop, const uint64_t* rng, int64_t rng_offset,
+                                 const int32_t* lens, int64_t T, float* Y, int nln,
+                                 const float* ln_w0, const float* ln_b0, float eps0, float* ln_y0,
+                                 float* ln_mean0, float* ln_rstd0, const float* ln_w1,
+                                 const float* ln_b1, float eps1, float* ln_y1, float* ln_mean1,
+                                 float* ln_rstd1, void* stream) {
+  if (int st = fused_gemm_check(X, P, M, K, codes2, codes1, pass_bits, alpha, N, Y, p_drop, rng))
+    return st;
+  if (nln < 1 || nln > 2) return OB_ERR_SHAPE;
+  if (!ternary_residual_ln_supported(K, N, alpha_raw)) return OB_ERR_SHAPE;  // caller falls back
+  if (M * N > 0 && (!R || !ln_y0 || !ln_mean0 || !ln_rstd0 ||
+                    (nln > 1 && (!ln_y1 || !ln_mean1 || !ln_rstd1))))
+    return OB_ERR_NULL;
+  if (lens && (T < 1 || (P * M) % T)) return OB_ERR_SHAPE;
+  if (T > 0x7fffffff) return OB_ERR_SHAPE;
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!a16(X) || !a16(R) || !a16(Y) || !a16(ln_y0) || !a16(ln_w0) || !a16(ln_b0) ||
+      (nln > 1 && (!a16(ln_y1) || !a16(ln_w1) || !a16(ln_b1))) || !aligned4(bias) ||
+      !aligned4(lens) || !aligned4(ln_mean0) || !aligned4(ln_rstd0) || !aligned4(ln_mean1) ||
+      !aligned4(ln_rstd1))
+    return OB_ERR_ALIGN;
+  TgemmEpi ep{};
+  ep.mode = kEpiResidual;
+  ep.R = R;
+  ep.rscale = rscale;
+  ep.lens = reinterpret_cast<const int*>(lens);
+  ep.T = (int)T;
+  ep.p_drop = p_drop;
+  ep.rng = rng;
+  ep.rng_off = (uint64_t)rng_offset;
+  ep.nln = nln;
+  ep.lng[0] = ln_w0;
+  ep.lnb[0] = ln_b0;
+  ep.lneps[0] = eps0;
+  ep.lny[0] = ln_y0;
+  ep.lnmean[0] = ln_mean0;
+  ep.lnrstd[0] = ln_rstd0;
+  ep.lng[1] = ln_w1;
+  ep.lnb[1] = ln_b1;
+  ep.lneps[1] = eps1;
+  ep.lny[1] = ln_y1;
+  ep.lnmean[1] = ln_mean1;
+  ep.lnrstd[1] = ln_rstd1;
+  launch_ternary_gemm_passes(X, (int)P, M, K, codes2, pass_bits ? codes1 : codes2,
+                             reinterpret_cast<const int*>(pass_bits), N, alpha, alpha_raw, bias, Y,
+                             as_stream(stream), &ep);
+  return launched();
+}
+
 int ob_bitlinear_bwd_dx_swish_drop(const float* dY, int64_t P, int64_t M, int64_t N,
                                    const uint32_t* codes2_t, const uint32_t* codes1_t,
                                    const int32_t* pass_bits, const float* alpha, int alpha_raw,

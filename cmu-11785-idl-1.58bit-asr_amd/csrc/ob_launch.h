@@ -98,7 +98,18 @@ struct TgemmEpi {
   float p_drop;
   const uint64_t* rng;  // device {seed, counter}; required when p_drop > 0
   uint64_t rng_off;     // added to the counter (per call site)
+  // residual epilogue only (N == 144, K = 576 byte path): nln LayerNorms of the produced
+  // rows, ln 1 normalising ln 0's output (the block-final LN and the next block's first)
+  int nln;
+  const float* lng[2];
+  const float* lnb[2];
+  float lneps[2];
+  float* lny[2];
+  float* lnmean[2];
+  float* lnrstd[2];
 };
+// the residual epilogue can normalise its rows (TgemmEpi::nln): the byte-image K = 576 launch
+bool ternary_residual_ln_supported(int64_t K, int64_t N, int alpha_raw);
 
 // out = R + rscale * rowvalid * drop(Y) over [rows][N] (forward twin of drop_scale_bwd).
 void launch_residual_drop_fwd(const float* R, const float* Y, int64_t rows, int64_t N,

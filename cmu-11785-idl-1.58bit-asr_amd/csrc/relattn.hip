@@ -41,6 +41,34 @@
 #include "ob_drop.h"
 #include "ob_launch.h"
 
+namespace {
+// Sums / max / or over the four 16-lane rows of a wave (x op x[lane ^ 16], then ^ 32) on the
+// gfx950 lane-swap instructions (VALU) instead of ds_bpermute round trips through the LDS
+// pipe this kernel's fragments keep busy. permlane16_swap(x, x) returns, per lane, x of
+// both lanes {l, l ^ 16} (in row order) and permlane32_swap those of {l, l ^ 32}; the
+// operations are commutative, so the results are the xor shuffles' bits.
+template <typename F>
+__device__ __forceinline__ uint32_t xrows_1632(uint32_t x, F op) {
+  const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  x = op(a[0], a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return op(b[0], b[1]);
+}
+__device__ __forceinline__ float xsum_1632(float v) {
+  return __builtin_bit_cast(float, xrows_1632(__builtin_bit_cast(uint32_t, v), [](uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b));
+  }));
+}
+__device__ __forceinline__ float xmax_1632(float v) {
+  return __builtin_bit_cast(float, xrows_1632(__builtin_bit_cast(uint32_t, v), [](uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, fmaxf(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b)));
+  }));
+}
+__device__ __forceinline__ uint32_t xor_1632(uint32_t v) {
+  return xrows_1632(v, [](uint32_t a, uint32_t b) { return a | b; });
+}
+}  // namespace
+
 namespace ob {
 
 namespace {
@@ -392,8 +420,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       }
     }
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 16));
-  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  mx = xmax_1632(mx);
   OB_STAMP(4);
   // v rows of the ctx product's first key chunk, in flight over the softmax (DQ <= 9: the
   // registers are free; wider heads load at staging)
@@ -426,8 +453,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       sum += e;
     }
   }
-  sum += __shfl_xor(sum, 16);
-  sum += __shfl_xor(sum, 32);
+  sum = xsum_1632(sum);
   const float rsum = row_live ? 1.0f / sum : 0.0f;
   const int Tp = 16 * nt;  // rows / keys of the saved state
   if (stats && g == 0 && qi < Tp) {
@@ -467,8 +493,7 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
 #pragma unroll
     for (int wd = 0; wd < (NTT + 1) / 2; ++wd) {
       uint32_t x = kw[wd];
-      x |= __shfl_xor(x, 16);
-      x |= __shfl_xor(x, 32);
+      x = xor_1632(x);
       if (wd < W && g == 0 && qi < Tp) kbits[((size_t)bh * Tp + qi) * W + wd] = x;
     }
   }
@@ -633,8 +658,7 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
     float a = 0.0f;
 #pragma unroll
     for (int s = 0; s < DQ; ++s) a = fmaf(dor[s], cr[s], a);
-    a += __shfl_xor(a, 16);
-    a += __shfl_xor(a, 32);
+    a = xsum_1632(a);
     delta = a;
   }
   OB_STAMP(0);
@@ -797,10 +821,8 @@ __global__ __launch_bounds__(kThreads) void relattn_bwd_kernel(
         if (col < D) dq[bo + (size_t)row * C + col] = oq[ct][j] + ov[ct][j];
       }
     }
-    su[ct] += __shfl_xor(su[ct], 16);
-    su[ct] += __shfl_xor(su[ct], 32);
-    sv[ct] += __shfl_xor(sv[ct], 16);
-    sv[ct] += __shfl_xor(sv[ct], 32);
+    su[ct] = xsum_1632(su[ct]);
+    sv[ct] = xsum_1632(sv[ct]);
   }
   const size_t tile_id = ((size_t)b * H + h) * nqt + qt;
 #pragma unroll
@@ -1541,8 +1563,7 @@ __global__ __launch_bounds__(64 * NW) void relattn_bwd_fused_kernel(
         cs += vsum;
       }
       // the job's column sums (du / dvb), accumulated over the chunks in its own LDS slot
-      cs += __shfl_xor(cs, 16);
-      cs += __shfl_xor(cs, 32);
+      cs = xsum_1632(cs);
       if (g == 0) sums[((which * 2 + a) * 2 + half) * DP + 16 * ct + r] += cs;
     }
   }

@@ -34,6 +34,7 @@
 
 #include "ob_drop.h"
 #include "ob_fp.h"
+#include "ob_ln.h"
 #include "ob_launch.h"
 #include "ob_quant.h"
 
@@ -159,6 +160,16 @@ struct EpiArgs {
   // MS > 1 (the dX of q / k / v summed in one launch): the A operand of source s (its rows
   // [P][M][K]); source s reduces against gcodes[s] / gcodes1[s], scaled by galpha[s]
   const float* gA[3];
+  // LayerNorms of the produced rows (residual epilogue, NT 9 byte image: a wave's 16 rows are
+  // complete in its registers): nln of them, LN 1 of LN 0's output (ob_ln.h: the LN kernels'
+  // own row code, so the results equal ob_layernorm_fwd / _pair bit for bit)
+  int nln;
+  const float* lng[2];
+  const float* lnb[2];
+  float lneps[2];
+  float* lny[2];
+  float* lnmean[2];
+  float* lnrstd[2];
   int mode;
   const float* R;
   float* C2;
@@ -255,7 +266,7 @@ __host__ __device__ inline size_t epi_stage_bytes(int nt) {
 // The same epilogue for 4 consecutive columns of one row (col % 4 == 0, N % 4 == 0): R loaded
 // and C / C2 stored as dwordx4, so 16 lanes cover 256 contiguous bytes of the row.
 template <int MODE>
-__device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, float* c,
+__device__ __forceinline__ f32x4 epi_store4(const EpiArgs& ep, uint32_t dkey, float* c,
                                            int64_t grow, int col, int N, f32x4 y, bool valid,
                                            const f32x4& rv) {
   const int64_t i = grow * N + col;
@@ -286,6 +297,7 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& ep, uint32_t dkey, flo
     }
   }
   *reinterpret_cast<f32x4*>(c) = out;
+  return out;
 }
 
 // MS (multi-source, > 1 only with BYTE): C = sum_s alpha_s A_s . Q_s over MS sources that share
@@ -385,8 +397,10 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     n = n < N ? n : N - 1;
     if constexpr (MS > 1) {  // source block q = w / (kwp / MS), its word ws
       const int wps = kwp / MS, q = w / wps, ws = w - q * wps;
-      const uint32_t* cq = q == 0 ? Cs0 : (q == 1 ? Cs1 : Cs2);
-      const uint32_t v = cq[n * KW + (ws < KW ? ws : KW - 1)];
+      // the source's base as an offset from source 0 by arithmetic (a select chain over the
+      // three pointers became a private lookup table in scratch)
+      const int64_t off = (int64_t)(q == 1) * (Cs1 - Cs0) + (int64_t)(q == 2) * (Cs2 - Cs0);
+      const uint32_t v = Cs0[off + n * KW + (ws < KW ? ws : KW - 1)];
       return ws < KW ? v : 0u;
     }
     const int wc = w < KW ? w : KW - 1;
@@ -421,7 +435,8 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
 #ifndef OB_TG_KWMAX_WIDE
 #define OB_TG_KWMAX_WIDE 3
 #endif
-  constexpr int kWmax = NT > 6 ? OB_TG_KWMAX_WIDE : 5;
+  // (multi-source: one block per CU with registers to spare, a deeper window)
+  constexpr int kWmax = MS > 1 ? 5 : NT > 6 ? OB_TG_KWMAX_WIDE : 5;
   // NT 12: the cross-tile live range spills (and a 2-deep window measured slower), so it
   // keeps the per-tile window (issued at the top of each row tile)
   constexpr bool kCross = NT <= 9;
@@ -476,6 +491,22 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     weight_image();
   } else {
     for (int idx = threadIdx.x; idx < nwords; idx += kThreads) decode_store(idx, word_at(idx));
+  }
+  // The residual byte launch's LayerNorm parameters (ep.nln, N = 144): gamma 0, beta 0,
+  // gamma 1, beta 1 staged once per block after the epilogue tiles (an absent gamma / beta
+  // as 1 / 0: the same fmaf) -- at one wave per SIMD nothing hides a global load's latency in
+  // the per-row-group LN.
+  [[maybe_unused]] float* lnp = nullptr;
+  if constexpr (EPI == kEpiResidual && BYTE && NT == 9 && MS == 1) {
+    lnp = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad, BYTE) +
+                                   (size_t)4 * 16 * (16 * NT + 4) * sizeof(float));
+    if (ep.nln > 0 && threadIdx.x < 16 * NT) {
+      const int c = threadIdx.x;
+      lnp[c] = ep.lng[0] ? ep.lng[0][c] : 1.0f;
+      lnp[16 * NT + c] = ep.lnb[0] ? ep.lnb[0][c] : 0.0f;
+      lnp[32 * NT + c] = ep.nln > 1 && ep.lng[1] ? ep.lng[1][c] : 1.0f;
+      lnp[48 * NT + c] = ep.nln > 1 && ep.lnb[1] ? ep.lnb[1][c] : 0.0f;
+    }
   }
   __syncthreads();
   TG_STAMP(0);
@@ -608,6 +639,71 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
       // in issue order; the waitcnt + sched barriers keep hipcc from reordering across them.
       float* stg = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad, BYTE)) + wave * 16 * kEpiLd;
       constexpr int kQ = kEpiCC / 4;  // float4s per staged row
+      // The residual byte-image launch (the FFN lin2 of every block): all 144 columns of the
+      // wave's 16 rows staged at once, then row group by row group (16 lanes a row, lane j
+      // columns 4 (j + 16 i): ob_ln.h's LN row mapping) the residual output formed, stored,
+      // and -- ep.nln -- normalised in registers: the LayerNorm(s) that read this output next
+      // need no launch of their own.
+      if constexpr (EPI == kEpiResidual && BYTE && NT == 9 && MS == 1) {
+        constexpr int kLd = 16 * NT + 4;  // staged row pitch (floats)
+        float* st = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad, BYTE)) + wave * 16 * kLd;
+        const int c4 = lane & 15;
+        auto r_of = [&](int it, f32x4 (&rr)[3]) {  // the residual operand of row group it
+          const int64_t orow = m0 + it * 4 + (lane >> 4);
+          const int64_t rr_row = rowbase + (orow < M ? orow : M - 1);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int col = min(n0 + 64 * i + 4 * c4, N - 4);
+            rr[i] = *reinterpret_cast<const f32x4*>(ep.R + rr_row * N + col);
+          }
+        };
+        f32x4 rr[2][3];
+        r_of(0, rr[0]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            st[(4 * g + reg) * kLd + 16 * t + r] = fmaf(a_eff, acc[t][reg], bcol[t]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          if (it + 1 < 4) r_of(it + 1, rr[(it + 1) & 1]);
+          const int row = it * 4 + (lane >> 4);
+          const int64_t orow = m0 + row;
+          bool valid = true;
+          if (ep.lens) {
+            const int64_t grow = rowbase + orow;
+            const int64_t bb = grow / ep.T;
+            valid = (grow - bb * ep.T) < ep.lens[bb];
+          }
+          float v[3][4];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int cl = 64 * i + 4 * c4;  // column within the tile row
+            f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (orow < M && cl < 16 * NT) {
+              const f32x4 y = *reinterpret_cast<const f32x4*>(st + row * kLd + cl);
+              o = epi_store4<EPI>(ep, dkey, C + orow * N + n0 + cl, rowbase + orow, n0 + cl, N, y,
+                                  valid, rr[it & 1][i]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[i][e] = o[e];  // (zero past the row: the LN load)
+          }
+          if (ep.nln > 0 && orow < M) {  // (uniform over the row's 16 lanes: the DPP sums)
+            float v2[3][4] = {};
+            lnrow::ln_row_v<3, 4>(v, lnp, lnp + 16 * NT, rowbase + orow, N, ep.lneps[0],
+                                  ep.lny[0], ep.lnmean[0], ep.lnrstd[0], nullptr, 0.0f, &v2);
+            if (ep.nln > 1)
+              lnrow::ln_row_v<3, 4>(v2, lnp + 32 * NT, lnp + 48 * NT, rowbase + orow, N,
+                                    ep.lneps[1], ep.lny[1], ep.lnmean[1], ep.lnrstd[1]);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        TG_STAMP(2);
+        continue;
+      }
       constexpr bool kHasR = EPI == kEpiResidual || EPI == kEpiSwishDropBwd;
       // residual rows past their utterance's length (pad-zeroed): a lane's rows are the same
       // in every column chunk, so each is tested once per row tile (32-bit division below
@@ -852,7 +948,12 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
   const int kpad = (int)((K + 31) & ~int64_t(31));
-  const size_t lds = epi_stage_off(NT, kpad, byte) + epi_stage_bytes(NT);
+  // (the residual byte-image launch stages all 16 * NT columns of a wave's rows at once)
+  // (+ the LN parameters: 4 x 16 NT floats)
+  const size_t lds = epi_stage_off(NT, kpad, byte) +
+                     (byte && ep.mode == kEpiResidual
+                          ? (size_t)4 * 16 * (16 * NT + 4) * sizeof(float) + 4 * 16 * NT * sizeof(float)
+                          : epi_stage_bytes(NT));
   const int KW = (int)ceil_div(K, 16);
   const bool vec = (N % 4 == 0) && aligned16(C) && (ep.mode != kEpiSwishDrop || aligned16(ep.C2)) &&
                    ((ep.mode != kEpiResidual && ep.mode != kEpiSwishDropBwd) || aligned16(ep.R));
@@ -921,6 +1022,15 @@ void launch_ternary_gemm_passes(const float* A, int P, int64_t M, int64_t K,
     ep.dc = make_drop(epi->p_drop);
     ep.rng = epi->rng;
     ep.rng_off = epi->rng_off;
+    ep.nln = epi->nln;
+    for (int i = 0; i < 2; ++i) {
+      ep.lng[i] = epi->lng[i];
+      ep.lnb[i] = epi->lnb[i];
+      ep.lneps[i] = epi->lneps[i];
+      ep.lny[i] = epi->lny[i];
+      ep.lnmean[i] = epi->lnmean[i];
+      ep.lnrstd[i] = epi->lnrstd[i];
+    }
   }
   const bool vec = (K % 4 == 0) && K >= 4 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
   const int nt = vec && !use_f32_gemm() ? pick_nt(N, K, ep.mode) : 0;
@@ -995,6 +1105,11 @@ bool launch_ternary_gemm_passes_group(const float* A, int P, int64_t M, int64_t 
     default: return false;
   }
 #undef OB_NTG
+}
+
+bool ternary_residual_ln_supported(int64_t K, int64_t N, int alpha_raw) {
+  return (K + 31) / 32 == 18 && K % 4 == 0 && N == 144 && alpha_raw < 2 && !use_f32_gemm() &&
+         pick_nt(N, K, kEpiResidual) > 0;  // exactly the byte-image branch's conditions
 }
 
 bool launch_ternary_dx_sum(int G, const float* const* dY, int P, int64_t M, int64_t N,

@@ -103,6 +103,10 @@ SIGNATURES = {
         _int, [_c_f, _c_f, _c_f, _i64, _i64, _i64, _int, _f32, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_bitlinear_bwd_dx_passes_sum": (
         _int, [_i64, _c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _i64, _c_f, _c_f]),
+    "ob_bitlinear_fwd_residual_ln": (
+        _int, [_c_f, _i64, _i64, _i64, _c_f, _c_f, _c_f, _c_f, _int, _c_f, _i64, _c_f, _f32, _f32,
+               _c_f, _i64, _c_f, _i64, _c_f, _int, _c_f, _c_f, _f32, _c_f, _c_f, _c_f, _c_f, _c_f,
+               _f32, _c_f, _c_f, _c_f, _c_f]),
     "ob_loss_combine_fwd": (_int, [_c_f, _c_f, _c_f, _f32, _f32, _f32, _c_f, _c_f, _c_f]),
     "ob_loss_combine_bwd": (_int, [_c_f, _f32, _f32, _f32, _c_f, _c_f, _c_f, _c_f]),
     "ob_att_kl_loss_bwd": (

@@ -106,7 +106,9 @@ class FeedForwardModule(nn.Module):
     # act_quant="absmax_int8" LN gets emit_amax (quant.set_act_quant)
     int8_ln = True
 
-    def forward(self, x, bitwidth: int, mask=None):
+    def forward(self, x, bitwidth: int, mask=None, ln_next=None):
+        """ln_next: the LayerNorm module(s) that normalise the output next, in order (training:
+        formed in the last GEMM's epilogue, fused.ffn_residual)."""
         if mask is None and i8_fused_supported(x, self.lin1, self.lin2, bitwidth=bitwidth,
                                                p_drop=self.dropout.p if self.training else 0.0):
             # inference, int8 activations: LN (+absmax) -> lin1 i8 + swish (+absmax of its
@@ -118,7 +120,9 @@ class FeedForwardModule(nn.Module):
             # same computation, elementwise ops in the GEMM epilogues (onebit_asr/fused.py)
             p = self.dropout.p if self.training else 0.0
             h, xr = self.ln.fork(x)
-            return ffn_residual(h, xr, self.lin1, self.lin2, bitwidth, p)
+            lnn = ([(l.ln.weight, l.ln.bias, l.ln.eps) for l in ln_next]
+                   if ln_next and not any(l.emit_amax for l in ln_next) else None)
+            return ffn_residual(h, xr, self.lin1, self.lin2, bitwidth, p, lnn)
         h = self.lin1(self.ln(x), bitwidth)
         h = self.dropout(swish(h))
         h = self.dropout(self.lin2(h, bitwidth))
@@ -398,14 +402,15 @@ class ConformerBlock(nn.Module):
         """next_ln: the LayerNorm that will normalise this block's output next (the following
         block's ff1.ln or the encoder's ln_out); its forward is formed together with this
         block's final LN (layernorm.layer_norm_pair)."""
-        x = self.ff1(x, bitwidth_linear)
+        x = self.ff1(x, bitwidth_linear, ln_next=[self.mhsa.ln])
         x = self.mhsa(x, src_mask, bitwidth_linear, pos_emb)
         passes = bitwidth_linear.passes if isinstance(bitwidth_linear, PassBits) else 1
         # the reference does not pass the mask here (:225); the bitwidth reaches only
         # opt-in ternary pointwise layers
         x = self.conv(x, passes=passes,
                       bitwidth=bitwidth_linear if self.conv.quantize_pointwise else None)
-        x = self.ff2(x, bitwidth_linear)
+        x = self.ff2(x, bitwidth_linear,
+                     ln_next=[self.ln] if next_ln is None or next_ln.emit_amax else [self.ln, next_ln])
         return self.ln(x) if next_ln is None else self.ln.pair(x, next_ln)
 
 

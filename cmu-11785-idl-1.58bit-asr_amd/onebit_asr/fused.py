@@ -202,7 +202,10 @@ class _FFNFn(torch.autograd.Function):
     """conformer.py:36-45 from the LN output h: x + 0.5 * drop(lin2(drop(swish(lin1(h)))))."""
 
     @staticmethod
-    def forward(ctx, h, x, w1, a1, b1, w2, a2, b2, meta):
+    def forward(ctx, h, x, w1, a1, b1, w2, a2, b2, meta, lnreq=None):
+        """lnreq: ([(weight, bias, eps)] x 1 or 2, box) -- the LayerNorm(s) that read the output
+        next, formed in lin2's epilogue (ob_bitlinear_fwd_residual_ln); their (y, mean, rstd)
+        go into box (left empty when the launch shape does not take them)."""
         P, pb, bits, codes1, codes2, p, rng, off1, off2, _ = meta
         rows, k = h.shape
         m = rows // P
@@ -216,11 +219,28 @@ class _FFNFn(torch.autograd.Function):
             a1.data_ptr(), codes1.fwd_raw, _lib.ptr(b1), n1, p, _lib.ptr(rng), off1, pre.data_ptr(),
             act.data_ptr(), stream), "ob_bitlinear_fwd_swish_drop")
         out = torch.empty((rows, n2), dtype=torch.float32, device=h.device)
-        _lib.check(lib.ob_bitlinear_fwd_residual(
-            act.data_ptr(), P, m, n1, codes2[0].data_ptr(), codes2[1].data_ptr(), _lib.ptr(pb),
-            a2.data_ptr(), codes2.fwd_raw, _lib.ptr(b2), n2, x.data_ptr(), 0.5, p, _lib.ptr(rng),
-            off2, None, 0,
-            out.data_ptr(), stream), "ob_bitlinear_fwd_residual")
+        st = _lib.OB_ERR_SHAPE
+        if lnreq is not None:
+            reqs, box = lnreq
+            lno = [(torch.empty_like(out), torch.empty((rows,), dtype=torch.float32, device=h.device),
+                    torch.empty((rows,), dtype=torch.float32, device=h.device)) for _ in reqs]
+            r1, o1 = (reqs[1], lno[1]) if len(reqs) > 1 else ((None, None, 0.0), (None,) * 3)
+            st = lib.ob_bitlinear_fwd_residual_ln(
+                act.data_ptr(), P, m, n1, codes2[0].data_ptr(), codes2[1].data_ptr(),
+                _lib.ptr(pb), a2.data_ptr(), codes2.fwd_raw, _lib.ptr(b2), n2, x.data_ptr(), 0.5,
+                p, _lib.ptr(rng), off2, None, 0, out.data_ptr(), len(reqs), _lib.ptr(reqs[0][0]),
+                _lib.ptr(reqs[0][1]), float(reqs[0][2]), *(_lib.ptr(t) for t in lno[0]),
+                _lib.ptr(r1[0]), _lib.ptr(r1[1]), float(r1[2]), *(_lib.ptr(t) for t in o1), stream)
+            if st == _lib.OB_OK:
+                box.extend((*r, *o) for r, o in zip(reqs, lno))
+            elif st != _lib.OB_ERR_SHAPE:
+                _lib.check(st, "ob_bitlinear_fwd_residual_ln")
+        if st != _lib.OB_OK:
+            _lib.check(lib.ob_bitlinear_fwd_residual(
+                act.data_ptr(), P, m, n1, codes2[0].data_ptr(), codes2[1].data_ptr(),
+                _lib.ptr(pb), a2.data_ptr(), codes2.fwd_raw, _lib.ptr(b2), n2, x.data_ptr(), 0.5,
+                p, _lib.ptr(rng), off2, None, 0, out.data_ptr(), stream),
+                "ob_bitlinear_fwd_residual")
         ctx.meta = meta
         ctx.has_bias = (b1 is not None, b2 is not None)
         ctx.biases = (b1, b2)
@@ -255,7 +275,11 @@ class _FFNFn(torch.autograd.Function):
         gh = _dx(lib, dpre, P, m, n1, codes1, pb, a1, k, stream) if ctx.needs_input_grad[0] else None
         gw1, ga1, gb1 = _dw(lib, dpre, h, P, m, n1, k, w1, a1, ctx.has_bias[0], pb, bits, stream,
                             ctx.biases[0], codes1.dense)
-        return gh, gout, gw1, ga1, gb1, gw2, ga2, gb2, None
+        return gh, gout, gw1, ga1, gb1, gw2, ga2, gb2, None, None
+
+
+# parity-test hook (tests/test_fused_gpu.py): False = the LNs after the FFN their own launches
+_LN_EPI = True
 
 
 class _LinearResidualFn(torch.autograd.Function):
@@ -461,8 +485,14 @@ def _flat(t: torch.Tensor, width: int) -> torch.Tensor:
 
 
 def ffn_residual(h: torch.Tensor, x: torch.Tensor, lin1: QuantizedLinear, lin2: QuantizedLinear,
-                 bitwidth, p_drop: float) -> torch.Tensor:
-    """x + 0.5 * dropout(lin2(dropout(swish(lin1(h))))) (conformer.py:36-45); h = LN(x)."""
+                 bitwidth, p_drop: float, ln_next=None) -> torch.Tensor:
+    """x + 0.5 * dropout(lin2(dropout(swish(lin1(h))))) (conformer.py:36-45); h = LN(x).
+
+    ln_next: [(weight, bias, eps)] of the LayerNorm that normalises the output next (and,
+    second entry, the LayerNorm of that one's output -- a block's final LN and the next
+    block's first): formed in lin2's epilogue and picked up by those LNs' layer_norm /
+    layer_norm_fork / layer_norm_pair calls (bit-identical to their own launches). Training
+    only (grad enabled): inference consumers may take the int8 LN instead."""
     P, pb, bits = _bits_args(bitwidth)
     h2, x2 = _flat(h, lin1.in_features), _flat(x, lin2.out_features)
     if h2.shape[0] % P:
@@ -472,9 +502,18 @@ def ffn_residual(h: torch.Tensor, x: torch.Tensor, lin1: QuantizedLinear, lin2: 
     spec = GradScale(0.5, p_drop, rng, off2)
     meta = (P, pb, bits, _codes(lin1, P, bits), _codes(lin2, P, bits), float(p_drop), rng,
             off1, off2, spec)
+    box = []
+    lnreq = (([(w, b, float(e)) for w, b, e in ln_next], box)
+             if ln_next and _LN_EPI and torch.is_grad_enabled() and 1 <= len(ln_next) <= 2
+             else None)
     out = _FFNFn.apply(h2, x2, lin1.weight, lin1.alpha, lin1.bias, lin2.weight, lin2.alpha,
-                       lin2.bias, meta)
-    return attach_grad_scale(out.view(x.shape), spec)
+                       lin2.bias, meta, lnreq)
+    out = attach_grad_scale(out.view(x.shape), spec)
+    if box:
+        out._ob_ln_pre = box[0]
+        if len(box) > 1:
+            out._ob_ln_pre2 = box[1]
+    return out
 
 
 def linear_residual(inp: torch.Tensor, x: torch.Tensor, lin: QuantizedLinear, bitwidth,

@@ -112,6 +112,13 @@ class _LayerNormFn(torch.autograd.Function):
         if pre is not None:
             y, mean, rstd = pre[:3]
             ctx.pre_link = pre[3] if len(pre) > 3 else None
+            if pair is not None and len(pair) > 4:
+                # the next LN of y was formed too (by the GEMM epilogue that produced x): hand
+                # it on as a pair launch would
+                w2, b2, eps2, box, (y2, mean2, rstd2) = pair
+                link = _PairLink(x2, weight, bias, mean, rstd, spec, ctx.needs_input_grad[:3])
+                ctx.link = link
+                box.append((w2, b2, float(eps2), y2, mean2, rstd2, link))
         elif pair is not None:
             w2, b2, eps2, box = pair
             y = torch.empty_like(x2)
@@ -200,6 +207,18 @@ def _take_pre(x: torch.Tensor, weight, bias, eps):
     return pre[3:]
 
 
+def _take_pre2(x: torch.Tensor, weight, bias, eps):
+    """The (y2, mean2, rstd2) of the LN following LN(x), formed with LN(x) by the epilogue of
+    the GEMM that produced x (fused.ffn_residual's ln_next)."""
+    pre = getattr(x, "_ob_ln_pre2", None)
+    if pre is None:
+        return None
+    x._ob_ln_pre2 = None
+    if pre[0] is not weight or pre[1] is not bias or pre[2] != float(eps):
+        return None
+    return pre[3:6]
+
+
 def layer_norm(x: torch.Tensor, weight, bias, eps: float = 1e-5) -> torch.Tensor:
     d = x.shape[-1]
     if not fused_layernorm_supported(x, d):
@@ -216,8 +235,10 @@ def layer_norm_pair(x: torch.Tensor, weight, bias, eps, weight2, bias2, eps2) ->
     if not (_PAIR and torch.is_grad_enabled() and fused_layernorm_supported(x, d)):
         return layer_norm(x, weight, bias, eps)
     box = []
-    y = _LayerNormFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None),
-                           _take_pre(x, weight, bias, eps), (weight2, bias2, eps2, box))
+    pre = _take_pre(x, weight, bias, eps)
+    pre2 = _take_pre2(x, weight2, bias2, eps2) if pre is not None else None
+    pair = (weight2, bias2, eps2, box) if pre2 is None else (weight2, bias2, eps2, box, pre2)
+    y = _LayerNormFn.apply(x, weight, bias, eps, getattr(x, "_ob_gscale", None), pre, pair)
     if box:
         y._ob_ln_pre = box[0]
     return y

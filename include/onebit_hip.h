@@ -710,6 +710,22 @@ OB_API int ob_bitlinear_fwd_residual(const float* X, int64_t P, int64_t M, int64
                                      const float* bias, int64_t N, const float* R, float rscale,
                                      float p_drop, const uint64_t* rng, int64_t rng_offset,
                                      const int32_t* lens, int64_t T, float* Y, void* stream);
+/* ob_bitlinear_fwd_residual whose epilogue also forms the LayerNorm(s) that read Y next
+ * (conformer.py:19-24, nn.LayerNorm(d)): nln = 1: ln_y0 = LN0(Y) with its per-row mean / rstd
+ * (the statistics ob_layernorm_bwd takes); nln = 2: also ln_y1 = LN1(ln_y0) (a block's final LN
+ * and the next block's first, as ob_layernorm_fwd_pair). Same row arithmetic as the LN kernels
+ * (bit-identical results). Taken for the K = 576 byte-image launch with N = 144 (the Conformer
+ * FFN's second linear); otherwise OB_ERR_SHAPE with nothing launched (run
+ * ob_bitlinear_fwd_residual and ob_layernorm_fwd[_pair]). X, R, Y, ln_y*, ln_w*, ln_b* 16-byte
+ * aligned; rows of all outputs [P*M][N]. */
+OB_API int ob_bitlinear_fwd_residual_ln(
+    const float* X, int64_t P, int64_t M, int64_t K, const uint32_t* codes2,
+    const uint32_t* codes1, const int32_t* pass_bits, const float* alpha, int alpha_raw,
+    const float* bias, int64_t N, const float* R, float rscale, float p_drop, const uint64_t* rng,
+    int64_t rng_offset, const int32_t* lens, int64_t T, float* Y, int nln, const float* ln_w0,
+    const float* ln_b0, float eps0, float* ln_y0, float* ln_mean0, float* ln_rstd0,
+    const float* ln_w1, const float* ln_b1, float eps1, float* ln_y1, float* ln_mean1,
+    float* ln_rstd1, void* stream);
 OB_API int ob_bitlinear_bwd_dx_swish_drop(const float* dY, int64_t P, int64_t M, int64_t N,
                                           const uint32_t* codes2_t, const uint32_t* codes1_t,
                                           const int32_t* pass_bits, const float* alpha,

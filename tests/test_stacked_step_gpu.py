@@ -119,9 +119,13 @@ def test_layernorm_pairs_equal_single_launches(gpu, monkeypatch):
     from onebit_asr.data import CFG1, synthetic_batch
     from onebit_asr.train_step import OneBitStep
 
+    from onebit_asr import fused
+
     cfg = dict(CFG1, enc_d_model=144, enc_d_ff=576)
     batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
     res, losses, taken = {}, {}, {}
+    # (the FFN epilogue would form these LNs too: left to the pair / single launches here)
+    monkeypatch.setattr(fused, "_LN_EPI", False)
     for on in (False, True):
         monkeypatch.setattr(layernorm, "_PAIR", on)
         calls = []
@@ -143,6 +147,54 @@ def test_layernorm_pairs_equal_single_launches(gpu, monkeypatch):
         taken[on] = sum(calls)
         res[on] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
     assert taken[False] == 0 and taken[True] >= 2, taken
+    assert torch.equal(losses[False], losses[True])
+    assert res[False].keys() == res[True].keys()
+    for k in res[False]:
+        assert torch.equal(res[False][k], res[True][k]), k
+
+
+def test_ffn_layernorm_epilogue_equals_separate(gpu, monkeypatch):
+    """The LayerNorms after each FFN (ff1 -> mhsa.ln; ff2 -> the block's final LN and the next
+    LN) formed in the FFN's second-GEMM epilogue (ob_bitlinear_fwd_residual_ln) == their own
+    launches (ob_layernorm_fwd / ob_layernorm_fwd_pair): loss and every gradient of the
+    stacked step bit for bit, and both epilogue forms (one LN, two LNs) were taken."""
+    from onebit_asr import fused, layernorm
+    from onebit_asr.conformer import ConformerASR
+    from onebit_asr.data import CFG1, synthetic_batch
+    from onebit_asr.train_step import OneBitStep
+
+    cfg = dict(CFG1, enc_d_model=144, enc_d_ff=576)
+    batch = synthetic_batch([400, 233], [17, 9], seed=0, device=gpu)
+    res, losses, taken = {}, {}, {}
+    for on in (False, True):
+        monkeypatch.setattr(fused, "_LN_EPI", on)
+        calls = {"pre": 0, "pre2": 0}
+
+        def spy(*a, orig=layernorm._take_pre, calls=calls):
+            r = orig(*a)
+            calls["pre"] += int(r is not None and len(r) == 3)  # (not a pair launch's)
+            return r
+
+        def spy2(*a, orig=layernorm._take_pre2, calls=calls):
+            r = orig(*a)
+            calls["pre2"] += int(r is not None)
+            return r
+
+        monkeypatch.setattr(layernorm, "_take_pre", spy)
+        monkeypatch.setattr(layernorm, "_take_pre2", spy2)
+        torch.manual_seed(0)
+        m = ConformerASR(80, 5004, **cfg).to(gpu)
+        step = OneBitStep(m, n_layers=2, stacked=True)
+        loss, _ = step(batch, [1, 0])
+        loss.backward()
+        torch.cuda.synchronize()
+        losses[on] = loss.detach().clone()
+        taken[on] = dict(calls)
+        res[on] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    n_blocks = len(m.encoder.blocks)
+    assert taken[False] == {"pre": 0, "pre2": 0}, taken
+    # every block: mhsa.ln from ff1, the final LN from ff2 (+ its pair partner)
+    assert taken[True]["pre"] >= 2 * n_blocks and taken[True]["pre2"] >= n_blocks, taken
     assert torch.equal(losses[False], losses[True])
     assert res[False].keys() == res[True].keys()
     for k in res[False]:
