@@ -9,7 +9,9 @@ B=$2; shift 2
 run() {  # side dir [switch]
   local side=$1 dir=$2 sw=$3
   local pre="import sys, runpy; sys.argv=['bench.py','--no-cpu-baseline','--no-roofline','--steps','20']; sys.path.insert(0, '$dir/cmu-11785-idl-1.58bit-asr_amd')"
-  if [ -n "$sw" ]; then
+  if [ "${sw#env:}" != "$sw" ]; then  # env:NAME=VALUE (e.g. ONEBIT_HIP_LIB=exp/lib_x.so)
+    pre="$pre; import os; os.environ['${sw#env:}'.split('=')[0]] = '$R/' + '${sw#env:}'.split('=', 1)[1]"
+  elif [ -n "$sw" ]; then
     local mod=${sw%%.*} rest=${sw#*.}
     pre="$pre; from onebit_asr import $mod; $mod.${rest}"
   fi
