@@ -203,12 +203,14 @@ int64_t image_slots(int C, int im) {
 
 // ------------------------------------------------------------------------------------
 // ss_gemm6<NT, MR, DGRAD>: C_tile[64 MR][16 NT] = A[rows][K] . B[K][16 NT] with A gathered
-// from Y1 (fwd) or G (dgrad class), split into bf16 planes in LDS; B = a weight image.
-// Block = 4 waves (16 MR rows each, all 16 NT columns); a block takes a contiguous range of
-// its class's row tiles (blockIdx.y = class; fwd: one class), consecutive ranges on one XCD
-// (the taps of neighbouring tiles overlap in Y1 / G). One LDS stage; the next k step's A
-// (2 MR dwordx4 per thread) and B (image slots) are loaded into registers while the
+// from Y1 (fwd) or G (dgrad class) and split into bf16 planes in registers (each wave's rows
+// are its own: no LDS round trip for A); B = a weight image, staged in LDS double-buffered
+// (one barrier per k step). Block = 4 waves (16 MR rows each, all 16 NT columns); a block
+// takes a contiguous range of its class's row tiles (blockIdx.y = class; fwd: one class),
+// consecutive ranges on one XCD (the taps of neighbouring tiles overlap in Y1 / G). The next
+// k step's A (2 MR dwordx4 per lane) and B (image slots) are loaded into registers while the
 // current step's MFMAs run. The image is re-read per tile (L2-resident, 64 MR rows share it).
+// Same products in the same order as the LDS-A form (round 4): the same bits.
 // ------------------------------------------------------------------------------------
 struct GemmArgs {
   const float* src;             // fwd: Y1; dgrad: G
@@ -229,21 +231,24 @@ struct GemmArgs {
 template <int NT, int MR, bool DGRAD>
 struct GemmCfg {
   static constexpr int BN = 16 * NT;
-  static constexpr int BM = 64 * MR;
-  static constexpr int kBSlotsPT = (BN * kSlot / 16 + kThr - 1) / kThr;  // B dwordx4 / thread
-  static constexpr size_t kLdsMain = (size_t)(BM + BN) * kSlot;
+  // waves per block (8-wave forward blocks, one per CU, a B step serving 256 rows: 417 ->
+  // 494 us a call -- the B image's L2 reads are not what limits it)
+  static constexpr int WV = 4;
+  static constexpr int kT = 64 * WV;
+  static constexpr int BM = 16 * WV * MR;
+  static constexpr int kBSlotsPT = (BN * kSlot / 16 + kT - 1) / kT;  // B dwordx4 / thread
+  static constexpr size_t kLdsMain = (size_t)2 * BN * kSlot;  // B image steps, double-buffered
   static constexpr size_t kLdsEpi = DGRAD ? (size_t)(BM * 16 + 4 * BN * 16) * 4 : 0;
   static constexpr size_t kW0Off = kLdsMain > kLdsEpi ? kLdsMain : kLdsEpi;  // dgrad: W0|b0
   static constexpr size_t kLds = kW0Off + (DGRAD ? (size_t)BN * 12 * 4 : 0);
 };
 
 template <int NT, int MR, bool DGRAD>
-__global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
+__global__ __launch_bounds__((GemmCfg<NT, MR, DGRAD>::kT), 2) void ss_gemm6_kernel(
+    GemmArgs ga) {
   using Cf = GemmCfg<NT, MR, DGRAD>;
-  constexpr int BN = Cf::BN, BM = Cf::BM, kBSlotsPT = Cf::kBSlotsPT;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  unsigned char* la = lds;                // A: BM rows x 224 B
-  unsigned char* lb = lds + BM * kSlot;   // B: BN columns x 224 B
+  constexpr int BN = Cf::BN, BM = Cf::BM, kBSlotsPT = Cf::kBSlotsPT, WV = Cf::WV, kT = Cf::kT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // B: 2 x BN columns x 224 B
   const SsDims& d = ga.d;
   const int C = d.C;
   const int cl = DGRAD ? (int)blockIdx.y : 0;
@@ -284,34 +289,35 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
 
   if (DGRAD) {  // conv0's weights and bias, [C][12], for the relu'(Y1) recompute
     float* w0s = reinterpret_cast<float*>(lds + Cf::kW0Off);
-    for (int e = threadIdx.x; e < BN * 12; e += kThr) {
+    for (int e = threadIdx.x; e < BN * 12; e += kT) {
       const int c = e / 12, tp = e - 12 * (e / 12);
       w0s[e] = tp < 9 ? ga.W0[c * 9 + tp] : (tp == 9 ? ga.b0[c] : 0.0f);
     }
   }  // (read after the first tile's barriers)
   // conv0 weight-gradient running sums (dgrad): o = threadIdx.x + 256 j = c * 16 + tap
-  constexpr int kW0J = DGRAD ? (BN * 16 + kThr - 1) / kThr : 1;
+  constexpr int kW0J = DGRAD ? (BN * 16 + kT - 1) / kT : 1;
   float w0acc[kW0J];
 #pragma unroll
   for (int j = 0; j < kW0J; ++j) w0acc[j] = 0.0f;
 
   for (int64_t tile = t_begin; tile < t_end; ++tile) {
     const int64_t m0 = tile * BM;
-    // A loader units: row ar[u] = threadIdx.x / 4 + 64 u of the tile, k group threadIdx.x % 4
-    const int aq = threadIdx.x & 3;
+    // A never touches LDS: each wave loads, splits and feeds its own rows from registers --
+    // lane (r, g) holds row 16 (wave + WV u) + r of the tile, k = 8g .. 8g + 7 of the step,
+    // exactly the MFMA A fragment (A rows are not shared between waves).
     int ab[MR], ap1[MR], ap2[MR];
     bool aok[MR];
 #pragma unroll
     for (int u = 0; u < MR; ++u) {
-      const int64_t am = m0 + (threadIdx.x >> 2) + 64 * u;
+      const int64_t am = m0 + 16 * (wave + WV * u) + r;
       aok[u] = am < rows;
       geom(aok[u] ? am : rows - 1, ab[u], ap1[u], ap2[u]);
     }
     // Loads are unconditional from clamped addresses, and rows / taps outside the image are
-    // zeroed at the LDS store (a guarded load makes hipcc branch and wait vmcnt(0) at it,
+    // zeroed before the split (a guarded load makes hipcc branch and wait vmcnt(0) at it,
     // which serializes the prefetch with the MFMAs).
     auto load_a = [&](int st, f32x4 (&ax)[MR][2], uint32_t& aval) {
-      const int k = 32 * st + 8 * aq;  // 8 consecutive k within one tap (C % 8 == 0)
+      const int k = 32 * st + 8 * g;  // 8 consecutive k within one tap (C % 8 == 0)
       const bool kok = k < K;
       const int kc = kok ? k : 0;
       const int tt = kc / C, cc = kc - tt * C;
@@ -346,9 +352,17 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
       const f32x4* s4 = reinterpret_cast<const f32x4*>(img + (int64_t)st * BN * kSlot);
 #pragma unroll
       for (int j = 0; j < kBSlotsPT; ++j) {
-        const int e = threadIdx.x + j * kThr;
+        const int e = threadIdx.x + j * kT;
         const int ec = e < BN * kSlot / 16 ? e : BN * kSlot / 16 - 1;  // clamped, unguarded
         bv[j] = s4[ec];
+      }
+    };
+    auto store_b = [&](int buf, const f32x4 (&bv)[kBSlotsPT]) {
+      f32x4* d4 = reinterpret_cast<f32x4*>(lds + (size_t)buf * BN * kSlot);
+#pragma unroll
+      for (int j = 0; j < kBSlotsPT; ++j) {
+        const int e = threadIdx.x + j * kT;
+        if (e < BN * kSlot / 16) d4[e] = bv[j];
       }
     };
     f32x4 ax[MR][2], bv[kBSlotsPT];
@@ -360,12 +374,16 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
     for (int u = 0; u < MR; ++u)
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();  // (dgrad: the previous tile's epilogue is done with the LDS)
+    store_b(0, bv);
+    __syncthreads();
+    // One barrier a step: step st reads B buffer st & 1 (stored during step st - 1) while
+    // step st + 1's B goes into the other buffer, whose last readers (step st - 1) all
+    // passed the previous barrier.
     for (int st = 0; st < ks; ++st) {
-      __syncthreads();  // the previous step's fragment reads are done
+      bf16x8 a[MR][3];
 #pragma unroll
       for (int u = 0; u < MR; ++u) {
-        // A: split 8 values (k = 8 aq .. +7 of row ar) into the row's slot
-        unsigned char* s = la + ((threadIdx.x >> 2) + 64 * u) * kSlot + 16 * aq;
         const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
         const bool ok = (aval >> u) & 1u;
         const f32x4 x0 = ok ? ax[u][0] : z4, x1 = ok ? ax[u][1] : z4;
@@ -374,30 +392,15 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
         split2(x0[2], x0[3], ph[1], pm[1], pl[1]);
         split2(x1[0], x1[1], ph[2], pm[2], pl[2]);
         split2(x1[2], x1[3], ph[3], pm[3], pl[3]);
-        *reinterpret_cast<uint4*>(s) = uint4{ph[0], ph[1], ph[2], ph[3]};
-        *reinterpret_cast<uint4*>(s + 64) = uint4{pm[0], pm[1], pm[2], pm[3]};
-        *reinterpret_cast<uint4*>(s + 128) = uint4{pl[0], pl[1], pl[2], pl[3]};
+        a[u][0] = __builtin_bit_cast(bf16x8, uint4{ph[0], ph[1], ph[2], ph[3]});
+        a[u][1] = __builtin_bit_cast(bf16x8, uint4{pm[0], pm[1], pm[2], pm[3]});
+        a[u][2] = __builtin_bit_cast(bf16x8, uint4{pl[0], pl[1], pl[2], pl[3]});
       }
-      {
-        f32x4* d4 = reinterpret_cast<f32x4*>(lb);
-#pragma unroll
-        for (int j = 0; j < kBSlotsPT; ++j) {
-          const int e = threadIdx.x + j * kThr;
-          if (e < BN * kSlot / 16) d4[e] = bv[j];
-        }
-      }
-      __syncthreads();
       if (st + 1 < ks) {
         load_a(st + 1, ax, aval);
         load_b(st + 1, bv);
       }
-      bf16x8 a[MR][3];
-#pragma unroll
-      for (int u = 0; u < MR; ++u) {
-        const unsigned char* sa = la + (16 * (wave + 4 * u) + r) * kSlot + 16 * g;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) a[u][q] = *reinterpret_cast<const bf16x8*>(sa + 64 * q);
-      }
+      const unsigned char* lb = lds + (size_t)(st & 1) * BN * kSlot;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const unsigned char* sb = lb + (16 * t + r) * kSlot + 16 * g;
@@ -411,9 +414,11 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
             acc[u][t] = mfma_bf16(a[u][kProdA[p]], bq[kProdB[p]], acc[u][t]);
           }
       }
+      if (st + 1 < ks) store_b((st + 1) & 1, bv);
+      __syncthreads();
     }
 
-    // D[row = 4g + reg][col = r] of (row frag u, column tile t): tile row 16 (wave + 4u) +
+    // D[row = 4g + reg][col = r] of (row frag u, column tile t): tile row 16 (wave + WV u) +
     // 4g + reg, column 16t + r
     if (!DGRAD) {
       // branch-free stores: rows past the end get an offset outside the descriptor (dropped)
@@ -425,7 +430,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
       for (int u = 0; u < MR; ++u)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
-          const int64_t m = m0 + 16 * (wave + 4 * u) + 4 * g + reg;
+          const int64_t m = m0 + 16 * (wave + WV * u) + 4 * g + reg;
           const uint32_t ob = m < rows ? (uint32_t)(m * C + r) * 4 : 0xFFFFFFF0u;
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
       float* xw = reinterpret_cast<float*>(lds);  // [BM][16]
       float* wred = xw + BM * 16;                 // [4 waves][BN][16]
       const float* w0s = reinterpret_cast<const float*>(lds + Cf::kW0Off);  // [BN][12]
-      for (int e = threadIdx.x; e < BM * 16; e += kThr) {
+      for (int e = threadIdx.x; e < BM * 16; e += kT) {
         const int lr = e >> 4, tp = e & 15;
         const int64_t m = m0 + lr;
         int bb, t1, f1;
@@ -467,7 +472,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
         for (int u = 0; u < MR; ++u)
 #pragma unroll
           for (int reg = 0; reg < 4; ++reg) {
-            const int lr = 16 * (wave + 4 * u) + 4 * g + reg;
+            const int lr = 16 * (wave + WV * u) + 4 * g + reg;
             const bool ok = m0 + lr < rows;
             const f32x4 x0 = *reinterpret_cast<const f32x4*>(xw + lr * 16);
             const f32x4 x1 = *reinterpret_cast<const f32x4*>(xw + lr * 16 + 4);
@@ -493,7 +498,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
       for (int u = 0; u < MR; ++u)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
-          const float xb = xw[(16 * (wave + 4 * u) + 4 * g + reg) * 16 + r];
+          const float xb = xw[(16 * (wave + WV * u) + 4 * g + reg) * 16 + r];
 #pragma unroll
           for (int t = 0; t < NT; ++t)
             dw[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(acc[u][t][reg], xb, dw[t], 0, 0, 0);
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < kW0J; ++j) {
-        const int o = threadIdx.x + j * kThr;
+        const int o = threadIdx.x + j * kT;
         if (o < BN * 16)
           w0acc[j] += ((wred[o] + wred[BN * 16 + o]) + wred[2 * BN * 16 + o]) +
                       wred[3 * BN * 16 + o];
@@ -518,7 +523,7 @@ __global__ __launch_bounds__(kThr, 2) void ss_gemm6_kernel(GemmArgs ga) {
     float* dst = ga.part0 + (int64_t)(ga.blk_off[cl] + L) * (BN * 10);
 #pragma unroll
     for (int j = 0; j < kW0J; ++j) {
-      const int o = threadIdx.x + j * kThr, c = o >> 4, tp = o & 15;
+      const int o = threadIdx.x + j * kT, c = o >> 4, tp = o & 15;
       if (o < BN * 16 && tp < 10) dst[c * 10 + tp] = w0acc[j];
     }
   }
@@ -892,7 +897,8 @@ template <int NT, bool DG>
 static void launch_gemm6(const GemmArgs& ga, dim3 grid, hipStream_t s) {
   constexpr int MR = 2;
   constexpr size_t lds = GemmCfg<NT, MR, DG>::kLds;
-  hipLaunchKernelGGL((ss_gemm6_kernel<NT, MR, DG>), grid, dim3(kThr), lds, s, ga);
+  hipLaunchKernelGGL((ss_gemm6_kernel<NT, MR, DG>), grid, dim3(GemmCfg<NT, MR, DG>::kT), lds, s,
+                     ga);
 }
 
 template <bool DG>
@@ -922,7 +928,8 @@ void launch_subsample_fwd(const float* X, int64_t B, int64_t T, int64_t F, int64
   ga.bias = b2;
   ga.out = Y2;
   ga.d = d;
-  const int64_t tiles = (ga.rows[0] + 2 * kBM - 1) / (2 * kBM);
+  const int64_t bm = GemmCfg<9, 2, false>::BM;  // (BM does not depend on NT)
+  const int64_t tiles = (ga.rows[0] + bm - 1) / bm;
   const dim3 grid((unsigned)(tiles < 512 ? tiles : 512));  // 2 resident per CU
   launch_gemm6_c<false>(C, ga, grid, s);
 }
