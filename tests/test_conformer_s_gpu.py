@@ -100,9 +100,11 @@ def test_s_literal_matches_stacked_and_replays(s_model, gpu, stacked_ref):
         elif k.endswith(".alpha"):
             d = abs(g_l[k].item() - g_s[k].item())
             assert d <= max(2e-3 * abs(g_s[k].item()), 1e-3 * med), (k, g_l[k], g_s[k], med)
-        elif k.endswith(("pos_bias_u", "pos_bias_v")):
+        elif k.endswith(("pos_bias_u", "pos_bias_v", "pos_proj.weight")):
             # like alpha: one column sum over all 23904 query rows of dQ (csrc/relattn.hip
-            # bias reduce), summed in a different order in the two layouts (seen 1.3e-4)
+            # bias reduce), summed in a different order in the two layouts (seen 1.3e-4);
+            # pos_proj's weight gradient is dpos . pos with dpos the sum over every batch
+            # row of the pass (the same reduce launch, seen 1.1e-4)
             assert e <= 5e-4, (k, e)
         else:
             assert e <= 1e-4, (k, e)
