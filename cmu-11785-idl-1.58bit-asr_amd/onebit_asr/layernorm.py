@@ -385,7 +385,13 @@ def _pair_backward(ctx, link, gy, gres):
 def _pair_correction(ctx, gy, du, dw1, db1, deferred1):
     """The first LN of a pair whose output had another consumer: du, dw1, db1 are its
     backward for the pair consumer's gradient only; add the LN backward of the rest
-    (g_other = gy - du) -- dgamma / dbeta after the deferred tables have written theirs."""
+    (g_other = gy - du) -- dgamma / dbeta after the deferred tables have written theirs.
+
+    A fallback, accurate to the rounding of the TOTAL gradient: g_other is recovered by a
+    subtraction, so each element carries an error up to ulp(|du|); when |du| >> |g_other| the
+    other consumer's share is resolved only to that absolute level (tests/
+    test_defer_safety_gpu.py bounds it at 1e-5 of max |dx|). The Conformer never takes this
+    path (a block's output feeds only the LN pair), so it guards correctness, not speed."""
     x2, weight, mean, rstd = ctx.saved_tensors
     rows, d = x2.shape
     g_other = (gy.reshape(rows, d) - du.view(rows, d)).contiguous()
