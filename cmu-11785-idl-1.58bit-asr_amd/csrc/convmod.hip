@@ -437,6 +437,12 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int off) {
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r, off, 0, 0);
 }
+typedef float cm_f32x4 __attribute__((ext_vector_type(4)));
+// four consecutive channels (off 16-byte aligned: C % 4 == 0, channel groups of 4)
+__device__ __forceinline__ cm_f32x4 bload4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(cm_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+constexpr int kLBQ = 4;  // channel quads per thread and batch of the tiles' window loads
 
 // ------------------------------------------------------------------ channel-split tiles
 // The kernels above give one block a [W][C] window (all channels: 94 x 144 x 2 floats of LDS
@@ -454,28 +460,34 @@ __global__ __launch_bounds__(kThreads) void cm_fwd_tile_kernel(
     const float* __restrict__ u, const float* __restrict__ wdw, const float* __restrict__ bdw,
     int T, int C, float* __restrict__ z, float* __restrict__ gout) {
   constexpr int P = KT / 2, W = kTT + KT - 1, NW = W * CG;
-  __shared__ float gs[NW];
+  constexpr int CQ = CG / 4, NQ = W * CQ;  // window loads in channel quads (dwordx4)
+  __shared__ __attribute__((aligned(16))) float gs[NW];
   const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
   const size_t rb = (size_t)b * T;
   const __amdgpu_buffer_rsrc_t ru = rsrc(u + rb * 2 * C, (size_t)T * 2 * C * 4);
-  for (int i0 = 0; i0 < NW; i0 += kLB * kThreads) {
-    float va[kLB], vb[kLB];
+  for (int i0 = 0; i0 < NQ; i0 += kLBQ * kThreads) {
+    cm_f32x4 va[kLBQ], vb[kLBQ];
 #pragma unroll
-    for (int q = 0; q < kLB; ++q) {
+    for (int q = 0; q < kLBQ; ++q) {
       const int i = i0 + threadIdx.x + q * kThreads;
-      const int tl = i / CG, c = i - tl * CG;
+      const int tl = i / CQ, cq = i - tl * CQ;
       const int t = t0 - P + tl;
       const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const int off = 4 * (tc * 2 * C + c0 + (i < NW ? c : 0));
-      va[q] = bload(ru, off);
-      vb[q] = bload(ru, off + 4 * C);
+      const int off = 4 * (tc * 2 * C + c0 + 4 * (i < NQ ? cq : 0));
+      va[q] = bload4(ru, off);
+      vb[q] = bload4(ru, off + 4 * C);
     }
 #pragma unroll
-    for (int q = 0; q < kLB; ++q) {
+    for (int q = 0; q < kLBQ; ++q) {
       const int i = i0 + threadIdx.x + q * kThreads;
-      if (i >= NW) break;
-      const int t = t0 - P + i / CG;
-      gs[i] = (t >= 0 && t < T) ? va[q] * sigm(vb[q]) : 0.0f;
+      if (i >= NQ) break;
+      const int tl = i / CQ, cq = i - tl * CQ;
+      const int t = t0 - P + tl;
+      const bool in = t >= 0 && t < T;
+      cm_f32x4 g4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g4[k] = in ? va[q][k] * sigm(vb[q][k]) : 0.0f;
+      *reinterpret_cast<cm_f32x4*>(gs + tl * CG + 4 * cq) = g4;
     }
   }
   __syncthreads();
@@ -507,9 +519,10 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
     const float* __restrict__ wdw, int64_t rows_pp, int T, int C, float* __restrict__ du,
     float* __restrict__ wpart, CmWgradEntry* __restrict__ tslot, CmWgradEntry ent) {
   constexpr int P = KT / 2, W = kTT + KT - 1, NW = W * CG;
+  constexpr int CQ = CG / 4, NQ = W * CQ;  // window loads in channel quads (dwordx4)
   if (tslot && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) *tslot = ent;
-  __shared__ float dzs[NW];  // dz over frames [t0-P, t0+kTT+P), the group's channels
-  __shared__ float gs[NW];   // g over the same window
+  __shared__ __attribute__((aligned(16))) float dzs[NW];  // dz over frames [t0-P, t0+kTT+P)
+  __shared__ __attribute__((aligned(16))) float gs[NW];   // g over the same window
   const int t0 = blockIdx.x * kTT, b = blockIdx.y, c0 = blockIdx.z * CG;
   const size_t rb = (size_t)b * T;
   const int pass = (int)(rb / rows_pp);  // every frame of utterance b is in its pass
@@ -518,33 +531,39 @@ __global__ __launch_bounds__(kThreads) void cm_bwd_tile_kernel(
                                rg = rsrc(g + rb * C, sl);
   const __amdgpu_buffer_rsrc_t ru = rsrc(u + rb * 2 * C, 2 * sl), rdu = rsrc(du + rb * 2 * C, 2 * sl);
   // window: dz = BatchNorm + swish backward (per-pass statistics, cm_dz_kernel's formula)
-  for (int i0 = 0; i0 < NW; i0 += kLB * kThreads) {
-    float va[kLB], vz[kLB], vg[kLB];
+  for (int i0 = 0; i0 < NQ; i0 += kLBQ * kThreads) {
+    cm_f32x4 va[kLBQ], vz[kLBQ], vg[kLBQ];
 #pragma unroll
-    for (int q = 0; q < kLB; ++q) {
+    for (int q = 0; q < kLBQ; ++q) {
       const int i = i0 + threadIdx.x + q * kThreads;
-      const int tl = i / CG, c = i - tl * CG;
+      const int tl = i / CQ, cq = i - tl * CQ;
       const int t = t0 - P + tl;
       const int tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const int e = 4 * (tc * C + c0 + (i < NW ? c : 0));
-      va[q] = bload(rdv, e);
-      vz[q] = bload(rz, e);
-      vg[q] = bload(rg, e);
+      const int e = 4 * (tc * C + c0 + 4 * (i < NQ ? cq : 0));
+      va[q] = bload4(rdv, e);
+      vz[q] = bload4(rz, e);
+      vg[q] = bload4(rg, e);
     }
 #pragma unroll
-    for (int q = 0; q < kLB; ++q) {
+    for (int q = 0; q < kLBQ; ++q) {
       const int i = i0 + threadIdx.x + q * kThreads;
-      if (i >= NW) break;
-      const int tl = i / CG, c = i - tl * CG;
+      if (i >= NQ) break;
+      const int tl = i / CQ, cq = i - tl * CQ;
       const int t = t0 - P + tl;
       const bool in = t >= 0 && t < T;
-      const int cg = c0 + c;
-      const int pc = 2 * (pass * C + cg);
-      float xh;
-      const float dy = bn_dy(va[q], vz[q], stats + pc, gamma[cg], beta[cg], xh);
-      const float dzv = gamma[cg] * stats[pc + 1] * (dy - coef[pc] - xh * coef[pc + 1]);
-      dzs[i] = in ? dzv : 0.0f;
-      gs[i] = in ? vg[q] : 0.0f;
+      cm_f32x4 dz4, g4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cg = c0 + 4 * cq + k;
+        const int pc = 2 * (pass * C + cg);
+        float xh;
+        const float dy = bn_dy(va[q][k], vz[q][k], stats + pc, gamma[cg], beta[cg], xh);
+        const float dzv = gamma[cg] * stats[pc + 1] * (dy - coef[pc] - xh * coef[pc + 1]);
+        dz4[k] = in ? dzv : 0.0f;
+        g4[k] = in ? vg[q][k] : 0.0f;
+      }
+      *reinterpret_cast<cm_f32x4*>(dzs + tl * CG + 4 * cq) = dz4;
+      *reinterpret_cast<cm_f32x4*>(gs + tl * CG + 4 * cq) = g4;
     }
   }
   __syncthreads();
