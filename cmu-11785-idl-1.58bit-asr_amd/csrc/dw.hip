@@ -1119,10 +1119,14 @@ __global__ __launch_bounds__(kDwgThreads) void dw_grouped_kernel(
       // the descriptors' range check (no memory traffic). With the loads conditional the
       // compiler's wait counts had to cover the path without them, and each store then
       // waited for the NEXT step's loads too (one step of prefetch instead of two).
+      // The next step's split and LDS store first, then this step's MFMAs: the split's VALU
+      // runs while this step's fragment reads are in flight (compute-then-store measured
+      // 2.5 % slower per launch; interleaving them with sched_group_barrier, no better:
+      // profiles/r5/dwg_sched/). The two touch different LDS buffers.
       auto phase = [&](int cb, Raw& nxt, int sb, bool do_store, int ld_step) {
-        compute(cb);
         (void)do_store;  // (the last phase stores the zeros read past the piece: never read)
         store(nxt, sb);
+        compute(cb);
         load(nxt, ld_step);
       };
       Raw ra, rb;
