@@ -38,7 +38,7 @@ from .fused import (ffn_residual, ffn_residual_i8, fused_supported, i8_fused_sup
 from .layernorm import (Int8Act, fused_layernorm_supported, layer_norm, layer_norm_amax,
                         layer_norm_pair,
                         layer_norm_fork, layer_norm_i8)
-from .linear import linear
+from .linear import linear, linear_rows_split
 from .quant import DeviceBits, PassBits, QuantizedLinear, StackedBits
 
 __all__ = [
@@ -527,8 +527,8 @@ class TransformerDecoder(nn.Module):
                 ctx = dec_attention(linear(x, w, b), None, h, kmask, causal, mha.dropout,
                                     training)
             else:
-                ctx = dec_attention(linear(x, w[:e], b[:e]), linear(mem, w[e:], b[e:]), h,
-                                    kmask, causal, mha.dropout, training)
+                qp, kvp = linear_rows_split(x, mem, w, b, e)
+                ctx = dec_attention(qp, kvp, h, kmask, causal, mha.dropout, training)
             return linear(ctx, mha.out_proj.weight, mha.out_proj.bias)
         if mem is None:  # self-attention: one packed projection, chunks q | k | v
             q, k, v = linear(x, w, b).chunk(3, dim=-1)

@@ -33,7 +33,7 @@ import torch.nn.functional as F
 
 from . import _lib, deferred
 
-__all__ = ["linear", "colsum"]
+__all__ = ["linear", "linear_rows_split", "colsum"]
 
 
 
@@ -135,6 +135,85 @@ class _LinearFn(torch.autograd.Function):
         if has_b and ctx.needs_input_grad[2]:
             gb = colsum(g2)
         return gx, gw, gb, None
+
+
+class _RowsSplitFn(torch.autograd.Function):
+    """(F.linear(x, w[:e], b[:e]), F.linear(y, w[e:], b[e:])) for ONE packed weight: the
+    cross-attention in-projection of nn.MultiheadAttention (query rows from the decoder
+    state, key / value rows from the encoder memory; reference conformer.py:275-299 via
+    torch's multi_head_attention_forward). Sliced through autograd, each slice's weight /
+    bias gradient is scattered into a zero-filled full-size tensor and the two summed
+    (fills, copies and adds of [3e, e] a layer); here the two dW GEMMs write their row ranges
+    of the one gradient buffer directly, on the deferred / grouped weight-gradient path."""
+
+    @staticmethod
+    def forward(ctx, x, y, weight, bias, e):
+        k = x.shape[-1]
+        x2, y2 = x.reshape(-1, k), y.reshape(-1, k)
+        w1, w2 = weight[:e], weight[e:]  # row ranges: contiguous views
+        b1 = bias[:e] if bias is not None else None
+        b2 = bias[e:] if bias is not None else None
+        o1 = _dense(x2, w1, 0, b1, e)
+        o2 = _dense(y2, w2, 0, b2, weight.shape[0] - e)
+        ctx.save_for_backward(x2, y2, weight)
+        ctx.meta = (e, x.shape, y.shape)
+        ctx.bias = bias
+        deferred.note(weight, bias)
+        return o1.view(*x.shape[:-1], e), o2.view(*y.shape[:-1], weight.shape[0] - e)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        x2, y2, weight = ctx.saved_tensors
+        e, xs, ys = ctx.meta
+        n, k = weight.shape
+        bias = ctx.bias
+        dev = x2.device
+        outs = []
+        for g, inp, lo, hi, shp in ((g1, x2, 0, e, xs), (g2, y2, e, n, ys)):
+            g = torch.zeros((inp.shape[0], hi - lo), dtype=torch.float32, device=dev) \
+                if g is None else g.reshape(-1, hi - lo).contiguous()
+            outs.append(g)
+        gx = _dense(outs[0], weight[:e], 1, None, k).view(xs) if ctx.needs_input_grad[0] else None
+        gy = _dense(outs[1], weight[e:], 1, None, k).view(ys) if ctx.needs_input_grad[1] else None
+        gw = gb = None
+        if ctx.needs_input_grad[2]:
+            gw = deferred.grad_buf(weight)
+            if bias is not None and ctx.needs_input_grad[3]:
+                gb = deferred.grad_buf(bias, (n,), dev)
+            stream = _lib.stream_of(outs[0])
+            for g, inp, lo, hi in ((outs[0], x2, 0, e), (outs[1], y2, e, n)):
+                ws_b = int(_lib.load().ob_dense_dw_workspace(g.shape[0], hi - lo, k))
+                if not ws_b:  # (not on the dW kernels: torch, bias by the column sum)
+                    gw[lo:hi] = g.t() @ inp
+                    if gb is not None:
+                        gb[lo:hi] = colsum(g)
+                    continue
+                ws = torch.empty((ws_b,), dtype=torch.uint8, device=dev)
+                deferred.dense_dw(g, inp, g.shape[0], hi - lo, k, gw[lo:hi],
+                                  gb[lo:hi] if gb is not None else None, ws, ws_b, stream,
+                                  weight, bias)
+        elif bias is not None and ctx.needs_input_grad[3]:
+            gb = torch.cat([colsum(outs[0]), colsum(outs[1])])
+        return gx, gy, gw, gb, None
+
+
+def linear_rows_split(x: torch.Tensor, y: torch.Tensor, weight: torch.Tensor,
+                      bias: Optional[torch.Tensor], e: int):
+    """(linear(x, weight[:e], bias[:e]), linear(y, weight[e:], bias[e:])) with the packed
+    weight's gradient formed in place (_RowsSplitFn); the sliced form where the fused path does
+    not apply (CPU, shapes / alignment the dense GEMM refuses)."""
+    n, k = weight.shape
+    ok = (x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32
+          and x.is_contiguous() and y.is_contiguous() and weight.is_contiguous()
+          and (bias is None or bias.is_contiguous()) and 0 < e < n
+          and _dense_ok(x.reshape(-1, k), weight, k, e)
+          and _dense_ok(y.reshape(-1, k), weight[e:], k, n - e)
+          and _dense_ok(x.reshape(-1, k), weight, e, k) and _dense_ok(y.reshape(-1, k), weight, n - e, k)
+          and (weight[e:].data_ptr() % 16 == 0))
+    if not ok:
+        return (linear(x, weight[:e], bias[:e] if bias is not None else None),
+                linear(y, weight[e:], bias[e:] if bias is not None else None))
+    return _RowsSplitFn.apply(x, y, weight, bias, e)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
