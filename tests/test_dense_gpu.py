@@ -240,3 +240,41 @@ def test_decattn_abi_errors(gpu):
                               36, 0.1, None, 0, probs.data_ptr(), ctx.data_ptr(), st) == -1
     assert lib.ob_decattn_fwd(base, 432, base + 576, 432, base + 1152, 432, None, 1, 2, 4, 5, 5,
                               36, 0.0, None, 0, probs.data_ptr(), ctx.data_ptr() + 4, st) == -5
+
+
+@pytest.mark.parametrize("deferred_scope", [False, True])
+def test_linear_rows_split_matches_sliced_linears(gpu, deferred_scope):
+    """linear_rows_split (the decoder cross-attention in-projection as one node, its two dW
+    GEMMs writing the row ranges of the packed weight's gradient) == two sliced ``linear``
+    calls: outputs bit for bit (same GEMM launches), input gradients bit for bit, weight /
+    bias gradients within 1e-6 of max (the deferred path may take the grouped dW launch,
+    a different summation order than the per-layer dW kernel)."""
+    from onebit_asr import deferred
+    from onebit_asr.linear import linear, linear_rows_split
+
+    g = torch.Generator().manual_seed(3)
+    e, k = 144, 144
+    x = torch.randn(96, 41, k, generator=g).to(gpu)
+    mem = torch.randn(96, 249, k, generator=g).to(gpu)
+    w0 = (0.05 * torch.randn(3 * e, k, generator=g)).to(gpu)
+    b0 = (0.05 * torch.randn(3 * e, generator=g)).to(gpu)
+    gq = torch.randn(96, 41, e, generator=g).to(gpu)
+    gkv = torch.randn(96, 249, 2 * e, generator=g).to(gpu)
+    res = {}
+    for fused in (False, True):
+        w = torch.nn.Parameter(w0.clone())
+        b = torch.nn.Parameter(b0.clone())
+        xi, mi = x.clone().requires_grad_(), mem.clone().requires_grad_()
+        with deferred.scope(deferred_scope):
+            if fused:
+                q, kv = linear_rows_split(xi, mi, w, b, e)
+            else:
+                q, kv = linear(xi, w[:e], b[:e]), linear(mi, w[e:], b[e:])
+            ((q * gq).sum() + (kv * gkv).sum()).backward()
+        torch.cuda.synchronize()
+        res[fused] = (q.detach(), kv.detach(), xi.grad, mi.grad, w.grad, b.grad)
+    for i, (a, c) in enumerate(zip(res[False], res[True])):
+        if i < 4:
+            assert torch.equal(a, c), i
+        else:
+            assert (a - c).abs().max().item() <= 1e-6 * a.abs().max().item(), i
