@@ -918,9 +918,14 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // Fused epilogues: widths whose instantiation spills are excluded (checked with
 // -Rpass-analysis=kernel-resource-usage on the row-coalesced (VEC_EPI) kernels: every
 // epilogue is spill-free up to NT 9 at K <= 160 and up to NT 4 beyond).
+// K <= 160: the swish epilogues (lin1 forward, lin2 dX) at 64-column tiles -- 9 x 16
+// columns measured 6 % / 2.4 % slower per launch than 4 (profiles/r5/ab_prof/r6o: the
+// epilogue's VALU and stores spread over 2.25x the blocks); the residual epilogue keeps 9
+// (3 tiles at N = 144 were 7 % slower)
 bool epi_nt_ok(int nt, int64_t K, int epi_mode) {
   if (epi_mode == kEpiNone) return true;
-  return K <= 160 ? nt <= 9 : nt <= 4;
+  if (K <= 160) return nt <= (epi_mode == kEpiResidual ? 9 : 4);
+  return nt <= 4;
 }
 
 int pick_nt(int64_t N, int64_t K, int epi_mode) {
