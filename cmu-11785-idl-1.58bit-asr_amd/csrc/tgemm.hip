@@ -921,9 +921,10 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // K <= 160: the swish epilogues (lin1 forward, lin2 dX) at 64-column tiles -- 9 x 16
 // columns measured 6 % / 2.4 % slower per launch than 4 (profiles/r5/ab_prof/r6o: the
 // epilogue's VALU and stores spread over 2.25x the blocks); the residual epilogue keeps 9
-// (3 tiles at N = 144 were 7 % slower)
+// (3 tiles at N = 144 were 7 % slower); the plain launches at N = 144 (the grouped q / k / v
+// forward, out_proj dX) take 3 tiles of 48 (8 % faster than 9 x 16: r6t)
 bool epi_nt_ok(int nt, int64_t K, int epi_mode) {
-  if (epi_mode == kEpiNone) return true;
+  if (epi_mode == kEpiNone) return K > 160 || nt <= 4;
   if (K <= 160) return nt <= (epi_mode == kEpiResidual ? 9 : 4);
   return nt <= 4;
 }
