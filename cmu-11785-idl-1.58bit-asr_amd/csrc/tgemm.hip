@@ -949,7 +949,12 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
                    hipStream_t s, bool byte = false) {
   const int n_ct = ep.glayers * (int)ceil_div(N, 16 * NT);  // all layers' column tiles
   const int n_rt = (int)ceil_div(M, kRows);
-  int rgroups = (K > 256 ? kTargetBlocksLongK : kTargetBlocks) / (n_ct * P);
+  // (the swish-backward epilogue -- lin2 dX, NT 4 -- at 768 blocks: 37.5 -> 35.8 us a call,
+  // profiles/r5/ab_prof/r6w; the other K <= 256 kinds measured neutral or slower there)
+  const int target = K > 256 ? kTargetBlocksLongK
+                     : ep.mode == kEpiSwishDropBwd ? kTargetBlocks * 3 / 2
+                                                   : kTargetBlocks;
+  int rgroups = target / (n_ct * P);
   if (rgroups < 1) rgroups = 1;
   if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
