@@ -73,6 +73,7 @@ class _State:
         self.uses: Dict[int, int] = {}
         self.tables: Dict[int, tuple] = {}  # device index -> (dw, ln, cm tables)
         self.home: Optional[int] = None  # the stream current when the scope opened
+        self.home_dev: Optional[int] = None  # ... and the device it belongs to
         self.reset()
 
     def reset(self):
@@ -114,12 +115,19 @@ def set_arena(entries) -> None:
 
 def grad_buf(param, shape=None, device=None) -> torch.Tensor:
     """The tensor a backward writes ``param``'s gradient into: its view of the registered flat
-    buffer when autograd will adopt it (inside an active scope, ``param.grad`` None), else a
-    new fp32 tensor of ``shape`` (default: the parameter's). A NEW view object every call:
-    an extra reference held here would make AccumulateGrad copy instead of adopt."""
+    buffer when autograd will adopt it (inside an active scope, ``param.grad`` None, and the
+    parameter has exactly ONE producing site in this scope), else a new fp32 tensor of
+    ``shape`` (default: the parameter's). A NEW view object every call: an extra reference
+    held here would make AccumulateGrad copy instead of adopt.
+
+    The single-producer rule matters for the literal three-pass step: with several uses,
+    ``param.grad`` stays None until autograd has SUMMED every incoming gradient, so each
+    site would otherwise write the same flat slice and clobber the previous pass's
+    contribution before autograd's input buffer adds them. Such parameters get
+    fresh tensors; the exchange copies their summed ``.grad`` into the flat buffer."""
     if param is not None and _S.active and _ARENA:
         e = _ARENA.get(id(param))
-        if e is not None and param.grad is None:
+        if e is not None and param.grad is None and _S.uses.get(id(param), 0) == 1:
             flat, off, shp = e
             n = 1
             for d in shp:
@@ -139,8 +147,9 @@ def scope(enabled: bool = True):
     prev = _S.active
     _S.active = bool(enabled)
     _S.uses = {}
-    _S.home = (torch.cuda.current_stream().cuda_stream
-               if enabled and torch.cuda.is_available() and torch.cuda.is_initialized() else None)
+    on = enabled and torch.cuda.is_available() and torch.cuda.is_initialized()
+    _S.home = torch.cuda.current_stream().cuda_stream if on else None
+    _S.home_dev = torch.cuda.current_device() if on else None
     ok = False
     try:
         yield
@@ -197,7 +206,8 @@ def _begin(dev: torch.device, stream: int) -> None:
     if _S.stream is None:
         # the flush stream: the scope's own (home) stream when it is on this device
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
-        home_ok = _S.home is not None and torch.cuda.current_device() == idx
+        # (compared with the device the home stream was taken on, not the engine thread's)
+        home_ok = _S.home is not None and _S.home_dev == idx
         _S.stream = _S.home if home_ok else stream
         _S.dev = idx
     _S.streams.add(stream)
@@ -269,6 +279,10 @@ def dwg_take(dy, x, P, m, n, k, gw, gb, stream, weight, bias, alpha=None, ga=Non
     if (not lib.ob_dw_grouped_supported(n, k) or m < 1 or not 1 <= P <= 4
             or dy.data_ptr() % 16 or x.data_ptr() % 16
             or not dy.is_contiguous() or not x.is_contiguous()):
+        return False
+    # the grouped launch's 32-bit index limits (dwg_plan in csrc/dw.hip rejects the whole
+    # table otherwise): such a gemm finishes on the per-layer path instead
+    if m * P >= 1 << 30 or m * max(n, k) * 4 >= 1 << 31 or n * k * 4 >= 1 << 31:
         return False
     _begin(dy.device, stream)
     _tables(dy.device)

@@ -30,14 +30,19 @@ What changes per step without re-capture:
 N > 1 (reference train.py:116-118 is single-device: loss.backward(), clip, step), the
 ``exchange``:
 
-* ``"deferred"`` (default): the backward runs exactly as at N == 1 -- autograd's own
-  gradient buffers, every weight-gradient finish deferred to one table launch per kind at
-  the end (deferred.py) -- then the gradients are packed into one flat fp32 buffer (one
-  ``cat``), all-reduced (SUM) in one call and copied back (one ``foreach`` copy), all
-  inside the step graph with RCCL. Measured per rank on one GPU (world size 1 through the
-  test hook below, ``tools/multi_path_bench.py``): the bucketed path's on-the-spot finishes
-  cost ~2.3 ms/step (28.6 vs 26.3 ms) -- more than the exchange it overlaps (47 MB: a few
-  hundred us on a ring over xGMI) -- so the deferred exchange is the default.
+* ``"deferred"`` (default): the backward runs exactly as at N == 1 -- every weight
+  gradient in the grouped launch, the other finishes deferred to one table launch per kind
+  at the end (deferred.py) -- but the gradient sites write IN PLACE into their views of one
+  flat fp32 buffer (``deferred.grad_buf`` over the ``arena``; autograd adopts the views).
+  Only a parameter with a single producing site in the step gets its view (with several --
+  the literal three-pass step -- autograd sums the contributions before ``.grad`` exists,
+  so each site gets a fresh tensor); the gradients formed elsewhere (that case, and sites
+  that do not take a view) are copied into the buffer with one ``foreach`` copy, the buffer
+  is all-reduced (SUM) in one call, and those gradients are copied back out -- all inside
+  the step graph with RCCL. Measured per rank on one GPU (world size 1 through the test
+  hook below, ``tools/multi_path_bench.py``): +0.09 ms/step over the single-GPU path; the
+  bucketed path's on-the-spot finishes cost ~2.3 ms/step more than the exchange they would
+  overlap (47 MB: a few hundred us on a ring over xGMI).
 * ``"bucketed"``: gradients are views of the flat buffer (parameter order), cut into
   ``bucket_mb`` buckets (default 12 MB: 4 for Conformer-S's 47 MB) of contiguous parameters
   taken in REVERSE order (the backward produces the decoder / CTC-head and last-block
@@ -167,13 +172,24 @@ def flat_offsets(params, align: int = 4):
 _MULTI_RANK_PATH_AT_WORLD_1 = False
 
 
+_CAPTURE_GROUPS: Dict[tuple, dist.ProcessGroup] = {}
+
+
 def capture_group(pg: dist.ProcessGroup, device: torch.device) -> dist.ProcessGroup:
     """A second RCCL process group over ``pg``'s ranks for the collectives captured into the
     step graph, its communicator connected now (no collective, so its watchdog never tracks
-    an eager event; module docstring). Every rank of ``pg`` calls this in the same order."""
+    an eager event; module docstring). Every rank of ``pg`` calls this in the same order.
+    Cached per (group, device): every GraphedTrainStep of a process (one per padded batch
+    shape) shares one communicator instead of leaking one each. Only captured collectives
+    ever run on it, so sharing it keeps its watchdog free of eager events."""
+    key = (id(pg), device.index)
+    g = _CAPTURE_GROUPS.get(key)
+    if g is not None:
+        return g
     ranks = dist.get_process_group_ranks(pg)
     g = dist.new_group(ranks=ranks, backend="nccl", use_local_synchronization=True)
     g._get_backend(device).eager_connect_single_device(device)
+    _CAPTURE_GROUPS[key] = g
     return g
 
 

@@ -2,7 +2,8 @@
 multi-rank step path over RCCL at world size 1 (graph_step._MULTI_RANK_PATH_AT_WORLD_1),
 both exchanges captured into the same graph as the forward, backward and update: the
 bucketed all-reduce started from the backward's gradient hooks, and the default deferred
-one (pack, one all-reduce, unpack). With one rank the all-reduce is an identity, so two
+one (gradients written in place into the flat buffer, one all-reduce), the latter also with
+the literal three-pass step body (OneBitStep(stacked=False)). With one rank the all-reduce is an identity, so two
 steps must give the parameters of the single-GPU path.
 Writes result.pt: whether the collectives were captured, bucket count, the parameters of
 both runs."""
@@ -36,12 +37,13 @@ def main():
     batch = synthetic_batch([400, 333], [20, 13], seed=100, device=dev)
     sp_mask = sample_sp_mask(CFG1["enc_layers"], generator=torch.Generator().manual_seed(9))
 
-    def run(multi, exchange="deferred"):
+    def run(multi, exchange="deferred", stacked=None):
         graph_step._MULTI_RANK_PATH_AT_WORLD_1 = multi
         torch.manual_seed(0)
         model = ConformerASR(80, 5004, **CFG1).to(dev)
         # small buckets: several captured collectives (Conformer cfg1 has ~2 MB of gradients)
-        gs = GraphedTrainStep(OneBitStep(model, n_layers=CFG1["enc_layers"]), CFG1["enc_layers"],
+        gs = GraphedTrainStep(OneBitStep(model, n_layers=CFG1["enc_layers"], stacked=stacked),
+                              CFG1["enc_layers"],
                               process_group=dist.group.WORLD, warmup_iters=1, bucket_mb=0.25,
                               exchange=exchange)
         for _ in range(2):
@@ -54,9 +56,15 @@ def main():
     cap, nb, multi, p_multi = run(True, "bucketed")
     cap_d, nb_d, multi_d, p_dfr = run(True, "deferred")
     _, _, plain_multi, p_plain = run(False)
+    # the reference's literal three forwards (several producing sites per parameter: ADVICE r5,
+    # no site may write the shared flat slice) through the deferred exchange
+    cap_l, _, multi_l, p_lit = run(True, "deferred", stacked=False)
+    _, _, _, p_lit_plain = run(False, stacked=False)
     torch.save({"captured": cap, "buckets": nb, "multi": multi, "plain_multi": plain_multi,
                 "p_multi": p_multi, "p_plain": p_plain, "captured_deferred": cap_d,
-                "buckets_deferred": nb_d, "multi_deferred": multi_d, "p_deferred": p_dfr},
+                "buckets_deferred": nb_d, "multi_deferred": multi_d, "p_deferred": p_dfr,
+                "captured_literal": cap_l, "multi_literal": multi_l, "p_literal": p_lit,
+                "p_literal_plain": p_lit_plain},
                os.path.join(out_dir, "result.pt"))
     dist.destroy_process_group()
 

@@ -5,7 +5,8 @@
     captured into the step's single graph (no fallback to the eager exchange);
   * two graphed steps give the parameters of the single-GPU path (the one-rank all-reduce is
     an identity; the multi-rank path finishes its gradients on the spot instead of deferring
-    them, which is bit-identical)."""
+    them, which is bit-identical);
+  * the same for the reference's literal three-pass body through the deferred exchange."""
 import socket
 import subprocess
 import sys
@@ -37,3 +38,10 @@ def test_bucketed_allreduce_captured_over_rccl(gpu, tmp_path):
             q = res[key][k]
             err = (q.double() - p.double()).abs().max().item()
             assert err <= 1e-6 * max(p.abs().max().item(), 1e-30), (key, k, err)
+    # the literal three-pass body: every parameter is used by three passes, so no gradient
+    # site may write its flat slice in place (a pass's write clobbering another's)
+    assert res["multi_literal"] and res["captured_literal"]
+    for k, p in res["p_literal_plain"].items():
+        q = res["p_literal"][k]
+        err = (q.double() - p.double()).abs().max().item()
+        assert err <= 1e-6 * max(p.abs().max().item(), 1e-30), ("p_literal", k, err)
