@@ -452,11 +452,26 @@ def traffic_from(path, kernel):
 
 
 # ------------------------------------------------------------------------- cpu baseline
+def _cgroup_cpus():
+    """The job's cgroup CPU quota in CPUs (cgroup v2 cpu.max / v1 cfs quota), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q <= 0 else round(q / per, 2)
+    except Exception:
+        return None
+
+
 def cpu_baseline(seconds: float, bsz: int = 4, progress=lambda msg: None):
     """The oracle step (CPU restatement) on a bounded sample of the same workload on the
-    host's cores: torch intra-op threads = the faster of 16 (the box's CPU share for a
-    one-GPU job) and 8, both timed on one step and stated in the sample with the
-    affinity and os.cpu_count() core counts."""
+    host's cores: torch intra-op threads swept 8, 16, 32, ... up to the affinity count
+    (the host's best, not a fixed count) and the fastest used; the sweep, the
+    affinity / os.cpu_count() / cgroup-quota core counts are stated in the sample."""
     from onebit_asr.conformer import ConformerASR
     from onebit_asr.data import CONFORMER_S, synthetic_batch
     from onebit_asr.train_step import sample_sp_mask
@@ -485,17 +500,24 @@ def cpu_baseline(seconds: float, bsz: int = 4, progress=lambda msg: None):
         opt.step()
 
     # The GPU box gives a one-GPU job a 16-CPU share (cgroup quota) although affinity and
-    # os.cpu_count() show the whole machine: more intra-op threads than the share only
-    # oversubscribes it (measured: minutes per step at the affinity count). Threads tried:
-    # 16 and 8, the faster is used; the counts seen are reported in the sample.
+    # os.cpu_count() show the whole machine: more intra-op threads than the share
+    # oversubscribes it. Thread counts are swept upwards (8, 16, 32, 64, 128, ... up to the
+    # affinity count) and the sweep stops at the first count slower than 1.25x the best so
+    # far (every count past it only oversubscribes more); the fastest is used. The first
+    # count also warms the model up (the thread pool's start at a new count is milliseconds).
+    quota = _cgroup_cpus()
+    cands = sorted({c for c in (8, 16, 32, 64, 128, 256) if c <= n_aff} | {min(8, n_aff)})
     trial = {}
-    for th in sorted({min(16, n_aff), min(8, n_aff)}):
+    for th in cands:
         torch.set_num_threads(th)
-        one()  # warm-up at this thread count
+        if not trial:
+            one()  # warm-up
         t0 = time.perf_counter()
         one()
         trial[th] = time.perf_counter() - t0
         progress(f"cpu baseline: {th} threads, one step {trial[th]:.1f} s")
+        if trial[th] > 1.25 * min(trial.values()):
+            break
     threads = min(trial, key=trial.get)
     torch.set_num_threads(threads)
     times = []
@@ -520,7 +542,8 @@ def cpu_baseline(seconds: float, bsz: int = 4, progress=lambda msg: None):
            "sample": f"oracle (CPU fp32 restatement) full 3-pass step + AdamW on Conformer-S, "
                      f"B={bsz} x 1000 frames, median of {len(times)} steps after warm-up; "
                      f"{threads} torch threads on {cpu} (affinity {n_aff} cores, "
-                     f"os.cpu_count() {n_cpu}; one-step trial mel-frames/s: {tried})"}
+                     f"os.cpu_count() {n_cpu}, cgroup CPU quota {quota}; thread sweep, "
+                     f"one-step mel-frames/s: {tried})"}
     out["cfg1"] = cpu_cfg1(progress)
     out["ql_microbench"] = cpu_ql_microbench(progress)
     return out

@@ -12,8 +12,9 @@
 // Block = WAVES waves, 16*WAVES rows x BN = 16*NT columns. At entry the block splits its BN
 // columns of W (read straight from the fp32 weight, L2-resident) into a three-plane bf16
 // image in LDS ([BN][3][Kpad+8]; the pad keeps the B-fragment ds_read_b128 conflict-free),
-// then loops over its row tiles: each wave streams 16 rows of A (two dwordx4 per lane per
-// 32-wide k-chunk, a window of chunks in flight across row tiles), splits them in
+// then loops over its 16-row subtiles (an even share of M per block, dealt round-robin to
+// the waves): each wave streams 16 rows of A (two dwordx4 per lane per
+// 32-wide k-chunk, a window of chunks in flight across subtiles), splits them in
 // registers and issues 6 MFMAs per 16-column tile. Blocks sharing a row tile are dealt to
 // the same XCD (one L2 serves their A reads).
 //
@@ -97,9 +98,9 @@ __host__ __device__ inline size_t dg_lds_bytes(int nt, int kpad) {
 template <int NT, int NCH, int WAVES, bool TRANS, bool RES = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
     const float* __restrict__ A, int64_t M, int K, const float* __restrict__ W, int N, int n_ct,
-    int n_rt, int rgroups, const float* __restrict__ bias, float* __restrict__ C,
+    int n16, int rgroups, const float* __restrict__ bias, float* __restrict__ C,
     const float* __restrict__ R, DropCfg dc, const uint64_t* __restrict__ rng, uint64_t rng_off) {
-  constexpr int kThr = 64 * WAVES, kRowsT = 16 * WAVES, BN = 16 * NT;
+  constexpr int kThr = 64 * WAVES, BN = 16 * NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* bimg = reinterpret_cast<__bf16*>(smem);
   const int kpad = dg_kpad(K, NCH);
@@ -110,6 +111,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
   const int ct = L % n_ct;
   const int rg = L / n_ct;
   const int n0 = ct * BN;
+  // this block's 16-row subtiles [s0, s1) (an even share of the n16 subtiles of M), dealt
+  // round-robin to its waves: a block's waves -- and so its SIMDs -- differ by at most one
+  // subtile, where whole 16*WAVES-row tiles left half the blocks a second round
+  const int s0 = (int)((int64_t)rg * n16 / rgroups), s1 = (int)((int64_t)(rg + 1) * n16 / rgroups);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15;
@@ -159,11 +164,11 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
     *reinterpret_cast<bf16x4*>(col + stride) = m;
     *reinterpret_cast<bf16x4*>(col + 2 * stride) = l;
   };
-  auto arow_of = [&](int rt) {
-    const int64_t m0 = (int64_t)rt * kRowsT + wave * 16;
-    const int64_t row = m0 + r < M ? m0 + r : M - 1;
+  auto arow_of = [&](int j) {  // row r of subtile j (clamped into M)
+    const int64_t row = (int64_t)16 * j + r < M ? (int64_t)16 * j + r : M - 1;
     return A + row * (int64_t)K;
   };
+  const int j0 = s0 + wave;  // this wave's first subtile (>= s1: no work)
 
   constexpr int kWmax = NT > 6 ? 3 : 5;
   constexpr int kWin = NCH > 0 ? (NCH < kWmax ? NCH : kWmax) : 1;
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
     f32x4 wv[kUpt];
 #pragma unroll
     for (int i = 0; i < kUpt; ++i) wv[i] = unit_load(threadIdx.x + i * kThr);
-    const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
+    const float* a0 = arow_of(j0 < s1 ? j0 : s0);  // (s0 < s1: a real subtile)
 #pragma unroll
     for (int c = 0; c < kWin; ++c) load8(a0, 32 * c + kg, K, buf[c][0], buf[c][1]);
     __builtin_amdgcn_sched_barrier(0);
@@ -194,9 +199,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
     bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
   }
 
-  for (int rt = rg; rt < n_rt; rt += rgroups) {
-    const int64_t m0 = (int64_t)rt * kRowsT + wave * 16;
-    const float* arow = arow_of(rt);
+  for (int j = j0; j < s1; j += WAVES) {
+    const int64_t m0 = (int64_t)16 * j;
+    const float* arow = arow_of(j);
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -232,8 +237,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
       // Fully unrolled; kWin chunks in flight, the next row tile's first chunks issued
       // while this tile computes its last ones (the last tile re-reads its own rows as the
       // "next" tile: L2 hits, never used).
-      const int rt_next = rt + rgroups < n_rt ? rt + rgroups : rt;
-      const float* anext = arow_of(rt_next);
+      const float* anext = arow_of(j + WAVES < s1 ? j + WAVES : j);
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + kWin < NCH) load8(arow, 32 * (c + kWin) + kg, K, buf[c + kWin][0], buf[c + kWin][1]);
@@ -334,13 +338,18 @@ bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int
   const DgCfg cfg = pick_cfg(N, K);
   const int kpad = dg_kpad((int)K, 0);
   const size_t lds = dg_lds_bytes(cfg.nt, kpad);
-  const int rows_t = 16 * cfg.waves;
   const int n_ct = (int)ceil_div(N, 16 * cfg.nt);
-  const int n_rt = (int)ceil_div(M, rows_t);
+  const int n16 = (int)ceil_div(M, 16);
   const int per_cu = (int)std::min<size_t>(kLdsCU / lds, (size_t)(8 / cfg.waves));
+  // row groups: fill every CU, but give each block at least one subtile per wave (more
+  // blocks than that only repeat the B-image prologue: measured +0.5 us at N = 144). The
+  // conv module's pw1 forward (N = 288, two column tiles): 128 groups of 11-12 subtiles,
+  // three per SIMD at most, where whole 128-row tiles left half the blocks a second round of
+  // two per SIMD: 21.9 -> 18.9 us; pw1 dX (three tiles) 22.6 -> 20.1 us; the decoder's
+  // K = 1024 linear 36.2 -> 26.8 us (tools/dense_bench.py, profiles/r6/dense_ab/)
   int rgroups = 256 * per_cu / n_ct;
+  rgroups = std::min<int64_t>(rgroups, ceil_div(n16, cfg.waves));
   if (rgroups < 1) rgroups = 1;
-  if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct));
   const int nch = kpad == 160 ? 5 : kpad == 288 ? 9 : 0;
   const float* R = epi ? epi->R : nullptr;
@@ -351,11 +360,11 @@ bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int
   if (cfg.nt == NT && nch == NCH && cfg.waves == WV) {                                           \
     if (trans)                                                                                   \
       hipLaunchKernelGGL((dgemm_kernel<NT, NCH, WV, true>), grid, dim3(64 * WV), lds, s, A, M,    \
-                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C, nullptr, dc,    \
+                         (int)K, W, (int)N, n_ct, n16, rgroups, bias, C, nullptr, dc,    \
                          nullptr, 0);                                                            \
     else                                                                                         \
       hipLaunchKernelGGL((dgemm_kernel<NT, NCH, WV, false>), grid, dim3(64 * WV), lds, s, A, M,   \
-                         (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C, nullptr, dc,    \
+                         (int)K, W, (int)N, n_ct, n16, rgroups, bias, C, nullptr, dc,    \
                          nullptr, 0);                                                            \
     return true;                                                                                 \
   }
@@ -364,7 +373,7 @@ bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int
 #define OB_DGR(WV)                                                                               \
     if (cfg.waves == WV) {                                                                       \
       hipLaunchKernelGGL((dgemm_kernel<9, 5, WV, false, true>), grid, dim3(64 * WV), lds, s, A,   \
-                         M, (int)K, W, (int)N, n_ct, n_rt, rgroups, bias, C, R, dc, rng,         \
+                         M, (int)K, W, (int)N, n_ct, n16, rgroups, bias, C, R, dc, rng,         \
                          rng_off);                                                               \
       return true;                                                                               \
     }

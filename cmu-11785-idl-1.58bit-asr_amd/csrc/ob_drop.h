@@ -43,6 +43,25 @@ __device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t idx) {
   return fmix32((uint32_t)idx ^ ((hi << 16) | (hi >> 16)) ^ key);
 }
 
+// A run of consecutive element pairs from pair index p (64-bit): the hash of pair p + off
+// (off < 2^32) from 32-bit arithmetic -- the low word plus a carry into the high word --
+// bit-equal to drop_hash(key, p + off), without the 64-bit index math per pair.
+struct DropPairRow {
+  uint32_t lo, k0, k1;  // low word of p; key ^ rot16(high word), the same with the carry
+};
+
+__device__ __forceinline__ uint32_t drop_rot16(uint32_t x) { return (x << 16) | (x >> 16); }
+
+__device__ __forceinline__ DropPairRow drop_pair_row(uint32_t key, uint64_t p) {
+  const uint32_t hi = (uint32_t)(p >> 32);
+  return DropPairRow{(uint32_t)p, key ^ drop_rot16(hi), key ^ drop_rot16(hi + 1u)};
+}
+
+__device__ __forceinline__ uint32_t drop_hash_at(const DropPairRow& r, uint32_t off) {
+  const uint32_t lo = r.lo + off;
+  return fmix32(lo ^ (lo < r.lo ? r.k1 : r.k0));
+}
+
 struct DropCfg {
   uint32_t thresh;  // keep iff the element's 16-bit field >= thresh
   float scale;      // 1 / (1 - p)

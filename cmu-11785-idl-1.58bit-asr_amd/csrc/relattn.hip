@@ -223,16 +223,6 @@ __device__ __forceinline__ uint64_t drop_row_base(int bh, int T, int i) {  // ev
   return ((uint64_t)bh * T + i) * (uint64_t)(T + (T & 1));
 }
 
-// keep bits of keys 16t+4g .. +3 of a row (idx even: the two pairs of a dwordx4 group)
-__device__ __forceinline__ void keep4(uint32_t key, uint64_t idx, const DropCfg& dc,
-                                      bool (&keep)[4]) {
-  const uint32_t h0 = drop_hash(key, idx >> 1), h1 = drop_hash(key, (idx >> 1) + 1);
-  keep[0] = (h0 & 0xFFFFu) >= dc.thresh;
-  keep[1] = (h0 >> 16) >= dc.thresh;
-  keep[2] = (h1 & 0xFFFFu) >= dc.thresh;
-  keep[3] = (h1 >> 16) >= dc.thresh;
-}
-
 #ifdef OB_ATTN_STAMPS
 // diagnostic build only (tools/attn_stamps.py): per-wave cycles of up to 10 phases of ONE
 // kernel (OB_ATTN_STAMPS = 1 flash-style backward, 2 query-side backward, 3 forward,
@@ -461,22 +451,34 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
     stats[2 * ((size_t)bh * Tp + qi) + 1] = rsum;
   }
   const uint32_t dkey = dc.on ? drop_key(rng[0], rng[1] + rng_off) : 0u;
+  // keys 16t+4g .. +3 are the element pairs pb + 8t and pb + 8t + 1 of the row's hash index
+  // (drop_row_base is even): 32-bit pair arithmetic, the hashes keep4 draws
+  const DropPairRow dr = drop_pair_row(dkey, (drop_row_base(bh, T, qi) + 4 * g) >> 1);
+  const bool want_kw = kbits != nullptr && dc.on;  // keep bits saved (flash-style backward)
   uint32_t kw[(NTT + 1) / 2];  // keep bits of keys 32wd .. 32wd + 31 (this lane's share)
 #pragma unroll
   for (int wd = 0; wd < (NTT + 1) / 2; ++wd) kw[wd] = 0u;
-  const uint64_t didx = drop_row_base(bh, T, qi) + 4 * g;  // + 16t
   // this wave's row tile of probs (waves past the last row tile -- T not a multiple of
-  // 64 -- store nothing)
-  const int arow = (i0 >> 4) + w;
-  float* pf = probs && arow < nt ? probs + frag_off(bh, arow, 0, nt) + 4 * lane : nullptr;
+  // 64 -- store nothing); the test is wave-uniform
+  const int arow = (i0 >> 4) + __builtin_amdgcn_readfirstlane(w);
+  const bool store_p = probs != nullptr && arow < nt;
+  float* pf = probs + (store_p ? frag_off(bh, arow, 0, nt) : 0) + 4 * lane;
 #pragma unroll
   for (int t = 0; t < NTT; ++t) {
     if (t >= nt) continue;
-    bool keep[4] = {true, true, true, true};
-    if (dc.on) keep4(dkey, didx + 16 * t, dc, keep);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      kw[t >> 1] |= (keep[j] ? 1u : 0u) << (16 * (t & 1) + 4 * g + j);
+    // dropout off: thresh 0, every field keeps
+    uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFFu;
+    if (dc.on) {
+      h0 = drop_hash_at(dr, 8 * t);
+      h1 = drop_hash_at(dr, 8 * t + 1);
+    }
+    const bool keep[4] = {(h0 & 0xFFFFu) >= dc.thresh, (h0 >> 16) >= dc.thresh,
+                          (h1 & 0xFFFFu) >= dc.thresh, (h1 >> 16) >= dc.thresh};
+    if (want_kw) {
+      const uint32_t nib = (keep[0] ? 1u : 0u) | (keep[1] ? 2u : 0u) | (keep[2] ? 4u : 0u) |
+                           (keep[3] ? 8u : 0u);
+      kw[t >> 1] |= nib << (16 * (t & 1) + 4 * g);
+    }
     f32x4 st;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -484,11 +486,12 @@ __global__ __launch_bounds__(kThreads) void relattn_fwd_kernel(
       // the keep decision rides in the sign bit (P >= 0): the backward kernels read it
       // back instead of re-hashing every element
       st[j] = keep[j] ? pr : -pr;
-      sreg[t][j] = dc.on ? (keep[j] ? pr * dc.scale : 0.0f) : pr;
+      // (dropout off: every element keeps and dc.scale is 1, so this is pr)
+      sreg[t][j] = keep[j] ? pr * dc.scale : 0.0f;
     }
-    if (pf) *reinterpret_cast<f32x4*>(pf + 256 * t) = st;
+    if (store_p) *reinterpret_cast<f32x4*>(pf + 256 * t) = st;
   }
-  if (kbits && dc.on) {
+  if (want_kw) {
     const int W = (nt + 1) >> 1;
 #pragma unroll
     for (int wd = 0; wd < (NTT + 1) / 2; ++wd) {

@@ -211,11 +211,18 @@ def c_bitlinear_fwd(X, W, alpha, bias, bits, alpha_raw=True) -> np.ndarray:
 
 
 # ----------------------------------------------------------------------------- torch fp32
+# Test hook (tests/test_conformer_s_oracle_gpu.py): when a dict, every backward adds the
+# float64 sum of |grad_out * term| -- the magnitude of the terms the alpha gradient sums,
+# the natural scale of its rounding error -- under id(W) of the layer's weight.
+TERM_SCALE = None
+
+
 class _RefQuantizeSTE(torch.autograd.Function):
     """quant.py:38-92 in plain torch fp32 ops (CPU)."""
 
     @staticmethod
     def forward(ctx, W, alpha, bitwidth: int):
+        ctx.key = id(W)
         if bitwidth == 32:
             ctx.bits = 32
             return W
@@ -242,7 +249,10 @@ class _RefQuantizeSTE(torch.autograd.Function):
         s = wa.sign()
         piece = torch.where(awa >= 0.5, s, torch.zeros_like(wa)) if ctx.bits == 2 else s
         term = torch.where(awa < 1.0, -wa + piece, s)
-        return grad_w, (grad_out * term).sum(), None
+        prod = grad_out * term
+        if TERM_SCALE is not None:
+            TERM_SCALE[ctx.key] = TERM_SCALE.get(ctx.key, 0.0) + prod.abs().double().sum().item()
+        return grad_w, prod.sum(), None
 
 
 def ref_quantize_weight(W, alpha, bitwidth):

@@ -28,8 +28,11 @@ Bars (the cfg1 bars of tests/test_model_gpu.py):
     (linear1 moves 6.8e-4 in the oracle itself) and the subsampling convs (3.4e-3);
     everything else keeps the 1e-3 bar. Alpha gradients (ONE sum of N*K terms that
     can cancel: its rounding noise scales with the terms, not with the sum) within
-    max(2e-3 relative, 1e-3 x the model's median |alpha gradient|, 3 x its own move in the
-    perturbed oracle), the rule of tests/test_conformer_s_gpu.py; the perturbation also
+    C_ALPHA x that layer's own sum of |G * term| over its passes (G = dW_hat, term of
+    quant.py:86-90, both from the ORACLE's backward: quant_oracle.TERM_SCALE) -- the bar the
+    per-layer test puts on a single layer (tests/test_dw_grouped_gpu.py: 1e-5 x the same
+    scale) widened 5x for G itself reaching the layer through 16 blocks of fp32 rounding
+    (C_ALPHA = 5e-5; the worst observed ratio, 6.7e-6 at B = 32, is printed). The perturbation also
     scales the decoder's token embeddings by 1 + 1e-6 N(0,1) (the decoder's own input at fp32
     rounding size); parameters whose true gradient is zero (key biases, the depthwise bias before BatchNorm, the key third of the
     decoder's in_proj_bias) within 1e-6 absolute.
@@ -45,7 +48,7 @@ S_ORACLE = dict(input_dim=80, vocab_size=5004, d_model=144, n_layers=16, n_heads
                 conv_kernel=31, dec_layers=2, dec_heads=4, dec_d_ff=1024, dropout=0.0)
 SP_MASK = [1, 0, 1, 1, 0, 0, 1, 0, 1, 0, 0, 1, 1, 0, 1, 0]
 ZERO_GRAD = ("k_proj.bias", "conv.dw.bias", "in_proj_bias")
-BAR_ALPHA = 2e-3
+C_ALPHA = 5e-5  # observed worst 6.7e-6 (ragged32), 2.8e-6 (full), 1.0e-6 (ragged): round 6
 BAR = 1e-3
 
 
@@ -122,8 +125,15 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
         loss_p.backward()
     torch.cuda.synchronize()
     assert len(deferred.LAST_DWG) > 100, "the grouped dW launch did not run"
-    loss_o, parts_o = oracle_step_loss(orc, s_batch, SP_MASK)
-    loss_o.backward()
+    from oracle import quant_oracle
+
+    quant_oracle.TERM_SCALE = {}
+    try:
+        loss_o, parts_o = oracle_step_loss(orc, s_batch, SP_MASK)
+        loss_o.backward()
+        term_scale = quant_oracle.TERM_SCALE
+    finally:
+        quant_oracle.TERM_SCALE = None
     # the oracle's own sensitivity: the same step on features perturbed by 1e-5 relative
     from oracle.conformer_oracle import OracleConformer
 
@@ -139,11 +149,10 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
         emb.mul_(1 + 1e-6 * torch.randn(emb.shape, generator=g))
     loss_q, _ = oracle_step_loss(orc2, pert, SP_MASK)
     loss_q.backward()
-    sens, sens_abs = {}, {}
+    sens = {}
     for (k1, p1), (k2, p2) in zip(orc.named_reference_parameters(), orc2.named_reference_parameters()):
         a, c = p1.grad.double(), p2.grad.double()
         sens[k1] = ((a - c).norm() / a.norm().clamp_min(1e-30)).item()
-        sens_abs[k1] = (a - c).abs().max().item()
     assert abs(loss_p.item() - loss_o.item()) <= 1e-4 * abs(loss_o.item()), (loss_p, loss_o)
     np.testing.assert_allclose(parts_p.cpu().numpy(), parts_o.numpy(), rtol=1e-4, atol=1e-6)
     ref = dict(orc.named_reference_parameters())
@@ -153,8 +162,7 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
     worst = (None, 0.0)
     bad = []
     errs = {}
-    med = sorted(abs(ref[n].grad.item()) for n in names if n.endswith(".alpha"))
-    med = med[len(med) // 2]
+    alpha_ratio = {}
     for name, p in prod.named_parameters():
         g_p = p.grad.detach().cpu().double()
         g_o = ref[name].grad.detach().double()
@@ -173,14 +181,19 @@ def test_s_step_loss_and_every_grad_match_oracle(s_pair, s_batch, gpu):
         rel = d.norm().item() / max(g_o.norm().item(), 1e-12)
         errs[name] = rel
         if name.endswith(".alpha"):
-            if abs(d.item()) > max(BAR_ALPHA * abs(g_o.item()), 1e-3 * med, 3 * sens_abs[name]):
-                bad.append((name, rel, d.item(), g_o.item(), med))
+            scale = term_scale[id(ref[name[:-len("alpha")] + "weight"])]
+            alpha_ratio[name] = abs(d.item()) / scale
+            if abs(d.item()) > C_ALPHA * scale:
+                bad.append((name, rel, d.item(), g_o.item(), scale))
         elif rel > max(BAR, 3 * sens[name]) and d.abs().max().item() > 1e-7:
             bad.append((name, rel, sens[name]))
         if rel > worst[1] and not name.endswith(".alpha"):
             worst = (name, rel)
         checked += 1
     print("largest rel-L2:", [(k, f"{e:.2e}") for k, e in sorted(errs.items(), key=lambda kv: -kv[1])[:24]])
+    print("largest |alpha-grad error| / sum|G term|:",
+          [(k, f"{e:.2e}") for k, e in sorted(alpha_ratio.items(), key=lambda kv: -kv[1])[:8]])
+    assert len(alpha_ratio) == 16 * 9, len(alpha_ratio)
     assert not bad, bad
     # 16 blocks x (9 BitLinears x 3 params + LNs, conv module, pos biases) + the rest
     assert checked > 700, checked

@@ -37,7 +37,12 @@ def main():
     st = _lib.stream_of(torch.empty(1, device=dev))
     m = a.m
     torch.backends.cuda.preferred_blas_library("cublas")
-    for k, n, trans in [(144, 288, 0), (144, 144, 0), (288, 144, 1), (144, 144, 1)]:
+    shapes = [(m, 144, 288, 0), (m, 144, 144, 0), (m, 288, 144, 1), (m, 144, 144, 1),
+              (m, 144, 5004, 0), (3936, 144, 144, 0), (3936, 144, 432, 0), (3936, 144, 144, 1),
+              (3936, 144, 1024, 0), (3936, 1024, 144, 0)]
+    for m, k, n, trans in shapes:
+        if n % 4:
+            continue
         x = torch.randn(m, k, device=dev)
         w = torch.randn((k, n) if trans else (n, k), device=dev)
         b = None if trans else torch.randn(n, device=dev)
@@ -50,8 +55,9 @@ def main():
             blas = timeit(lambda: torch.addmm(b, x, w.t()), a.iters)
         byt = 4 * m * (k + n)
         fl = 2 * m * n * k
-        print(f"gemm K={k} N={n} trans={trans}: hip {hip:7.1f} us ({byt / hip / 1e3:6.0f} GB/s, "
+        print(f"gemm M={m} K={k} N={n} trans={trans}: hip {hip:7.1f} us ({byt / hip / 1e3:6.0f} GB/s, "
               f"{6 * fl / hip / 1e6:6.0f} bf16-TFLOP/s)  rocBLAS {blas:7.1f} us", flush=True)
+    m = a.m
     for n, k in [(288, 144), (144, 144)]:
         dy = torch.randn(m, n, device=dev)
         x = torch.randn(m, k, device=dev)

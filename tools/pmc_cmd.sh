@@ -10,7 +10,7 @@ mkdir -p $O
 cd /tmp
 G1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA"
 G2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
-G3="SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VMEM SQ_LEVEL_WAVES GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum"
+G3="SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VMEM SQ_LEVEL_WAVES SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum"
 G4="FETCH_SIZE"
 G5="WRITE_SIZE"
 i=0
