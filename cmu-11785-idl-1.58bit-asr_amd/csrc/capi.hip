@@ -144,6 +144,18 @@ int ob_bitlinear_fwd(const float* X, int64_t M, int64_t K, const uint32_t* codes
   return launched();
 }
 
+int ob_bitlinear_fwd_signacc(const float* X, int64_t M, int64_t K, const uint32_t* codes,
+                             const float* alpha, int alpha_raw, const float* bias, int64_t N,
+                             float* Y, void* stream) {
+  if (M < 0 || K < 0 || N < 0) return OB_ERR_SHAPE;
+  if (!alpha || (M * N > 0 && !Y) || (M * K > 0 && !X) || (N * K > 0 && !codes))
+    return OB_ERR_NULL;
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || !aligned4(Y) || !aligned4(bias)) return OB_ERR_ALIGN;
+  if (!launch_ternary_gemm_signacc(X, M, K, codes, N, alpha, alpha_raw, bias, Y, as_stream(stream)))
+    return OB_ERR_SHAPE;
+  return launched();
+}
+
 int ob_bitlinear_bwd_dx(const float* dY, int64_t M, int64_t N, const uint32_t* codes_t,
                         const float* alpha, int alpha_raw, int64_t K, float* dX, void* stream) {
   if (M < 0 || K < 0 || N < 0) return OB_ERR_SHAPE;

@@ -45,6 +45,11 @@ void launch_ste_reduce_passes(const float* part, int P, int cpp, int64_t nk, con
 
 // gemm.hip
 // C[M][N] = a * (A[M][K] . Q^T) + bias, Q given as 2-bit codes [N][ceil(K/16)].
+// the VALU sign-accumulate form of the forward (tgemm_va.hip; the north-star inner-product
+// A/B, not on the product path): false for K % 4 != 0
+bool launch_ternary_gemm_signacc(const float* A, int64_t M, int64_t K, const uint32_t* codes,
+                                 int64_t N, const float* alpha, int alpha_raw, const float* bias,
+                                 float* C, hipStream_t s);
 void launch_ternary_gemm(const float* A, int64_t M, int64_t K, const uint32_t* codes, int64_t N,
                          const float* alpha, int alpha_raw, const float* bias, float* C,
                          hipStream_t s);

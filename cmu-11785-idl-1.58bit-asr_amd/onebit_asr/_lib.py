@@ -115,6 +115,7 @@ SIGNATURES = {
     "ob_quant_ste_bwd_workspace": (_sz, [_i64]),
     "ob_quant_ste_bwd": (_int, [_c_f, _c_f, _c_f, _int, _int, _i64, _c_f, _c_f, _c_f, _sz, _c_f]),
     "ob_bitlinear_fwd": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
+    "ob_bitlinear_fwd_signacc": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _int, _c_f, _i64, _c_f, _c_f]),
     "ob_bitlinear_bwd_dx": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _int, _i64, _c_f, _c_f]),
     "ob_bitlinear_bwd_dw_workspace": (_sz, [_i64, _i64, _i64]),
     "ob_bitlinear_bwd_dw": (

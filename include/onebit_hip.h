@@ -129,6 +129,17 @@ OB_API int ob_bitlinear_fwd(const float* X, int64_t M, int64_t K, const uint32_t
                             float* Y, void* stream);
 
 /*
+ * The same forward as a VALU sign-accumulate (north_star's first inner-product option: every
+ * x * q with q in {-1, 0, +1} an exact signed add on packed fp32 FMA, one k-ordered chain
+ * per output) -- the A/B partner of ob_bitlinear_fwd's bf16x3 MFMA kernel, not used by the
+ * module path. K % 4 == 0 and X 16-B aligned, else OB_ERR_SHAPE / OB_ERR_ALIGN.
+ * Replaces the same call (quant.py:126).
+ */
+OB_API int ob_bitlinear_fwd_signacc(const float* X, int64_t M, int64_t K, const uint32_t* codes,
+                                    const float* alpha, int alpha_raw, const float* bias,
+                                    int64_t N, float* Y, void* stream);
+
+/*
  * BitLinear backward, input gradient (autograd of F.linear at quant.py:126):
  *   dX[M][K] = a * (dY[M][N] . Q)       using codes_t (layout above)
  */

@@ -252,3 +252,36 @@ def test_pack_group_matches_oracle(gpu):
     grp.run()
     c_ref, _ = qo.np_codes(mod[0].weight.detach().cpu().numpy(), np.float32(mod[0].alpha.item()), 2)
     assert np.array_equal(grp.codes[0][2][0].cpu().numpy().view(np.uint32), c_ref)
+
+
+@pytest.mark.parametrize("bits", [1, 2])
+@pytest.mark.parametrize("shape", [(7, 144, 576), (130, 576, 144), (64, 16, 20), (1, 4, 4),
+                                   (0, 144, 144)])
+def test_signacc_forward_matches_oracle(gpu, bits, shape):
+    """The VALU sign-accumulate forward (ob_bitlinear_fwd_signacc, the north-star inner-product
+    A/B partner of the MFMA kernel) vs the float64 oracle at the module path's bar; ragged
+    M / N (tile edges), K % 16 != 0 (a partial code word), no rows; misaligned K refused."""
+    from onebit_asr import _lib
+    from onebit_asr.quant import pack_codes
+
+    M, K, N = shape
+    g = torch.Generator().manual_seed(M * 131 + K * 7 + N + bits)
+    W, alpha, _ = qo.ref_layer_init(K, N, g)
+    bias = torch.randn(N, generator=g) * 0.1
+    X = torch.randn(M, K, generator=g)
+    lib = _lib.load()
+    w, a = W.to(gpu), alpha.reshape(()).to(gpu)
+    codes, _ = pack_codes(w, a, bits)
+    x, b = X.to(gpu), bias.to(gpu)
+    y = torch.full((M, N), float("nan"), device=gpu)
+    _lib.check(lib.ob_bitlinear_fwd_signacc(x.data_ptr() if M else None, M, K, codes.data_ptr(),
+                                            a.data_ptr(), 1, b.data_ptr(), N,
+                                            y.data_ptr() if M else None, _lib.stream_of(y)),
+               "ob_bitlinear_fwd_signacc")
+    torch.cuda.synchronize()
+    if M:
+        _close(y.cpu().numpy(), qo.np_bitlinear_fwd(X.numpy(), W.numpy(), float(alpha), bias.numpy(),
+                                                     bits))
+    if K % 4 == 0 and M:
+        assert lib.ob_bitlinear_fwd_signacc(x.data_ptr(), M, K - 1, codes.data_ptr(), a.data_ptr(), 1,
+                                            None, N, y.data_ptr(), None) == -2  # K % 4 != 0
