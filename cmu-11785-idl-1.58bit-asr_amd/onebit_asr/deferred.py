@@ -328,6 +328,85 @@ def add_grad_after_flush(param: torch.Tensor, src: torch.Tensor) -> None:
     _S.post.append((param, src))
 
 
+def _grouped(lib, gemms, tk) -> None:
+    """ONE ob_dw_grouped launch of ``gemms`` on the flush stream."""
+    n = len(gemms)
+    arr = (DwgGemm * n)(*gemms)
+    ad = ctypes.addressof(arr)
+    wsb = lib.ob_dw_grouped_workspace(ad, n)
+    need = lib.ob_dw_grouped_tickets(ad, n)
+    if not wsb or need > tk.numel():
+        raise _lib.OneBitHipError(f"ob_dw_grouped: {n} gradients do not fit "
+                                  f"(workspace {wsb}, tickets {need} > {tk.numel()})")
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=tk.device)
+    _lib.check(lib.ob_dw_grouped(ad, n, ws.data_ptr(), wsb, tk.data_ptr(), tk.numel(),
+                                 _S.stream), "ob_dw_grouped")
+    keep(ws)
+
+
+# The N > 1 deferred exchange's overlap (graph_step._ChunkedExchange; None: one grouped launch,
+# the exchange after the backward). When set, the flush runs the finish tables first, hands
+# the gradients formed outside the flat buffer to ``copy_in()``, then splits the grouped launch
+# into ``chunks`` launches of whole gemms in DESCENDING flat-buffer order and calls
+# ``start(lo, hi)`` (element offsets) after each: that bucket is complete, so its all-reduce
+# runs on the exchange's stream under the next chunk's weight gradients; ``start(0, rest)``
+# covers the buffer's head (no grouped gradient left in it).
+_XCHG = None
+PLAN_NOTE = ""  # why the latest flush with an exchange set ran one launch (diagnostics)
+
+
+def set_exchange(x) -> None:
+    global _XCHG
+    _XCHG = x
+
+
+def _chunk_plan(x):
+    """([(gemms, lo, hi)] in launch order, rest) or None (an output outside the flat buffer:
+    no overlap, one launch)."""
+    global PLAN_NOTE
+    base, n = x.flat.data_ptr(), x.flat.numel()
+    items = []
+    for g in _S.dwg:
+        outs = [(g.dW, g.N * g.K)] + ([(g.db, g.N)] if g.db else []) + \
+               ([(g.dalpha, 1)] if g.dalpha else [])
+        lo, hi = n, 0
+        for ptr, size in outs:
+            off = (ptr - base) // 4
+            if ptr < base or (ptr - base) % 4 or off + size > n:
+                PLAN_NOTE = f"output outside the flat buffer (N {g.N} K {g.K} M {g.M})"
+                return None
+            lo, hi = min(lo, off), max(hi, off + size)
+        items.append((lo, hi, g.M * g.P * g.N * g.K, [g]))
+    # gemms whose output ranges overlap (the row halves of one packed weight and its bias,
+    # linear.linear_rows_split) are one unit: a chunk boundary never separates them
+    items.sort(key=lambda t: t[0])
+    units = []
+    for t in items:
+        if units and t[0] < units[-1][1]:
+            lo, hi, w, gs = units[-1]
+            units[-1] = (lo, max(hi, t[1]), w + t[2], gs + t[3])
+        else:
+            units.append(t)
+    items = units[::-1]  # descending flat offset: launch order
+    k = max(1, min(int(x.chunks), len(items)))
+    total = sum(t[2] for t in items)
+    chunks, cur, acc = [], [], 0
+    for t in items:
+        cur.append(t)
+        acc += t[2]
+        if len(chunks) < k - 1 and acc * k >= total * (len(chunks) + 1):
+            chunks.append(cur)
+            cur = []
+    if cur:
+        chunks.append(cur)
+    out, upper = [], n
+    for ch in chunks:
+        lo = min(t[0] for t in ch)
+        out.append(([g for t in ch for g in t[3]], lo, upper))
+        upper = lo
+    return out, upper
+
+
 def _flush() -> None:
     if _S.stream is None:
         _S.reset()
@@ -353,21 +432,12 @@ def _flush_tables() -> None:
         for t in _S.refs:
             if t.is_cuda:
                 t.record_stream(home)
+    plan = _chunk_plan(_XCHG) if (_XCHG is not None and _S.dwg) else None
     if _S.dwg:
-        n = len(_S.dwg)
         xs = [g.X for g in _S.dwg]  # (q / k / v of one LN output share X)
         LAST_DWG[:] = [(g.N, g.K, g.M, g.P, bool(g.W), xs.index(g.X)) for g in _S.dwg]
-        arr = (DwgGemm * n)(*_S.dwg)
-        ad = ctypes.addressof(arr)
-        wsb = lib.ob_dw_grouped_workspace(ad, n)
-        need = lib.ob_dw_grouped_tickets(ad, n)
-        if not wsb or need > tk.numel():
-            raise _lib.OneBitHipError(f"ob_dw_grouped: {n} gradients do not fit "
-                                      f"(workspace {wsb}, tickets {need} > {tk.numel()})")
-        ws = torch.empty((wsb,), dtype=torch.uint8, device=tk.device)
-        _lib.check(lib.ob_dw_grouped(ad, n, ws.data_ptr(), wsb, tk.data_ptr(), tk.numel(),
-                                     _S.stream), "ob_dw_grouped")
-        keep(ws)
+        if plan is None:
+            _grouped(lib, _S.dwg, tk)
     if _S.dw_n:
         _lib.check(lib.ob_dw_finish_table(dw.data_ptr(), _S.dw_n, _S.dw_blocks, _S.stream),
                    "ob_dw_finish_table")
@@ -382,4 +452,17 @@ def _flush_tables() -> None:
         with torch.cuda.stream(torch.cuda.ExternalStream(_S.stream, device=dev)):
             for param, src in _S.post:
                 param.grad.add_(src)
+    if plan is not None:
+        # every gradient outside the grouped launch is final here: into the flat buffer, then
+        # the grouped weight gradients chunk by chunk, each chunk's bucket all-reduced on the
+        # exchange's stream while the next chunk runs (the flat buffer's tail first)
+        chunks, rest = plan
+        dev = torch.device("cuda", _S.dev)
+        with torch.cuda.stream(torch.cuda.ExternalStream(_S.stream, device=dev)):
+            _XCHG.copy_in()
+            for gemms, lo, hi in chunks:
+                _grouped(lib, gemms, tk)
+                _XCHG.start(lo, hi)
+            if rest > 0:
+                _XCHG.start(0, rest)
     _S.reset()

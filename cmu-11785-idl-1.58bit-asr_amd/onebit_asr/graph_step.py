@@ -38,11 +38,16 @@ N > 1 (reference train.py:116-118 is single-device: loss.backward(), clip, step)
   the literal three-pass step -- autograd sums the contributions before ``.grad`` exists,
   so each site gets a fresh tensor); the gradients formed elsewhere (that case, and sites
   that do not take a view) are copied into the buffer with one ``foreach`` copy, the buffer
-  is all-reduced (SUM) in one call, and those gradients are copied back out -- all inside
-  the step graph with RCCL. Measured per rank on one GPU (world size 1 through the test
-  hook below, ``tools/multi_path_bench.py``): +0.09 ms/step over the single-GPU path; the
-  bucketed path's on-the-spot finishes cost ~2.3 ms/step more than the exchange they would
-  overlap (47 MB: a few hundred us on a ring over xGMI).
+  is all-reduced (SUM), and those gradients are copied back out -- all inside the step
+  graph with RCCL. Over RCCL the all-reduce is overlapped (round 6, ``overlap_chunks``,
+  ``_ChunkedExchange``): the end-of-backward flush runs the finish tables, copies the
+  gradients formed elsewhere into the buffer, then launches the grouped weight gradients in
+  ``overlap_chunks`` launches of whole gemms, highest flat offsets first, and all-reduces
+  each finished bucket on a communication stream while the next launch runs (the buffer's
+  head, which holds no grouped gradient, last). Measured per rank on one GPU (world size 1
+  through the test hook below, ``tools/multi_path_bench.py``); the bucketed path's
+  on-the-spot finishes cost ~2.3 ms/step more than the exchange they would overlap (47 MB:
+  a few hundred us on a ring over xGMI).
 * ``"bucketed"``: gradients are views of the flat buffer (parameter order), cut into
   ``bucket_mb`` buckets (default 12 MB: 4 for Conformer-S's 47 MB) of contiguous parameters
   taken in REVERSE order (the backward produces the decoder / CTC-head and last-block
@@ -155,6 +160,49 @@ class BucketedAllReduce:
         self.works = []
 
 
+class _ChunkedExchange:
+    """The deferred exchange overlapped with the grouped weight gradients (deferred.set_exchange,
+    RCCL only): the flush splits the grouped dW launch into ``chunks`` launches in descending
+    flat-buffer order and starts each finished bucket's SUM all-reduce on ``comm`` while the
+    next chunk runs; ``finish`` makes the current stream wait and copies the reduced buffer
+    back into the gradients that live outside it."""
+
+    def __init__(self, gs: "GraphedTrainStep", chunks: int):
+        self.gs = gs
+        self.flat = gs.flat
+        self.chunks = chunks
+        self.comm = torch.cuda.Stream(gs.device)
+        self.out = []
+        self.started = False
+
+    def reset(self):
+        self.out = []
+        self.started = False
+
+    def copy_in(self):
+        """The gradients formed outside the flat buffer, into it (one foreach copy)."""
+        gs = self.gs
+        self.out = [(p.grad, v) for p, v in zip(gs.params, gs.flat_views)
+                    if p.grad.data_ptr() != v.data_ptr()]
+        if self.out:
+            torch._foreach_copy_([v for _, v in self.out], [g for g, _ in self.out])
+
+    def start(self, lo: int, hi: int):
+        self.comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+        with torch.cuda.stream(self.comm):
+            dist.all_reduce(self.flat[lo:hi], group=self.gs.xpg)
+        self.started = True
+
+    def finish(self):
+        torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)
+        gs = self.gs
+        if not gs.fused:
+            self.flat.div_(gs.world)
+        if self.out:
+            torch._foreach_copy_([g for g, _ in self.out], [v for _, v in self.out])
+        gs.copied = len(self.out)
+
+
 def flat_offsets(params, align: int = 4):
     """Element offset of every parameter in the flat gradient buffer: each one starts on a
     16-byte boundary (the HIP kernels that write gradients in place store dwordx4), the gaps
@@ -198,7 +246,8 @@ class GraphedTrainStep:
                  total_steps: int = 100000, max_norm: float = 5.0,
                  process_group: Optional[dist.ProcessGroup] = None, warmup_iters: int = 2,
                  use_graph: bool = True, fused_optimizer: bool = True,
-                 bucket_mb: Optional[float] = 12.0, exchange: str = "deferred"):
+                 bucket_mb: Optional[float] = 12.0, exchange: str = "deferred",
+                 overlap_chunks: int = 3):
         if exchange not in ("deferred", "bucketed", "flat"):
             raise ValueError(f"exchange must be 'deferred', 'bucketed' or 'flat', got {exchange!r}")
         self.step_module = step_module
@@ -234,6 +283,10 @@ class GraphedTrainStep:
         self.buckets: Optional[BucketedAllReduce] = None
         self.comm_in_graph = False
         self.xpg = process_group  # the group the exchange's collectives run on
+        # deferred exchange over RCCL: the grouped dW in this many launches, each finished
+        # bucket all-reduced under the next (_ChunkedExchange); 1 = one launch, then exchange
+        self.overlap_chunks = overlap_chunks
+        self.xchg: Optional[_ChunkedExchange] = None
 
     # ------------------------------------------------------------------ setup
     def _set_batch(self, batch):
@@ -272,6 +325,9 @@ class GraphedTrainStep:
                 # the backward's gradient sites write into the flat buffer's views
                 # (deferred.grad_buf): only the gradients formed elsewhere are copied in
                 self.arena = [(p, self.flat, off) for p, off in zip(self.params, offs)]
+                if (self.overlap_chunks > 1 and self.pg is not None
+                        and dist.get_backend(self.pg) == dist.Backend.NCCL):
+                    self.xchg = _ChunkedExchange(self, self.overlap_chunks)
             if self.bucket_bytes:
                 self.buckets = BucketedAllReduce(self.params, self.flat, self.pg, self.bucket_bytes,
                                                  offs)
@@ -308,12 +364,16 @@ class GraphedTrainStep:
             self.buckets.begin()
             self.buckets.enabled = overlap
         deferred.set_arena(self.arena)
+        if self.xchg is not None:
+            self.xchg.reset()
+            deferred.set_exchange(self.xchg)
         try:
             with deferred.scope():  # one finish launch per kind at the end of the backward
                 loss, parts = self.step_module(self.batch, self.bits)
                 loss.backward()
         finally:
             deferred.set_arena(None)
+            deferred.set_exchange(None)
             if self.buckets is not None:
                 self.buckets.enabled = False
         return loss.detach(), parts
@@ -330,7 +390,9 @@ class GraphedTrainStep:
     def _allreduce(self, overlapped: bool = False):
         if not self.multi:
             return
-        if self.exchange == "deferred":
+        if self.exchange == "deferred" and self.xchg is not None and self.xchg.started:
+            self.xchg.finish()  # the buckets were reduced under the grouped dW chunks
+        elif self.exchange == "deferred":
             # the gradients the backward wrote into the flat buffer (deferred.grad_buf) are in
             # place; the rest are copied in (one foreach copy), one all-reduce, and copied back
             # out; the non-fused update takes the average here (the fused one scales by 1/world)
