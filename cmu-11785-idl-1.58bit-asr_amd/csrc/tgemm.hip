@@ -57,6 +57,8 @@ constexpr int kTargetBlocks = 512;  // 2 per CU
 // 32.8 -> 29.2 us same box; the K = 144 launches stay at 512 (256 measured 2-6 us slower).
 // (profiles/r4/tgemm_blocks/)
 constexpr int kTargetBlocksLongK = 256;
+// waves a byte-image block (K = 576; the q / k / v input-gradient sum): 8, two per SIMD
+constexpr int kByteWaves = 8;
 constexpr int kBPad = 16;           // B-image row pad (bf16 elements), see the header
 // Byte image (K = 576 and N a multiple of 144: all 144 columns of a row tile in one block,
 // so each A element is split once instead of once per 48 columns): one byte per weight,
@@ -107,7 +109,7 @@ __device__ uint64_t g_tg_rt[16384];
 #define TG_WRITE                                                                          \
   {                                                                                       \
     const uint64_t tg_rt1 = __builtin_amdgcn_s_memrealtime();                             \
-    const size_t tg_w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;         \
+    const size_t tg_w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x / 64) + wave; \
     if (lane == 0 && tg_w * 4 + 4 <= 32768)                                               \
       for (int k_ = 0; k_ < 4; ++k_) g_tg_stamps[tg_w * 4 + k_] = tg_acc[k_];             \
     if (lane == 0 && tg_w * 2 + 2 <= 16384) {                                             \
@@ -258,9 +260,9 @@ __host__ __device__ inline size_t epi_stage_off(int nt, int kpad, bool byte = fa
   return ((byte ? (size_t)16 * nt * (kpad + kBytePad) : (size_t)2 * 16 * nt * (kpad + kBPad)) + 15) &
          ~(size_t)15;
 }
-__host__ __device__ inline size_t epi_stage_bytes(int nt) {
+__host__ __device__ inline size_t epi_stage_bytes(int nt, int waves = 4) {
   const int cw = nt < 4 ? nt : 4;
-  return (size_t)4 * 16 * (16 * cw + 4) * sizeof(float);
+  return (size_t)waves * 16 * (16 * cw + 4) * sizeof(float);
 }
 
 // The same epilogue for 4 consecutive columns of one row (col % 4 == 0, N % 4 == 0): R loaded
@@ -306,13 +308,19 @@ __device__ __forceinline__ f32x4 epi_store4(const EpiArgs& ep, uint32_t dkey, fl
 // from its source, pre-scaled by that source's alpha (fp32 multiply: the product the
 // reference forms with its alpha * Q weight, quant.py:126), the byte image holding the MS
 // code blocks side by side.
-template <int NT, int NCH, int EPI, bool VEC_EPI, bool BYTE = false, int MS = 1>
-__global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
+// WV waves a block (8 for the byte-image launches: two per SIMD beside the one 84 KB image a
+// CU holds, so one wave's loads / epilogue run under the other's MFMAs). Rows (n16 16-row
+// subtiles a pass): WV > 4 -- an even, contiguous share of the subtiles per row group, dealt
+// round-robin to the block's waves; WV == 4 -- 64-row tiles dealt round-robin to the row
+// groups (measured 0.4-0.9 us a call faster than the even share for the K = 144 launches).
+template <int NT, int NCH, int EPI, bool VEC_EPI, bool BYTE = false, int MS = 1, int WV = 4>
+__global__ __launch_bounds__(64 * WV, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     const float* __restrict__ A, int64_t M, int K, const uint32_t* __restrict__ codes, int KW,
-    int N, int n_ct, int n_rt, int rgroups, const float* __restrict__ alpha, int alpha_raw,
+    int N, int n_ct, int n16, int rgroups, const float* __restrict__ alpha, int alpha_raw,
     const float* __restrict__ bias, float* __restrict__ C, const uint32_t* __restrict__ codes1,
     const int* __restrict__ pass_bits, EpiArgs ep) {
   TG_DECL
+  constexpr int kThr = 64 * WV;
   const int L = xcd_logical(blockIdx.x, gridDim.x);
   const int n_ct_l = n_ct / ep.glayers;  // column tiles of one layer
   if (ep.glayers > 1) {
@@ -355,6 +363,11 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   const int ct = (L % n_ct) % n_ct_l;
   const int rg = L / n_ct;
   const int n0 = ct * (16 * NT);
+  // this row group's subtiles [s0, s1) (rgroups <= n16 / WV: at least one per wave), or its
+  // 64-row tiles rg, rg + rgroups, ... (subtiles 4 rt .. 4 rt + 3)
+  constexpr bool kShare = WV > 4;
+  const int s0 = (int)((int64_t)rg * n16 / rgroups), s1 = (int)((int64_t)(rg + 1) * n16 / rgroups);
+  const int n_rt4 = (n16 + 3) >> 2;
 
   // Decode this block's Q rows: one code word -> 16 bf16 (two 16-byte LDS stores).
   // Consecutive threads take consecutive words of the block's (contiguous) code rows, and
@@ -411,11 +424,13 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   const int r = lane & 15;
   const int g = lane >> 4;
   const int kg = 8 * g;
-  auto arow_of = [&](int rt) {
-    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
-    const int64_t row = m0 + r < M ? m0 + r : M - 1;
+  auto arow_of = [&](int j) {  // row r of subtile j (clamped into M)
+    const int64_t row = (int64_t)16 * j + r < M ? (int64_t)16 * j + r : M - 1;
     return A + row * (int64_t)K;
   };
+  // row loop: it = subtile (share) or 64-row tile (round-robin), this wave's subtile jof(it)
+  const int it0 = kShare ? s0 + wave : rg, itN = kShare ? s1 : n_rt4, istep = kShare ? WV : rgroups;
+  auto jof = [&](int it) { return kShare ? it : 4 * it + wave; };
   // chunk c of a row tile (arow = arow_of's pointer): multi-source, chunk c is chunk c % NCHS
   // of source c / NCHS (c is a compile-time constant wherever the chunk loops are unrolled)
   auto ldc = [&](const float* arow, int c, f32x4& x, f32x4& y) {
@@ -436,7 +451,10 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
 #define OB_TG_KWMAX_WIDE 3
 #endif
   // (multi-source: one block per CU with registers to spare, a deeper window)
-  constexpr int kWmax = MS > 1 ? 5 : NT > 6 ? OB_TG_KWMAX_WIDE : 5;
+#ifndef OB_TG_KWMAX_BYTE8
+#define OB_TG_KWMAX_BYTE8 2  // (8-wave byte image: 2 chunks ahead 36.8 us a residual-LN call, 3: 38.1, 4: 40.1)
+#endif
+  constexpr int kWmax = MS > 1 ? 5 : (BYTE && WV > 4) ? OB_TG_KWMAX_BYTE8 : NT > 6 ? OB_TG_KWMAX_WIDE : 5;
   // NT 12: the cross-tile live range spills (and a 2-deep window measured slower), so it
   // keeps the per-tile window (issued at the top of each row tile)
   constexpr bool kCross = NT <= 9;
@@ -448,7 +466,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     if constexpr (BYTE) return;  // (the host never pairs the byte image with alpha_raw 2)
     const uint16_t* Wb = reinterpret_cast<const uint16_t*>(codes);
     const int upr = kpad >> 3;
-    for (int u = threadIdx.x; u < 16 * NT * upr; u += kThreads) {
+    for (int u = threadIdx.x; u < 16 * NT * upr; u += kThr) {
       const int nl = u / upr, k0 = 8 * (u - nl * upr);
       const int n = n0 + nl;
       u32x4 v = u32x4{0u, 0u, 0u, 0u};
@@ -467,30 +485,30 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   if constexpr (NCH > 0) {
     if (alpha_raw >= 2) {
       if constexpr (kCross) {
-        const float* a0 = arow_of(rg);
+        const float* a0 = arow_of(jof(it0 < itN ? it0 : rg));
 #pragma unroll
         for (int c = 0; c < kWin; ++c) ldc(a0, c, buf[c][0], buf[c][1]);
       }
       __builtin_amdgcn_sched_barrier(0);
       weight_image();
     } else {
-      constexpr int kWpt = (16 * NT * 2 * NCH + kThreads - 1) / kThreads;
+      constexpr int kWpt = (16 * NT * 2 * NCH + kThr - 1) / kThr;
       uint32_t wv[kWpt];
 #pragma unroll
-      for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThreads);
+      for (int i = 0; i < kWpt; ++i) wv[i] = word_at(threadIdx.x + i * kThr);
       if constexpr (kCross) {
-        const float* a0 = arow_of(rg);  // rg < rgroups <= n_rt: a real tile
+        const float* a0 = arow_of(jof(it0 < itN ? it0 : rg));  // (a real row, clamped)
 #pragma unroll
         for (int c = 0; c < kWin; ++c) ldc(a0, c, buf[c][0], buf[c][1]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThreads, wv[i]);
+      for (int i = 0; i < kWpt; ++i) decode_store(threadIdx.x + i * kThr, wv[i]);
     }
   } else if (alpha_raw >= 2) {
     weight_image();
   } else {
-    for (int idx = threadIdx.x; idx < nwords; idx += kThreads) decode_store(idx, word_at(idx));
+    for (int idx = threadIdx.x; idx < nwords; idx += kThr) decode_store(idx, word_at(idx));
   }
   // The residual byte launch's LayerNorm parameters (ep.nln, N = 144): gamma 0, beta 0,
   // gamma 1, beta 1 staged once per block after the epilogue tiles (an absent gamma / beta
@@ -499,7 +517,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
   [[maybe_unused]] float* lnp = nullptr;
   if constexpr (EPI == kEpiResidual && BYTE && NT == 9 && MS == 1) {
     lnp = reinterpret_cast<float*>(smem + epi_stage_off(NT, kpad, BYTE) +
-                                   (size_t)4 * 16 * (16 * NT + 4) * sizeof(float));
+                                   (size_t)WV * 16 * (16 * NT + 4) * sizeof(float));
     if (ep.nln > 0 && threadIdx.x < 16 * NT) {
       const int c = threadIdx.x;
       lnp[c] = ep.lng[0] ? ep.lng[0][c] : 1.0f;
@@ -524,10 +542,9 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
     bcol[t] = (bias && col < N) ? bias[col] : 0.0f;
   }
 
-  for (int rt = rg; rt < n_rt; rt += rgroups) {
-    const int64_t m0 = (int64_t)rt * kRows + wave * 16;
-    const int64_t row = m0 + r < M ? m0 + r : M - 1;
-    const float* arow = A + row * (int64_t)K;
+  for (int it = it0; it < itN; it += istep) {
+    const int64_t m0 = (int64_t)16 * jof(it);
+    const float* arow = arow_of(jof(it));
 
     f32x4 acc[NT];
 #pragma unroll
@@ -592,8 +609,7 @@ __global__ __launch_bounds__(kThreads, BYTE ? 1 : 2) void tgemm_bf16x3_kernel(
         for (int c = 0; c < kWin; ++c) ldc(arow, c, buf[c][0], buf[c][1]);
         __builtin_amdgcn_sched_barrier(0);
       }
-      const int rt_next = rt + rgroups < n_rt ? rt + rgroups : rt;
-      const float* anext = arow_of(rt_next);
+      const float* anext = arow_of(jof(it + istep < itN ? it + istep : it));
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + kWin < NCH)
@@ -948,45 +964,48 @@ void launch_bf16x3(const float* A, int64_t M, int64_t K, const uint32_t* codes, 
                    const uint32_t* codes1, const int* pass_bits, int P, const EpiArgs& ep,
                    hipStream_t s, bool byte = false) {
   const int n_ct = ep.glayers * (int)ceil_div(N, 16 * NT);  // all layers' column tiles
-  const int n_rt = (int)ceil_div(M, kRows);
+  const int n16 = (int)ceil_div(M, 16);  // 16-row subtiles of a pass
+  const int wv = byte ? kByteWaves : 4;
   // (the swish-backward epilogue -- lin2 dX, NT 4 -- at 768 blocks: 37.5 -> 35.8 us a call,
   // profiles/r5/ab_prof/r6w; the other K <= 256 kinds measured neutral or slower there)
   const int target = K > 256 ? kTargetBlocksLongK
                      : ep.mode == kEpiSwishDropBwd ? kTargetBlocks * 3 / 2
                                                    : kTargetBlocks;
   int rgroups = target / (n_ct * P);
+  if (rgroups > ceil_div(n16, wv)) rgroups = (int)ceil_div(n16, wv);  // >= a subtile a wave
   if (rgroups < 1) rgroups = 1;
-  if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
   const int kpad = (int)((K + 31) & ~int64_t(31));
   // (the residual byte-image launch stages all 16 * NT columns of a wave's rows at once)
   // (+ the LN parameters: 4 x 16 NT floats)
   const size_t lds = epi_stage_off(NT, kpad, byte) +
                      (byte && ep.mode == kEpiResidual
-                          ? (size_t)4 * 16 * (16 * NT + 4) * sizeof(float) + 4 * 16 * NT * sizeof(float)
-                          : epi_stage_bytes(NT));
+                          ? (size_t)wv * 16 * (16 * NT + 4) * sizeof(float) + 4 * 16 * NT * sizeof(float)
+                          : epi_stage_bytes(NT, wv));
   const int KW = (int)ceil_div(K, 16);
   const bool vec = (N % 4 == 0) && aligned16(C) && (ep.mode != kEpiSwishDrop || aligned16(ep.C2)) &&
                    ((ep.mode != kEpiResidual && ep.mode != kEpiSwishDropBwd) || aligned16(ep.R));
 #define OB_TGEMM_E(NCH, E)                                                                     \
   if (vec)                                                                                    \
     hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E, true>), grid, dim3(kThreads), lds, s,  \
-                       A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,  \
+                       A, M, (int)K, codes, KW, (int)N, n_ct, n16, rgroups, alpha, alpha_raw,  \
                        bias, C, codes1, pass_bits, ep);                                         \
   else                                                                                        \
     hipLaunchKernelGGL((tgemm_bf16x3_kernel<NT, NCH, E, false>), grid, dim3(kThreads), lds, s, \
-                       A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,  \
+                       A, M, (int)K, codes, KW, (int)N, n_ct, n16, rgroups, alpha, alpha_raw,  \
                        bias, C, codes1, pass_bits, ep)
   if constexpr (NT == 9) {
     if (byte) {  // byte image: K = 576 (18 chunks), codes (alpha_raw < 2), plain / residual
 #define OB_TGEMM_B(E)                                                                            \
   if (vec)                                                                                      \
-    hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, 18, E, true, true>), grid, dim3(kThreads), lds, s, \
-                       A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw,    \
+    hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, 18, E, true, true, 1, kByteWaves>), grid,         \
+                       dim3(64 * kByteWaves), lds, s,                                            \
+                       A, M, (int)K, codes, KW, (int)N, n_ct, n16, rgroups, alpha, alpha_raw,    \
                        bias, C, codes1, pass_bits, ep);                                           \
   else                                                                                          \
-    hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, 18, E, false, true>), grid, dim3(kThreads), lds,  \
-                       s, A, M, (int)K, codes, KW, (int)N, n_ct, n_rt, rgroups, alpha, alpha_raw, \
+    hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, 18, E, false, true, 1, kByteWaves>), grid,        \
+                       dim3(64 * kByteWaves), lds,                                               \
+                       s, A, M, (int)K, codes, KW, (int)N, n_ct, n16, rgroups, alpha, alpha_raw, \
                        bias, C, codes1, pass_bits, ep)
       if (ep.mode == kEpiResidual) OB_TGEMM_B(kEpiResidual);
       else OB_TGEMM_B(kEpiNone);
@@ -1145,15 +1164,16 @@ bool launch_ternary_dx_sum(int G, const float* const* dY, int P, int64_t M, int6
   }
   constexpr int kNch = 15;  // 3 sources x 5 chunks (144 zero-padded to 160)
   const int n_ct = (int)(K / 144);
-  const int n_rt = (int)ceil_div(M, kRows);
+  const int n16 = (int)ceil_div(M, 16);
   int rgroups = kTargetBlocksLongK / (n_ct * P);
+  if (rgroups > ceil_div(n16, kByteWaves)) rgroups = (int)ceil_div(n16, kByteWaves);
   if (rgroups < 1) rgroups = 1;
-  if (rgroups > n_rt) rgroups = n_rt;
   const dim3 grid((unsigned)(rgroups * n_ct), (unsigned)P);
-  const size_t lds = epi_stage_off(9, 32 * kNch, true) + epi_stage_bytes(9);
-  hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, kNch, kEpiNone, true, true, 3>), grid, dim3(kThreads),
-                     lds, s, dY[0], M, (int)N, codes_t[0], (int)ceil_div(N, 16), (int)K, n_ct,
-                     n_rt, rgroups, alpha[0], alpha_raw, nullptr, dX, codes_t1[0], pass_bits, ep);
+  const size_t lds = epi_stage_off(9, 32 * kNch, true) + epi_stage_bytes(9, kByteWaves);
+  hipLaunchKernelGGL((tgemm_bf16x3_kernel<9, kNch, kEpiNone, true, true, 3, kByteWaves>), grid,
+                     dim3(64 * kByteWaves), lds, s, dY[0], M, (int)N, codes_t[0],
+                     (int)ceil_div(N, 16), (int)K, n_ct, n16, rgroups, alpha[0], alpha_raw,
+                     nullptr, dX, codes_t1[0], pass_bits, ep);
   return true;
 }
 
