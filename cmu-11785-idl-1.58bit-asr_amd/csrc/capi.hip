@@ -506,6 +506,13 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 int ob_dense_supported(int64_t K, int64_t N) { return dense_gemm_supported(K, N) ? 1 : 0; }
 
+int ob_silu_fast_monotone_check(uint32_t lo_bits, uint32_t hi_bits, uint32_t* bad, void* stream) {
+  if (!bad) return OB_ERR_NULL;
+  if (lo_bits > hi_bits || hi_bits >= 0x7F800000u) return OB_ERR_SHAPE;  // finite, >= +0
+  launch_silu_monotone_check(lo_bits, hi_bits, bad, as_stream(stream));
+  return launched();
+}
+
 int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_trans,
                   const float* bias, int64_t N, float* Y, void* stream) {
   if (M < 0 || M > ((int64_t)1 << 40) || !dense_gemm_supported(K, N)) return OB_ERR_SHAPE;

@@ -41,6 +41,115 @@ __device__ __forceinline__ int64_t ext_label(const int64_t* tg, int s, int blank
   return (s & 1) ? tg[s >> 1] : blank;
 }
 
+// One state per thread (2 L + 1 <= kThreads): the thread's extended label and its skip
+// rule are read once, before the recursion (not per step from global memory), and the
+// log-probs of its next kRing steps are kept in flight in a register ring (the loop is
+// unrolled by kRing, so every ring index is static; the loads are unconditional, clamped to
+// the last frame): a step then waits only on its LDS neighbours and the barrier. The same
+// operations in the same order as the strided loop: the same bits.
+constexpr int kRing = 8;
+
+// A barrier that orders LDS only: __syncthreads()'s workgroup release also covers global
+// memory, which on gfx950 waits for every outstanding vector-memory operation -- the ring's
+// loads included -- at each step. The alpha / beta rows written to global memory are read
+// only by later launches.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ void ctc_alpha_one(const float* __restrict__ lpb,
+                                              const int64_t* __restrict__ tg, int Tb, int NS,
+                                              int V, int SS, int blank, float (*buf)[kMaxStates + 2],
+                                              float* __restrict__ ab, float* __restrict__ nll,
+                                              int b) {
+  const int s = threadIdx.x;
+  const bool act = s < NS;
+  const int64_t lab = act ? ext_label(tg, s, blank) : 0;
+  const bool skip = act && s >= 2 && lab != blank && lab != ext_label(tg, s - 2, blank);
+  const float* col = lpb + lab;  // this state's column (inactive threads: column 0)
+  const int tl = Tb > 0 ? Tb - 1 : 0;
+  float ring[kRing];
+#pragma unroll
+  for (int i = 0; i < kRing; ++i) ring[i] = col[(int64_t)(i < tl ? i : tl) * V];
+  for (int t0 = 0; t0 < Tb; t0 += kRing) {
+#pragma unroll
+    for (int i = 0; i < kRing; ++i) {
+      const int t = t0 + i;
+      if (t >= Tb) break;  // block-uniform
+      const float l = ring[i];
+      float* cur = buf[t & 1];
+      const float* prev = buf[(t & 1) ^ 1];
+      if (act) {
+        float a;
+        if (t == 0) {
+          a = (s <= 1) ? l : -INFINITY;
+        } else {
+          const float x0 = prev[s];
+          const float x1 = s >= 1 ? prev[s - 1] : -INFINITY;
+          const float x2 = skip ? prev[s - 2] : -INFINITY;
+          a = lse3(x0, x1, x2) + l;
+        }
+        cur[s] = a;
+        ab[(int64_t)t * SS + s] = a;
+      }
+      // the slot's next value (step t + kRing), issued after l's last use so the load can
+      // land in the slot's own register (no copy, hence no wait for it before the barrier)
+      ring[i] = col[(int64_t)(t + kRing < tl ? t + kRing : tl) * V];
+      lds_barrier();
+    }
+  }
+  if (threadIdx.x == 0) {
+    float ll = -INFINITY;
+    if (Tb > 0) {
+      const float* last = buf[(Tb - 1) & 1];
+      ll = NS >= 2 ? lse2(last[NS - 1], last[NS - 2]) : last[NS - 1];
+    }
+    nll[b] = -ll;
+  }
+}
+
+__device__ __forceinline__ void ctc_beta_one(const float* __restrict__ lpb,
+                                             const int64_t* __restrict__ tg, int Tb, int NS, int V,
+                                             int SS, int blank, float (*buf)[kMaxStates + 2],
+                                             float* __restrict__ bb) {
+  const int s = threadIdx.x;
+  const bool act = s < NS;
+  const int64_t lab = act ? ext_label(tg, s, blank) : 0;
+  const bool skip = act && s + 2 < NS && lab != blank && lab != ext_label(tg, s + 2, blank);
+  const float* col = lpb + lab;
+  const int tl = Tb > 0 ? Tb - 1 : 0;
+  float ring[kRing];
+#pragma unroll
+  for (int i = 0; i < kRing; ++i) ring[i] = col[(int64_t)(tl - i > 0 ? tl - i : 0) * V];
+  for (int t0 = Tb - 1; t0 >= 0; t0 -= kRing) {
+#pragma unroll
+    for (int i = 0; i < kRing; ++i) {
+      const int t = t0 - i;
+      if (t < 0) break;  // block-uniform
+      const float l = ring[i];
+      float* cur = buf[t & 1];
+      const float* nxt = buf[(t & 1) ^ 1];
+      if (act) {
+        float v;
+        if (t == Tb - 1) {
+          v = (s >= NS - 2) ? l : -INFINITY;
+        } else {
+          const float x0 = nxt[s];
+          const float x1 = s + 1 < NS ? nxt[s + 1] : -INFINITY;
+          const float x2 = skip ? nxt[s + 2] : -INFINITY;
+          v = lse3(x0, x1, x2) + l;
+        }
+        cur[s] = v;
+        bb[(int64_t)t * SS + s] = v;
+      }
+      ring[i] = col[(int64_t)(t - kRing > 0 ? t - kRing : 0) * V];
+      lds_barrier();
+    }
+  }
+}
+
 // alpha[b][t][s] for t < T_b (log space); nll[b] = -log p(l | x).
 __device__ __forceinline__ void ctc_alpha_body(
     const float* __restrict__ lp, const int64_t* __restrict__ targets,
@@ -54,9 +163,12 @@ __device__ __forceinline__ void ctc_alpha_body(
   const float* lpb = lp + (int64_t)b * T * V;
   float* ab = alpha + (int64_t)b * T * (2 * S + 1);
   const int SS = 2 * S + 1;
-  // NS <= kThreads (the common case): each thread owns one state and loads its next step's
-  // log-prob while the current step computes (the load is off the recursion's chain)
-  const bool one = NS <= kThreads;
+  if (NS <= kThreads) {  // the common case: alpha_one_state (same operations, same bits)
+    ctc_alpha_one(lpb, tg, Tb, NS, V, SS, blank, buf, ab, nll, b);
+    return;
+  }
+  // NS > kThreads: states strided over the threads
+  const bool one = false;
   const int s1 = threadIdx.x;
   const int64_t lab1 = s1 < NS ? ext_label(tg, s1, blank) : 0;
   float l_next = (one && s1 < NS && Tb > 0) ? lpb[lab1] : 0.0f;
@@ -114,7 +226,11 @@ __device__ __forceinline__ void ctc_beta_body(
   const float* lpb = lp + (int64_t)b * T * V;
   const int SS = 2 * S + 1;
   float* bb = beta + (int64_t)b * T * SS;
-  const bool one = NS <= kThreads;  // (as in the alpha kernel: next step's log-prob prefetched)
+  if (NS <= kThreads) {
+    ctc_beta_one(lpb, tg, Tb, NS, V, SS, blank, buf, bb);
+    return;
+  }
+  const bool one = false;
   const int s1 = threadIdx.x;
   const int64_t lab1 = s1 < NS ? ext_label(tg, s1, blank) : 0;
   float l_next = (one && s1 < NS && Tb > 0) ? lpb[(int64_t)(Tb - 1) * V + lab1] : 0.0f;

@@ -296,6 +296,163 @@ __global__ __launch_bounds__(64 * WAVES, 2) void dgemm_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Long-K form (K too long for a whole-K image: the CTC head's input gradient, K = V = 5004,
+// the reference's fp32 `g @ W` of linear.py / losses.py:41-47 through conformer.py:275):
+// the block holds all 16 NT columns and walks K in chunks of kKc = 64, the chunk's B image
+// (three planes, [BN][3][kKc + 8] bf16) double-buffered in LDS and built from W while the
+// previous chunk's MFMAs run; each wave owns one 16-row subtile (a block = 16 WAVES rows).
+// Same six products per k-step as dgemm_kernel, k in order: an fp32 GEMM up to summation
+// order. Units of the loader: 4 consecutive k of one column (TRANS: W [K][N], consecutive
+// lanes on consecutive columns of a W row; else W [N][K], one dwordx4).
+// ---------------------------------------------------------------------------------
+constexpr int kKc = 64;
+constexpr int kKcStride = kKc + 8;  // bf16 per plane row (conflict-free ds_read_b128)
+
+__host__ __device__ inline size_t dgkc_lds_bytes(int nt) {
+  return (size_t)2 * 16 * nt * 3 * kKcStride * sizeof(uint16_t);
+}
+
+template <int NT, int WAVES, bool TRANS>
+__global__ __launch_bounds__(64 * WAVES, 1) void dgemm_kc_kernel(
+    const float* __restrict__ A, int64_t M, int K, const float* __restrict__ W, int N,
+    const float* __restrict__ bias, float* __restrict__ C) {
+  constexpr int kThr = 64 * WAVES, BN = 16 * NT;
+  constexpr int kCpitch = 3 * kKcStride;            // bf16 per image column
+  constexpr int kBuf = BN * kCpitch;                // bf16 per buffer
+  constexpr int kUnits = BN * (kKc / 4);            // loader units per chunk
+  constexpr int kUpt = (kUnits + kThr - 1) / kThr;  // units per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* img = reinterpret_cast<__bf16*>(smem);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4, kg = 8 * g;
+  const int L = xcd_logical(blockIdx.x, gridDim.x);
+  const int64_t m0 = ((int64_t)L * WAVES + wave) * 16;  // this wave's subtile
+  const int64_t arow_i = m0 + r < M ? m0 + r : M - 1;
+  const float* arow = A + arow_i * (int64_t)K;
+  const int nck = (K + kKc - 1) / kKc;
+
+  auto unit_cols = [&](int u, int& c, int& k4) {
+    if constexpr (TRANS) {
+      k4 = u / BN;
+      c = u - k4 * BN;
+    } else {
+      c = u / (kKc / 4);
+      k4 = u - c * (kKc / 4);
+    }
+  };
+  auto unit_load = [&](int ch, int u) -> f32x4 {
+    u = u < kUnits ? u : kUnits - 1;
+    int c, k4;
+    unit_cols(u, c, k4);
+    const int n = c < N ? c : N - 1;
+    int kk = ch * kKc + 4 * k4;
+    kk = kk < K - 4 ? kk : K - 4;  // clamped (zeros selected at the store)
+    if constexpr (TRANS) {
+      const float* p = W + (int64_t)kk * N + n;
+      return f32x4{p[0], p[N], p[2 * N], p[3 * N]};
+    } else {
+      return *reinterpret_cast<const f32x4*>(W + (int64_t)n * K + kk);
+    }
+  };
+  // (u >= kUnits: the clamped unit again -- the same value to the same address, so the
+  // store needs no branch, which would let hipcc sink the unit's load into it)
+  auto unit_store = [&](int ch, int buf, int u, f32x4 v) {
+    u = u < kUnits ? u : kUnits - 1;
+    int c, k4;
+    unit_cols(u, c, k4);
+    const bool ok = ch * kKc + 4 * k4 < K && c < N;
+    const f32x4 x = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x4 h, m, l;
+    split3x4(x, h, m, l);
+    __bf16* col = img + buf * kBuf + c * kCpitch + 4 * k4;
+    *reinterpret_cast<bf16x4*>(col) = h;
+    *reinterpret_cast<bf16x4*>(col + kKcStride) = m;
+    *reinterpret_cast<bf16x4*>(col + 2 * kKcStride) = l;
+  };
+  // A: two dwordx4 per lane per 32-wide k step (clamped: k >= K meets zero image rows)
+  constexpr int kWin = 4;  // k steps in flight (2 chunks)
+  f32x4 abuf[kWin][2];
+  auto load_a = [&](int st, f32x4& x0, f32x4& x1) { load8(arow, 32 * st + kg, K, x0, x1); };
+
+  f32x4 wv[kUpt];
+#pragma unroll
+  for (int i = 0; i < kUpt; ++i) wv[i] = unit_load(0, threadIdx.x + i * kThr);
+#pragma unroll
+  for (int w = 0; w < kWin; ++w) load_a(w, abuf[w][0], abuf[w][1]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < kUpt; ++i) unit_store(0, 0, threadIdx.x + i * kThr, wv[i]);
+  __syncthreads();
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Chunks in pairs, so every A ring slot (2 * cc + hs) and LDS buffer (cc) is a static
+  // index: a dynamic index into abuf makes hipcc move the ring through gpr-indexed copies
+  // behind a vmcnt(0) per k step (every A load then waited for where it is issued). The
+  // loads are unconditional (clamped addresses; k >= K meets zero image rows).
+  for (int ch0 = 0; ch0 < nck; ch0 += 2) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int ch = ch0 + cc;
+      if (ch >= nck) break;  // block-uniform
+      // the next chunk's W units in flight over this chunk's MFMAs
+      const int chn = ch + 1 < nck ? ch + 1 : ch;
+#pragma unroll
+      for (int i = 0; i < kUpt; ++i) wv[i] = unit_load(chn, threadIdx.x + i * kThr);
+      const __bf16* brow = img + cc * kBuf + r * kCpitch + kg;
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const int st = 2 * ch + hs, slot = 2 * cc + hs;
+        const f32x4 x0 = abuf[slot][0], x1 = abuf[slot][1];
+        load_a(st + kWin, abuf[slot][0], abuf[slot][1]);
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int kG = NT < 3 ? NT : 3;
+#pragma unroll
+        for (int t0 = 0; t0 < NT; t0 += kG) {
+          bf16x8 b[kG][3];
+#pragma unroll
+          for (int t = 0; t < kG; ++t)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              if (t0 + t < NT)
+                b[t][q] = *reinterpret_cast<const bf16x8*>(brow + (t0 + t) * 16 * kCpitch +
+                                                            q * kKcStride + 32 * hs);
+          __builtin_amdgcn_sched_barrier(0);
+          bf16x8 a[3];
+          split3x8(x0, x1, a[0], a[1], a[2]);
+#pragma unroll
+          for (int p = 0; p < 6; ++p)
+#pragma unroll
+            for (int t = 0; t < kG; ++t)
+              if (t0 + t < NT) acc[t0 + t] = mfma_bf16(a[kProdA[p]], b[t][kProdB[p]], acc[t0 + t]);
+        }
+      }
+      // (unconditional, so hipcc keeps the W loads where they are issued instead of sinking
+      // them into a guarded store: after the last chunk the idle buffer -- whose readers all
+      // passed the previous barrier -- just takes a copy of that chunk)
+#pragma unroll
+      for (int i = 0; i < kUpt; ++i) unit_store(chn, cc ^ 1, threadIdx.x + i * kThr, wv[i]);
+      __syncthreads();  // the next buffer is complete; this buffer's reads are done
+    }
+  }
+  // D[row = 4g + reg][col = r]
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = 16 * t + r;
+    if (col >= N) continue;
+    const float bc = bias ? bias[col] : 0.0f;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int64_t orow = m0 + 4 * g + reg;
+      if (orow < M) C[orow * N + col] = acc[t][reg] + bc;
+    }
+  }
+}
+
 struct DgCfg {
   int nt, waves;
 };
@@ -325,9 +482,16 @@ DgCfg pick_cfg(int64_t N, int64_t K) {
 
 }  // namespace
 
+// the long-K form: every column in one block (N <= 144), K past what the whole-K image holds
+static bool dense_kc_shape(int64_t K, int64_t N) {
+  return N >= 4 && N <= 144 && N % 4 == 0 && K >= 4 && K % 4 == 0 && K <= (1 << 20) &&
+         pick_cfg(N, K).nt == 0;
+}
+
 bool dense_gemm_supported(int64_t K, int64_t N) {
-  return K >= 4 && N >= 4 && K % 4 == 0 && N % 4 == 0 && K <= (1 << 20) && N <= (1 << 20) &&
-         pick_cfg(N, K).nt > 0;
+  return (K >= 4 && N >= 4 && K % 4 == 0 && N % 4 == 0 && K <= (1 << 20) && N <= (1 << 20) &&
+          pick_cfg(N, K).nt > 0) ||
+         dense_kc_shape(K, N);
 }
 
 bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int trans,
@@ -335,6 +499,19 @@ bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int
                        const DenseEpi* epi) {
   if (!dense_gemm_supported(K, N)) return false;
   if (M == 0) return true;
+  if (dense_kc_shape(K, N)) {  // long K: K-chunked images (epilogue: bias only)
+    if (epi && epi->R) return false;
+    constexpr int kW = 8;
+    const dim3 grid((unsigned)ceil_div(M, 16 * kW));
+    const size_t lds = dgkc_lds_bytes(9);
+    if (trans)
+      hipLaunchKernelGGL((dgemm_kc_kernel<9, kW, true>), grid, dim3(64 * kW), lds, s, A, M, (int)K,
+                         W, (int)N, bias, C);
+    else
+      hipLaunchKernelGGL((dgemm_kc_kernel<9, kW, false>), grid, dim3(64 * kW), lds, s, A, M,
+                         (int)K, W, (int)N, bias, C);
+    return true;
+  }
   const DgCfg cfg = pick_cfg(N, K);
   const int kpad = dg_kpad((int)K, 0);
   const size_t lds = dg_lds_bytes(cfg.nt, kpad);

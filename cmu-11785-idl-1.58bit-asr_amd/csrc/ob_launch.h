@@ -300,6 +300,8 @@ bool launch_dense_gemm(const float* A, int64_t M, int64_t K, const float* W, int
 
 // tgemm_i8.hip (opt-in absmax-int8 activations x ternary codes on the i8 matrix cores)
 bool ternary_gemm_i8_supported(int64_t K, int64_t N);
+// violations of fast_silu(next float) >= fast_silu(x) over bit patterns [lo, hi), added to *bad
+void launch_silu_monotone_check(uint32_t lo, uint32_t hi, uint32_t* bad, hipStream_t s);
 size_t act_absmax_workspace(int P);
 void launch_act_absmax(const float* X, int P, int64_t n_per_pass, float* amax, void* ws,
                        hipStream_t s);

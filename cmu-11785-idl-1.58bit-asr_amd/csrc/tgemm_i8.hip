@@ -327,15 +327,36 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
         }
       }
     } else if constexpr (EPI == kI8SwishAmax) {
-      // max only: straight from the accumulators (the element order does not matter)
+      // max only: fast_silu is non-decreasing on y >= 0 (v_exp_f32 / v_rcp_f32 monotone:
+      // checked over every fp32 in [0, 128] by ob_silu_fast_monotone_check,
+      // tests/test_i8_fused_gpu.py) and |fast_silu(y)| < 0.28 for y < 0 (its minimum is
+      // -0.2785 at y = -1.2785), so this lane's max|silu| over the row tile is silu(max y)
+      // whenever that is >= 0.28 -- one silu a lane instead of one an element, the same
+      // float as the max over every element; otherwise every element (the exact fallback)
+      float ym = -INFINITY;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int col = n0 + 16 * t + r;
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
           const int64_t orow = m0 + 4 * g + reg;
-          const float v = fabsf(silu_fast(epilogue(acc[t][reg], osc, bcol[t])));
-          amx = (orow < M && col < N) ? fmaxf(amx, v) : amx;
+          const float y = epilogue(acc[t][reg], osc, bcol[t]);
+          ym = (orow < M && col < N) ? fmaxf(ym, y) : ym;
+        }
+      }
+      const float cand = silu_fast(ym);
+      if (ym >= 0.0f && cand >= 0.28f) {
+        amx = fmaxf(amx, cand);
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int col = n0 + 16 * t + r;
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int64_t orow = m0 + 4 * g + reg;
+            const float v = fabsf(silu_fast(epilogue(acc[t][reg], osc, bcol[t])));
+            amx = (orow < M && col < N) ? fmaxf(amx, v) : amx;
+          }
         }
       }
     } else if constexpr (EPI == kI8SwishQ) {
@@ -436,6 +457,20 @@ __global__ __launch_bounds__(kThreads) void tgemm_i8_kernel(
   }
 }
 
+// fast_silu(next float) >= fast_silu(x) for every fp32 x in [lo, hi) (bit patterns; both
+// non-negative): the property the I8_SWISH_AMAX epilogue's one-silu-a-lane max relies on
+__global__ __launch_bounds__(kThreads) void silu_monotone_kernel(uint32_t lo, uint32_t hi,
+                                                                 uint32_t* __restrict__ bad) {
+  uint32_t n = 0;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t b = lo + blockIdx.x * kThreads + threadIdx.x; b < hi; b += stride) {
+    const float a = __uint_as_float(b), c = __uint_as_float(b + 1);
+    n += silu_fast(c) < silu_fast(a) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
+}
+
 size_t i8_image_bytes(int nt, int64_t K) {
   return (size_t)(16 * nt) * (size_t)(64 * ceil_div(K, 64) + 16);
 }
@@ -531,6 +566,11 @@ bool ternary_gemm_i8_supported(int64_t K, int64_t N) {
 }
 
 size_t act_absmax_workspace(int P) { return sizeof(uint32_t) * (size_t)P * kAbsParts; }
+
+void launch_silu_monotone_check(uint32_t lo, uint32_t hi, uint32_t* bad, hipStream_t s) {
+  if (hi <= lo) return;
+  hipLaunchKernelGGL(silu_monotone_kernel, dim3(2048), dim3(kThreads), 0, s, lo, hi, bad);
+}
 
 void launch_act_absmax(const float* X, int P, int64_t n_per_pass, float* amax, void* ws,
                        hipStream_t s) {

@@ -75,6 +75,7 @@ SIGNATURES = {
     "ob_colsum_workspace": (_sz, [_i64]),
     "ob_colsum": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _sz, _c_f]),
     "ob_dense_supported": (_int, [_i64, _i64]),
+    "ob_silu_fast_monotone_check": (_int, [ctypes.c_uint32, ctypes.c_uint32, _c_f, _c_f]),
     "ob_dense_gemm_residual_drop": (_int, [_c_f, _i64, _i64, _c_f, _c_f, _i64, _c_f, _f32, _c_f,
                                             _i64, _c_f, _c_f]),
     "ob_dense_gemm": (_int, [_c_f, _i64, _i64, _c_f, _int, _c_f, _i64, _c_f, _c_f]),

@@ -39,7 +39,12 @@ __all__ = ["linear", "linear_rows_split", "colsum"]
 
 def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
     """ob_dense_gemm's preconditions (capi.hip: aligned16 of BOTH operands), so an operand
-    it would refuse takes the library path instead of raising."""
+    it would refuse takes the library path instead of raising. A long reduction (K > 2048:
+    the CTC head's input gradient, K = V = 5004) runs on the K-chunked kernel only for
+    full-size batches: one 128-row block per CU sweeps all of K, so the decoder output
+    layer's 3936 rows (31 blocks) stay on the library GEMM."""
+    if k > 2048 and x.shape[0] < 16384:
+        return False
     return (k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
             and w.data_ptr() % 16 == 0 and _lib.load().ob_dense_supported(k, n) == 1)
 

@@ -776,10 +776,20 @@ OB_API int ob_colsum(const float* x, int64_t rows, int64_t N, float* out, void* 
  *   ob_dense_gemm: w_trans = 0: Y[M][N] = X[M][K] . W^T + bias, W [N][K] (the forward);
  *                  w_trans = 1: Y[M][N] = X[M][K] . W,          W [K][N] (dX = dY . W).
  *                  bias may be NULL. X, W, Y 16-byte aligned; K, N multiples of 4.
+ *                  A K too long for the whole-K weight image (N <= 144) runs the K-chunked
+ *                  form (round 6): the CTC head's input gradient, K = V = 5004, replacing the
+ *                  library fp32 `g @ W` of the head's backward (losses.py:41-47 through
+ *                  conformer.py:275).
  *   ob_dense_dw:   dW[N][K] = dY[M][N]^T . X[M][K], db[N] = column sums of dY (db may be
  *                  NULL); N, K multiples of 48. Deterministic (fixed-order chunk sums).
  * ob_dense_supported(K, N) / ob_dense_dw_workspace(M, N, K) == 0: the shape is not taken.
  * ------------------------------------------------------------------------------------ */
+/* The property the int8 inference path's absmax launch relies on (round 6: max|silu| over a
+ * lane's elements taken as silu(max y), csrc/tgemm_i8.hip): adds to *bad (a device uint32 the
+ * caller zeroes) the count of fp32 bit patterns b in [lo_bits, hi_bits) with
+ * fast_silu(float(b + 1)) < fast_silu(float(b)). Non-negative finite patterns only. */
+OB_API int ob_silu_fast_monotone_check(uint32_t lo_bits, uint32_t hi_bits, uint32_t* bad,
+                                       void* stream);
 OB_API int ob_dense_supported(int64_t K, int64_t N);
 OB_API int ob_dense_gemm(const float* X, int64_t M, int64_t K, const float* W, int w_trans,
                          const float* bias, int64_t N, float* Y, void* stream);

@@ -40,6 +40,10 @@ def _bound(x, w, trans):
     (23904, 144, 144, True),   # pw2 dX
     (1000, 144, 288, False), (777, 288, 144, True), (65, 144, 144, True),
     (1, 144, 288, False), (130, 64, 48, False), (100, 20, 36, True), (513, 96, 192, False),
+    # long K on the K-chunked images (round 6): the CTC head's input gradient (K = V = 5004),
+    # ragged chunks / rows, W either way round, fewer than 144 columns
+    (23904, 5004, 144, True), (333, 5004, 144, True), (129, 4100, 144, False),
+    (17, 2052, 96, True), (40, 10000, 4, False),
 ])
 def test_dense_gemm_matches_fp64(gpu, m, k, n, trans):
     assert _lib().load().ob_dense_supported(k, n) == 1
@@ -182,8 +186,9 @@ def test_linear_dense_path_matches_float64(gpu, m, k, n):
         err = (got.double().cpu() - ref).abs().max().item()
         assert err <= 1e-5 * ref.abs().max().item(), err
     lib = _lib.load()
-    # the forward took the HIP kernel (K 2736: its weight image exceeds LDS; library GEMM)
-    assert lib.ob_dense_supported(k, n) == (0 if k == 2736 else 1)
+    # the HIP kernel takes the shape (K 2736: its weight image exceeds LDS, so the K-chunked
+    # kernel; linear._dense_ok still leaves K > 2048 at M < 16384 on the library GEMM)
+    assert lib.ob_dense_supported(k, n) == 1
     if n % 48 == 0 and k % 48 == 0:
         assert lib.ob_dense_dw_workspace(m, n, k) > 0  # the weight gradient on the dW kernels
 

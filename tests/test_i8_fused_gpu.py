@@ -151,3 +151,41 @@ def test_mhsa_i8_int8_operands_equal_unfused(gpu, monkeypatch):
         monkeypatch.setenv("OB_FUSED", "0")
         y0 = m(x, None, 2, pos)
     assert torch.equal(y1, y0), (y1 - y0).abs().max().item()
+
+
+def test_fast_silu_monotone_on_nonnegatives(gpu):
+    """The int8 absmax launch (I8_SWISH_AMAX, csrc/tgemm_i8.hip) takes a lane's max|silu| as
+    silu(max y): exact only if fast_silu is non-decreasing on y >= 0. Checked here over EVERY
+    fp32 in [0, 128] on the device (past 128, exp(-y) is 0 in fp32 and silu(y) = y)."""
+    from onebit_asr import _lib
+
+    lib = _lib.load()
+    bad = torch.zeros(1, dtype=torch.int32, device=gpu)
+    lo, hi = 0, int(np.float32(128.0).view(np.uint32))
+    _lib.check(lib.ob_silu_fast_monotone_check(lo, hi, bad.data_ptr(), _lib.stream_of(bad)),
+               "ob_silu_fast_monotone_check")
+    torch.cuda.synchronize()
+    assert bad.item() == 0
+    assert lib.ob_silu_fast_monotone_check(hi, lo, bad.data_ptr(), None) == -2
+
+
+@pytest.mark.parametrize("scale", [1e-4, 0.05])
+def test_i8_swish_amax_small_outputs(gpu, scale):
+    """Outputs too small for the one-silu-a-lane max (silu(max y) < 0.28, or every y < 0 in a
+    lane): the exact fallback gives the same absmax as the every-element epilogue."""
+    from onebit_asr.fused import _i8_epi, _i8q
+    from onebit_asr.quant import QuantizedLinear, act_absmax
+
+    torch.manual_seed(5)
+    M, K, N = 700, 144, 576
+    lin = QuantizedLinear(K, N, act_quant="absmax_int8").to(gpu)
+    with torch.no_grad():
+        lin.bias.uniform_(-scale, 0.0)
+    x = torch.randn(M, K, device=gpu) * scale
+    amax = act_absmax(x, 1)
+    xq = torch.from_numpy(_np_quant(x.cpu().numpy(), amax.item())).to(gpu)
+    with torch.no_grad():
+        y3, a3 = _i8q(xq, amax, lin, 2, 3)
+        s1, a1 = _i8_epi(x, amax, lin, 2, 1)
+    assert a3.item() == a1.item() == s1.abs().max().item()
+    assert np.array_equal(y3.cpu().numpy(), _np_quant(s1.cpu().numpy(), a1.item()))
