@@ -39,7 +39,9 @@ def main():
     torch.backends.cuda.preferred_blas_library("cublas")
     shapes = [(m, 144, 288, 0), (m, 144, 144, 0), (m, 288, 144, 1), (m, 144, 144, 1),
               (m, 144, 5004, 0), (3936, 144, 144, 0), (3936, 144, 432, 0), (3936, 144, 144, 1),
-              (3936, 144, 1024, 0), (3936, 1024, 144, 0), (m, 5004, 144, 1), (3936, 5004, 144, 1)]
+              (3936, 144, 1024, 0), (3936, 1024, 144, 0), (m, 5004, 144, 1), (3936, 5004, 144, 1),
+              # subsampling's output linear (K = 144 x 19): training B = 32, inference B = 256
+              (7968, 2736, 144, 0), (63744, 2736, 144, 0)]
     for m, k, n, trans in shapes:
         if n % 4:
             continue
