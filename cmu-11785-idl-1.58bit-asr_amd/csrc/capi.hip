@@ -11,7 +11,7 @@ using namespace ob;
 
 namespace {
 
-constexpr int kAbiVersion = 3;  // 3 (round 5): ob_relattn_bwd takes saved_elems
+constexpr int kAbiVersion = 4;  // 4 (round 6): ob_decattn_bwd consumes probs (dS' written there)
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -1571,7 +1571,7 @@ int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const
 
 int ob_decattn_bwd(const float* dctx, const float* ctx, const float* q, int64_t sq, const float* k,
                    int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                   int64_t dh, float p_drop, const float* probs, float* dq, int64_t gq, float* dk,
+                   int64_t dh, float p_drop, float* probs, float* dq, int64_t gq, float* dk,
                    int64_t gk, float* dv, int64_t gv, void* stream) {
   if (int st = decattn_check(B, H, Lq, Lk, dh, sq, sk, sv, p_drop)) return st;
   if (gq < H * dh || gk < H * dh || gv < H * dh) return OB_ERR_SHAPE;

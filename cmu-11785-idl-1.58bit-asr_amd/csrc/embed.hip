@@ -39,11 +39,23 @@ __global__ __launch_bounds__(kThreads) void embed_bwd_kernel(const int64_t* __re
   for (int64_t base = 0; base < N; base += kIdxChunk) {
     const int cnt = (int)min((int64_t)kIdxChunk, N - base);
     int nhit = 0;  // block-uniform
-    for (int off = 0; off < cnt; off += kThreads) {
+    // the chunk's indices are all loaded before the first ballot (one memory latency per
+    // chunk, not one per 256 indices)
+    constexpr int kPass = kIdxChunk / kThreads;
+    int64_t vv[kPass];
+#pragma unroll
+    for (int q = 0; q < kPass; ++q) {
+      const int i = q * kThreads + threadIdx.x;
+      vv[q] = i < cnt ? idx[base + i] : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < kPass; ++q) {
+      const int off = q * kThreads;
+      if (off >= cnt) break;  // block-uniform
       const int i = off + threadIdx.x;
       int slot = -1;
       if (i < cnt) {
-        const int64_t v = idx[base + i];
+        const int64_t v = vv[q];
         if (v >= v0 && v < v0 + kRowsPerBlock && v != pad) slot = (int)(v - v0);
       }
       const unsigned long long m = __ballot(slot >= 0);
@@ -59,10 +71,18 @@ __global__ __launch_bounds__(kThreads) void embed_bwd_kernel(const int64_t* __re
       for (int w = 0; w < kThreads / 64; ++w) nhit += wave_cnt[w];
       __syncthreads();
     }
-    for (int h = 0; h < nhit; ++h) {
-      const float* gr = g + (base + hit_n[h]) * C;
-      float* ar = acc + hit_slot[h] * C;
-      for (int c = threadIdx.x; c < C; c += kThreads) ar[c] += gr[c];
+    // the hits' gradient rows, 8 loads in flight (a dependent load per hit was the kernel's
+    // time); each accumulator still adds its rows in ascending n (the same sums)
+    for (int c = threadIdx.x; c < C; c += kThreads) {
+      int h = 0;
+      for (; h + 8 <= nhit; h += 8) {
+        float gv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) gv[u] = g[(base + hit_n[h + u]) * C + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[hit_slot[h + u] * C + c] += gv[u];
+      }
+      for (; h < nhit; ++h) acc[hit_slot[h] * C + c] += g[(base + hit_n[h]) * C + c];
     }
     __syncthreads();
   }

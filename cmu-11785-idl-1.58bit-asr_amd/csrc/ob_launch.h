@@ -142,7 +142,7 @@ void launch_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, 
                         uint64_t rng_off, float* probs, float* ctx, hipStream_t s);
 void launch_decattn_bwd(const float* dctx, const float* ctxo, const float* q, int64_t sq,
                         const float* k, int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                        int64_t dh, float p_drop, const float* probs, float* dq, int64_t gq,
+                        int64_t dh, float p_drop, float* probs, float* dq, int64_t gq,
                         float* dk, int64_t gk, float* dv, int64_t gv, hipStream_t s);
 
 // convmod.hip (conv module core, channels-last; see the file header)

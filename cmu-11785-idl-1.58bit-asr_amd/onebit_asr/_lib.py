@@ -222,7 +222,7 @@ SIGNATURES = {
                _sz, _c_f]),
 }
 
-ABI_VERSION = 3  # 3 (round 5): ob_relattn_bwd takes saved_elems
+ABI_VERSION = 4  # 4 (round 6): ob_decattn_bwd consumes probs (dS' written there)
 
 _lib = None
 

@@ -55,6 +55,11 @@ class _DecAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        # the library's backward overwrites probs with dS' (ob_decattn_bwd consumes it)
+        if getattr(ctx, "consumed", False):
+            raise RuntimeError("decoder attention: backward ran twice on one forward "
+                               "(retain_graph); its saved probabilities were consumed")
+        ctx.consumed = True
         heads, p, self_mode, e, Lk, sq, skv, koff, voff = ctx.meta
         xq, xkv, probs, out = ctx.saved_tensors
         dout = dout.contiguous()

@@ -466,7 +466,8 @@ OB_API int ob_dw_grouped(const ob_dwg_gemm* gemms, int64_t G, void* ws, size_t w
  * Lk <= 256 and the per-(b, h) working set within LDS (ob_decattn_supported).
  * ctx must be 16-byte aligned. bwd (ctx = the forward's output): dq [B][Lq][*] (row stride
  * gq), dk / dv [B][Lk][*] (gk / gv), every element of the heads' columns written -- e.g.
- * straight into the packed projection's gradient. */
+ * straight into the packed projection's gradient. The backward CONSUMES probs: it holds the
+ * score gradients dS' afterwards (two launches: dk / dv, then dq from dS'); ABI 4. */
 OB_API int ob_decattn_supported(int64_t Lq, int64_t Lk, int64_t dh);
 OB_API int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk, const float* v,
                           int64_t sv, const uint8_t* kmask, int64_t causal, int64_t B, int64_t H,
@@ -474,7 +475,7 @@ OB_API int ob_decattn_fwd(const float* q, int64_t sq, const float* k, int64_t sk
                           int64_t rng_offset, float* probs, float* ctx, void* stream);
 OB_API int ob_decattn_bwd(const float* dctx, const float* ctx, const float* q, int64_t sq,
                           const float* k, int64_t sk, const float* v, int64_t sv, int64_t B, int64_t H, int64_t Lq,
-                          int64_t Lk, int64_t dh, float p_drop, const float* probs, float* dq,
+                          int64_t Lk, int64_t dh, float p_drop, float* probs, float* dq,
                           int64_t gq, float* dk, int64_t gk, float* dv, int64_t gv, void* stream);
 
 /* ------------------------------------------------------------------------------------

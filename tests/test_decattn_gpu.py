@@ -24,6 +24,8 @@ CASES = [  # (B, H, Lq, Lk, dh, self_mode)
     (2, 4, 7, 256, 16, False),
     (2, 2, 64, 64, 64, True),
     (5, 4, 13, 97, 36, False),
+    (2, 4, 100, 130, 36, False),  # dq in 48-query tiles, the last one ragged
+    (2, 2, 100, 100, 32, True),
 ]
 
 
@@ -159,3 +161,16 @@ def test_decoder_hip_path_equals_additive_path(gpu):
         ref = grads[1][n]
         err = (grads[0][n] - ref).abs().max().item()
         assert err <= 1e-4 * ref.abs().max().item() + 1e-6, (n, err)
+
+
+def test_decattn_second_backward_refused(gpu):
+    """The backward writes dS' over the saved probabilities (ob_decattn_bwd consumes them), so
+    a second backward through the same forward (retain_graph) raises instead of reading dS'
+    as P."""
+    from onebit_asr.decattn import _DecAttnFn
+
+    xq = torch.randn(2, 5, 3 * 64, device=gpu, requires_grad=True)
+    ctx = _DecAttnFn.apply(xq, None, 4, None, True, 0.0, None, 0)
+    ctx.sum().backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="consumed"):
+        ctx.sum().backward()
