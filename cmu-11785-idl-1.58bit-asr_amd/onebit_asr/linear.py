@@ -37,13 +37,20 @@ __all__ = ["linear", "linear_rows_split", "colsum"]
 
 
 
+# K above this at M < 16384 rows: the library GEMM (see _dense_ok). 512: the decoder FFN's
+# K = 1024 products (linear2 forward, linear1 dX, M = 3936) ran at 30.7 / 31.0 us on the
+# dgemm kernel (one 16-column tile per block: the K = 1024 image leaves no room for more)
+# against 17.9 / 17.0 us on hipBLASLt (same-box A/B, profiles/r6/lib_k/).
+_LIB_K = 512
+
+
 def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
     """ob_dense_gemm's preconditions (capi.hip: aligned16 of BOTH operands), so an operand
-    it would refuse takes the library path instead of raising. A long reduction (K > 2048:
-    the CTC head's input gradient, K = V = 5004) runs on the K-chunked kernel only for
-    full-size batches: one 128-row block per CU sweeps all of K, so the decoder output
-    layer's 3936 rows (31 blocks) stay on the library GEMM."""
-    if k > 2048 and x.shape[0] < 16384:
+    it would refuse takes the library path instead of raising. A long reduction (K >
+    _LIB_K: the CTC head's input gradient, K = V = 5004) runs on the HIP kernels only for
+    full-size batches (the K-chunked kernel: one 128-row block per CU sweeps all of K), so
+    the decoder's 3936-row products with K = 1024 / 5004 stay on the library GEMM."""
+    if k > _LIB_K and x.shape[0] < 16384:
         return False
     return (k % 4 == 0 and n % 4 == 0 and x.data_ptr() % 16 == 0
             and w.data_ptr() % 16 == 0 and _lib.load().ob_dense_supported(k, n) == 1)
