@@ -37,11 +37,12 @@ __all__ = ["linear", "linear_rows_split", "colsum"]
 
 
 
-# K above this at M < 16384 rows: the library GEMM (see _dense_ok). 512: the decoder FFN's
+# K above this at M < 16384 rows: the library GEMM (see _dense_ok). The decoder FFN's
 # K = 1024 products (linear2 forward, linear1 dX, M = 3936) ran at 30.7 / 31.0 us on the
 # dgemm kernel (one 16-column tile per block: the K = 1024 image leaves no room for more)
-# against 17.9 / 17.0 us on hipBLASLt (same-box A/B, profiles/r6/lib_k/).
-_LIB_K = 512
+# against 17.9 / 17.0 us on hipBLASLt, the self-attention in-projection's dX (K = 432) at
+# 18.7 against 14.6 us (same-box A/Bs, profiles/r6/lib_k/).
+_LIB_K = 256
 
 
 def _dense_ok(x: torch.Tensor, w: torch.Tensor, k: int, n: int) -> bool:
