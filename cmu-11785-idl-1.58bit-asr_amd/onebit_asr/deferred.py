@@ -418,6 +418,19 @@ def _flush() -> None:
         _flush_tables()
 
 
+_SIDE_TABLES = True  # finish tables beside the grouped launch (tests flip it)
+_SIDES: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """One side stream per device for the finish tables (created once: a captured graph keeps
+    the stream it forked to)."""
+    st = _SIDES.get(dev.index)
+    if st is None:
+        st = _SIDES[dev.index] = torch.cuda.Stream(device=dev)
+    return st
+
+
 def _flush_tables() -> None:
     lib = _lib.load()
     dw, ln, cm, tk = _S.tables[_S.dev]
@@ -433,20 +446,41 @@ def _flush_tables() -> None:
             if t.is_cuda:
                 t.record_stream(home)
     plan = _chunk_plan(_XCHG) if (_XCHG is not None and _S.dwg) else None
+
+    def tables(stream: int) -> None:
+        if _S.dw_n:
+            _lib.check(lib.ob_dw_finish_table(dw.data_ptr(), _S.dw_n, _S.dw_blocks, stream),
+                       "ob_dw_finish_table")
+        if _S.ln_n:
+            _lib.check(lib.ob_ln_param_table(ln.data_ptr(), _S.ln_n, _S.ln_dmax, stream),
+                       "ob_ln_param_table")
+        if _S.cm_n:
+            _lib.check(lib.ob_cm_wgrad_table(cm.data_ptr(), _S.cm_n, _S.cm_nmax, stream),
+                       "ob_cm_wgrad_table")
+
     if _S.dwg:
         xs = [g.X for g in _S.dwg]  # (q / k / v of one LN output share X)
         LAST_DWG[:] = [(g.N, g.K, g.M, g.P, bool(g.W), xs.index(g.X)) for g in _S.dwg]
-        if plan is None:
+    if _S.dwg and plan is None and _SIDE_TABLES and (_S.dw_n or _S.ln_n or _S.cm_n):
+        # The finish tables (memory-bound, every input produced before the flush, outputs
+        # disjoint from the grouped launch's) on a side stream forked from the flush stream,
+        # joined before the post ops: they run beside the MFMA-bound grouped launch instead
+        # of after it (a fork / join in the captured step graph).
+        dev = torch.device("cuda", _S.dev)
+        home = torch.cuda.ExternalStream(_S.stream, device=dev)
+        side = _side_stream(dev)
+        fork = torch.cuda.Event()
+        fork.record(home)
+        side.wait_event(fork)
+        tables(side.cuda_stream)
+        _grouped(lib, _S.dwg, tk)
+        join = torch.cuda.Event()
+        join.record(side)
+        home.wait_event(join)
+    else:
+        if _S.dwg and plan is None:
             _grouped(lib, _S.dwg, tk)
-    if _S.dw_n:
-        _lib.check(lib.ob_dw_finish_table(dw.data_ptr(), _S.dw_n, _S.dw_blocks, _S.stream),
-                   "ob_dw_finish_table")
-    if _S.ln_n:
-        _lib.check(lib.ob_ln_param_table(ln.data_ptr(), _S.ln_n, _S.ln_dmax, _S.stream),
-                   "ob_ln_param_table")
-    if _S.cm_n:
-        _lib.check(lib.ob_cm_wgrad_table(cm.data_ptr(), _S.cm_n, _S.cm_nmax, _S.stream),
-                   "ob_cm_wgrad_table")
+        tables(_S.stream)
     if _S.post:
         dev = torch.device("cuda", _S.dev)
         with torch.cuda.stream(torch.cuda.ExternalStream(_S.stream, device=dev)):
